@@ -1,0 +1,148 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Run here (where /root/reference exists):  python tests/golden/make_golden.py
+
+Every expected value is produced by oracle/_ref/libpqp_ref.so -- PQP_CPU.c
+compiled unmodified from /root/reference by oracle/Makefile -- or parsed from
+its own stdout.  The only inputs not taken from the reference are the synthetic
+primal problems, which come from the counter-based generator shared by the
+oracle and the device code (oracle/pqp_oracle.c orc_synth_primal); the
+reference then performs the dual conversion, the updates and the solve on them.
+
+Outputs (all small):
+  bundled.npz           bundled example: dual data, Y after k updates, Y*, U*,
+                        h, per-iteration (Jp, Jd), fixed-999 Y*, FMA negative control
+  bundled_stdout.txt    the reference program's stdout (PQP_CPU.c main)
+  synth_converge.npz    converge-mode (N, M, seed) cases that the reference solves
+  synth_large.npz       N=1024/M=512 and N=1000/M=500: dual-data digests and Y
+                        after a few reference updates
+"""
+from __future__ import annotations
+
+import hashlib
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT / "oracle"))
+from oracle import Oracle, Reference, REF_BIN, build  # noqa: E402
+
+OUT = Path(__file__).resolve().parent
+REFERENCE_DIR = Path("/root/reference")
+
+CONVERGE_CASES = [(8, 4, 1), (8, 4, 2), (8, 4, 4), (12, 6, 1), (12, 6, 5), (16, 8, 1), (16, 8, 4),
+                  (24, 12, 3), (32, 16, 3), (32, 16, 4)]
+LARGE_CASES = [(1024, 512, 1, 0, 3), (1000, 500, 2, 7, 2)]  # N, M, seed, instance, updates
+
+
+def digest(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float32).tobytes()).hexdigest()
+
+
+def bundled(ref: Reference):
+    P = ref.bundled_problem(REFERENCE_DIR)
+    N, M = P["N"], P["M"]
+    S = ref.split(P["Qd"], P["Fd"], N)
+    Y = np.full(N, 1000.0, np.float32)
+    snaps, jp, jd, feas = {}, [], [], []
+    for h in range(1, 314):          # terminate() is evaluated before update h
+        U = ref.u_from_y(Y, P)
+        f = ref.feasible(U, P)
+        feas.append(f)
+        jd.append(ref.cost(Y, P["Qd"], P["Fd"], P["Md"], N))
+        jp.append(ref.cost(U, P["Qp"], P["Fp"], P["Mp"], M))
+        if h in (1, 2, 10, 100, 312, 313):
+            snaps[h] = Y.copy()
+        if h == 313:
+            break
+        Y = ref.update(Y, S, P["Fd"], N)
+    h, Ystar, _ = ref.solve(P)
+    assert h == 313, h
+    assert np.array_equal(Ystar.view(np.uint32), snaps[313].view(np.uint32))
+    Ufinal = ref.u_from_y(Ystar, P)
+    Jp = ref.cost(Ufinal, P["Qp"], P["Fp"], P["Mp"], M)
+    Jd = ref.cost(Ystar, P["Qd"], P["Fd"], P["Md"], N)
+    # fixed 1000-iteration mode: while(h<1000) -> 999 updates
+    Yf = np.full(N, 1000.0, np.float32)
+    for _ in range(999):
+        Yf = ref.update(Yf, S, P["Fd"], N)
+    theta_diag = S["theta"].reshape(N, N).diagonal().copy()
+    out = dict(N=np.int64(N), M=np.int64(M), h=np.int64(h), Qd=P["Qd"], Fd=P["Fd"], Md=P["Md"], Qp=P["Qp"],
+               Qp_inv=P["Qp_inv"], Fp=P["Fp"], Mp=P["Mp"], Gp=P["Gp"], Kp=P["Kp"], theta=theta_diag,
+               Fdp=S["Fdp"], Fdn=S["Fdn"], Ystar=Ystar, Ustar=Ufinal, Jp=np.float32(Jp), Jd=np.float32(Jd),
+               Y_h1=snaps[1], Y_h2=snaps[2], Y_h10=snaps[10], Y_h100=snaps[100], Y_h312=snaps[312],
+               iter_Jp=np.asarray(jp, np.float32), iter_Jd=np.asarray(jd, np.float32),
+               iter_feasible=np.asarray(feas, np.int8), Y_fixed999=Yf)
+    fma = fma_negative_control(P)
+    if fma is not None:
+        out["Ystar_fma_contracted"] = fma
+    np.savez(OUT / "bundled.npz", **out)
+    stdout = subprocess.run([str(REF_BIN)], cwd=REFERENCE_DIR, capture_output=True, text=True, check=True).stdout
+    (OUT / "bundled_stdout.txt").write_text(stdout)
+    print("bundled: h", h, "Jp", Jp, "Jd", Jd)
+
+
+def fma_negative_control(P):
+    """Y* of the reference built WITH fused multiply-add contraction: a result
+    the product must NOT reproduce (FMA note)."""
+    so = ROOT / "oracle" / "_ref" / "libpqp_ref_fma.so"
+    src = REFERENCE_DIR / "PQP_CPU.c"
+    r = subprocess.run(["gcc", "-O2", "-mfma", "-ffp-contract=fast", "-fPIC", "-shared", "-w",
+                        "-Dmain=pqp_ref_main", str(src), "-o", str(so), "-lm"])
+    if r.returncode != 0:
+        return None
+    h, Y, _ = Reference(so).solve(P)
+    return Y
+
+
+def synth_converge(ref: Reference, orc: Oracle):
+    rows, ys, us = [], [], []
+    for (N, M, seed) in CONVERGE_CASES:
+        P = orc.synth_primal(seed, 0, N, M)
+        P["Qd"], P["Fd"], P["Md"] = ref.convert_to_dual(P["Qp_inv"], P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+        P["Qp"] = ref.gauss_jordan(P["Qp_inv"], M)
+        h, Y, U = ref.solve(P)
+        U = ref.u_from_y(Y, P)
+        rows.append((N, M, seed, h))
+        ys.append(Y)
+        us.append(U)
+        print("converge", N, M, seed, "h", h)
+    np.savez(OUT / "synth_converge.npz", cases=np.asarray(rows, np.int64),
+             Y=np.concatenate(ys), U=np.concatenate(us))
+
+
+def synth_large(ref: Reference, orc: Oracle):
+    out = {}
+    for (N, M, seed, inst, ups) in LARGE_CASES:
+        P = orc.synth_primal(seed, inst, N, M)
+        Qd, Fd, Md = ref.convert_to_dual(P["Qp_inv"], P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+        S = ref.split(Qd, Fd, N)
+        Y = np.full(N, 1000.0, np.float32)
+        for _ in range(ups):
+            Y = ref.update(Y, S, Fd, N)
+        tag = f"n{N}_m{M}_s{seed}_i{inst}"
+        out[f"{tag}_meta"] = np.asarray([N, M, seed, inst, ups], np.int64)
+        out[f"{tag}_Qd_sha256"] = np.frombuffer(bytes.fromhex(digest(Qd)), np.uint8)
+        out[f"{tag}_Fd"] = Fd
+        out[f"{tag}_Md"] = Md
+        out[f"{tag}_theta"] = S["theta"].reshape(N, N).diagonal().copy()
+        out[f"{tag}_Qd_row0"] = Qd[:N].copy()
+        out[f"{tag}_Qd_diag"] = Qd.reshape(N, N).diagonal().copy()
+        out[f"{tag}_Y"] = Y
+        print("large", tag, "done")
+    np.savez(OUT / "synth_large.npz", **out)
+
+
+def main():
+    build()
+    ref, orc = Reference(), Oracle()
+    bundled(ref)
+    synth_converge(ref, orc)
+    synth_large(ref, orc)
+
+
+if __name__ == "__main__":
+    main()
