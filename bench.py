@@ -1,0 +1,242 @@
+"""bench.py -- PQP dual-update throughput on MI355X (BASELINE.json configs).
+
+Workload (one line of JSON on rank 0): BASELINE configs[3] at N=1 and
+configs[4] across N GPUs -- synthetic dense dual problems of n_dual = 1024
+(M = 512 primal), 4096 independent problems per GPU (weak scaling), each
+with its own Qd (16 GiB of fp32 Qd per GPU, generated on device), run in the
+reference's fixed-iteration mode (testing/ harness: updateY2 only).
+
+A *step* is one updateY2 of every problem of the batch (one PQP iteration of
+the whole job).  `value` = problems x steps over all ranks / max-over-ranks
+wall time of exactly K steps (inputs already resident in HBM), in
+instance-iterations per second.
+
+Extra keys:
+  roofline      the fused update kernel vs the 8 TB/s HBM peak, algorithmic
+                bytes ALG(N) = 4N^2 + 16N per problem-iteration,
+                duration from HIP events on the launch stream; `traffic` is
+                the PMC-measured HBM bytes per launch (profiles/pmc_traffic.json)
+  cpu_baseline  PQP_CPU.c's own updateY2 (oracle/_ref, compiled from the
+                reference) -- or the bit-exact restatement if that build is
+                absent -- single thread on this host, bounded sample
+  bundled       the bundled example (configs[0]/[1]) on 1 GPU through the
+                C ABI: fixed 1000-iteration mode and converge mode (h = 313)
+  gather_ms     RCCL gather of every rank's Y* to rank 0 (outside the timed
+                region)
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+KERNEL = "k_batch_iterate<256>"
+
+
+def alg_bytes(n: int) -> int:
+    """Algorithmic HBM bytes per problem-iteration: Qd read once (the split
+    matrices and Theta are derived in registers) + theta, Fd, y_in, y_out."""
+    return 4 * n * n + 16 * n
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1024, help="n_dual")
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--chunk", type=int, default=1, help="iterations per kernel launch")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bundled", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(n: int, seconds: float, seed: int) -> dict:
+    """Time the reference's updateY2 on one problem of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+
+    from oracle import REF_SO, Oracle, Reference
+
+    orc = Oracle()
+    P = orc.synth_problem(seed, 0, n, n // 2, with_qp=False)
+    if REF_SO.exists():
+        ref = Reference()
+        S = ref.split(P["Qd"], P["Fd"], n)
+        Y = np.full(n, 1000.0, np.float32)
+        ups, t0 = 0, time.perf_counter()
+        while True:
+            Y = ref.update(Y, S, P["Fd"], n)
+            ups += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        kind = "reference"
+        what = "oracle/_ref/libpqp_ref.so (PQP_CPU.c, gcc -O2 -ffp-contract=off) updateY2"
+    else:
+        per, _ = orc.time_updates(P["Qd"], P["Fd"], n, 3)
+        ups = max(3, int(seconds / max(per / 3, 1e-6)))
+        el, _ = orc.time_updates(P["Qd"], P["Fd"], n, ups)
+        kind = "port"
+        what = "oracle/pqp_oracle.c (bit-exact restatement, -O2 -ffp-contract=off) updateY2"
+    return {"value": ups / el, "unit": "instance-iterations/s", "cores": 1, "kind": kind,
+            "sample": f"{what}: {ups} fixed-mode updates of 1 synthetic problem (n_dual={n}, M={n // 2}, seed "
+                      f"{seed}) in {el:.1f} s, 1 thread, setup excluded; host has {os.cpu_count()} logical CPUs"}
+
+
+def bundled_bench(pqp_amd) -> dict:
+    import numpy as np
+
+    P = pqp_amd.example_problem(ROOT / "tests" / "golden" / "example")
+    pqp_amd.solve_dual(P, mode=pqp_amd.MODE_FIXED, num_iter=1000)  # warm
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = pqp_amd.solve_dual(P, mode=pqp_amd.MODE_FIXED, num_iter=1000)
+    fixed_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        c = pqp_amd.solve_dual(P)
+    conv_s = (time.perf_counter() - t0) / reps
+    return {"n_dual": int(P["N"]), "fixed1000_ms": fixed_s * 1e3, "fixed1000_iter_per_s": 999 / fixed_s,
+            "converge_ms": conv_s * 1e3, "converge_h": c["h"], "converge_iter_per_s": c["h"] / conv_s,
+            "y_fixed_finite": bool(np.all(np.isfinite(r["Y"]))),
+            "note": "wall time of one pqp_solve_dual call incl. H2D/D2H and setup (single problem, 1 GPU)"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    import pqp_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, B, K, W, C = args.n, args.batch, args.steps, args.warmup, max(1, args.chunk)
+    # "scatter inputs": rank 0 hands each rank its (seed, first problem, count)
+    cfg = torch.tensor([args.seed, rank * B, B], dtype=torch.int64, device=dev)
+    if dist is not None:
+        parts = [torch.tensor([args.seed, r * B, B], dtype=torch.int64, device=dev) for r in range(world)]
+        dist.scatter(cfg, parts if rank == 0 else None, src=0)
+    seed, inst0, B = (int(v) for v in cfg.tolist())
+
+    batch = pqp_amd.Batch(B, N, device=dev)
+    batch.generate(seed, inst0=inst0, M=N // 2)
+    stream = torch.cuda.current_stream(dev)
+
+    def run(steps):
+        launches = 0
+        done = 0
+        first = True
+        while done < steps:
+            c = min(C, steps - done)
+            batch.iterate(c, from_start=first and done == 0)
+            first = False
+            done += c
+            launches += 1
+        return launches
+
+    run(max(W, 1))
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    launches = run(K)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    # gather Y* to rank 0 over RCCL (reported separately, not in `value`)
+    gather_ms = None
+    if dist is not None:
+        y = batch.Y[:, :N].contiguous()
+        outs = [torch.empty_like(y) for _ in range(world)] if rank == 0 else None
+        torch.cuda.synchronize(dev)
+        g0 = time.perf_counter()
+        dist.gather(y, outs, dst=0)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+    Yh = batch.Y[:, :N]
+    finite = bool(torch.isfinite(Yh).all().item()) and bool((Yh >= 0).all().item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    per_launch_ms = kern_ms / launches
+    achieved = alg_bytes(N) * B * C / (per_launch_ms * 1e-3) / 1e9 if launches else 0.0
+    traffic = None
+    tf = ROOT / "profiles" / "pmc_traffic.json"
+    if tf.exists():
+        rec = json.loads(tf.read_text()).get(f"n{N}_b{B}_c{C}")
+        if rec:
+            traffic = rec.get("hbm_bytes_per_launch")
+    result = {
+        "metric": "PQP iterations/sec (and QP-instances/sec) at fixed n_dual",
+        "value": B * world * K / elapsed,
+        "unit": "instance-iterations/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed * 1e3 / K,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (counter-based generator, dual built on device with convertToDual's exact arithmetic)",
+        "config": {"workload": "BASELINE configs[3] (N=1) / configs[4] (N=8): synthetic n_dual=1024, M=512, "
+                               f"{B} independent problems per GPU, fixed-iteration updateY2",
+                   "n_dual": N, "batch_per_gpu": B, "global_batch": B * world, "iters_per_launch": C,
+                   "parallelism": f"problem-sharded x{world} (no data-path collective)"},
+        "qp_instances_per_s_at_1000_iters": B * world * K / elapsed / 999.0,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL,
+                     "alg_bytes_per_launch": alg_bytes(N) * B * C, "avg_launch_ms": per_launch_ms},
+        "results_finite_nonneg": finite,
+        "gather_ms": gather_ms,
+    }
+    if world == 1 and not args.no_bundled:
+        result["bundled"] = bundled_bench(pqp_amd)
+    if world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed)
+    print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

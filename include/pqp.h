@@ -1,0 +1,174 @@
+/*
+ * include/pqp.h -- C ABI of libpqp (pqp-for-mpc_amd), the MI355X-native
+ * drop-in for the PQP dual-update hot path of yashsoni501/PQP-for-MPC.
+ *
+ * Two layers:
+ *
+ *  1. Drop-in entry points.  Same names, argument order and meaning as the
+ *     reference's C functions (PQP_CPU.c), on caller-owned HOST buffers of
+ *     row-major fp32.  They run on the GPU (HIP, gfx950) and return results
+ *     identical to PQP_CPU.c.  Like the reference they have no status return;
+ *     on a HIP/allocation failure they print a message and exit(EXIT_FAILURE)
+ *     (the reference's own failure behaviour, PQP_GPU_optimized.cu:83-89).
+ *
+ *  2. pqp_* entry points.  Status-returning (PQP_OK or a negative PQP_ERR_*;
+ *     pqp_last_error() explains), explicit sizes, and the batched device API
+ *     that works on DEVICE pointers on the caller's hipStream_t (passed as
+ *     void*).  Nothing here takes framework types.
+ *
+ * Device layout of a batch of B dual problems of size N:
+ *   QdT   [B][N][ldq]  Qd stored column-major per instance: element (i,k)
+ *                      of Qd is QdT[b*qstride + k*ldq + i]; ldq >= N, ldq % 4 == 0
+ *   theta, Fd, Y       [B][ldv] fp32 vectors, ldv >= N
+ */
+#ifndef PQP_H
+#define PQP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQP_OK 0
+#define PQP_ERR_ARG (-1)           /* bad size / pointer / layout                 */
+#define PQP_ERR_HIP (-2)           /* a HIP runtime call or kernel launch failed  */
+#define PQP_ERR_ALLOC (-3)         /* device allocation failed                    */
+#define PQP_ERR_IO (-4)            /* input file missing or short                 */
+#define PQP_ERR_NOT_CONVERGED (-5) /* converge mode hit its update cap            */
+#define PQP_ERR_NO_DEVICE (-6)     /* no gfx950 device visible                    */
+
+/* Solve modes of pqp_solve_dual. */
+#define PQP_MODE_CONVERGE 0 /* while(!terminate(Y)) update  (PQP_CPU.c:718)            */
+#define PQP_MODE_FIXED 1    /* while(h < num_iter) update   (testing/ harness, no terminate) */
+
+const char *pqp_last_error(void);
+int pqp_version(void);
+
+/* ======================================================================
+ * 1. Drop-in entry points (reference signatures, host pointers)
+ * ==================================================================== */
+
+/* PQP_CPU.c:694-750.  Runs the whole solve on the GPU in one persistent
+ * workgroup (setup, terminate() before every update, updateY2) and prints
+ * "Printing number of iterations = %ld\n" exactly as the reference does.
+ * Y (N) and U (M) are outputs; the rest are inputs. */
+void solveQuadraticDual(float *Y, float *Qd, float *Fd, float *Md, float *U, float *Qp, float *Qp_inv,
+                        float *Fp, float *Mp, float *Gp, float *Kp, int N, int M);
+
+/* PQP_CPU.c:603-618.  One multiplicative update from the stored split
+ * matrices Qdp_theta = max(0,Qd)+Theta, Qdn_theta = max(0,-Qd)+Theta and
+ * Fdp = max(0,Fd), Fdn = max(0,-Fd).  Fd is accepted and unused, as in the
+ * reference. */
+void updateY2(float *Y_next, float *Y, float *Qdp_theta, float *Qdn_theta, float *Fd, float *Fdp,
+              float *Fdn, int N);
+
+/* PQP_CPU.c:673-687.  Writes U = -Qp_inv(Gp'Y + Fp) and returns 1 when the
+ * feasibility and duality-gap tests all pass. */
+int terminate(float *Y, float *Qd, float *Fd, float *Md, float *U, float *Qp, float *Qp_inv, float *Fp,
+              float *Mp, float *Gp, float *Kp, int N, int M);
+
+/* PQP_CPU.c:489-498: Qd = (Gp Qp_inv) Gp', Fd = (Gp Qp_inv) Fp + Kp,
+ * Md = (Fp' Qp_inv) Fp - Mp. */
+void convertToDual(float *Qd, float *Fd, float *Md, float *Qp_inv, float *Gp, float *Kp, float *Fp,
+                   float *Mp, int N, int M);
+
+/* PQP_CPU.c:352-360: U = -Qp_inv (Gp'Y + Fp). */
+void computeUfromY(float *U, float *Y, float *Fp, float *Gp, float *Qp_inv, int N, int M);
+
+/* PQP_CPU.c:648-666: J = 0.5 (Z'Q) Z + F'Z + M[0]/2. */
+float computeCost(float *Z, float *Q, float *F, float *M, int N);
+
+/* PQP_CPU.c:632-641: 1 iff Gp U <= Kp + max(1e-6 Kp, 1e-6) element-wise. */
+int checkFeas(float *U, float *Gp, float *Kp, int N, int M);
+
+/* PQP_CPU.c:503-519: theta (N x N, caller-zeroed as in the reference) gets
+ * theta[i][i] = max(sum_j max(0,-Qd[i][j]), 5); other entries untouched. */
+void computeTheta(float *theta, float *Qd, int N);
+
+/* PQP_CPU.c:84-147: output[a x c] = op(mat1)[a x b] * op(mat2)[b x c];
+ * output may alias an input. */
+void matrixMultiply(float *output, float *mat1, int transpose1, float *mat2, int transpose2, int a, int b,
+                    int c);
+
+/* PQP_CPU.c:251-326: res = inverse(A) by the reference's Gauss-Jordan
+ * (one bubble pass on column 0, no pivoting). */
+void Gauss_Jordan(float *A, float *res, int N);
+
+/* PQP_CPU.c:373-382 / 395-428, with the reference's compile-time problem
+ * dimensions (pHorizon=1, nState=29, nInput=7, nDis=1; PQP_CPU.c:13-17). */
+void computeFp(float *Fp, float *Fp1, float *Fp2, float *Fp3, float *D, float *x);
+void computeMp(float *Mp, float *Mp1, float *Mp2, float *Mp3, float *Mp4, float *Mp5, float *Mp6, float *D,
+               float *x);
+
+/* PQP_CPU.c:757-930: reads ./example/{Qp_inv,Fp1,Fp2,Fp3,Mp1..Mp6,Gp,Kp,Z,Theta,D,x}.txt
+ * relative to the current directory, with the reference's transposed
+ * layout and compile-time dimensions.  (Host I/O; no GPU work.) */
+void input(float *qp_inv, float *Fp1, float *Fp2, float *Fp3, float *Mp1, float *Mp2, float *Mp3, float *Mp4,
+           float *Mp5, float *Mp6, float *Gp, float *Kp, float *x, float *D, float *theta, float *Z);
+
+/* ======================================================================
+ * 2a. Status-returning host-pointer API
+ * ==================================================================== */
+
+/* solveQuadraticDual without the printf and with explicit control:
+ *   mode PQP_MODE_CONVERGE: iterate until terminate() passes; gives up with
+ *     PQP_ERR_NOT_CONVERGED after max_updates updates (<= 0: no cap).
+ *   mode PQP_MODE_FIXED: num_iter-1 updates, no terminate (testing/ harness).
+ * On return *h_out is the reference's printed h (updates + 1), Y and U hold
+ * the final iterate, Jp_out and Jd_out get the costs of the last terminate() that
+ * got past the feasibility test (NaN if none).  Any of the out pointers
+ * except Y may be NULL. */
+int pqp_solve_dual(const float *Qd, const float *Fd, const float *Md, const float *Qp, const float *Qp_inv,
+                   const float *Fp, const float *Mp, const float *Gp, const float *Kp, int N, int M, int mode,
+                   long long num_iter, long long max_updates, float *Y, float *U, long long *h_out,
+                   float *Jp_out, float *Jd_out);
+
+/* One update on host buffers from Qd/theta-diag/Fd (the fused form used by
+ * the solver: Qd+-, Theta and Fd+- derived on the fly). */
+int pqp_update_host(const float *Qd, const float *theta_diag, const float *Fd, const float *Y, float *Y_next,
+                    int N);
+
+/* Bundled-example reader with explicit dimensions: m = nInput*pHorizon,
+ * nd = nDis*pHorizon, ns = nState, N = 4m.  Files are read from `dir`. */
+int pqp_read_example(const char *dir, int m, int nd, int ns, float *Qp_inv, float *Fp1, float *Fp2,
+                     float *Fp3, float *Mp1, float *Mp2, float *Mp3, float *Mp4, float *Mp5, float *Mp6,
+                     float *Gp, float *Kp, float *x, float *D);
+
+/* main() of PQP_CPU.c:935-1013 on the GPU: read `dir`, build the dual, solve,
+ * recompute U, print the reference's stdout to `out` (a FILE*; NULL = stdout). */
+int pqp_run_example(const char *dir, void *out);
+
+/* ======================================================================
+ * 2b. Batched device API (device pointers, caller's stream; async)
+ * ==================================================================== */
+
+/* Synthetic dual problems: instance b of the batch is problem
+ * number inst0+b of `seed`; primal Qp_inv = diag(0.1+u), Gp in {-1,0,1},
+ * Kp = 10u, Fp = 20u-10, Mp = 1, converted to the dual with
+ * convertToDual's exact arithmetic.  Writes QdT (column-major, padded rows
+ * zeroed), Fd, Md (may be NULL) and theta. */
+int pqp_batch_generate(uint32_t seed, long long inst0, int B, int N, int M, float *d_QdT, int ldq,
+                       long long qstride, float *d_Fd, float *d_Md, float *d_theta, int ldv, void *stream);
+
+/* Pack B row-major N x N Qd matrices (device, contiguous) into QdT layout. */
+int pqp_batch_pack(int B, int N, const float *d_Qd, float *d_QdT, int ldq, long long qstride, void *stream);
+
+/* theta[b][i] = max(sum_j max(0,-Qd_b[i][j]), 5)  (computeTheta). */
+int pqp_batch_theta(int B, int N, const float *d_QdT, int ldq, long long qstride, float *d_theta, int ldv,
+                    void *stream);
+
+/* One updateY2 for every instance: Y_next = num/den * Y. */
+int pqp_batch_update(int B, int N, const float *d_QdT, int ldq, long long qstride, const float *d_theta,
+                     const float *d_Fd, int ldv, const float *d_Y, float *d_Ynext, void *stream);
+
+/* `updates` consecutive updateY2 per instance in ONE launch, the iterate
+ * resident in LDS (fixed-iteration mode).  d_Y0 == NULL starts from the
+ * reference's Y = 1000.  Requires 8*ldq bytes of LDS (ldq <= 20480). */
+int pqp_batch_iterate(int B, int N, const float *d_QdT, int ldq, long long qstride, const float *d_theta,
+                      const float *d_Fd, int ldv, const float *d_Y0, float *d_Y, int updates, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PQP_H */

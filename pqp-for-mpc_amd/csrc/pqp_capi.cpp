@@ -1,0 +1,792 @@
+// pqp_capi.cpp -- the C ABI of libpqp (include/pqp.h): a thin host shim that
+// validates arguments, moves caller buffers to/from HBM and launches the
+// gfx950 kernels of pqp_kernels.hip.  No arithmetic of the solver runs on the
+// host: every drop-in function is computed on the GPU and fails loudly (status
+// code, or exit(EXIT_FAILURE) for the void drop-ins) when no gfx950 device or
+// kernel is available -- there is no CPU fallback.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pqp_internal.h"
+#include "pqp_launch.h"
+
+namespace pqp {
+
+static thread_local std::string t_err;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+namespace {
+
+std::mutex g_mu;  // drop-in calls share the library stream and are serialized
+
+inline int round4(int n) { return (n + 3) & ~3; }
+
+// RAII device allocation.
+struct DevBuf {
+    void* p = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int alloc(size_t bytes) {
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+        }
+        if (bytes == 0) bytes = 16;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return set_error(PQP_ERR_ALLOC, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+        }
+        return PQP_OK;
+    }
+    int floats(size_t n) { return alloc(n * sizeof(float)); }
+    float* f() const { return static_cast<float*>(p); }
+};
+
+// Verify that the current device is a gfx950 (the only code object we ship).
+int ensure_device() {
+    static std::mutex mu;
+    static int checked[64] = {0};  // 0 unknown, 1 ok, <0 error code
+    int dev = 0;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return set_error(PQP_ERR_NO_DEVICE, "libpqp: no HIP device visible");
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return set_error(PQP_ERR_NO_DEVICE, "libpqp: cannot query the current device");
+    std::lock_guard<std::mutex> lk(mu);
+    if (checked[dev] == 0) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+            checked[dev] = PQP_ERR_NO_DEVICE;
+        } else if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            checked[dev] = PQP_ERR_NO_DEVICE;
+            return set_error(PQP_ERR_NO_DEVICE, "libpqp is built for gfx950 only; device %d is %s", dev,
+                             prop.gcnArchName);
+        } else {
+            checked[dev] = 1;
+        }
+    }
+    if (checked[dev] < 0) return set_error(checked[dev], "libpqp: device %d is not a usable gfx950", dev);
+    return PQP_OK;
+}
+
+hipStream_t lib_stream() {
+    static hipStream_t streams[64] = {nullptr};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!streams[dev]) (void)hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
+    return streams[dev];
+}
+
+int upload(DevBuf& d, const float* h, size_t n, hipStream_t s) {
+    PQP_TRY(d.floats(n));
+    if (n) PQP_HIP(hipMemcpyAsync(d.p, h, n * sizeof(float), hipMemcpyHostToDevice, s));
+    return PQP_OK;
+}
+int download(float* h, const void* d, size_t n, hipStream_t s) {
+    if (n) PQP_HIP(hipMemcpyAsync(h, d, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    return PQP_OK;
+}
+
+// ---- device compositions of the reference's helper functions -------------
+int dev_matmul(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c, hipStream_t s) {
+    PQP_HIP(launch_matmul_seq(out, A, tA, B, tB, a, b, c, s));
+    return PQP_OK;
+}
+
+// convertToDual (PQP_CPU.c:489-498)
+int dev_convert_to_dual(float* Qd, float* Fd, float* Md, const float* Qinv, const float* Gp, const float* Kp,
+                        const float* Fp, const float* Mp, int N, int M, hipStream_t s) {
+    DevBuf GQ, fq;
+    PQP_TRY(GQ.floats((size_t)N * M));
+    PQP_TRY(fq.floats(M));
+    PQP_TRY(dev_matmul(GQ.f(), Gp, 0, Qinv, 0, N, M, M, s));  // Gp_Qp_inv          :492
+    PQP_TRY(dev_matmul(Qd, GQ.f(), 0, Gp, 1, N, M, N, s));    // computeQd          :442
+    PQP_TRY(dev_matmul(Fd, GQ.f(), 0, Fp, 0, N, M, 1, s));    // computeFd          :458
+    PQP_HIP(launch_axpy(Fd, Kp, 1.0f, N, s));                  //                    :459
+    PQP_TRY(dev_matmul(fq.f(), Fp, 1, Qinv, 0, 1, M, M, s));  // computeMd          :475
+    PQP_TRY(dev_matmul(Md, fq.f(), 0, Fp, 0, 1, M, 1, s));    //                    :476
+    PQP_HIP(launch_axpy(Md, Mp, -1.0f, 1, s));                 // Md[0] -= Mp[0]     :478
+    PQP_HIP(hipStreamSynchronize(s));                          // before scratch is freed
+    return PQP_OK;
+}
+
+// computeUfromY (PQP_CPU.c:352-360)
+int dev_u_from_y(float* U, const float* Y, const float* Fp, const float* Gp, const float* Qinv, int N, int M,
+                 hipStream_t s) {
+    DevBuf t;
+    PQP_TRY(t.floats(M));
+    PQP_TRY(dev_matmul(t.f(), Gp, 1, Y, 0, M, N, 1, s));
+    PQP_HIP(launch_axpy(t.f(), Fp, 1.0f, M, s));
+    PQP_TRY(dev_matmul(U, Qinv, 0, t.f(), 0, M, M, 1, s));
+    PQP_HIP(launch_negate(U, M, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// checkFeas (PQP_CPU.c:632-641) -> host int
+int dev_check_feas(const float* U, const float* Gp, const float* Kp, int N, int M, int* out, hipStream_t s) {
+    DevBuf gu, flag;
+    PQP_TRY(gu.floats(N));
+    PQP_TRY(flag.alloc(sizeof(int)));
+    const int one = 1;
+    PQP_HIP(hipMemcpyAsync(flag.p, &one, sizeof(int), hipMemcpyHostToDevice, s));
+    PQP_TRY(dev_matmul(gu.f(), Gp, 0, U, 0, N, M, 1, s));
+    PQP_HIP(launch_compare(gu.f(), Kp, N, static_cast<int*>(flag.p), s));
+    PQP_HIP(hipMemcpyAsync(out, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// computeCost (PQP_CPU.c:648-666) -> device scalar J
+int dev_cost(float* J, const float* Z, const float* Q, const float* F, const float* Mc, int n, hipStream_t s) {
+    DevBuf row, quad, lin;
+    PQP_TRY(row.floats(n));
+    PQP_TRY(quad.floats(1));
+    PQP_TRY(lin.floats(1));
+    PQP_TRY(dev_matmul(row.f(), Z, 1, Q, 0, 1, n, n, s));
+    PQP_TRY(dev_matmul(quad.f(), row.f(), 0, Z, 0, 1, n, 1, s));
+    PQP_TRY(dev_matmul(lin.f(), F, 1, Z, 0, 1, n, 1, s));
+    PQP_HIP(launch_cost_finish(quad.f(), lin.f(), Mc, J, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// computeFp (PQP_CPU.c:373-382)
+int dev_compute_fp(float* Fp, const float* Fp1, const float* Fp2, const float* Fp3, const float* D, const float* x,
+                   int m, int nd, int ns, hipStream_t s) {
+    DevBuf t;
+    PQP_TRY(t.floats(m));
+    PQP_TRY(dev_matmul(Fp, Fp1, 0, D, 0, m, nd, 1, s));
+    PQP_TRY(dev_matmul(t.f(), Fp2, 0, x, 0, m, ns, 1, s));
+    PQP_HIP(launch_axpy(Fp, t.f(), 1.0f, m, s));
+    PQP_HIP(launch_axpy(Fp, Fp3, -1.0f, m, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// computeMp (PQP_CPU.c:395-428)
+int dev_compute_mp(float* Mp, const float* Mp1, const float* Mp2, const float* Mp3, const float* Mp4,
+                   const float* Mp5, const float* Mp6, const float* D, const float* x, int nd, int ns,
+                   hipStream_t s) {
+    DevBuf row, terms;
+    PQP_TRY(row.floats(ns > nd ? ns : nd));
+    PQP_TRY(terms.floats(5));
+    float* T = terms.f();
+    PQP_TRY(dev_matmul(row.f(), x, 1, Mp1, 0, 1, ns, ns, s));     // x' Mp1
+    PQP_TRY(dev_matmul(T + 0, row.f(), 0, x, 0, 1, ns, 1, s));    //  . x
+    PQP_TRY(dev_matmul(row.f(), D, 1, Mp2, 0, 1, nd, ns, s));     // D' Mp2
+    PQP_TRY(dev_matmul(T + 1, row.f(), 0, x, 0, 1, ns, 1, s));    //  . x
+    PQP_TRY(dev_matmul(T + 2, Mp4, 1, x, 0, 1, ns, 1, s));        // Mp4' x
+    PQP_TRY(dev_matmul(row.f(), D, 1, Mp3, 0, 1, nd, nd, s));     // D' Mp3
+    PQP_TRY(dev_matmul(T + 3, row.f(), 0, D, 0, 1, nd, 1, s));    //  . D
+    PQP_TRY(dev_matmul(T + 4, Mp5, 1, D, 0, 1, nd, 1, s));        // Mp5' D
+    PQP_HIP(launch_mp_finish(T, Mp6, Mp, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// Gauss_Jordan (PQP_CPU.c:251-326)
+int dev_gauss_jordan(float* res, const float* A, int n, hipStream_t s) {
+    DevBuf aug, fac;
+    PQP_TRY(aug.floats((size_t)2 * n * n));
+    PQP_TRY(fac.floats(n));
+    PQP_HIP(launch_gauss_jordan(A, aug.f(), fac.f(), res, n, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// Persistent single-problem solve on device data (see k_solve_single).
+struct SolveOut {
+    long long h = 0;
+    float Jp = NAN, Jd = NAN;
+    int have_costs = 0, last_stop = 0, status = 0;
+};
+
+int dev_solve(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qinv,
+              const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
+              long long num_iter, long long max_updates, float* Y, float* U, bool resume, SolveOut& out,
+              hipStream_t s) {
+    const int ldq = round4(N), ldm = round4(M > 0 ? M : 1);
+    const size_t lds = solve_single_lds_bytes(ldq, ldm);
+    if (lds > 150 * 1024)
+        return set_error(PQP_ERR_ARG, "single-problem solve: N=%d, M=%d needs %zu bytes of LDS (max 150 KiB)", N, M,
+                         lds);
+    DevBuf QdT, theta, state, Udummy;
+    PQP_TRY(QdT.floats((size_t)N * ldq));
+    PQP_TRY(theta.floats(N));
+    PQP_TRY(state.alloc(sizeof(SolveState)));
+    PQP_HIP(launch_pack_colmajor(1, Qd, N, (long long)N * N, QdT.f(), ldq, (long long)N * ldq, s));
+    PQP_HIP(launch_theta(1, QdT.f(), ldq, (long long)N * ldq, N, theta.f(), N, s));
+    if (!U) {
+        PQP_TRY(Udummy.floats(M > 0 ? M : 1));
+        U = Udummy.f();
+    }
+    SolveState st{};
+    st.h = 1;
+    st.resume = resume ? 1 : 0;
+    PQP_HIP(hipMemcpyAsync(state.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    SolveArgs a{};
+    a.QdT = QdT.f();
+    a.Qd = Qd;
+    a.theta = theta.f();
+    a.Fd = Fd;
+    a.Md = Md;
+    a.Qp = Qp;
+    a.Qinv = Qinv;
+    a.Fp = Fp;
+    a.Mp = Mp;
+    a.Gp = Gp;
+    a.Kp = Kp;
+    a.Y = Y;
+    a.U = U;
+    a.N = N;
+    a.M = M;
+    a.ldq = ldq;
+    a.ldm = ldm;
+    a.mode = mode;
+    a.num_iter = num_iter;
+    a.max_updates = max_updates;
+    // bound each launch to ~2^26 multiply-adds of work so no launch runs long
+    const double per_update = (double)N * N * 2.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
+    long long chunk = (long long)((double)(1 << 26) / per_update);
+    a.chunk = chunk < 1 ? 1 : chunk;
+    for (;;) {
+        PQP_HIP(launch_solve_single(a, static_cast<SolveState*>(state.p), s));
+        PQP_HIP(hipMemcpyAsync(&st, state.p, sizeof st, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (st.status != kStatusContinue) break;
+    }
+    out.h = st.h;
+    out.status = st.status;
+    out.have_costs = st.have_costs;
+    out.last_stop = st.last_stop;
+    if (st.have_costs) {
+        out.Jp = st.Jp;
+        out.Jd = st.Jd;
+    }
+    return PQP_OK;
+}
+
+// Uploaded dual problem + primal data for the host-pointer solve paths.
+struct HostProblem {
+    DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;
+    int upload_all(const float* qd, const float* fd, const float* md, const float* qp, const float* qinv,
+                   const float* fp, const float* mp, const float* gp, const float* kp, int N, int M, hipStream_t s) {
+        PQP_TRY(upload(Qd, qd, (size_t)N * N, s));
+        PQP_TRY(upload(Fd, fd, N, s));
+        PQP_TRY(upload(Md, md, 1, s));
+        PQP_TRY(upload(Qp, qp, (size_t)M * M, s));
+        PQP_TRY(upload(Qinv, qinv, (size_t)M * M, s));
+        PQP_TRY(upload(Fp, fp, M, s));
+        PQP_TRY(upload(Mp, mp, 1, s));
+        PQP_TRY(upload(Gp, gp, (size_t)N * M, s));
+        PQP_TRY(upload(Kp, kp, N, s));
+        return PQP_OK;
+    }
+};
+
+[[noreturn]] void die(const char* fn) {
+    std::fprintf(stderr, "libpqp: %s failed: %s\n", fn, t_err.c_str());
+    std::exit(EXIT_FAILURE);
+}
+
+int check_dims(int N, int M) {
+    if (N <= 0 || M <= 0) return set_error(PQP_ERR_ARG, "N and M must be positive (N=%d, M=%d)", N, M);
+    return PQP_OK;
+}
+
+}  // namespace
+}  // namespace pqp
+
+using namespace pqp;
+
+extern "C" {
+
+const char* pqp_last_error(void) { return t_err.c_str(); }
+int pqp_version(void) { return 100; }
+
+// ---------------------------------------------------------------------------
+// 2a. status-returning host API
+// ---------------------------------------------------------------------------
+int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
+                   const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
+                   long long num_iter, long long max_updates, float* Y, float* U, long long* h_out,
+                   float* Jp_out, float* Jd_out) {
+    PQP_TRY(check_dims(N, M));
+    if (!Qd || !Fd || !Md || !Qp || !Qp_inv || !Fp || !Mp || !Gp || !Kp || !Y)
+        return set_error(PQP_ERR_ARG, "pqp_solve_dual: null input");
+    if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
+        return set_error(PQP_ERR_ARG, "pqp_solve_dual: unknown mode %d", mode);
+    std::lock_guard<std::mutex> lk(g_mu);
+    PQP_TRY(ensure_device());
+    hipStream_t s = lib_stream();
+    HostProblem P;
+    PQP_TRY(P.upload_all(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
+    DevBuf dY, dU;
+    PQP_TRY(dY.floats(N));
+    PQP_TRY(dU.floats(M));
+    PQP_HIP(hipMemsetAsync(dU.p, 0, sizeof(float) * M, s));
+    SolveOut o;
+    PQP_TRY(dev_solve(P.Qd.f(), P.Fd.f(), P.Md.f(), P.Qp.f(), P.Qinv.f(), P.Fp.f(), P.Mp.f(), P.Gp.f(), P.Kp.f(), N,
+                      M, mode == PQP_MODE_CONVERGE ? kModeConverge : kModeFixed, num_iter, max_updates, dY.f(),
+                      dU.f(), false, o, s));
+    PQP_TRY(download(Y, dY.p, N, s));
+    if (U && mode == PQP_MODE_CONVERGE) PQP_TRY(download(U, dU.p, M, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    if (h_out) *h_out = o.h;
+    if (Jp_out) *Jp_out = o.Jp;
+    if (Jd_out) *Jd_out = o.Jd;
+    if (o.status == kStatusCapped)
+        return set_error(PQP_ERR_NOT_CONVERGED, "no convergence within %lld updates (h=%lld)", max_updates, o.h);
+    return PQP_OK;
+}
+
+int pqp_update_host(const float* Qd, const float* theta_diag, const float* Fd, const float* Y, float* Y_next,
+                    int N) {
+    if (N <= 0 || !Qd || !theta_diag || !Fd || !Y || !Y_next) return set_error(PQP_ERR_ARG, "pqp_update_host");
+    std::lock_guard<std::mutex> lk(g_mu);
+    PQP_TRY(ensure_device());
+    hipStream_t s = lib_stream();
+    const int ldq = round4(N);
+    DevBuf dQd, dQdT, dth, dFd, dY, dYn;
+    PQP_TRY(upload(dQd, Qd, (size_t)N * N, s));
+    PQP_TRY(upload(dth, theta_diag, N, s));
+    PQP_TRY(upload(dFd, Fd, N, s));
+    PQP_TRY(upload(dY, Y, N, s));
+    PQP_TRY(dYn.floats(N));
+    PQP_TRY(dQdT.floats((size_t)N * ldq));
+    PQP_HIP(launch_pack_colmajor(1, dQd.f(), N, (long long)N * N, dQdT.f(), ldq, (long long)N * ldq, s));
+    PQP_HIP(launch_batch_update(1, dQdT.f(), (long long)N * ldq, ldq, N, dth.f(), dFd.f(), N, dY.f(), dYn.f(), s));
+    PQP_TRY(download(Y_next, dYn.p, N, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+int pqp_read_example(const char* dir, int m, int nd, int ns, float* Qp_inv, float* Fp1, float* Fp2, float* Fp3,
+                     float* Mp1, float* Mp2, float* Mp3, float* Mp4, float* Mp5, float* Mp6, float* Gp, float* Kp,
+                     float* x, float* D) {
+    ExampleData e;
+    PQP_TRY(read_example(dir, m, nd, ns, e));
+    auto put = [](float* dst, const std::vector<float>& v) {
+        if (dst) std::memcpy(dst, v.data(), v.size() * sizeof(float));
+    };
+    put(Qp_inv, e.Qp_inv);
+    put(Fp1, e.Fp1);
+    put(Fp2, e.Fp2);
+    put(Fp3, e.Fp3);
+    put(Mp1, e.Mp1);
+    put(Mp2, e.Mp2);
+    put(Mp3, e.Mp3);
+    put(Mp4, e.Mp4);
+    put(Mp5, e.Mp5);
+    put(Mp6, e.Mp6);
+    put(Gp, e.Gp);
+    put(Kp, e.Kp);
+    put(x, e.x);
+    put(D, e.D);
+    return PQP_OK;
+}
+
+int pqp_run_example(const char* dir, void* out_file) {
+    FILE* out = out_file ? static_cast<FILE*>(out_file) : stdout;
+    ExampleData e;
+    const int m = kRefNInput * kRefPHorizon, nd = kRefNDis * kRefPHorizon, ns = kRefNState;
+    PQP_TRY(read_example(dir, m, nd, ns, e));
+    const int M = m, N = 4 * m;
+    std::lock_guard<std::mutex> lk(g_mu);
+    PQP_TRY(ensure_device());
+    hipStream_t s = lib_stream();
+    DevBuf Qinv, Fp1, Fp2, Fp3, Mp1, Mp2, Mp3, Mp4, Mp5, Mp6, Gp, Kp, x, D;
+    PQP_TRY(upload(Qinv, e.Qp_inv.data(), e.Qp_inv.size(), s));
+    PQP_TRY(upload(Fp1, e.Fp1.data(), e.Fp1.size(), s));
+    PQP_TRY(upload(Fp2, e.Fp2.data(), e.Fp2.size(), s));
+    PQP_TRY(upload(Fp3, e.Fp3.data(), e.Fp3.size(), s));
+    PQP_TRY(upload(Mp1, e.Mp1.data(), e.Mp1.size(), s));
+    PQP_TRY(upload(Mp2, e.Mp2.data(), e.Mp2.size(), s));
+    PQP_TRY(upload(Mp3, e.Mp3.data(), e.Mp3.size(), s));
+    PQP_TRY(upload(Mp4, e.Mp4.data(), e.Mp4.size(), s));
+    PQP_TRY(upload(Mp5, e.Mp5.data(), e.Mp5.size(), s));
+    PQP_TRY(upload(Mp6, e.Mp6.data(), e.Mp6.size(), s));
+    PQP_TRY(upload(Gp, e.Gp.data(), e.Gp.size(), s));
+    PQP_TRY(upload(Kp, e.Kp.data(), e.Kp.size(), s));
+    PQP_TRY(upload(x, e.x.data(), e.x.size(), s));
+    PQP_TRY(upload(D, e.D.data(), e.D.size(), s));
+    DevBuf Qp, Fp, Mp, Qd, Fd, Md, Y, U, Jp, Jd;
+    PQP_TRY(Qp.floats((size_t)M * M));
+    PQP_TRY(Fp.floats(M));
+    PQP_TRY(Mp.floats(1));
+    PQP_TRY(Qd.floats((size_t)N * N));
+    PQP_TRY(Fd.floats(N));
+    PQP_TRY(Md.floats(1));
+    PQP_TRY(Y.floats(N));
+    PQP_TRY(U.floats(M));
+    PQP_TRY(Jp.floats(1));
+    PQP_TRY(Jd.floats(1));
+    PQP_TRY(dev_gauss_jordan(Qp.f(), Qinv.f(), M, s));                                                   // :989
+    PQP_TRY(dev_compute_fp(Fp.f(), Fp1.f(), Fp2.f(), Fp3.f(), D.f(), x.f(), m, nd, ns, s));             // :991
+    PQP_TRY(dev_compute_mp(Mp.f(), Mp1.f(), Mp2.f(), Mp3.f(), Mp4.f(), Mp5.f(), Mp6.f(), D.f(), x.f(), nd, ns,
+                           s));                                                                         // :992
+    PQP_TRY(dev_convert_to_dual(Qd.f(), Fd.f(), Md.f(), Qinv.f(), Gp.f(), Kp.f(), Fp.f(), Mp.f(), N, M, s));  // :994
+    SolveOut o;
+    PQP_TRY(dev_solve(Qd.f(), Fd.f(), Md.f(), Qp.f(), Qinv.f(), Fp.f(), Mp.f(), Gp.f(), Kp.f(), N, M, kModeConverge,
+                      0, 0, Y.f(), U.f(), false, o, s));                                                // :996
+    std::fprintf(out, "Printing number of iterations = %ld\n", (long)o.h);                              // :741
+    PQP_TRY(dev_u_from_y(U.f(), Y.f(), Fp.f(), Gp.f(), Qinv.f(), N, M, s));                              // :999
+    PQP_TRY(dev_cost(Jp.f(), U.f(), Qp.f(), Fp.f(), Mp.f(), M, s));                                      // :1002
+    PQP_TRY(dev_cost(Jd.f(), Y.f(), Qd.f(), Fd.f(), Md.f(), N, s));                                      // :1003
+    std::vector<float> hU(M);
+    float jp = 0, jd = 0;
+    PQP_TRY(download(hU.data(), U.p, M, s));
+    PQP_TRY(download(&jp, Jp.p, 1, s));
+    PQP_TRY(download(&jd, Jd.p, 1, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    std::fprintf(out, "Jp = %f\n", jp);
+    std::fprintf(out, "Jd = %f\n", jd);
+    std::fprintf(out, "Printing U*\n");
+    for (int i = 0; i < M; ++i) std::fprintf(out, "\t%f\n", hU[i]);
+    std::fflush(out);
+    return PQP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// 2b. batched device API
+// ---------------------------------------------------------------------------
+static int check_batch(int B, int N, const void* QdT, int ldq, long long qstride, int ldv) {
+    if (B <= 0 || N <= 0) return set_error(PQP_ERR_ARG, "B and N must be positive (B=%d, N=%d)", B, N);
+    if (!QdT || (reinterpret_cast<uintptr_t>(QdT) & 15))
+        return set_error(PQP_ERR_ARG, "QdT must be a 16-byte aligned device pointer");
+    if (ldq < N || (ldq & 3)) return set_error(PQP_ERR_ARG, "ldq (%d) must be >= N (%d) and a multiple of 4", ldq, N);
+    if (qstride < (long long)N * ldq || (qstride & 3))
+        return set_error(PQP_ERR_ARG, "qstride (%lld) must be >= N*ldq and a multiple of 4", qstride);
+    if (ldv < N) return set_error(PQP_ERR_ARG, "ldv (%d) must be >= N (%d)", ldv, N);
+    return ensure_device();
+}
+
+int pqp_batch_generate(uint32_t seed, long long inst0, int B, int N, int M, float* d_QdT, int ldq,
+                       long long qstride, float* d_Fd, float* d_Md, float* d_theta, int ldv, void* stream) {
+    PQP_TRY(check_batch(B, N, d_QdT, ldq, qstride, ldv));
+    if (M <= 0 || !d_Fd || !d_theta) return set_error(PQP_ERR_ARG, "pqp_batch_generate: bad M or null output");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    PQP_HIP(launch_synth(seed, inst0, B, N, M, d_QdT, ldq, qstride, d_Fd, ldv, d_Md, s));
+    PQP_HIP(launch_theta(B, d_QdT, ldq, qstride, N, d_theta, ldv, s));
+    return PQP_OK;
+}
+
+int pqp_batch_pack(int B, int N, const float* d_Qd, float* d_QdT, int ldq, long long qstride, void* stream) {
+    PQP_TRY(check_batch(B, N, d_QdT, ldq, qstride, N));
+    if (!d_Qd) return set_error(PQP_ERR_ARG, "pqp_batch_pack: null input");
+    PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, d_QdT, ldq, qstride, static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
+int pqp_batch_theta(int B, int N, const float* d_QdT, int ldq, long long qstride, float* d_theta, int ldv,
+                    void* stream) {
+    PQP_TRY(check_batch(B, N, d_QdT, ldq, qstride, ldv));
+    if (!d_theta) return set_error(PQP_ERR_ARG, "pqp_batch_theta: null output");
+    PQP_HIP(launch_theta(B, d_QdT, ldq, qstride, N, d_theta, ldv, static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
+int pqp_batch_update(int B, int N, const float* d_QdT, int ldq, long long qstride, const float* d_theta,
+                     const float* d_Fd, int ldv, const float* d_Y, float* d_Ynext, void* stream) {
+    PQP_TRY(check_batch(B, N, d_QdT, ldq, qstride, ldv));
+    if (!d_theta || !d_Fd || !d_Y || !d_Ynext) return set_error(PQP_ERR_ARG, "pqp_batch_update: null pointer");
+    if (d_Y == d_Ynext) return set_error(PQP_ERR_ARG, "pqp_batch_update: d_Y and d_Ynext must not alias");
+    if ((size_t)ldq * sizeof(float) > 150 * 1024) return set_error(PQP_ERR_ARG, "pqp_batch_update: N too large");
+    PQP_HIP(launch_batch_update(B, d_QdT, qstride, ldq, N, d_theta, d_Fd, ldv, d_Y, d_Ynext,
+                                static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
+int pqp_batch_iterate(int B, int N, const float* d_QdT, int ldq, long long qstride, const float* d_theta,
+                      const float* d_Fd, int ldv, const float* d_Y0, float* d_Y, int updates, void* stream) {
+    PQP_TRY(check_batch(B, N, d_QdT, ldq, qstride, ldv));
+    if (!d_theta || !d_Fd || !d_Y || updates < 0) return set_error(PQP_ERR_ARG, "pqp_batch_iterate: bad argument");
+    if ((size_t)2 * ldq * sizeof(float) > 160 * 1024)
+        return set_error(PQP_ERR_ARG, "pqp_batch_iterate: ldq=%d needs more than 160 KiB of LDS", ldq);
+    PQP_HIP(launch_batch_iterate(B, d_QdT, qstride, ldq, N, d_theta, d_Fd, ldv, d_Y0, d_Y, updates,
+                                 static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// 1. drop-in entry points (reference signatures)
+// ---------------------------------------------------------------------------
+void solveQuadraticDual(float* Y, float* Qd, float* Fd, float* Md, float* U, float* Qp, float* Qp_inv, float* Fp,
+                        float* Mp, float* Gp, float* Kp, int N, int M) {
+    long long h = 0;
+    long long cap = 0;  // the reference has no cap (PQP_CPU.c:718); PQP_MAX_UPDATES adds one
+    if (const char* env = std::getenv("PQP_MAX_UPDATES")) cap = std::atoll(env);
+    int rc = pqp_solve_dual(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, PQP_MODE_CONVERGE, 0, cap, Y, U, &h,
+                            nullptr, nullptr);
+    if (rc != PQP_OK && rc != PQP_ERR_NOT_CONVERGED) die("solveQuadraticDual");
+    std::printf("Printing number of iterations = %ld\n", (long)h);
+}
+
+void updateY2(float* Y_next, float* Y, float* Qdp_theta, float* Qdn_theta, float* Fd, float* Fdp, float* Fdn,
+              int N) {
+    (void)Fd;
+    auto run = [&]() -> int {
+        if (N <= 0) return set_error(PQP_ERR_ARG, "updateY2: N must be positive");
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        const int ldq = round4(N);
+        DevBuf qp, qn, qpT, qnT, fdp, fdn, y, yn;
+        PQP_TRY(upload(qp, Qdp_theta, (size_t)N * N, s));
+        PQP_TRY(upload(qn, Qdn_theta, (size_t)N * N, s));
+        PQP_TRY(upload(fdp, Fdp, N, s));
+        PQP_TRY(upload(fdn, Fdn, N, s));
+        PQP_TRY(upload(y, Y, N, s));
+        PQP_TRY(yn.floats(N));
+        PQP_TRY(qpT.floats((size_t)N * ldq));
+        PQP_TRY(qnT.floats((size_t)N * ldq));
+        PQP_HIP(launch_pack_colmajor(1, qp.f(), N, (long long)N * N, qpT.f(), ldq, (long long)N * ldq, s));
+        PQP_HIP(launch_pack_colmajor(1, qn.f(), N, (long long)N * N, qnT.f(), ldq, (long long)N * ldq, s));
+        PQP_HIP(launch_update_split(qpT.f(), qnT.f(), ldq, N, fdp.f(), fdn.f(), y.f(), yn.f(), s));
+        PQP_TRY(download(Y_next, yn.p, N, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("updateY2");
+}
+
+int terminate(float* Y, float* Qd, float* Fd, float* Md, float* U, float* Qp, float* Qp_inv, float* Fp, float* Mp,
+              float* Gp, float* Kp, int N, int M) {
+    int result = 0;
+    auto run = [&]() -> int {
+        PQP_TRY(check_dims(N, M));
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        HostProblem P;
+        PQP_TRY(P.upload_all(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
+        DevBuf dY, dU;
+        PQP_TRY(upload(dY, Y, N, s));
+        PQP_TRY(dU.floats(M));
+        SolveOut o;
+        PQP_TRY(dev_solve(P.Qd.f(), P.Fd.f(), P.Md.f(), P.Qp.f(), P.Qinv.f(), P.Fp.f(), P.Mp.f(), P.Gp.f(),
+                          P.Kp.f(), N, M, kModeTerminate, 0, 0, dY.f(), dU.f(), true, o, s));
+        PQP_TRY(download(U, dU.p, M, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        result = o.last_stop;
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("terminate");
+    return result;
+}
+
+void convertToDual(float* Qd, float* Fd, float* Md, float* Qp_inv, float* Gp, float* Kp, float* Fp, float* Mp, int N,
+                   int M) {
+    auto run = [&]() -> int {
+        PQP_TRY(check_dims(N, M));
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf qinv, gp, kp, fp, mp, qd, fd, md;
+        PQP_TRY(upload(qinv, Qp_inv, (size_t)M * M, s));
+        PQP_TRY(upload(gp, Gp, (size_t)N * M, s));
+        PQP_TRY(upload(kp, Kp, N, s));
+        PQP_TRY(upload(fp, Fp, M, s));
+        PQP_TRY(upload(mp, Mp, 1, s));
+        PQP_TRY(qd.floats((size_t)N * N));
+        PQP_TRY(fd.floats(N));
+        PQP_TRY(md.floats(1));
+        PQP_TRY(dev_convert_to_dual(qd.f(), fd.f(), md.f(), qinv.f(), gp.f(), kp.f(), fp.f(), mp.f(), N, M, s));
+        PQP_TRY(download(Qd, qd.p, (size_t)N * N, s));
+        PQP_TRY(download(Fd, fd.p, N, s));
+        PQP_TRY(download(Md, md.p, 1, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("convertToDual");
+}
+
+void computeUfromY(float* U, float* Y, float* Fp, float* Gp, float* Qp_inv, int N, int M) {
+    auto run = [&]() -> int {
+        PQP_TRY(check_dims(N, M));
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf u, y, fp, gp, qinv;
+        PQP_TRY(upload(y, Y, N, s));
+        PQP_TRY(upload(fp, Fp, M, s));
+        PQP_TRY(upload(gp, Gp, (size_t)N * M, s));
+        PQP_TRY(upload(qinv, Qp_inv, (size_t)M * M, s));
+        PQP_TRY(u.floats(M));
+        PQP_TRY(dev_u_from_y(u.f(), y.f(), fp.f(), gp.f(), qinv.f(), N, M, s));
+        PQP_TRY(download(U, u.p, M, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("computeUfromY");
+}
+
+float computeCost(float* Z, float* Q, float* F, float* Mc, int N) {
+    float J = 0.0f;
+    auto run = [&]() -> int {
+        if (N <= 0) return set_error(PQP_ERR_ARG, "computeCost: N must be positive");
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf z, q, f, m, j;
+        PQP_TRY(upload(z, Z, N, s));
+        PQP_TRY(upload(q, Q, (size_t)N * N, s));
+        PQP_TRY(upload(f, F, N, s));
+        PQP_TRY(upload(m, Mc, 1, s));
+        PQP_TRY(j.floats(1));
+        PQP_TRY(dev_cost(j.f(), z.f(), q.f(), f.f(), m.f(), N, s));
+        PQP_TRY(download(&J, j.p, 1, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("computeCost");
+    return J;
+}
+
+int checkFeas(float* U, float* Gp, float* Kp, int N, int M) {
+    int flag = 0;
+    auto run = [&]() -> int {
+        PQP_TRY(check_dims(N, M));
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf u, gp, kp;
+        PQP_TRY(upload(u, U, M, s));
+        PQP_TRY(upload(gp, Gp, (size_t)N * M, s));
+        PQP_TRY(upload(kp, Kp, N, s));
+        return dev_check_feas(u.f(), gp.f(), kp.f(), N, M, &flag, s);
+    };
+    if (run() != PQP_OK) die("checkFeas");
+    return flag;
+}
+
+void computeTheta(float* theta, float* Qd, int N) {
+    auto run = [&]() -> int {
+        if (N <= 0) return set_error(PQP_ERR_ARG, "computeTheta: N must be positive");
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf th, qd;
+        PQP_TRY(upload(th, theta, (size_t)N * N, s));
+        PQP_TRY(upload(qd, Qd, (size_t)N * N, s));
+        PQP_HIP(launch_theta_rowmajor(qd.f(), N, th.f(), s));
+        PQP_TRY(download(theta, th.p, (size_t)N * N, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("computeTheta");
+}
+
+void matrixMultiply(float* output, float* mat1, int transpose1, float* mat2, int transpose2, int a, int b, int c) {
+    auto run = [&]() -> int {
+        if (a <= 0 || b < 0 || c <= 0) return set_error(PQP_ERR_ARG, "matrixMultiply: bad sizes");
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf A, B, O;
+        PQP_TRY(upload(A, mat1, (size_t)a * b, s));
+        PQP_TRY(upload(B, mat2, (size_t)b * c, s));
+        PQP_TRY(O.floats((size_t)a * c));
+        PQP_TRY(dev_matmul(O.f(), A.f(), transpose1, B.f(), transpose2, a, b, c, s));
+        PQP_TRY(download(output, O.p, (size_t)a * c, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("matrixMultiply");
+}
+
+void Gauss_Jordan(float* A, float* res, int N) {
+    auto run = [&]() -> int {
+        if (N <= 0) return set_error(PQP_ERR_ARG, "Gauss_Jordan: N must be positive");
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf a, r;
+        PQP_TRY(upload(a, A, (size_t)N * N, s));
+        PQP_TRY(r.floats((size_t)N * N));
+        PQP_TRY(dev_gauss_jordan(r.f(), a.f(), N, s));
+        PQP_TRY(download(res, r.p, (size_t)N * N, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("Gauss_Jordan");
+}
+
+void computeFp(float* Fp, float* Fp1, float* Fp2, float* Fp3, float* D, float* x) {
+    const int m = kRefNInput * kRefPHorizon, nd = kRefNDis * kRefPHorizon, ns = kRefNState;
+    auto run = [&]() -> int {
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf fp, f1, f2, f3, d, xx;
+        PQP_TRY(upload(f1, Fp1, (size_t)m * nd, s));
+        PQP_TRY(upload(f2, Fp2, (size_t)m * ns, s));
+        PQP_TRY(upload(f3, Fp3, m, s));
+        PQP_TRY(upload(d, D, nd, s));
+        PQP_TRY(upload(xx, x, ns, s));
+        PQP_TRY(fp.floats(m));
+        PQP_TRY(dev_compute_fp(fp.f(), f1.f(), f2.f(), f3.f(), d.f(), xx.f(), m, nd, ns, s));
+        PQP_TRY(download(Fp, fp.p, m, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("computeFp");
+}
+
+void computeMp(float* Mp, float* Mp1, float* Mp2, float* Mp3, float* Mp4, float* Mp5, float* Mp6, float* D,
+               float* x) {
+    const int nd = kRefNDis * kRefPHorizon, ns = kRefNState;
+    auto run = [&]() -> int {
+        std::lock_guard<std::mutex> lk(g_mu);
+        PQP_TRY(ensure_device());
+        hipStream_t s = lib_stream();
+        DevBuf mp, m1, m2, m3, m4, m5, m6, d, xx;
+        PQP_TRY(upload(m1, Mp1, (size_t)ns * ns, s));
+        PQP_TRY(upload(m2, Mp2, (size_t)nd * ns, s));
+        PQP_TRY(upload(m3, Mp3, (size_t)nd * nd, s));
+        PQP_TRY(upload(m4, Mp4, ns, s));
+        PQP_TRY(upload(m5, Mp5, nd, s));
+        PQP_TRY(upload(m6, Mp6, 1, s));
+        PQP_TRY(upload(d, D, nd, s));
+        PQP_TRY(upload(xx, x, ns, s));
+        PQP_TRY(mp.floats(1));
+        PQP_TRY(dev_compute_mp(mp.f(), m1.f(), m2.f(), m3.f(), m4.f(), m5.f(), m6.f(), d.f(), xx.f(), nd, ns, s));
+        PQP_TRY(download(Mp, mp.p, 1, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return PQP_OK;
+    };
+    if (run() != PQP_OK) die("computeMp");
+}
+
+void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float* Mp2, float* Mp3, float* Mp4,
+           float* Mp5, float* Mp6, float* Gp, float* Kp, float* x, float* D, float* theta, float* Z) {
+    const int m = kRefNInput * kRefPHorizon, nd = kRefNDis * kRefPHorizon, ns = kRefNState;
+    if (pqp_read_example("./example", m, nd, ns, qp_inv, Fp1, Fp2, Fp3, Mp1, Mp2, Mp3, Mp4, Mp5, Mp6, Gp, Kp, x, D) !=
+            PQP_OK ||
+        read_unused_example("./example", ns, kRefNOutput * kRefPHorizon, nd, Z, theta) != PQP_OK)
+        die("input");
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// pqp_device.h -- device-side arithmetic shared by every PQP kernel (gfx950).
+//
+// Float rules: the whole library is compiled with
+// -ffp-contract=off, so `a * b + c` is a rounded product followed by a rounded
+// add, exactly like PQP_CPU.c built without FMA.  Division uses the default
+// correctly rounded fp32 divide (never __fdividef / fast-math).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace pqp {
+
+// The reference's max(): `a > b ? a : b` on floats (PQP_CPU.c:32-36).  Not
+// fmaxf: max(0,-0.0f) is -0.0f and a NaN second operand propagates.
+__host__ __device__ __forceinline__ float max_ref(float a, float b) { return (a > b) ? a : b; }
+
+// Tolerances erc = eac = eaj = erj (PQP_CPU.c:19-22).
+constexpr double kTol = 1e-6;
+
+// ---------------------------------------------------------------------------
+// Counter-based synthetic generator.  MUST stay identical to
+// oracle/pqp_oracle.c (orc_hash32 / orc_synth_key / orc_synth_bits / orc_u01).
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t synth_key(uint32_t seed, uint32_t inst, uint32_t tag) {
+    uint32_t k = hash32(seed * 0x9E3779B9U + 0x632BE5ABU);
+    k = hash32(k ^ (inst * 0x85EBCA6BU + 0x27D4EB2FU));
+    return hash32(k + tag * 0xC2B2AE35U);
+}
+__host__ __device__ __forceinline__ uint32_t synth_bits(uint32_t key, uint32_t idx) {
+    return hash32(key ^ hash32(idx + 0x165667B1U));
+}
+__host__ __device__ __forceinline__ float u01(uint32_t bits) {
+    return (float)(bits >> 8) * (1.0f / 16777216.0f);
+}
+enum SynthTag : uint32_t { kTagQinv = 1, kTagGp = 2, kTagKp = 3, kTagFp = 4 };
+
+struct SynthKeys {
+    uint32_t q, g, k, f;
+};
+__host__ __device__ __forceinline__ SynthKeys synth_keys(uint32_t seed, uint32_t inst) {
+    return SynthKeys{synth_key(seed, inst, kTagQinv), synth_key(seed, inst, kTagGp),
+                     synth_key(seed, inst, kTagKp), synth_key(seed, inst, kTagFp)};
+}
+// Qp_inv diagonal entry q_j = 0.1 + u
+__host__ __device__ __forceinline__ float synth_qinv(const SynthKeys& K, int j) {
+    return 0.1f + u01(synth_bits(K.q, (uint32_t)j));
+}
+// Gp[i][j] in {-1, 0, +1}
+__host__ __device__ __forceinline__ float synth_gp(const SynthKeys& K, int i, int j, int M) {
+    uint32_t idx = (uint32_t)i * (uint32_t)M + (uint32_t)j;
+    return (float)((int)(synth_bits(K.g, idx) % 3U) - 1);
+}
+__host__ __device__ __forceinline__ float synth_kp(const SynthKeys& K, int i) {
+    return 10.0f * u01(synth_bits(K.k, (uint32_t)i));
+}
+__host__ __device__ __forceinline__ float synth_fp(const SynthKeys& K, int j) {
+    float s = 20.0f * u01(synth_bits(K.f, (uint32_t)j));
+    return s - 10.0f;
+}
+
+}  // namespace pqp

@@ -1,0 +1,735 @@
+// pqp_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the PQP dual update.
+//
+// Hot path: the reference's updateY2
+// (PQP_CPU.c:603-618) is two N x N mat-vecs over the stored split matrices
+//   num = (max(0,-Qd)+Theta) Y + max(0,-Fd)      den = (max(0,Qd)+Theta) Y + max(0,Fd)
+//   Y_next[i] = num[i] / den[i] * Y[i]                                  (updY, :590-596)
+// Here one pass streams Qd ONCE (4 N^2 bytes instead of 8 N^2), derives both
+// split entries in registers, and applies the update in the epilogue.
+//
+// Bit-exactness with PQP_CPU.c: every row keeps the reference's sequential
+// k = 0..N-1 fp32 accumulation (one lane owns a row, no reduction tree), each
+// product is rounded before it is added (-ffp-contract=off), and the
+// +0.0/Theta additions of the stored matrices are reproduced literally inside
+// the diagonal window.  Off the diagonal the "lean" form is used:
+//   den += (q < 0) ? 0*y : q*y ;   num += (q > 0) ? 0*y : -(q*y)
+// which is bit-identical to (max(0,+-q) + 0.0f) * y for every q (incl. +-0,
+// NaN) and every y (incl. inf/NaN): see DESIGN.md "Lean form".
+//
+// Layout: Qd is stored column-major per problem (QdT, element (i,k) at
+// k*ldq + i) so that at a fixed k a wave's 64 lanes x 4 rows read 1 KiB of
+// contiguous HBM with one global_load_dwordx4 each (fully coalesced), while
+// y[k] is a wave-uniform LDS broadcast.
+#include "pqp_device.h"
+#include "pqp_launch.h"
+
+namespace pqp {
+
+// ---------------------------------------------------------------------------
+// Row-update building blocks
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+struct Acc4 {
+    float p[4];  // den accumulators (Qd+ side)
+    float n[4];  // num accumulators (Qd- side)
+};
+
+// lean step for one k and this lane's 4 rows (off-diagonal entries only)
+__device__ __forceinline__ void lean4(Acc4& a, float4 q, float y) {
+    const float z = 0.0f * y;  // (+0)*y: +0 for finite y >= 0, NaN for inf/NaN y
+    float p;
+    p = q.x * y; a.p[0] += (q.x < 0.0f) ? z : p; a.n[0] += (q.x > 0.0f) ? z : -p;
+    p = q.y * y; a.p[1] += (q.y < 0.0f) ? z : p; a.n[1] += (q.y > 0.0f) ? z : -p;
+    p = q.z * y; a.p[2] += (q.z < 0.0f) ? z : p; a.n[2] += (q.z > 0.0f) ? z : -p;
+    p = q.w * y; a.p[3] += (q.w < 0.0f) ? z : p; a.n[3] += (q.w > 0.0f) ? z : -p;
+}
+
+// literal step: (max(0,+-q) + (k==i ? theta_i : +0)) * y, PQP_CPU.c:524-537 + :608-609
+__device__ __forceinline__ void literal1(float& ap, float& an, float q, float y, float t) {
+    const float qp = max_ref(0.0f, q) + t;
+    const float qn = max_ref(0.0f, -q) + t;
+    ap += qp * y;
+    an += qn * y;
+}
+__device__ __forceinline__ void literal4(Acc4& a, float4 q, float y, int k, int row, const float th[4]) {
+    literal1(a.p[0], a.n[0], q.x, y, (k == row + 0) ? th[0] : 0.0f);
+    literal1(a.p[1], a.n[1], q.y, y, (k == row + 1) ? th[1] : 0.0f);
+    literal1(a.p[2], a.n[2], q.z, y, (k == row + 2) ? th[2] : 0.0f);
+    literal1(a.p[3], a.n[3], q.w, y, (k == row + 3) ? th[3] : 0.0f);
+}
+
+// Stream k in [ka, kb) with the lean form.  ka % 4 == 0.  `col` points at
+// QdT + row (this lane's 4 rows), y is the iterate (LDS).
+__device__ __forceinline__ void lean_segment(Acc4& a, const float* __restrict__ col, int ldq, int ka, int kb,
+                                             const float* __restrict__ y) {
+    int k = ka;
+    const float* src = col + (size_t)k * ldq;
+    for (; k + 8 <= kb; k += 8) {
+        float4 q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = ld4(src + (size_t)j * ldq);
+        src += (size_t)8 * ldq;
+        const float4 y0 = *reinterpret_cast<const float4*>(y + k);
+        const float4 y1 = *reinterpret_cast<const float4*>(y + k + 4);
+        lean4(a, q[0], y0.x);
+        lean4(a, q[1], y0.y);
+        lean4(a, q[2], y0.z);
+        lean4(a, q[3], y0.w);
+        lean4(a, q[4], y1.x);
+        lean4(a, q[5], y1.y);
+        lean4(a, q[6], y1.z);
+        lean4(a, q[7], y1.w);
+    }
+    for (; k < kb; ++k) {
+        lean4(a, ld4(src), y[k]);
+        src += ldq;
+    }
+}
+
+__device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict__ col, int ldq, int ka, int kb,
+                                                const float* __restrict__ y, int row, const float th[4]) {
+    int k = ka;
+    const float* src = col + (size_t)k * ldq;
+    for (; k + 4 <= kb; k += 4) {
+        float4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = ld4(src + (size_t)j * ldq);
+        src += (size_t)4 * ldq;
+        const float4 y0 = *reinterpret_cast<const float4*>(y + k);
+        literal4(a, q[0], y0.x, k + 0, row, th);
+        literal4(a, q[1], y0.y, k + 1, row, th);
+        literal4(a, q[2], y0.z, k + 2, row, th);
+        literal4(a, q[3], y0.w, k + 3, row, th);
+    }
+    for (; k < kb; ++k) {
+        literal4(a, ld4(src), y[k], k, row, th);
+        src += ldq;
+    }
+}
+
+// One lane: num/den for rows [row,row+4) of one problem, then
+// out[i] = num/den * y[i] for the rows < N.  w0 = first row of this lane's
+// wave (wave-uniform): the diagonal of the wave's 256 rows lies in
+// k in [w0, w0+256) and only that window needs the literal form.
+template <typename OutPtr>
+__device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ldq, int N, int row, int w0,
+                                             const float* __restrict__ th_g, const float* __restrict__ fd_g,
+                                             const float* __restrict__ y, OutPtr out) {
+    Acc4 a;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.p[r] = a.n[r] = 0.0f;
+    float th[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) th[r] = (row + r < N) ? th_g[row + r] : 0.0f;
+    const float* col = Q + row;
+    const int wa = w0 < N ? w0 : N;
+    const int wb = (w0 + 256) < N ? (w0 + 256) : N;
+    lean_segment(a, col, ldq, 0, wa, y);
+    literal_segment(a, col, ldq, wa, wb, y, row, th);
+    lean_segment(a, col, ldq, wb, N, y);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = row + r;
+        if (i < N) {
+            const float f = fd_g[i];
+            const float num = a.n[r] + 1.0f * max_ref(0.0f, -f);  // matrixAdd(num, Fdn, 1) :611
+            const float den = a.p[r] + 1.0f * max_ref(0.0f, f);   // matrixAdd(den, Fdp, 1) :612
+            out[i] = num / den * y[i];                            // updY :594
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_batch_iterate: `updates` fixed-mode iterations of every problem in ONE
+// launch.  One workgroup owns one problem; its iterate ping-pongs between two
+// LDS buffers, so the only HBM traffic per iteration is Qd (streamed once).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ QdT, long long qstride, int ldq,
+                                                      int N, const float* __restrict__ theta,
+                                                      const float* __restrict__ Fd, int ldv,
+                                                      const float* __restrict__ Y0, float* __restrict__ Y,
+                                                      int updates) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* ya = lds;
+    float* yb = lds + ldq;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float* Q = QdT + (size_t)b * (size_t)qstride;
+    const float* th = theta + (size_t)b * ldv;
+    const float* fd = Fd + (size_t)b * ldv;
+    for (int i = tid; i < ldq; i += NT) {
+        ya[i] = (i < N) ? (Y0 ? Y0[(size_t)b * ldv + i] : 1000.0f) : 0.0f;  // initMat(Y,1000) :710
+        yb[i] = 0.0f;
+    }
+    __syncthreads();
+    const int wave = tid >> 6;
+    for (int u = 0; u < updates; ++u) {
+        float* cur = (u & 1) ? yb : ya;
+        float* nxt = (u & 1) ? ya : yb;
+        for (int r0 = 0; r0 < N; r0 += 4 * NT) {
+            const int row = r0 + 4 * tid;
+            const int w0 = r0 + 256 * wave;
+            if (row < N) update_rows4(Q, ldq, N, row, w0, th, fd, cur, nxt);
+        }
+        __syncthreads();
+    }
+    const float* fin = (updates & 1) ? yb : ya;
+    for (int i = tid; i < N; i += NT) Y[(size_t)b * ldv + i] = fin[i];
+}
+
+// ---------------------------------------------------------------------------
+// k_batch_update: one iteration; grid = (row blocks, problems).  The iterate
+// is staged into LDS once per workgroup; Y_next goes straight to HBM.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(NT) k_batch_update(const float* __restrict__ QdT, long long qstride, int ldq,
+                                                     int N, const float* __restrict__ theta,
+                                                     const float* __restrict__ Fd, int ldv,
+                                                     const float* __restrict__ Yin, float* __restrict__ Yout) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.y;
+    const int tid = threadIdx.x;
+    const float* yg = Yin + (size_t)b * ldv;
+    for (int i = tid; i < ldq; i += NT) lds[i] = (i < N) ? yg[i] : 0.0f;
+    __syncthreads();
+    const int r0 = blockIdx.x * 4 * NT;
+    const int row = r0 + 4 * tid;
+    const int w0 = r0 + 256 * (tid >> 6);
+    if (row < N)
+        update_rows4(QdT + (size_t)b * (size_t)qstride, ldq, N, row, w0, theta + (size_t)b * ldv,
+                     Fd + (size_t)b * ldv, lds, Yout + (size_t)b * ldv);
+}
+
+// ---------------------------------------------------------------------------
+// k_update_split: the reference's own updateY2 interface -- two STORED split
+// matrices (column-major here), Fdp/Fdn given.  PQP_CPU.c:603-618.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_update_split(const float* __restrict__ QpT, const float* __restrict__ QnT,
+                                                      int ldq, int N, const float* __restrict__ Fdp,
+                                                      const float* __restrict__ Fdn, const float* __restrict__ Y,
+                                                      float* __restrict__ Ynext) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    float num = 0.0f, den = 0.0f;
+    for (int k = 0; k < N; ++k) num += QnT[(size_t)k * ldq + i] * Y[k];
+    for (int k = 0; k < N; ++k) den += QpT[(size_t)k * ldq + i] * Y[k];
+    num = num + 1.0f * Fdn[i];
+    den = den + 1.0f * Fdp[i];
+    Ynext[i] = num / den * Y[i];
+}
+
+// ---------------------------------------------------------------------------
+// Setup kernels
+// ---------------------------------------------------------------------------
+// Row-major N x N (contiguous per problem) -> column-major QdT with padding.
+__global__ void __launch_bounds__(256) k_pack_colmajor(const float* __restrict__ Qd, int N, long long in_stride,
+                                                       float* __restrict__ QdT, int ldq, long long qstride) {
+    __shared__ float tile[32][33];
+    const int b = blockIdx.z;
+    const int k0 = blockIdx.x * 32, i0 = blockIdx.y * 32;  // output column k, rows i
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    const float* src = Qd + (size_t)b * in_stride;
+    float* dst = QdT + (size_t)b * qstride;
+    for (int r = ty; r < 32; r += 8) {
+        const int i = i0 + r, k = k0 + tx;
+        tile[r][tx] = (i < N && k < N) ? src[(size_t)i * N + k] : 0.0f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int k = k0 + r, i = i0 + tx;
+        if (k < N && i < ldq) dst[(size_t)k * ldq + i] = tile[tx][r];
+    }
+}
+
+// theta_i = max( sum_k max(0,-Qd[i][k]) * 1.0f , 5 )   computeTheta + diagonalAdd
+// (PQP_CPU.c:503-519, 235-242), sequential k; one lane per row, coalesced.
+__global__ void __launch_bounds__(256) k_theta(const float* __restrict__ QdT, int ldq, long long qstride, int N,
+                                               float* __restrict__ theta, int ldv) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const float* col = QdT + (size_t)b * (size_t)qstride + i;
+    float s = 0.0f;
+    for (int k = 0; k < N; ++k) s += max_ref(0.0f, -col[(size_t)k * ldq]) * 1.0f;
+    theta[(size_t)b * ldv + i] = max_ref(s, 5.0f);
+}
+
+// Synthetic dual: Qd(i,j) = sum_k (Gp(i,k) q_k) Gp(j,k), k sequential.  The
+// convertToDual products Gp.Qp_inv are exact for a diagonal Qp_inv (all other
+// terms are +-0), so (Gp Qp_inv)(i,k) = Gp(i,k)*q_k bit for bit.  64x64 output
+// tile per 256-thread workgroup, 4x4 per thread, Gp regenerated from the
+// counter hash into LDS per 32-deep k chunk.
+constexpr int SYN_T = 64, SYN_K = 32;
+__global__ void __launch_bounds__(256) k_synth_qd(uint32_t seed, long long inst0, int N, int M,
+                                                  float* __restrict__ QdT, int ldq, long long qstride) {
+    __shared__ float gq[SYN_K][SYN_T + 4];  // (Gp Qinv)(i0+ii, k0+kk) stored [kk][ii]
+    __shared__ float gj[SYN_K][SYN_T + 4];  // Gp(j0+jj, k0+kk) stored [kk][jj]
+    const int b = blockIdx.z;
+    const SynthKeys K = synth_keys(seed, (uint32_t)(inst0 + b));
+    const int i0 = blockIdx.x * SYN_T, j0 = blockIdx.y * SYN_T;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    float acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = 0.0f;
+    for (int k0 = 0; k0 < M; k0 += SYN_K) {
+        // fill: 64 x 32 each; thread covers (kk = tid & 31, rows (tid >> 5) + 8*s)
+        {
+            const int kk = tid & 31, k = k0 + kk;
+            const float q = (k < M) ? synth_qinv(K, k) : 0.0f;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int rr = (tid >> 5) + 8 * s;
+                const int i = i0 + rr, j = j0 + rr;
+                gq[kk][rr] = (k < M && i < N) ? synth_gp(K, i, k, M) * q : 0.0f;
+                gj[kk][rr] = (k < M && j < N) ? synth_gp(K, j, k, M) : 0.0f;
+            }
+        }
+        __syncthreads();
+        const int kend = (M - k0) < SYN_K ? (M - k0) : SYN_K;
+        for (int kk = 0; kk < kend; ++kk) {
+            float a[4], g[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = gq[kk][tx + 16 * r];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) g[c] = gj[kk][ty + 16 * c];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] += a[r] * g[c];
+        }
+        __syncthreads();
+    }
+    float* dst = QdT + (size_t)b * (size_t)qstride;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int j = j0 + ty + 16 * c;
+        if (j >= N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + tx + 16 * r;
+            if (i < ldq) dst[(size_t)j * ldq + i] = (i < N) ? acc[r][c] : 0.0f;  // Qd(i,j) at col j
+        }
+    }
+}
+
+// Synthetic Fd(i) = sum_k (Gp(i,k) q_k) Fp_k + Kp_i  and  Md = sum_j (Fp_j q_j) Fp_j - Mp
+// (computeFd / computeMd, PQP_CPU.c:456-479).
+__global__ void __launch_bounds__(256) k_synth_fd(uint32_t seed, long long inst0, int N, int M,
+                                                  float* __restrict__ Fd, int ldv, float* __restrict__ Md) {
+    const int b = blockIdx.y;
+    const SynthKeys K = synth_keys(seed, (uint32_t)(inst0 + b));
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < N) {
+        float s = 0.0f;
+        for (int k = 0; k < M; ++k) s += (synth_gp(K, i, k, M) * synth_qinv(K, k)) * synth_fp(K, k);
+        Fd[(size_t)b * ldv + i] = s + 1.0f * synth_kp(K, i);
+    }
+    for (int i2 = N + i; i2 < ldv; i2 += gridDim.x * 256) Fd[(size_t)b * ldv + i2] = 0.0f;
+    if (Md && blockIdx.x == 0 && threadIdx.x == 0) {
+        float s = 0.0f;
+        for (int j = 0; j < M; ++j) {
+            const float f = synth_fp(K, j);
+            s += (f * synth_qinv(K, j)) * f;
+        }
+        Md[b] = s - 1.0f;  // Md[0] -= Mp[0], Mp = 1
+    }
+}
+
+// Zero the padding rows [N, ldq) of every column k < N (used when the
+// generator's tiles do not cover them).
+__global__ void k_zero_pad(float* __restrict__ QdT, int N, int ldq, long long qstride) {
+    const int b = blockIdx.y;
+    const int k = blockIdx.x;
+    float* col = QdT + (size_t)b * qstride + (size_t)k * ldq;
+    for (int i = N + threadIdx.x; i < ldq; i += blockDim.x) col[i] = 0.0f;
+}
+
+// ---------------------------------------------------------------------------
+// Generic sequential-k product: out[a x c] = op(A)[a x b] op(B)[b x c]
+// (matrixMultiply, PQP_CPU.c:84-147).  One thread per output element; used
+// for setup and for the drop-in helpers, not on the iteration path.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_matmul_seq(float* __restrict__ out, const float* __restrict__ A, int tA,
+                                                    const float* __restrict__ B, int tB, int a, int bdim, int c) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long long)a * c) return;
+    const int i = (int)(e / c), j = (int)(e % c);
+    float s = 0.0f;
+    for (int k = 0; k < bdim; ++k) {
+        const float x = tA ? A[(size_t)k * a + i] : A[(size_t)i * bdim + k];
+        const float y = tB ? B[(size_t)j * bdim + k] : B[(size_t)k * c + j];
+        s += x * y;
+    }
+    out[e] = s;
+}
+
+// A[i] += sign * B[i]   (matrixAdd, PQP_CPU.c:157-163)
+__global__ void k_axpy(float* __restrict__ A, const float* __restrict__ B, float sign, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) A[i] += sign * B[i];
+}
+// A[i] = -A[i]   (negateMatrix, PQP_CPU.c:171-177)
+__global__ void k_negate(float* __restrict__ A, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) A[i] = -A[i];
+}
+// flag = all(GpU <= Kp + max(erc*Kp, eac))   (compare, PQP_CPU.c:334-343); flag preset to 1
+__global__ void k_compare(const float* __restrict__ gu, const float* __restrict__ Kp, int n, int* flag) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const float kp = Kp[i];
+        if (gu[i] > kp + max_ref((float)(kTol * kp), (float)kTol)) atomicAnd(flag, 0);
+    }
+}
+// theta matrix diagonal from a row-major Qd (computeTheta, :503-519): rows in parallel
+__global__ void k_theta_rowmajor(const float* __restrict__ Qd, int N, float* __restrict__ theta_mat) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    float s = 0.0f;
+    for (int k = 0; k < N; ++k) s += max_ref(0.0f, -Qd[(size_t)i * N + k]) * 1.0f;
+    theta_mat[(size_t)i * N + i] = max_ref(s, 5.0f);
+}
+// computeCost's scalar tail (PQP_CPU.c:655-661): J = 0; J += 0.5*q; J += f; J += M/2
+__global__ void k_cost_finish(const float* __restrict__ quad, const float* __restrict__ lin,
+                              const float* __restrict__ Mc, float* __restrict__ J) {
+    float j = 0.0f;
+    j = (float)((double)j + 0.5 * (double)quad[0]);
+    j += lin[0];
+    j += Mc[0] / 2;
+    J[0] = j;
+}
+// computeMp's accumulation (PQP_CPU.c:397-425): terms t[0..4] then Mp6, each halved
+__global__ void k_mp_finish(const float* __restrict__ t, const float* __restrict__ Mp6, float* __restrict__ Mp) {
+    float m = 0.0f;
+    for (int s = 0; s < 5; ++s) m += t[s] / 2;
+    m += Mp6[0] / 2;
+    Mp[0] = m;
+}
+
+// Gauss_Jordan (PQP_CPU.c:251-326) in one workgroup.  aug is n x 2n scratch
+// (global).  Row updates of one pivot are independent (row j reads only rows
+// i and j), so computing every factor first and then updating all rows in
+// parallel is the reference's arithmetic exactly.
+__global__ void __launch_bounds__(256) k_gauss_jordan(const float* __restrict__ A, float* __restrict__ aug,
+                                                      float* __restrict__ fac, float* __restrict__ res, int n) {
+    const int tid = threadIdx.x, w = 2 * n;
+    for (int e = tid; e < n * w; e += 256) {
+        const int r = e / w, c = e % w;
+        aug[e] = (c < n) ? A[(size_t)r * n + c] : ((c == n + r) ? 1.0f : 0.0f);
+    }
+    __syncthreads();
+    __shared__ int do_swap;
+    for (int r = n - 1; r > 0; --r) {  // one bubble pass on column 0 (:280-289)
+        if (tid == 0) do_swap = aug[(size_t)(r - 1) * w] < aug[(size_t)r * w];
+        __syncthreads();
+        if (do_swap)
+            for (int c = tid; c < w; c += 256) {
+                const float t = aug[(size_t)r * w + c];
+                aug[(size_t)r * w + c] = aug[(size_t)(r - 1) * w + c];
+                aug[(size_t)(r - 1) * w + c] = t;
+            }
+        __syncthreads();
+    }
+    for (int p = 0; p < n; ++p) {  // :291-305
+        for (int r = tid; r < n; r += 256) fac[r] = aug[(size_t)r * w + p] / aug[(size_t)p * w + p];
+        __syncthreads();
+        for (int e = tid; e < n * w; e += 256) {
+            const int r = e / w, c = e % w;
+            if (r != p) aug[e] -= aug[(size_t)p * w + c] * fac[r];
+        }
+        __syncthreads();
+    }
+    for (int r = tid; r < n; r += 256) fac[r] = aug[(size_t)r * w + r];  // :307-314
+    __syncthreads();
+    for (int e = tid; e < n * w; e += 256) {
+        const int r = e / w;
+        aug[e] = aug[e] / fac[r];
+    }
+    __syncthreads();
+    for (int e = tid; e < n * n; e += 256) {
+        const int r = e / n, c = e % n;
+        res[e] = aug[(size_t)r * w + n + c];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_solve_single: the whole solveQuadraticDual (PQP_CPU.c:694-750) in ONE
+// persistent workgroup: terminate() before every update, bit-exact, no host
+// round trip per iteration.  Resumable in chunks (state in SolveState) so no
+// single launch runs unbounded.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float seq_dot(const float* x, const float* y, int n) {
+    float s = 0.0f;
+    for (int k = 0; k < n; ++k) s += x[k] * y[k];
+    return s;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __restrict__ st) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int N = A.N, M = A.M, ldq = A.ldq;
+    float* ya = lds;              // ldq
+    float* yb = ya + ldq;         // ldq
+    float* tq = yb + ldq;         // N   (Y'Qd row, Jd)
+    float* tM = tq + ldq;         // M   (Gp'Y + Fp)
+    float* Us = tM + A.ldm;       // M   (U)
+    float* tu = Us + A.ldm;       // M   (U'Qp row, Jp)
+    __shared__ float s_J[2];
+    const int tid = threadIdx.x;
+
+    long long h = st->h;  // printed h of the current iterate
+    for (int i = tid; i < ldq; i += NT) {
+        ya[i] = (i < N) ? (st->resume ? A.Y[i] : 1000.0f) : 0.0f;
+        yb[i] = 0.0f;
+    }
+    __syncthreads();
+    float* cur = ya;
+    float* nxt = yb;
+    int status = kStatusContinue;
+    long long done_here = 0;
+    for (;;) {
+        if (A.mode != kModeFixed) {
+            // ---- terminate(Y)  PQP_CPU.c:673-687 ----
+            // computeUfromY :352-360
+            for (int j = tid; j < M; j += NT) {
+                float s = 0.0f;
+                for (int k = 0; k < N; ++k) s += A.Gp[(size_t)k * M + j] * cur[k];
+                tM[j] = s + 1.0f * A.Fp[j];
+            }
+            __syncthreads();
+            for (int i = tid; i < M; i += NT) {
+                float s = 0.0f;
+                for (int j = 0; j < M; ++j) s += A.Qinv[(size_t)i * M + j] * tM[j];
+                Us[i] = -s;
+            }
+            __syncthreads();
+            // checkFeas :632-641
+            int bad = 0;
+            for (int i = tid; i < N; i += NT) {
+                float s = 0.0f;
+                for (int j = 0; j < M; ++j) s += A.Gp[(size_t)i * M + j] * Us[j];
+                const float kp = A.Kp[i];
+                if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+            }
+            const int infeasible = __syncthreads_or(bad);
+            int stop = 0;
+            if (!infeasible) {
+                // computeCost(Y, Qd, Fd, Md) and computeCost(U, Qp, Fp, Mp) :648-666
+                for (int j = tid; j < N; j += NT) {
+                    float s = 0.0f;
+                    for (int k = 0; k < N; ++k) s += cur[k] * A.Qd[(size_t)k * N + j];
+                    tq[j] = s;
+                }
+                for (int j = tid; j < M; j += NT) {
+                    float s = 0.0f;
+                    for (int k = 0; k < M; ++k) s += Us[k] * A.Qp[(size_t)k * M + j];
+                    tu[j] = s;
+                }
+                __syncthreads();
+                const int jt = (NT >= 128) ? 64 : 1;  // second scalar chain on another wave
+                if (tid == 0 || tid == jt) {
+                    const bool dual = (tid == 0);
+                    const float* row = dual ? tq : tu;
+                    const float* z = dual ? cur : Us;
+                    const float* F = dual ? A.Fd : A.Fp;
+                    const int n = dual ? N : M;
+                    const float quad = seq_dot(row, z, n);
+                    float lin = 0.0f;
+                    for (int k = 0; k < n; ++k) lin += F[k] * z[k];
+                    float J = 0.0f;
+                    J = (float)((double)J + 0.5 * (double)quad);
+                    J += lin;
+                    J += (dual ? A.Md[0] : A.Mp[0]) / 2;
+                    s_J[dual ? 1 : 0] = J;
+                }
+                __syncthreads();
+                const float Jp = s_J[0], Jd = s_J[1];
+                stop = 1;
+                if (Jp > -Jd) stop = 0;
+                if ((double)(Jp + Jd) > kTol) stop = 0;
+                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                if (tid == 0) {
+                    st->Jp = Jp;
+                    st->Jd = Jd;
+                    st->have_costs = 1;
+                }
+            }
+            if (A.mode == kModeTerminate) {
+                if (tid == 0) st->last_stop = stop;
+                status = kStatusDone;
+                break;
+            }
+            if (stop) {
+                status = kStatusDone;
+                break;
+            }
+            if (A.max_updates > 0 && h - 1 >= A.max_updates) {
+                status = kStatusCapped;
+                break;
+            }
+        } else {
+            if (h >= A.num_iter) {  // while(h < NUM_ITER)
+                status = kStatusDone;
+                break;
+            }
+        }
+        if (done_here >= A.chunk) {
+            status = kStatusContinue;
+            break;
+        }
+        // ---- updateY2  PQP_CPU.c:603-618 (one lane per row, literal form) ----
+        for (int i = tid; i < N; i += NT) {
+            float ap = 0.0f, an = 0.0f;
+            const float thi = A.theta[i];
+            const float* col = A.QdT + i;
+            for (int k = 0; k < N; ++k) {
+                const float q = col[(size_t)k * ldq];
+                const float yk = cur[k];
+                if (k == i) {
+                    literal1(ap, an, q, yk, thi);
+                } else {
+                    const float z = 0.0f * yk;
+                    const float p = q * yk;
+                    ap += (q < 0.0f) ? z : p;
+                    an += (q > 0.0f) ? z : -p;
+                }
+            }
+            const float f = A.Fd[i];
+            const float num = an + 1.0f * max_ref(0.0f, -f);
+            const float den = ap + 1.0f * max_ref(0.0f, f);
+            nxt[i] = num / den * cur[i];
+        }
+        __syncthreads();
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+        ++h;
+        ++done_here;
+    }
+    for (int i = tid; i < N; i += NT) A.Y[i] = cur[i];
+    if (A.mode != kModeFixed)
+        for (int i = tid; i < M; i += NT) A.U[i] = Us[i];
+    if (tid == 0) {
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (declared in pqp_launch.h)
+// ---------------------------------------------------------------------------
+static inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
+                                  const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
+    const size_t lds = (size_t)2 * ldq * sizeof(float);
+    if (N <= 256)
+        hipLaunchKernelGGL(k_batch_iterate<64>, dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv, Y0,
+                           Y, updates);
+    else
+        hipLaunchKernelGGL(k_batch_iterate<256>, dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv,
+                           Y0, Y, updates);
+    return hipGetLastError();
+}
+
+hipError_t launch_batch_update(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
+                               const float* Fd, int ldv, const float* Yin, float* Yout, hipStream_t s) {
+    const size_t lds = (size_t)ldq * sizeof(float);
+    if (N <= 256) {
+        dim3 grid(cdiv(N, 4 * 64), B);
+        hipLaunchKernelGGL(k_batch_update<64>, grid, dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv, Yin,
+                           Yout);
+    } else {
+        dim3 grid(cdiv(N, 4 * 256), B);
+        hipLaunchKernelGGL(k_batch_update<256>, grid, dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv, Yin,
+                           Yout);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_update_split(const float* QpT, const float* QnT, int ldq, int N, const float* Fdp,
+                               const float* Fdn, const float* Y, float* Ynext, hipStream_t s) {
+    hipLaunchKernelGGL(k_update_split, dim3(cdiv(N, 256)), dim3(256), 0, s, QpT, QnT, ldq, N, Fdp, Fdn, Y, Ynext);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_colmajor(int B, const float* Qd, int N, long long in_stride, float* QdT, int ldq,
+                                long long qstride, hipStream_t s) {
+    dim3 grid(cdiv(N, 32), cdiv(ldq, 32), B);
+    hipLaunchKernelGGL(k_pack_colmajor, grid, dim3(256), 0, s, Qd, N, in_stride, QdT, ldq, qstride);
+    return hipGetLastError();
+}
+
+hipError_t launch_theta(int B, const float* QdT, int ldq, long long qstride, int N, float* theta, int ldv,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_theta, dim3(cdiv(N, 256), B), dim3(256), 0, s, QdT, ldq, qstride, N, theta, ldv);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, float* QdT, int ldq, long long qstride,
+                        float* Fd, int ldv, float* Md, hipStream_t s) {
+    // B may exceed the 65535 grid-z limit: chunk it
+    for (int b0 = 0; b0 < B; b0 += 65535) {
+        const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        dim3 grid(cdiv(ldq, SYN_T), cdiv(N, SYN_T), nb);
+        hipLaunchKernelGGL(k_synth_qd, grid, dim3(256), 0, s, seed, inst0 + b0, N, M, QdT + (size_t)b0 * qstride,
+                           ldq, qstride);
+        hipLaunchKernelGGL(k_synth_fd, dim3(cdiv(N, 256), nb), dim3(256), 0, s, seed, inst0 + b0, N, M,
+                           Fd + (size_t)b0 * ldv, ldv, Md ? Md + b0 : nullptr);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c,
+                             hipStream_t s) {
+    const long long n = (long long)a * c;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_matmul_seq, dim3(cdiv(n, 256)), dim3(256), 0, s, out, A, tA, B, tB, a, b, c);
+    return hipGetLastError();
+}
+hipError_t launch_axpy(float* A, const float* B, float sign, int n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_axpy, dim3(cdiv(n, 256)), dim3(256), 0, s, A, B, sign, n);
+    return hipGetLastError();
+}
+hipError_t launch_negate(float* A, int n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_negate, dim3(cdiv(n, 256)), dim3(256), 0, s, A, n);
+    return hipGetLastError();
+}
+hipError_t launch_compare(const float* gu, const float* Kp, int n, int* flag, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_compare, dim3(cdiv(n, 256)), dim3(256), 0, s, gu, Kp, n, flag);
+    return hipGetLastError();
+}
+hipError_t launch_theta_rowmajor(const float* Qd, int N, float* theta_mat, hipStream_t s) {
+    if (N > 0) hipLaunchKernelGGL(k_theta_rowmajor, dim3(cdiv(N, 256)), dim3(256), 0, s, Qd, N, theta_mat);
+    return hipGetLastError();
+}
+hipError_t launch_cost_finish(const float* quad, const float* lin, const float* Mc, float* J, hipStream_t s) {
+    hipLaunchKernelGGL(k_cost_finish, dim3(1), dim3(1), 0, s, quad, lin, Mc, J);
+    return hipGetLastError();
+}
+hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStream_t s) {
+    hipLaunchKernelGGL(k_mp_finish, dim3(1), dim3(1), 0, s, t, Mp6, Mp);
+    return hipGetLastError();
+}
+hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_gauss_jordan, dim3(1), dim3(256), 0, s, A, aug, fac, res, n);
+    return hipGetLastError();
+}
+
+size_t solve_single_lds_bytes(int ldq, int ldm) { return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm); }
+
+hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s) {
+    const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm);
+    if (a.N <= 64)
+        hipLaunchKernelGGL(k_solve_single<64>, dim3(1), dim3(64), lds, s, a, st);
+    else
+        hipLaunchKernelGGL(k_solve_single<256>, dim3(1), dim3(256), lds, s, a, st);
+    return hipGetLastError();
+}
+
+}  // namespace pqp

@@ -1,0 +1,56 @@
+// pqp_launch.h -- internal interface between the host shim (pqp_capi.cpp) and
+// the kernel translation unit (pqp_kernels.hip).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pqp {
+
+enum SolveStatus : int { kStatusContinue = 0, kStatusDone = 1, kStatusCapped = 2 };
+// SolveArgs::mode: 0 converge, 1 fixed, 2 evaluate terminate() once (no update)
+enum SolveMode : int { kModeConverge = 0, kModeFixed = 1, kModeTerminate = 2 };
+
+// Device-resident state of a (resumable) single-problem solve.
+struct SolveState {
+    long long h;     // reference's h of the current iterate (starts at 1)
+    int status;      // SolveStatus
+    int resume;      // 0: start from Y = 1000; 1: continue from SolveArgs::Y
+    float Jp, Jd;    // costs of the last terminate() that passed checkFeas
+    int have_costs;
+    int last_stop;   // result of the last terminate() (mode 2)
+};
+
+// All device pointers.  Qd row-major N x N (Jd's Y'Qd row), QdT column-major
+// (ldq) for the update, Gp row-major N x M, Qinv/Qp row-major M x M.
+struct SolveArgs {
+    const float *QdT, *Qd, *theta, *Fd, *Md, *Qp, *Qinv, *Fp, *Mp, *Gp, *Kp;
+    float *Y, *U;
+    int N, M, ldq, ldm, mode;
+    long long num_iter, max_updates, chunk;
+};
+
+hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
+                                const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s);
+hipError_t launch_batch_update(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
+                               const float* Fd, int ldv, const float* Yin, float* Yout, hipStream_t s);
+hipError_t launch_update_split(const float* QpT, const float* QnT, int ldq, int N, const float* Fdp,
+                               const float* Fdn, const float* Y, float* Ynext, hipStream_t s);
+hipError_t launch_pack_colmajor(int B, const float* Qd, int N, long long in_stride, float* QdT, int ldq,
+                                long long qstride, hipStream_t s);
+hipError_t launch_theta(int B, const float* QdT, int ldq, long long qstride, int N, float* theta, int ldv,
+                        hipStream_t s);
+hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, float* QdT, int ldq, long long qstride,
+                        float* Fd, int ldv, float* Md, hipStream_t s);
+hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c,
+                             hipStream_t s);
+hipError_t launch_axpy(float* A, const float* B, float sign, int n, hipStream_t s);
+hipError_t launch_negate(float* A, int n, hipStream_t s);
+hipError_t launch_compare(const float* gu, const float* Kp, int n, int* flag, hipStream_t s);
+hipError_t launch_theta_rowmajor(const float* Qd, int N, float* theta_mat, hipStream_t s);
+hipError_t launch_cost_finish(const float* quad, const float* lin, const float* Mc, float* J, hipStream_t s);
+hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStream_t s);
+hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
+size_t solve_single_lds_bytes(int ldq, int ldm);
+hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s);
+
+}  // namespace pqp

@@ -1,0 +1,344 @@
+"""pqp_amd -- Python mirror of the reference's solver interface over libpqp.
+
+The functions below keep the reference's names, argument order and meaning
+(PQP_CPU.c; see include/pqp.h for the C ABI they call): numpy float32 arrays
+stand in for the caller-owned ``float*`` buffers, outputs are written in place.
+Every call runs on the GPU through ``libpqp.so`` (built in-tree by
+``make -C pqp-for-mpc_amd``).  There is no CPU fallback: if the library or a
+gfx950 device is missing, calls raise :class:`PQPError`.
+
+Layers
+  * drop-in:  solveQuadraticDual, updateY2, terminate, convertToDual,
+    computeUfromY, computeCost, checkFeas, computeTheta, matrixMultiply,
+    Gauss_Jordan, computeFp, computeMp
+  * status API: solve_dual, update, read_example, run_example
+  * batched device API (torch tensors as device memory): :class:`Batch`
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libpqp.so"
+
+PQP_OK = 0
+PQP_ERR_ARG, PQP_ERR_HIP, PQP_ERR_ALLOC, PQP_ERR_IO, PQP_ERR_NOT_CONVERGED, PQP_ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
+MODE_CONVERGE, MODE_FIXED = 0, 1
+
+# The reference's compile-time problem dimensions (PQP_CPU.c:13-17).
+P_HORIZON, N_STATE, N_INPUT, N_OUTPUT, N_DIS = 1, 29, 7, 7, 1
+
+_fp = C.POINTER(C.c_float)
+_vp = C.c_void_p
+
+# name -> (restype, argtypes) for every symbol of include/pqp.h
+SIGNATURES = {
+    "pqp_last_error": (C.c_char_p, []),
+    "pqp_version": (C.c_int, []),
+    "solveQuadraticDual": (None, [_fp] * 11 + [C.c_int] * 2),
+    "updateY2": (None, [_fp] * 7 + [C.c_int]),
+    "terminate": (C.c_int, [_fp] * 11 + [C.c_int] * 2),
+    "convertToDual": (None, [_fp] * 8 + [C.c_int] * 2),
+    "computeUfromY": (None, [_fp] * 5 + [C.c_int] * 2),
+    "computeCost": (C.c_float, [_fp] * 4 + [C.c_int]),
+    "checkFeas": (C.c_int, [_fp] * 3 + [C.c_int] * 2),
+    "computeTheta": (None, [_fp, _fp, C.c_int]),
+    "matrixMultiply": (None, [_fp, _fp, C.c_int, _fp, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "Gauss_Jordan": (None, [_fp, _fp, C.c_int]),
+    "computeFp": (None, [_fp] * 6),
+    "computeMp": (None, [_fp] * 9),
+    "input": (None, [_fp] * 16),
+    "pqp_solve_dual": (C.c_int, [_fp] * 9 + [C.c_int] * 3 + [C.c_longlong] * 2 + [_fp, _fp,
+                                                                                   C.POINTER(C.c_longlong), _fp, _fp]),
+    "pqp_update_host": (C.c_int, [_fp] * 5 + [C.c_int]),
+    "pqp_read_example": (C.c_int, [C.c_char_p] + [C.c_int] * 3 + [_fp] * 14),
+    "pqp_run_example": (C.c_int, [C.c_char_p, _vp]),
+    "pqp_batch_generate": (C.c_int, [C.c_uint32, C.c_longlong, C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_longlong,
+                                     _vp, _vp, _vp, C.c_int, _vp]),
+    "pqp_batch_pack": (C.c_int, [C.c_int, C.c_int, _vp, _vp, C.c_int, C.c_longlong, _vp]),
+    "pqp_batch_theta": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, C.c_int, _vp]),
+    "pqp_batch_update": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp, _vp]),
+    "pqp_batch_iterate": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp,
+                                    C.c_int, _vp]),
+}
+
+
+class PQPError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libpqp error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree libpqp.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise PQPError(PQP_ERR_NO_DEVICE, f"{LIB_PATH} is missing: run `make -C pqp-for-mpc_amd` "
+                                              "(or __graft_entry__.build())")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def last_error() -> str:
+    return (lib().pqp_last_error() or b"").decode()
+
+
+def _check(rc: int):
+    if rc != PQP_OK:
+        raise PQPError(rc, last_error())
+
+
+def _f32(a) -> np.ndarray:
+    a = np.asarray(a, dtype=np.float32)
+    return np.ascontiguousarray(a)
+
+
+def _buf(a: np.ndarray):
+    if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]):
+        raise TypeError("buffers must be C-contiguous float32 numpy arrays")
+    return a.ctypes.data_as(_fp)
+
+
+# ---------------------------------------------------------------------------
+# drop-in entry points (reference names; outputs written in place)
+# ---------------------------------------------------------------------------
+def solveQuadraticDual(Y, Qd, Fd, Md, U, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M):
+    """PQP_CPU.c:694 -- prints 'Printing number of iterations = h'."""
+    lib().solveQuadraticDual(*[_buf(a) for a in (Y, Qd, Fd, Md, U, Qp, Qp_inv, Fp, Mp, Gp, Kp)], N, M)
+
+
+def updateY2(Y_next, Y, Qdp_theta, Qdn_theta, Fd, Fdp, Fdn, N):
+    """PQP_CPU.c:603."""
+    lib().updateY2(*[_buf(a) for a in (Y_next, Y, Qdp_theta, Qdn_theta, Fd, Fdp, Fdn)], N)
+
+
+def terminate(Y, Qd, Fd, Md, U, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M) -> int:
+    """PQP_CPU.c:673."""
+    return int(lib().terminate(*[_buf(a) for a in (Y, Qd, Fd, Md, U, Qp, Qp_inv, Fp, Mp, Gp, Kp)], N, M))
+
+
+def convertToDual(Qd, Fd, Md, Qp_inv, Gp, Kp, Fp, Mp, N, M):
+    """PQP_CPU.c:489."""
+    lib().convertToDual(*[_buf(a) for a in (Qd, Fd, Md, Qp_inv, Gp, Kp, Fp, Mp)], N, M)
+
+
+def computeUfromY(U, Y, Fp, Gp, Qp_inv, N, M):
+    """PQP_CPU.c:352."""
+    lib().computeUfromY(*[_buf(a) for a in (U, Y, Fp, Gp, Qp_inv)], N, M)
+
+
+def computeCost(Z, Q, F, Mc, N) -> float:
+    """PQP_CPU.c:648."""
+    return float(lib().computeCost(*[_buf(a) for a in (Z, Q, F, Mc)], N))
+
+
+def checkFeas(U, Gp, Kp, N, M) -> int:
+    """PQP_CPU.c:632."""
+    return int(lib().checkFeas(*[_buf(a) for a in (U, Gp, Kp)], N, M))
+
+
+def computeTheta(theta, Qd, N):
+    """PQP_CPU.c:503."""
+    lib().computeTheta(_buf(theta), _buf(Qd), N)
+
+
+def matrixMultiply(output, mat1, transpose1, mat2, transpose2, a, b, c):
+    """PQP_CPU.c:84."""
+    lib().matrixMultiply(_buf(output), _buf(mat1), transpose1, _buf(mat2), transpose2, a, b, c)
+
+
+def Gauss_Jordan(A, res, N):
+    """PQP_CPU.c:251."""
+    lib().Gauss_Jordan(_buf(A), _buf(res), N)
+
+
+def computeFp(Fp, Fp1, Fp2, Fp3, D, x):
+    """PQP_CPU.c:373 (bundled dimensions)."""
+    lib().computeFp(*[_buf(a) for a in (Fp, Fp1, Fp2, Fp3, D, x)])
+
+
+def computeMp(Mp, Mp1, Mp2, Mp3, Mp4, Mp5, Mp6, D, x):
+    """PQP_CPU.c:395 (bundled dimensions)."""
+    lib().computeMp(*[_buf(a) for a in (Mp, Mp1, Mp2, Mp3, Mp4, Mp5, Mp6, D, x)])
+
+
+# ---------------------------------------------------------------------------
+# status API
+# ---------------------------------------------------------------------------
+def solve_dual(P: dict, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0):
+    """pqp_solve_dual on a problem dict with keys Qd Fd Md Qp Qp_inv Fp Mp Gp Kp N M.
+
+    Returns dict(h, Y, U, Jp, Jd, converged).  Raises on any error other than
+    hitting the update cap in converge mode (then converged=False)."""
+    N, M = int(P["N"]), int(P["M"])
+    a = {k: _f32(P[k]) for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    Y, U = np.zeros(N, np.float32), np.zeros(M, np.float32)
+    h = C.c_longlong(0)
+    jp, jd = np.zeros(1, np.float32), np.zeros(1, np.float32)
+    rc = lib().pqp_solve_dual(*[_buf(a[k]) for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")],
+                              N, M, mode, num_iter, max_updates, _buf(Y), _buf(U), C.byref(h), _buf(jp), _buf(jd))
+    if rc not in (PQP_OK, PQP_ERR_NOT_CONVERGED):
+        _check(rc)
+    return dict(h=int(h.value), Y=Y, U=U, Jp=float(jp[0]), Jd=float(jd[0]), converged=(rc == PQP_OK))
+
+
+def update(Qd, theta_diag, Fd, Y, N) -> np.ndarray:
+    """One fused update (pqp_update_host)."""
+    out = np.zeros(N, np.float32)
+    _check(lib().pqp_update_host(_buf(_f32(Qd)), _buf(_f32(theta_diag)), _buf(_f32(Fd)), _buf(_f32(Y)),
+                                 _buf(out), N))
+    return out
+
+
+def read_example(directory, m=N_INPUT * P_HORIZON, nd=N_DIS * P_HORIZON, ns=N_STATE) -> dict:
+    """Host reader of example/*.txt (PQP_CPU.c:757-930).  No GPU work."""
+    N = 4 * m
+    shapes = dict(Qp_inv=m * m, Fp1=m * nd, Fp2=m * ns, Fp3=m, Mp1=ns * ns, Mp2=nd * ns, Mp3=nd * nd, Mp4=ns,
+                  Mp5=nd, Mp6=1, Gp=N * m, Kp=N, x=ns, D=nd)
+    arr = {k: np.zeros(v, np.float32) for k, v in shapes.items()}
+    order = ["Qp_inv", "Fp1", "Fp2", "Fp3", "Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "Gp", "Kp", "x", "D"]
+    _check(lib().pqp_read_example(str(directory).encode(), m, nd, ns, *[_buf(arr[k]) for k in order]))
+    arr.update(N=N, M=m, nd=nd, ns=ns)
+    return arr
+
+
+def example_problem(directory) -> dict:
+    """main() of PQP_CPU.c:935-994 up to the solve, on the GPU: read the
+    example files, Gauss_Jordan, computeFp, computeMp, convertToDual.  Returns
+    the dual problem dict accepted by solve_dual()."""
+    P = read_example(directory)
+    N, M = P["N"], P["M"]
+    Qp, Fp, Mp = np.zeros(M * M, np.float32), np.zeros(M, np.float32), np.zeros(1, np.float32)
+    Gauss_Jordan(P["Qp_inv"], Qp, M)
+    computeFp(Fp, P["Fp1"], P["Fp2"], P["Fp3"], P["D"], P["x"])
+    computeMp(Mp, P["Mp1"], P["Mp2"], P["Mp3"], P["Mp4"], P["Mp5"], P["Mp6"], P["D"], P["x"])
+    Qd, Fd, Md = np.zeros(N * N, np.float32), np.zeros(N, np.float32), np.zeros(1, np.float32)
+    convertToDual(Qd, Fd, Md, P["Qp_inv"], P["Gp"], P["Kp"], Fp, Mp, N, M)
+    P.update(Qp=Qp, Fp=Fp, Mp=Mp, Qd=Qd, Fd=Fd, Md=Md)
+    return P
+
+
+def run_example(directory) -> str:
+    """main() of PQP_CPU.c on the GPU; returns what it prints."""
+    libc = C.CDLL(None)
+    libc.fopen.restype = C.c_void_p
+    libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    libc.fclose.argtypes = [C.c_void_p]
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "out.txt")
+        fh = libc.fopen(path.encode(), b"w")
+        try:
+            rc = lib().pqp_run_example(str(directory).encode(), fh)
+        finally:
+            libc.fclose(fh)
+        _check(rc)
+        return Path(path).read_text()
+
+
+# ---------------------------------------------------------------------------
+# batched device API (torch provides the HBM buffers and the stream)
+# ---------------------------------------------------------------------------
+def round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+class Batch:
+    """B independent dual problems of size N resident in HBM.
+
+    QdT is [B][N][ldq] fp32 with Qd stored column-major per problem (element
+    (i,k) at k*ldq + i); theta/Fd/Y are [B][ldv].  All launches go to torch's
+    current HIP stream of ``device``.
+    """
+
+    def __init__(self, B: int, N: int, device=None, ldq: int | None = None, ldv: int | None = None):
+        import torch
+
+        self.torch = torch
+        self.B, self.N = int(B), int(N)
+        self.ldq = int(ldq) if ldq else round_up(self.N, 4)
+        self.ldv = int(ldv) if ldv else round_up(self.N, 4)
+        self.qstride = self.N * self.ldq
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        kw = dict(dtype=torch.float32, device=self.device)
+        self.QdT = torch.empty(self.B * self.qstride, **kw)
+        self.theta = torch.zeros(self.B, self.ldv, **kw)
+        self.Fd = torch.zeros(self.B, self.ldv, **kw)
+        self.Md = torch.zeros(self.B, **kw)
+        self.Y = torch.zeros(self.B, self.ldv, **kw)
+        self.Y2 = torch.zeros(self.B, self.ldv, **kw)
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def _p(t):
+        return C.c_void_p(t.data_ptr())
+
+    def generate(self, seed: int, inst0: int = 0, M: int | None = None):
+        """Synthetic problems inst0..inst0+B-1 of `seed` (M defaults to N/2)."""
+        M = int(M) if M else max(1, self.N // 2)
+        self.M = M
+        _check(lib().pqp_batch_generate(seed, inst0, self.B, self.N, M, self._p(self.QdT), self.ldq, self.qstride,
+                                        self._p(self.Fd), self._p(self.Md), self._p(self.theta), self.ldv,
+                                        self._stream()))
+        return self
+
+    def load(self, Qd, Fd):
+        """Load row-major Qd ([B][N*N] or [B][N][N]) and Fd ([B][N]) given as
+        numpy/torch; packs to QdT on the GPU and computes theta."""
+        torch = self.torch
+        Qd = torch.as_tensor(np.asarray(Qd, np.float32) if not torch.is_tensor(Qd) else Qd, dtype=torch.float32)
+        Qd = Qd.reshape(self.B, self.N * self.N).to(self.device).contiguous()
+        Fd = torch.as_tensor(np.asarray(Fd, np.float32) if not torch.is_tensor(Fd) else Fd, dtype=torch.float32)
+        self.Fd.zero_()
+        self.Fd[:, : self.N] = Fd.reshape(self.B, self.N).to(self.device)
+        self.QdT.zero_()
+        _check(lib().pqp_batch_pack(self.B, self.N, self._p(Qd), self._p(self.QdT), self.ldq, self.qstride,
+                                    self._stream()))
+        _check(lib().pqp_batch_theta(self.B, self.N, self._p(self.QdT), self.ldq, self.qstride, self._p(self.theta),
+                                     self.ldv, self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()  # Qd staging buffer goes out of scope
+        return self
+
+    def reset(self, value: float = 1000.0):
+        self.Y.fill_(value)
+        return self
+
+    def update(self):
+        """One updateY2 for every problem: Y <- Y_next (pqp_batch_update)."""
+        _check(lib().pqp_batch_update(self.B, self.N, self._p(self.QdT), self.ldq, self.qstride, self._p(self.theta),
+                                      self._p(self.Fd), self.ldv, self._p(self.Y), self._p(self.Y2), self._stream()))
+        self.Y, self.Y2 = self.Y2, self.Y
+        return self
+
+    def iterate(self, updates: int, from_start: bool = True):
+        """`updates` fused updates per problem in one launch (pqp_batch_iterate);
+        from_start=True begins at the reference's Y = 1000."""
+        y0 = None if from_start else self._p(self.Y)
+        _check(lib().pqp_batch_iterate(self.B, self.N, self._p(self.QdT), self.ldq, self.qstride, self._p(self.theta),
+                                       self._p(self.Fd), self.ldv, y0, self._p(self.Y2), int(updates),
+                                       self._stream()))
+        self.Y, self.Y2 = self.Y2, self.Y
+        return self
+
+    def result(self) -> np.ndarray:
+        return self.Y[:, : self.N].cpu().numpy()
+
+    def qd_rowmajor(self, b: int) -> np.ndarray:
+        """Problem b's Qd back in the reference's row-major layout (host)."""
+        qt = self.QdT[b * self.qstride:(b + 1) * self.qstride].reshape(self.N, self.ldq)[:, : self.N]
+        return qt.t().contiguous().cpu().numpy().reshape(-1)

@@ -1,0 +1,118 @@
+"""The C-ABI library: loads, exports every symbol include/pqp.h declares, and
+its host-only pieces (file reader, argument validation) behave like the
+reference.  No GPU compute is issued here."""
+from __future__ import annotations
+
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import EXAMPLE_DIR, ROOT, assert_bitwise
+
+HEADER = ROOT / "include" / "pqp.h"
+LIBSO = ROOT / "pqp-for-mpc_amd" / "pqp_amd" / "libpqp.so"
+
+
+def declared_functions() -> list[str]:
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s*([A-Za-z_][A-Za-z0-9_]*)\s*\(", text, re.M)
+    return sorted(set(names))
+
+
+def test_header_lists_reference_entry_points():
+    names = declared_functions()
+    for ref_name in ("solveQuadraticDual", "updateY2", "terminate", "convertToDual", "computeUfromY", "computeCost",
+                     "checkFeas", "computeTheta", "matrixMultiply", "Gauss_Jordan", "computeFp", "computeMp",
+                     "input"):
+        assert ref_name in names
+
+
+def test_library_exports_every_declared_symbol():
+    assert LIBSO.exists(), "libpqp.so not built (run __graft_entry__.build())"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIBSO)], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+
+
+def test_python_mirror_binds_every_symbol():
+    import pqp_amd
+
+    assert set(pqp_amd.SIGNATURES) == set(declared_functions())
+    L = pqp_amd.lib()
+    for n in declared_functions():
+        assert getattr(L, n) is not None
+    assert L.pqp_version() >= 100
+
+
+def test_hot_kernels_compile_for_gfx950_without_fma():
+    """The update kernels must not contract a*b+c into FMA (bit-parity rule,
+    SURVEY.md 8a): compile the kernel TU for gfx950 exactly as the Makefile
+    does and inspect the ISA of the hot kernels."""
+    import tempfile
+
+    hipcc = Path("/opt/rocm/bin/hipcc")
+    if not hipcc.exists():
+        pytest.skip("hipcc not present")
+    src = ROOT / "pqp-for-mpc_amd" / "csrc" / "pqp_kernels.hip"
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "k.s"
+        subprocess.run([str(hipcc), "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                        "-fno-fast-math", "--cuda-device-only", "-S", str(src), "-o", str(out)], check=True)
+        asm = out.read_text()
+    bodies = re.split(r"\n(?=_ZN3pqp[A-Za-z0-9_]*:)", asm)
+    hot = [b for b in bodies if re.match(r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single)", b)]
+    assert len(hot) >= 6, "hot kernels not found in the gfx950 assembly"
+    for body in hot:
+        name = body.split(":", 1)[0]
+        body = body.split(".Lfunc_end", 1)[0]
+        # the only FMAs allowed are the 5 inside each IEEE-correct division
+        # expansion (v_div_scale .. v_div_fmas .. v_div_fixup); none may come
+        # from contracting the solver's own products and sums
+        n_div = len(re.findall(r"\bv_div_fixup_f32", body))
+        n_fma = len(re.findall(r"\bv_(fma|fmac|mad|mac|pk_fma)_f32", body))
+        assert n_div > 0, name + ": division is not the IEEE-correct sequence"
+        assert n_fma == 5 * n_div, f"{name}: {n_fma} FMAs for {n_div} divisions"
+
+
+def test_read_example_matches_oracle_loader(orc):
+    import pqp_amd
+
+    got = pqp_amd.read_example(EXAMPLE_DIR)
+    exp = orc.load_example(EXAMPLE_DIR)
+    for k in ("Qp_inv", "Fp1", "Fp2", "Fp3", "Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "Gp", "Kp", "x", "D"):
+        assert_bitwise(got[k], exp[k], k)
+    assert got["N"] == 28 and got["M"] == 7
+
+
+def test_read_example_missing_file_is_an_error(tmp_path):
+    import pqp_amd
+
+    with pytest.raises(pqp_amd.PQPError) as ei:
+        pqp_amd.read_example(tmp_path)
+    assert ei.value.code == pqp_amd.PQP_ERR_IO
+    assert "Qp_inv.txt" in str(ei.value)
+
+
+def test_read_example_short_file_is_an_error(tmp_path):
+    import shutil
+
+    import pqp_amd
+
+    for f in EXAMPLE_DIR.glob("*.txt"):
+        shutil.copy(f, tmp_path / f.name)
+    (tmp_path / "Kp.txt").write_text("1.0 2.0 #")
+    with pytest.raises(pqp_amd.PQPError) as ei:
+        pqp_amd.read_example(tmp_path)
+    assert ei.value.code == pqp_amd.PQP_ERR_IO and "Kp.txt" in str(ei.value)
+
+
+def test_python_buffers_are_validated():
+    import pqp_amd
+
+    with pytest.raises(TypeError):
+        pqp_amd.computeTheta(np.zeros(4, np.float64), np.zeros(4, np.float32), 2)

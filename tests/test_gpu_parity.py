@@ -1,0 +1,275 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+fixtures and the oracle.  Bar: bit-exact fp32 (the north star's 1e-6 relative
+tolerance on y* is met with zero error), iterations-to-convergence identical.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import EXAMPLE_DIR, GOLDEN, assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
+
+
+def bundled_problem(g):
+    P = {k: np.ascontiguousarray(g[k], dtype=np.float32) for k in KEYS}
+    P.update(N=int(g["N"]), M=int(g["M"]))
+    return P
+
+
+# ---------------------------------------------------------------------------
+# bundled example (configs 1/2)
+# ---------------------------------------------------------------------------
+def test_bundled_converge_bit_exact(gpu_lib, golden_bundled):
+    g = golden_bundled
+    r = gpu_lib.solve_dual(bundled_problem(g))
+    assert r["converged"]
+    assert r["h"] == int(g["h"]) == 313
+    assert_bitwise(r["Y"], g["Ystar"], "Y*")
+    assert_bitwise(r["U"], g["Ustar"], "U from the final terminate()")
+    assert np.float32(r["Jp"]) == g["iter_Jp"][-1] and np.float32(r["Jd"]) == g["iter_Jd"][-1]
+    assert not np.array_equal(r["Y"].view(np.uint32), g["Ystar_fma_contracted"].view(np.uint32))
+
+
+def test_bundled_fixed_1000_bit_exact(gpu_lib, golden_bundled):
+    g = golden_bundled
+    r = gpu_lib.solve_dual(bundled_problem(g), mode=gpu_lib.MODE_FIXED, num_iter=1000)
+    assert r["h"] == 1000
+    assert_bitwise(r["Y"], g["Y_fixed999"], "fixed-999 Y")
+
+
+@pytest.mark.parametrize("k", [1, 2, 10, 100, 312])
+def test_bundled_fixed_k_updates(gpu_lib, golden_bundled, k):
+    g = golden_bundled
+    r = gpu_lib.solve_dual(bundled_problem(g), mode=gpu_lib.MODE_FIXED, num_iter=k)
+    want = g["Ystar"] if k == 313 else (g[f"Y_h{k}"])
+    assert_bitwise(r["Y"], want, f"Y after {k - 1} updates")
+
+
+def test_dropin_solveQuadraticDual_prints_h(gpu_lib, golden_bundled, capfd):
+    g = golden_bundled
+    P = bundled_problem(g)
+    Y, U = np.zeros(P["N"], np.float32), np.zeros(P["M"], np.float32)
+    gpu_lib.solveQuadraticDual(Y, P["Qd"], P["Fd"], P["Md"], U, P["Qp"], P["Qp_inv"], P["Fp"], P["Mp"], P["Gp"],
+                               P["Kp"], P["N"], P["M"])
+    out = capfd.readouterr().out
+    assert "Printing number of iterations = 313\n" in out
+    assert_bitwise(Y, g["Ystar"], "Y*")
+
+
+def test_cli_stdout_matches_reference_byte_for_byte(gpu_lib):
+    expected = (GOLDEN / "bundled_stdout.txt").read_text()
+    assert gpu_lib.run_example(EXAMPLE_DIR) == expected
+
+
+def test_pqp_cli_binary(tmp_path):
+    import shutil
+    import subprocess
+
+    from conftest import ROOT
+
+    (tmp_path / "example").mkdir()
+    for f in EXAMPLE_DIR.glob("*.txt"):
+        shutil.copy(f, tmp_path / "example" / f.name)
+    cli = ROOT / "pqp-for-mpc_amd" / "bin" / "pqp_cli"
+    out = subprocess.run([str(cli)], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout == (GOLDEN / "bundled_stdout.txt").read_text()
+
+
+# ---------------------------------------------------------------------------
+# drop-in helpers, one by one, vs the reference's values
+# ---------------------------------------------------------------------------
+def test_dropin_updateY2_split_matrices(gpu_lib, golden_bundled, orc):
+    g = golden_bundled
+    N = int(g["N"])
+    qp, qn = orc.split_theta(g["Qd"], g["theta"], N)
+    for a, b in ((1, 2), (100, None)):
+        Y = np.ascontiguousarray(g[f"Y_h{a}"])
+        out = np.zeros(N, np.float32)
+        gpu_lib.updateY2(out, Y.copy(), qp, qn, g["Fd"].copy(), g["Fdp"].copy(), g["Fdn"].copy(), N)
+        want = g[f"Y_h{b}"] if b else orc.update_split(Y, qp, qn, g["Fdp"], g["Fdn"], N)
+        assert_bitwise(out, want, f"updateY2 from Y_h{a}")
+
+
+def test_dropin_terminate(gpu_lib, golden_bundled):
+    g = golden_bundled
+    P = bundled_problem(g)
+    for key, flag_ref in (("Y_h1", 0), ("Y_h312", 0), ("Ystar", 1)):
+        U = np.zeros(P["M"], np.float32)
+        flag = gpu_lib.terminate(np.ascontiguousarray(g[key]), P["Qd"], P["Fd"], P["Md"], U, P["Qp"], P["Qp_inv"],
+                                 P["Fp"], P["Mp"], P["Gp"], P["Kp"], P["N"], P["M"])
+        assert flag == flag_ref, key
+    assert_bitwise(U, g["Ustar"], "U")
+
+
+def test_dropin_setup_functions(gpu_lib, golden_bundled, orc):
+    g = golden_bundled
+    ex = orc.load_example(EXAMPLE_DIR)
+    N, M = int(g["N"]), int(g["M"])
+    Qp = np.zeros(M * M, np.float32)
+    gpu_lib.Gauss_Jordan(ex["Qp_inv"].copy(), Qp, M)
+    assert_bitwise(Qp, g["Qp"], "Gauss_Jordan")
+    Fp = np.zeros(M, np.float32)
+    gpu_lib.computeFp(Fp, ex["Fp1"], ex["Fp2"], ex["Fp3"], ex["D"], ex["x"])
+    assert_bitwise(Fp, g["Fp"], "computeFp")
+    Mp = np.zeros(1, np.float32)
+    gpu_lib.computeMp(Mp, ex["Mp1"], ex["Mp2"], ex["Mp3"], ex["Mp4"], ex["Mp5"], ex["Mp6"], ex["D"], ex["x"])
+    assert_bitwise(Mp, g["Mp"], "computeMp")
+    Qd, Fd, Md = np.zeros(N * N, np.float32), np.zeros(N, np.float32), np.zeros(1, np.float32)
+    gpu_lib.convertToDual(Qd, Fd, Md, g["Qp_inv"].copy(), g["Gp"].copy(), g["Kp"].copy(), g["Fp"].copy(),
+                          g["Mp"].copy(), N, M)
+    assert_bitwise(Qd, g["Qd"], "Qd")
+    assert_bitwise(Fd, g["Fd"], "Fd")
+    assert_bitwise(Md, g["Md"], "Md")
+    th = np.zeros(N * N, np.float32)
+    gpu_lib.computeTheta(th, g["Qd"].copy(), N)
+    assert_bitwise(th.reshape(N, N).diagonal().copy(), g["theta"], "computeTheta")
+    assert np.count_nonzero(th) == N
+    U = np.zeros(M, np.float32)
+    gpu_lib.computeUfromY(U, g["Ystar"].copy(), g["Fp"].copy(), g["Gp"].copy(), g["Qp_inv"].copy(), N, M)
+    assert_bitwise(U, g["Ustar"], "computeUfromY")
+    assert gpu_lib.checkFeas(U, g["Gp"].copy(), g["Kp"].copy(), N, M) == 1
+    assert gpu_lib.checkFeas((U * 100).astype(np.float32), g["Gp"].copy(), g["Kp"].copy(), N, M) == 0
+    assert np.float32(gpu_lib.computeCost(U, g["Qp"].copy(), g["Fp"].copy(), g["Mp"].copy(), M)) == g["Jp"]
+    assert np.float32(gpu_lib.computeCost(g["Ystar"].copy(), g["Qd"].copy(), g["Fd"].copy(), g["Md"].copy(),
+                                          N)) == g["Jd"]
+
+
+def test_dropin_matrixMultiply_transposes(gpu_lib, orc):
+    rng = np.random.default_rng(7)
+    for (a, b, c) in [(1, 1, 1), (3, 7, 5), (17, 9, 1), (1, 33, 20), (64, 48, 40)]:
+        for tA in (0, 1):
+            for tB in (0, 1):
+                A = rng.standard_normal(a * b).astype(np.float32)
+                B = rng.standard_normal(b * c).astype(np.float32)
+                out = np.zeros(a * c, np.float32)
+                gpu_lib.matrixMultiply(out, A, tA, B, tB, a, b, c)
+                assert_bitwise(out, orc.matmul(A, tA, B, tB, a, b, c), f"{a}x{b}x{c} t{tA}{tB}")
+
+
+# ---------------------------------------------------------------------------
+# synthetic problems: converge mode (iterations identical) and large duals
+# ---------------------------------------------------------------------------
+def test_synthetic_converge_cases(gpu_lib, golden_converge, orc):
+    cases, Ys, Us = golden_converge["cases"], golden_converge["Y"], golden_converge["U"]
+    yo = uo = 0
+    for (N, M, seed, h_ref) in cases:
+        N, M = int(N), int(M)
+        P = orc.synth_problem(int(seed), 0, N, M)
+        r = gpu_lib.solve_dual(P, max_updates=100000)
+        assert r["converged"] and r["h"] == int(h_ref), (N, M, seed, r["h"])
+        assert_bitwise(r["Y"], Ys[yo:yo + N], f"Y {N}/{M}/{seed}")
+        yo += N
+        uo += M
+
+
+def test_converge_cap_reports_not_converged(gpu_lib, orc):
+    P = orc.synth_problem(2, 0, 16, 8)  # the reference does not converge on this one
+    r = gpu_lib.solve_dual(P, max_updates=500)
+    assert not r["converged"] and r["h"] == 501
+    h, Y, _ = orc.solve(P, mode=1, num_iter=501)
+    assert_bitwise(r["Y"], Y, "Y after 500 updates")
+
+
+@pytest.mark.parametrize("tag", ["n1024_m512_s1_i0", "n1000_m500_s2_i7"])
+def test_batch_generator_and_updates_match_reference(gpu_lib, golden_large, tag):
+    N, M, seed, inst, ups = (int(v) for v in golden_large[f"{tag}_meta"])
+    b = gpu_lib.Batch(1, N).generate(seed, inst0=inst, M=M)
+    Qd = b.qd_rowmajor(0)
+    assert hashlib.sha256(Qd.tobytes()).digest() == golden_large[f"{tag}_Qd_sha256"].tobytes()
+    assert_bitwise(b.Fd[0, :N].cpu().numpy(), golden_large[f"{tag}_Fd"], "Fd")
+    assert_bitwise(b.Md[:1].cpu().numpy(), golden_large[f"{tag}_Md"], "Md")
+    assert_bitwise(b.theta[0, :N].cpu().numpy(), golden_large[f"{tag}_theta"], "theta")
+    b.reset()
+    for _ in range(ups):
+        b.update()
+    assert_bitwise(b.result()[0], golden_large[f"{tag}_Y"], "Y via batch_update")
+    b.iterate(ups)
+    assert_bitwise(b.result()[0], golden_large[f"{tag}_Y"], "Y via batch_iterate")
+
+
+@pytest.mark.parametrize("N", [1, 3, 4, 28, 64, 255, 256, 257, 300, 1023, 1025, 2050])
+def test_batch_kernels_vs_oracle_edge_sizes(gpu_lib, orc, N):
+    """Ragged N (not multiples of 4 / 64 / 256 / 1024), several problems."""
+    B, M, ups = 3, max(1, N // 2), 4
+    b = gpu_lib.Batch(B, N).generate(seed=11, inst0=5, M=M)
+    b.iterate(ups)
+    it = b.result()
+    b.reset()
+    for _ in range(ups):
+        b.update()
+    up = b.result()
+    for j in range(B):
+        P = orc.synth_problem(11, 5 + j, N, M, with_qp=False)
+        want = orc.iterate(P["Qd"], P["Fd"], N, ups)
+        assert_bitwise(it[j], want, f"iterate N={N} problem {j}")
+        assert_bitwise(up[j], want, f"update N={N} problem {j}")
+
+
+def test_batch_load_bundled_fixed_999(gpu_lib, golden_bundled):
+    g = golden_bundled
+    N = int(g["N"])
+    b = gpu_lib.Batch(2, N).load(np.stack([g["Qd"], g["Qd"]]), np.stack([g["Fd"], g["Fd"]]))
+    assert_bitwise(b.theta[0, :N].cpu().numpy(), g["theta"], "theta")
+    b.iterate(999)
+    assert_bitwise(b.result()[0], g["Y_fixed999"], "iterate 999")
+    assert_bitwise(b.result()[1], g["Y_fixed999"], "iterate 999 (2nd copy)")
+
+
+def test_batch_problems_are_independent(gpu_lib):
+    """Problem inst0+j of a batch == the same problem generated alone."""
+    N, B = 512, 16
+    big = gpu_lib.Batch(B, N).generate(seed=3, inst0=100).iterate(7).result()
+    for j in (0, 5, 15):
+        one = gpu_lib.Batch(1, N).generate(seed=3, inst0=100 + j).iterate(7).result()[0]
+        assert_bitwise(big[j], one, f"problem {j}")
+
+
+def test_iterate_equals_repeated_update_large_batch(gpu_lib):
+    N, B, ups = 1024, 96, 12
+    b = gpu_lib.Batch(B, N).generate(seed=9)
+    b.iterate(ups)
+    a = b.result()
+    b.reset()
+    for _ in range(ups):
+        b.update()
+    assert_bitwise(b.result(), a, "iterate vs update")
+    assert np.all(np.isfinite(a)) and np.all(a >= 0)
+
+
+def test_full_size_batch_properties(gpu_lib, orc):
+    """BASELINE config 4 (N=1024, B=4096, 16 GiB of Qd): sampled problems
+    bit-exact against the oracle, all iterates finite and non-negative."""
+    import torch
+
+    N, B, ups = 1024, 4096, 3
+    b = gpu_lib.Batch(B, N).generate(seed=1)
+    b.iterate(ups)
+    Y = b.result()
+    assert np.all(np.isfinite(Y)) and np.all(Y >= 0)
+    for j in (0, 1777, 4095):
+        P = orc.synth_problem(1, j, N, N // 2, with_qp=False)
+        assert_bitwise(Y[j], orc.iterate(P["Qd"], P["Fd"], N, ups), f"problem {j}")
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_batch_argument_validation(gpu_lib):
+    import ctypes as C
+
+    import torch
+
+    L = gpu_lib.lib()
+    q = torch.zeros(64, device="cuda")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = C.c_void_p(q.data_ptr())
+    assert L.pqp_batch_update(1, 4, p, 3, 16, p, p, 4, p, p, s) == gpu_lib.PQP_ERR_ARG  # ldq < N
+    assert "ldq" in gpu_lib.last_error()
+    assert L.pqp_batch_update(1, 4, p, 4, 16, p, p, 4, p, p, s) == gpu_lib.PQP_ERR_ARG  # Y aliases Ynext
+    assert L.pqp_batch_iterate(1, 4, p, 4, 16, p, p, 4, None, p, -1, s) == gpu_lib.PQP_ERR_ARG

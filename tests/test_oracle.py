@@ -1,0 +1,187 @@
+"""The oracle (CPU restatement of PQP_CPU.c) pinned against the reference.
+
+Two anchors:
+  * the committed golden fixtures (tests/golden/*.npz, produced by the
+    reference itself via tests/golden/make_golden.py) -- always run;
+  * the compiled reference oracle/_ref/libpqp_ref.so -- run where it exists.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import EXAMPLE_DIR, assert_bitwise
+
+from oracle import REF_SO, Reference
+
+
+def test_bundled_setup_matches_golden(orc, golden_bundled):
+    P = orc.bundled_problem(EXAMPLE_DIR)
+    g = golden_bundled
+    for k in ("Qp_inv", "Gp", "Kp", "Fp", "Mp", "Qp", "Qd", "Fd", "Md"):
+        assert_bitwise(P[k], g[k], k)
+    assert_bitwise(orc.theta(P["Qd"], P["N"]), g["theta"], "theta")
+
+
+def test_bundled_iterates_match_golden(orc, golden_bundled):
+    g = golden_bundled
+    N = int(g["N"])
+    th = orc.theta(g["Qd"], N)
+    Y = np.full(N, 1000.0, np.float32)
+    snaps = {}
+    for h in range(1, 313):
+        if h in (1, 2, 10, 100, 312):
+            snaps[h] = Y
+        Y = orc.update(Y, g["Qd"], th, g["Fd"], N)
+    for h, y in snaps.items():
+        assert_bitwise(y, g[f"Y_h{h}"], f"Y_h{h}")
+    assert_bitwise(Y, g["Ystar"], "Y after 312 updates")
+
+
+def test_bundled_solve_matches_golden(orc, golden_bundled):
+    g = golden_bundled
+    P = {k: g[k] for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    P.update(N=int(g["N"]), M=int(g["M"]))
+    h, Y, U = orc.solve(P)
+    assert h == int(g["h"]) == 313
+    assert_bitwise(Y, g["Ystar"], "Ystar")
+    U = orc.u_from_y(Y, P["Fp"], P["Gp"], P["Qp_inv"], P["N"], P["M"])
+    assert_bitwise(U, g["Ustar"], "Ustar")
+    assert np.float32(orc.cost(U, P["Qp"], P["Fp"], P["Mp"], P["M"])) == g["Jp"]
+    assert np.float32(orc.cost(Y, P["Qd"], P["Fd"], P["Md"], P["N"])) == g["Jd"]
+    # the FMA-contracted reference build is a result we must NOT reproduce
+    assert not np.array_equal(Y.view(np.uint32), g["Ystar_fma_contracted"].view(np.uint32))
+
+
+def test_bundled_fixed_mode(orc, golden_bundled):
+    g = golden_bundled
+    P = {k: g[k] for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    P.update(N=int(g["N"]), M=int(g["M"]))
+    h, Y, _ = orc.solve(P, mode=1, num_iter=1000)
+    assert h == 1000
+    assert_bitwise(Y, g["Y_fixed999"], "fixed-999 Y")
+
+
+def test_bundled_per_iteration_costs(orc, golden_bundled):
+    g = golden_bundled
+    N, M = int(g["N"]), int(g["M"])
+    th = orc.theta(g["Qd"], N)
+    Y = np.full(N, 1000.0, np.float32)
+    for h in range(313):
+        flag, U, jp, jd = orc.terminate(Y, g["Qd"], g["Fd"], g["Md"], g["Qp"], g["Qp_inv"], g["Fp"], g["Mp"],
+                                        g["Gp"], g["Kp"], N, M)
+        assert int(g["iter_feasible"][h]) == 1
+        assert np.float32(jp) == g["iter_Jp"][h] and np.float32(jd) == g["iter_Jd"][h], h
+        assert flag == (1 if h == 312 else 0), h
+        Y = orc.update(Y, g["Qd"], th, g["Fd"], N)
+
+
+def test_synthetic_converge_cases(orc, golden_converge):
+    cases, Ys, Us = golden_converge["cases"], golden_converge["Y"], golden_converge["U"]
+    yo = uo = 0
+    for (N, M, seed, h_ref) in cases:
+        N, M = int(N), int(M)
+        P = orc.synth_problem(int(seed), 0, N, M)
+        h, Y, U = orc.solve(P, max_updates=100000)
+        assert h == int(h_ref), (N, M, seed)
+        assert_bitwise(Y, Ys[yo:yo + N], f"Y {N}/{M}/{seed}")
+        U = orc.u_from_y(Y, P["Fp"], P["Gp"], P["Qp_inv"], N, M)
+        assert_bitwise(U, Us[uo:uo + M], f"U {N}/{M}/{seed}")
+        yo += N
+        uo += M
+
+
+@pytest.mark.parametrize("tag", ["n1024_m512_s1_i0", "n1000_m500_s2_i7"])
+def test_synthetic_large_duals(orc, golden_large, tag):
+    N, M, seed, inst, ups = (int(v) for v in golden_large[f"{tag}_meta"])
+    P = orc.synth_problem(seed, inst, N, M, with_qp=False)
+    assert hashlib.sha256(P["Qd"].tobytes()).digest() == golden_large[f"{tag}_Qd_sha256"].tobytes()
+    assert_bitwise(P["Fd"], golden_large[f"{tag}_Fd"], "Fd")
+    assert_bitwise(P["Md"], golden_large[f"{tag}_Md"], "Md")
+    th = orc.theta(P["Qd"], N)
+    assert_bitwise(th, golden_large[f"{tag}_theta"], "theta")
+    Y = orc.iterate(P["Qd"], P["Fd"], N, ups)
+    assert_bitwise(Y, golden_large[f"{tag}_Y"], "Y")
+
+
+def test_split_update_equals_fused_update(orc):
+    """orc_update (split entries derived on the fly) == orc_update_split (stored)."""
+    rng = np.random.default_rng(0)
+    for N in (1, 5, 28, 64):
+        Qd = rng.standard_normal(N * N).astype(np.float32)
+        Qd[rng.random(N * N) < 0.2] = 0.0
+        Qd[rng.random(N * N) < 0.05] = -0.0
+        Fd = rng.standard_normal(N).astype(np.float32)
+        Y = rng.random(N).astype(np.float32) * 100
+        th = orc.theta(Qd, N)
+        qp, qn = orc.split_theta(Qd, th, N)
+        fdp, fdn = np.maximum(Fd, 0).astype(np.float32), np.maximum(-Fd, 0).astype(np.float32)
+        assert_bitwise(orc.update(Y, Qd, th, Fd, N), orc.update_split(Y, qp, qn, fdp, fdn, N), f"N={N}")
+
+
+# -- against the compiled reference (only where /root/reference was built) --
+needs_ref = pytest.mark.skipif(not REF_SO.exists(), reason="oracle/_ref not built (no /root/reference)")
+
+
+@needs_ref
+def test_matmul_all_transposes_vs_reference(orc):
+    ref = Reference()
+    rng = np.random.default_rng(1)
+    import ctypes as C
+
+    fp = C.POINTER(C.c_float)
+    for (a, b, c) in [(1, 1, 1), (3, 7, 5), (17, 9, 1), (1, 33, 20), (40, 40, 40)]:
+        for tA in (0, 1):
+            for tB in (0, 1):
+                A = rng.standard_normal(a * b).astype(np.float32)
+                B = rng.standard_normal(b * c).astype(np.float32)
+                out = np.zeros(a * c, np.float32)
+                ref.lib.matrixMultiply(out.ctypes.data_as(fp), A.copy().ctypes.data_as(fp), tA,
+                                       B.copy().ctypes.data_as(fp), tB, a, b, c)
+                assert_bitwise(orc.matmul(A, tA, B, tB, a, b, c), out, f"{a}x{b}x{c} t{tA}{tB}")
+
+
+@needs_ref
+def test_gauss_jordan_vs_reference(orc):
+    ref = Reference()
+    rng = np.random.default_rng(2)
+    for n in (1, 2, 7, 16, 33):
+        A = (rng.standard_normal((n, n)) + n * np.eye(n)).astype(np.float32).reshape(-1)
+        assert_bitwise(orc.gauss_jordan(A, n), ref.gauss_jordan(A, n), f"n={n}")
+    # a matrix whose column 0 triggers the bubble-pass swaps
+    A = np.array([[1, 2, 0], [3, 1, 1], [5, 0, 2]], np.float32).reshape(-1)
+    assert_bitwise(orc.gauss_jordan(A, 3), ref.gauss_jordan(A, 3), "swap case")
+
+
+@needs_ref
+def test_random_dense_duals_vs_reference(orc):
+    """Dense random primal data (not the generator's structure)."""
+    ref = Reference()
+    rng = np.random.default_rng(3)
+    for (N, M) in [(6, 3), (20, 11), (50, 25)]:
+        Qinv = rng.random((M, M)).astype(np.float32)
+        Qinv = ((Qinv + Qinv.T) / 2 + M * np.eye(M)).astype(np.float32).reshape(-1)
+        Gp = rng.standard_normal(N * M).astype(np.float32)
+        Kp = rng.random(N).astype(np.float32) * 5
+        Fp = rng.standard_normal(M).astype(np.float32)
+        Mp = np.ones(1, np.float32)
+        got = orc.convert_to_dual(Qinv, Gp, Kp, Fp, Mp, N, M)
+        exp = ref.convert_to_dual(Qinv, Gp, Kp, Fp, Mp, N, M)
+        for g_, e_, k in zip(got, exp, ("Qd", "Fd", "Md")):
+            assert_bitwise(g_, e_, k)
+        S = ref.split(exp[0], exp[1], N)
+        th = orc.theta(exp[0], N)
+        Y = np.full(N, 1000.0, np.float32)
+        Yr = Y.copy()
+        for _ in range(25):
+            Y = orc.update(Y, exp[0], th, exp[1], N)
+            Yr = ref.update(Yr, S, exp[1], N)
+        assert_bitwise(Y, Yr, f"updates N={N}")
+        P = dict(Qd=exp[0], Fd=exp[1], Md=exp[2], Qp=orc.gauss_jordan(Qinv, M), Qp_inv=Qinv, Fp=Fp, Mp=Mp, Gp=Gp,
+                 Kp=Kp, N=N, M=M)
+        flag_o, U_o, _, _ = orc.terminate(Y, P["Qd"], P["Fd"], P["Md"], P["Qp"], Qinv, Fp, Mp, Gp, Kp, N, M)
+        flag_r, U_r = ref.terminate(Y, P)
+        assert flag_o == flag_r
+        assert_bitwise(U_o, U_r, "U")
