@@ -84,6 +84,14 @@ def lib() -> C.CDLL:
         if not LIB_PATH.exists():
             raise PQPError(PQP_ERR_NO_DEVICE, f"{LIB_PATH} is missing: run `make -C pqp-for-mpc_amd` "
                                               "(or __graft_entry__.build())")
+        # One HIP runtime per process: PyTorch-ROCm ships its own
+        # libamdhip64.so.7.  Loading torch first makes libpqp's DT_NEEDED
+        # libamdhip64.so.7 bind to that copy, so torch streams/pointers and
+        # libpqp share a runtime (and a second runtime never starts).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
