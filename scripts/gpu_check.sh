@@ -9,5 +9,5 @@ echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/smoke.log
-timeout -k 10 300 python bench.py ${BENCH_ARGS:-"--steps 20 --warmup 3 --cpu-seconds 10"} > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 20 --warmup 3 --cpu-seconds 10} > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
 cat gpurun_out/bench.json

@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-r01}
-ARGS=${2:-"--steps 20 --warmup 3 --no-cpu-baseline --no-bundled"}
+ARGS=${2:---steps 20 --warmup 3 --no-cpu-baseline --no-bundled}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py $ARGS > $OUT/kt_bench.json 2> $OUT/kt.err || exit $?
