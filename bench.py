@@ -136,11 +136,9 @@ def main():
 
     N, B, K, W, C = args.n, args.batch, args.steps, args.warmup, max(1, args.chunk)
     # "scatter inputs": rank 0 hands each rank its (seed, first problem, count)
-    cfg = torch.tensor([args.seed, rank * B, B], dtype=torch.int64, device=dev)
-    if dist is not None:
-        parts = [torch.tensor([args.seed, r * B, B], dtype=torch.int64, device=dev) for r in range(world)]
-        dist.scatter(cfg, parts if rank == 0 else None, src=0)
-    seed, inst0, B = (int(v) for v in cfg.tolist())
+    from pqp_amd.shard import gather_rows, scatter_plan
+
+    seed, inst0, B = scatter_plan(dist, rank, world, B, args.seed, dev)
 
     batch = pqp_amd.Batch(B, N, device=dev)
     batch.generate(seed, inst0=inst0, M=N // 2)
@@ -183,10 +181,9 @@ def main():
     gather_ms = None
     if dist is not None:
         y = batch.Y[:, :N].contiguous()
-        outs = [torch.empty_like(y) for _ in range(world)] if rank == 0 else None
         torch.cuda.synchronize(dev)
         g0 = time.perf_counter()
-        dist.gather(y, outs, dst=0)
+        gather_rows(dist, rank, world, y)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
     Yh = batch.Y[:, :N]

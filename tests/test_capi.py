@@ -116,3 +116,21 @@ def test_python_buffers_are_validated():
 
     with pytest.raises(TypeError):
         pqp_amd.computeTheta(np.zeros(4, np.float64), np.zeros(4, np.float32), 2)
+
+
+def test_reference_main_driver_links_libpqp_first():
+    """oracle/_ref/ref_main_on_libpqp resolves the reference main()'s calls to
+    libpqp: libpqp.so must precede libpqp_ref.so in its DT_NEEDED order."""
+    exe = ROOT / "oracle" / "_ref" / "ref_main_on_libpqp"
+    if not exe.exists():
+        pytest.skip("needs /root/reference at build time")
+    dyn = subprocess.run(["readelf", "-d", str(exe)], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"Shared library: \[([^\]]+)\]", dyn)
+    assert needed.index("libpqp.so") < needed.index("libpqp_ref.so")
+    ref_syms = subprocess.run(["nm", "-D", "--defined-only", str(ROOT / "oracle/_ref/libpqp_ref.so")],
+                              capture_output=True, text=True, check=True).stdout
+    ours = set(declared_functions())
+    called_by_main = {"input", "Gauss_Jordan", "computeFp", "computeMp", "convertToDual", "solveQuadraticDual",
+                      "computeUfromY", "computeCost"}
+    assert called_by_main <= ours
+    assert all(f" {n}\n" in ref_syms for n in called_by_main)

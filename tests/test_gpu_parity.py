@@ -273,3 +273,23 @@ def test_batch_argument_validation(gpu_lib):
     assert "ldq" in gpu_lib.last_error()
     assert L.pqp_batch_update(1, 4, p, 4, 16, p, p, 4, p, p, s) == gpu_lib.PQP_ERR_ARG  # Y aliases Ynext
     assert L.pqp_batch_iterate(1, 4, p, 4, 16, p, p, 4, None, p, -1, s) == gpu_lib.PQP_ERR_ARG
+
+
+def test_reference_main_linked_against_libpqp(tmp_path):
+    """PQP_CPU.c's own main() (oracle/_ref, built from /root/reference) with
+    libpqp.so first in the symbol search order: the reference driver calls the
+    GPU drop-ins and must print exactly what the reference prints."""
+    import shutil
+    import subprocess
+
+    from conftest import ROOT
+
+    exe = ROOT / "oracle" / "_ref" / "ref_main_on_libpqp"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_main_on_libpqp not built (needs /root/reference at build time)")
+    (tmp_path / "example").mkdir()
+    for f in EXAMPLE_DIR.glob("*.txt"):
+        shutil.copy(f, tmp_path / "example" / f.name)
+    out = subprocess.run([str(exe)], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout == (GOLDEN / "bundled_stdout.txt").read_text()
