@@ -1,0 +1,26 @@
+/*
+ * include/pqp_tuning.h -- tuning/diagnostic entry points of libpqp.  Not part
+ * of the drop-in surface; used by scripts/ab_batch.py to A/B kernel variants
+ * interleaved in one process and to measure the practical HBM read ceiling of
+ * the hot kernel's access pattern on the device at hand.
+ */
+#ifndef PQP_TUNING_H
+#define PQP_TUNING_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Select the k_batch_iterate instantiation used by pqp_batch_iterate:
+ * 0 = shipped default; 1..5 = (unroll, non-temporal) variants, see
+ * pqp_kernels.hip launch_batch_iterate.  Returns the previous value. */
+int pqp_tune_set_variant(int variant);
+
+/* Stream B problems' QdT with the hot kernel's exact access pattern and no
+ * solver arithmetic (one float written per thread to d_out[B*256]). */
+int pqp_tune_stream_read(int B, int N, const float *d_QdT, int ldq, long long qstride, float *d_out, int nontemporal,
+                         void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

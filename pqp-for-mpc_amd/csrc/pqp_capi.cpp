@@ -790,3 +790,22 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// tuning / diagnostics (include/pqp_tuning.h)
+// ---------------------------------------------------------------------------
+#include "../../include/pqp_tuning.h"
+
+extern "C" int pqp_tune_set_variant(int variant) {
+    const int old = pqp::get_variant();
+    pqp::set_variant(variant);
+    return old;
+}
+
+extern "C" int pqp_tune_stream_read(int B, int N, const float* d_QdT, int ldq, long long qstride, float* d_out,
+                                    int nontemporal, void* stream) {
+    if (B <= 0 || N <= 0 || !d_QdT || !d_out || ldq < N || (ldq & 3) || qstride < (long long)N * ldq)
+        return pqp::set_error(PQP_ERR_ARG, "pqp_tune_stream_read: bad arguments");
+    PQP_HIP(pqp::launch_stream_read(B, d_QdT, qstride, ldq, N, d_out, nontemporal, static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}

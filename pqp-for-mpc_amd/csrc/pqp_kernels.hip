@@ -29,6 +29,17 @@ namespace pqp {
 // Row-update building blocks
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// streamed-once Qd: optionally non-temporal (global_load_dwordx4 ... nt)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <bool NTL>
+__device__ __forceinline__ float4 ldq4(const float* p) {
+    if constexpr (NTL) {
+        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const float4*>(p);
+    }
+}
 
 struct Acc4 {
     float p[4];  // den accumulators (Qd+ side)
@@ -61,32 +72,33 @@ __device__ __forceinline__ void literal4(Acc4& a, float4 q, float y, int k, int 
 
 // Stream k in [ka, kb) with the lean form.  ka % 4 == 0.  `col` points at
 // QdT + row (this lane's 4 rows), y is the iterate (LDS).
+template <int U, bool NTL>
 __device__ __forceinline__ void lean_segment(Acc4& a, const float* __restrict__ col, int ldq, int ka, int kb,
                                              const float* __restrict__ y) {
+    static_assert(U % 4 == 0, "unroll must be a multiple of 4 (one float4 of y per 4 k)");
     int k = ka;
     const float* src = col + (size_t)k * ldq;
-    for (; k + 8 <= kb; k += 8) {
-        float4 q[8];
+    for (; k + U <= kb; k += U) {
+        float4 q[U];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) q[j] = ld4(src + (size_t)j * ldq);
-        src += (size_t)8 * ldq;
-        const float4 y0 = *reinterpret_cast<const float4*>(y + k);
-        const float4 y1 = *reinterpret_cast<const float4*>(y + k + 4);
-        lean4(a, q[0], y0.x);
-        lean4(a, q[1], y0.y);
-        lean4(a, q[2], y0.z);
-        lean4(a, q[3], y0.w);
-        lean4(a, q[4], y1.x);
-        lean4(a, q[5], y1.y);
-        lean4(a, q[6], y1.z);
-        lean4(a, q[7], y1.w);
+        for (int j = 0; j < U; ++j) q[j] = ldq4<NTL>(src + (size_t)j * ldq);
+        src += (size_t)U * ldq;
+#pragma unroll
+        for (int j = 0; j < U; j += 4) {
+            const float4 yv = *reinterpret_cast<const float4*>(y + k + j);
+            lean4(a, q[j + 0], yv.x);
+            lean4(a, q[j + 1], yv.y);
+            lean4(a, q[j + 2], yv.z);
+            lean4(a, q[j + 3], yv.w);
+        }
     }
     for (; k < kb; ++k) {
-        lean4(a, ld4(src), y[k]);
+        lean4(a, ldq4<NTL>(src), y[k]);
         src += ldq;
     }
 }
 
+template <bool NTL>
 __device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict__ col, int ldq, int ka, int kb,
                                                 const float* __restrict__ y, int row, const float th[4]) {
     int k = ka;
@@ -94,7 +106,7 @@ __device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict
     for (; k + 4 <= kb; k += 4) {
         float4 q[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = ld4(src + (size_t)j * ldq);
+        for (int j = 0; j < 4; ++j) q[j] = ldq4<NTL>(src + (size_t)j * ldq);
         src += (size_t)4 * ldq;
         const float4 y0 = *reinterpret_cast<const float4*>(y + k);
         literal4(a, q[0], y0.x, k + 0, row, th);
@@ -103,7 +115,7 @@ __device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict
         literal4(a, q[3], y0.w, k + 3, row, th);
     }
     for (; k < kb; ++k) {
-        literal4(a, ld4(src), y[k], k, row, th);
+        literal4(a, ldq4<NTL>(src), y[k], k, row, th);
         src += ldq;
     }
 }
@@ -112,7 +124,7 @@ __device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict
 // out[i] = num/den * y[i] for the rows < N.  w0 = first row of this lane's
 // wave (wave-uniform): the diagonal of the wave's 256 rows lies in
 // k in [w0, w0+256) and only that window needs the literal form.
-template <typename OutPtr>
+template <int U, bool NTL, typename OutPtr>
 __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ldq, int N, int row, int w0,
                                              const float* __restrict__ th_g, const float* __restrict__ fd_g,
                                              const float* __restrict__ y, OutPtr out) {
@@ -125,9 +137,9 @@ __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ld
     const float* col = Q + row;
     const int wa = w0 < N ? w0 : N;
     const int wb = (w0 + 256) < N ? (w0 + 256) : N;
-    lean_segment(a, col, ldq, 0, wa, y);
-    literal_segment(a, col, ldq, wa, wb, y, row, th);
-    lean_segment(a, col, ldq, wb, N, y);
+    lean_segment<U, NTL>(a, col, ldq, 0, wa, y);
+    literal_segment<NTL>(a, col, ldq, wa, wb, y, row, th);
+    lean_segment<U, NTL>(a, col, ldq, wb, N, y);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = row + r;
@@ -145,7 +157,7 @@ __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ld
 // launch.  One workgroup owns one problem; its iterate ping-pongs between two
 // LDS buffers, so the only HBM traffic per iteration is Qd (streamed once).
 // ---------------------------------------------------------------------------
-template <int NT>
+template <int NT, int U = 8, bool NTL = false>
 __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ QdT, long long qstride, int ldq,
                                                       int N, const float* __restrict__ theta,
                                                       const float* __restrict__ Fd, int ldv,
@@ -171,7 +183,7 @@ __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ 
         for (int r0 = 0; r0 < N; r0 += 4 * NT) {
             const int row = r0 + 4 * tid;
             const int w0 = r0 + 256 * wave;
-            if (row < N) update_rows4(Q, ldq, N, row, w0, th, fd, cur, nxt);
+            if (row < N) update_rows4<U, NTL>(Q, ldq, N, row, w0, th, fd, cur, nxt);
         }
         __syncthreads();
     }
@@ -183,7 +195,7 @@ __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ 
 // k_batch_update: one iteration; grid = (row blocks, problems).  The iterate
 // is staged into LDS once per workgroup; Y_next goes straight to HBM.
 // ---------------------------------------------------------------------------
-template <int NT>
+template <int NT, int U = 8, bool NTL = false>
 __global__ void __launch_bounds__(NT) k_batch_update(const float* __restrict__ QdT, long long qstride, int ldq,
                                                      int N, const float* __restrict__ theta,
                                                      const float* __restrict__ Fd, int ldv,
@@ -198,8 +210,45 @@ __global__ void __launch_bounds__(NT) k_batch_update(const float* __restrict__ Q
     const int row = r0 + 4 * tid;
     const int w0 = r0 + 256 * (tid >> 6);
     if (row < N)
-        update_rows4(QdT + (size_t)b * (size_t)qstride, ldq, N, row, w0, theta + (size_t)b * ldv,
+        update_rows4<U, NTL>(QdT + (size_t)b * (size_t)qstride, ldq, N, row, w0, theta + (size_t)b * ldv,
                      Fd + (size_t)b * ldv, lds, Yout + (size_t)b * ldv);
+}
+
+// ---------------------------------------------------------------------------
+// k_stream_read: tuning reference only (include/pqp_tuning.h).  Streams QdT
+// with exactly the hot kernel's access pattern and no solver arithmetic, to
+// measure the practical read ceiling of that pattern on this device.
+// ---------------------------------------------------------------------------
+template <int U, bool NTL>
+__global__ void __launch_bounds__(256) k_stream_read(const float* __restrict__ QdT, long long qstride, int ldq, int N,
+                                                     float* __restrict__ out) {
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const float* Q = QdT + (size_t)b * (size_t)qstride;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r0 = 0; r0 < N; r0 += 1024) {
+        const int row = r0 + 4 * tid;
+        if (row >= N) continue;
+        const float* src = Q + row;
+        int k = 0;
+        for (; k + U <= N; k += U) {
+            float4 q[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) q[j] = ldq4<NTL>(src + (size_t)j * ldq);
+            src += (size_t)U * ldq;
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                acc.x += q[j].x;
+                acc.y += q[j].y;
+                acc.z += q[j].z;
+                acc.w += q[j].w;
+            }
+        }
+        for (; k < N; ++k, src += ldq) {
+            const float4 q = ldq4<NTL>(src);
+            acc.x += q.x;
+        }
+    }
+    out[(size_t)b * 256 + tid] = acc.x + acc.y + acc.z + acc.w;
 }
 
 // ---------------------------------------------------------------------------
@@ -625,15 +674,41 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
 // ---------------------------------------------------------------------------
 static inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
-hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
-                                  const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
+static int g_variant = 0;  // tuning knob (include/pqp_tuning.h); 0 = shipped default
+void set_variant(int v) { g_variant = v; }
+int get_variant() { return g_variant; }
+
+template <int U, bool NTL>
+static void launch_iterate_t(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
+                             const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
     const size_t lds = (size_t)2 * ldq * sizeof(float);
     if (N <= 256)
-        hipLaunchKernelGGL(k_batch_iterate<64>, dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv, Y0,
-                           Y, updates);
+        hipLaunchKernelGGL((k_batch_iterate<64, U, NTL>), dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd,
+                           ldv, Y0, Y, updates);
     else
-        hipLaunchKernelGGL(k_batch_iterate<256>, dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv,
-                           Y0, Y, updates);
+        hipLaunchKernelGGL((k_batch_iterate<256, U, NTL>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
+                           Fd, ldv, Y0, Y, updates);
+}
+
+hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
+                                const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
+    switch (g_variant) {
+        case 1: launch_iterate_t<8, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 2: launch_iterate_t<4, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 3: launch_iterate_t<16, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 4: launch_iterate_t<4, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 5: launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        default: launch_iterate_t<8, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,
+                              hipStream_t s) {
+    if (nt)
+        hipLaunchKernelGGL((k_stream_read<8, true>), dim3(B), dim3(256), 0, s, QdT, qstride, ldq, N, out);
+    else
+        hipLaunchKernelGGL((k_stream_read<8, false>), dim3(B), dim3(256), 0, s, QdT, qstride, ldq, N, out);
     return hipGetLastError();
 }
 

@@ -65,6 +65,9 @@ SIGNATURES = {
     "pqp_batch_update": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp, _vp]),
     "pqp_batch_iterate": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp,
                                     C.c_int, _vp]),
+    # include/pqp_tuning.h
+    "pqp_tune_set_variant": (C.c_int, [C.c_int]),
+    "pqp_tune_stream_read": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, C.c_int, _vp]),
 }
 
 
