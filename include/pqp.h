@@ -124,6 +124,17 @@ int pqp_solve_dual(const float *Qd, const float *Fd, const float *Md, const floa
                    long long num_iter, long long max_updates, float *Y, float *U, long long *h_out,
                    float *Jp_out, float *Jd_out);
 
+/* A dual problem resident in HBM: upload and prepare once, then solve any
+ * number of times (each solve restarts from Y = 1000).  Same semantics and
+ * outputs as pqp_solve_dual, which is create + solve + destroy. */
+typedef struct pqp_problem pqp_problem;
+int pqp_problem_create(const float *Qd, const float *Fd, const float *Md, const float *Qp, const float *Qp_inv,
+                       const float *Fp, const float *Mp, const float *Gp, const float *Kp, int N, int M,
+                       pqp_problem **out);
+int pqp_problem_solve(pqp_problem *p, int mode, long long num_iter, long long max_updates, float *Y, float *U,
+                      long long *h_out, float *Jp_out, float *Jd_out);
+int pqp_problem_destroy(pqp_problem *p);
+
 /* One update on host buffers from Qd/theta-diag/Fd (the fused form used by
  * the solver: Qd+-, Theta and Fd+- derived on the fly). */
 int pqp_update_host(const float *Qd, const float *theta_diag, const float *Fd, const float *Y, float *Y_next,

@@ -11,7 +11,8 @@ extern "C" {
 #endif
 
 /* Select the k_batch_iterate instantiation used by pqp_batch_iterate:
- * 0 = shipped default; 1..5 = (unroll, non-temporal) variants, see
+ * 0 = shipped default (unroll 16, non-temporal Qd loads); 1..5 = other
+ * (unroll, non-temporal) variants, see
  * pqp_kernels.hip launch_batch_iterate.  Returns the previous value. */
 int pqp_tune_set_variant(int variant);
 

@@ -216,64 +216,117 @@ int dev_gauss_jordan(float* res, const float* A, int n, hipStream_t s) {
     return PQP_OK;
 }
 
-// Persistent single-problem solve on device data (see k_solve_single).
+// ---- single-problem solve ---------------------------------------------------
 struct SolveOut {
     long long h = 0;
     float Jp = NAN, Jd = NAN;
     int have_costs = 0, last_stop = 0, status = 0;
 };
 
-int dev_solve(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qinv,
-              const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
-              long long num_iter, long long max_updates, float* Y, float* U, bool resume, SolveOut& out,
-              hipStream_t s) {
-    const int ldq = round4(N), ldm = round4(M > 0 ? M : 1);
-    const size_t lds = solve_single_lds_bytes(ldq, ldm);
-    if (lds > 150 * 1024)
-        return set_error(PQP_ERR_ARG, "single-problem solve: N=%d, M=%d needs %zu bytes of LDS (max 150 KiB)", N, M,
-                         lds);
-    DevBuf QdT, theta, state, Udummy;
-    PQP_TRY(QdT.floats((size_t)N * ldq));
-    PQP_TRY(theta.floats(N));
-    PQP_TRY(state.alloc(sizeof(SolveState)));
-    PQP_HIP(launch_pack_colmajor(1, Qd, N, (long long)N * N, QdT.f(), ldq, (long long)N * ldq, s));
-    PQP_HIP(launch_theta(1, QdT.f(), ldq, (long long)N * ldq, N, theta.f(), N, s));
-    if (!U) {
-        PQP_TRY(Udummy.floats(M > 0 ? M : 1));
-        U = Udummy.f();
+}  // namespace
+}  // namespace pqp
+
+// A dual problem resident in HBM, prepared once and solved any number of times
+// (include/pqp.h: pqp_problem_create / _solve / _destroy).
+struct pqp_problem {
+    int N = 0, M = 0;
+    bool small = false;  // fits k_solve_small (everything staged in LDS)
+    pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
+    pqp::DevBuf QdT, theta;                          // large path only
+    pqp::DevBuf Y, U, state;
+    pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
+    ~pqp_problem() {
+        if (hst) (void)hipHostFree(hst);
     }
-    SolveState st{};
+};
+
+namespace pqp {
+namespace {
+
+constexpr size_t kLdsBudget = 150 * 1024;
+
+// Allocate the per-problem work buffers and, for the large path, the
+// column-major copy and theta.  The nine input buffers must already hold the
+// problem.
+int problem_finish(pqp_problem& P, hipStream_t s) {
+    const int N = P.N, M = P.M;
+    P.small = solve_small_lds_bytes(N, M) <= kLdsBudget;
+    PQP_TRY(P.Y.floats(N));
+    PQP_TRY(P.U.floats(M));
+    PQP_TRY(P.state.alloc(sizeof(SolveState)));
+    PQP_HIP(hipMemsetAsync(P.U.p, 0, sizeof(float) * M, s));
+    if (!P.hst) PQP_HIP(hipHostMalloc((void**)&P.hst, sizeof(SolveState), hipHostMallocDefault));
+    if (!P.small) {
+        const int ldq = round4(N);
+        if (solve_single_lds_bytes(ldq, round4(M)) > kLdsBudget)
+            return set_error(PQP_ERR_ARG, "single-problem solve: N=%d, M=%d exceeds the LDS budget", N, M);
+        PQP_TRY(P.QdT.floats((size_t)N * ldq));
+        PQP_TRY(P.theta.floats(N));
+        PQP_HIP(launch_pack_colmajor(1, P.Qd.f(), N, (long long)N * N, P.QdT.f(), ldq, (long long)N * ldq, s));
+        PQP_HIP(launch_theta(1, P.QdT.f(), ldq, (long long)N * ldq, N, P.theta.f(), N, s));
+    }
+    return PQP_OK;
+}
+
+int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float* md, const float* qp,
+                   const float* qinv, const float* fp, const float* mp, const float* gp, const float* kp, int N, int M,
+                   hipStream_t s) {
+    P.N = N;
+    P.M = M;
+    PQP_TRY(upload(P.Qd, qd, (size_t)N * N, s));
+    PQP_TRY(upload(P.Fd, fd, N, s));
+    PQP_TRY(upload(P.Md, md, 1, s));
+    PQP_TRY(upload(P.Qp, qp, (size_t)M * M, s));
+    PQP_TRY(upload(P.Qinv, qinv, (size_t)M * M, s));
+    PQP_TRY(upload(P.Fp, fp, M, s));
+    PQP_TRY(upload(P.Mp, mp, 1, s));
+    PQP_TRY(upload(P.Gp, gp, (size_t)N * M, s));
+    PQP_TRY(upload(P.Kp, kp, N, s));
+    return problem_finish(P, s);
+}
+
+// Run the persistent solve kernel until it reports Done/Capped.  Each launch
+// is bounded (chunk updates) so no launch runs unbounded.  `resume` = start
+// from P.Y instead of Y = 1000 (used by the terminate() drop-in, mode 2).
+int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_updates, bool resume, SolveOut& out,
+                hipStream_t s) {
+    const int N = P.N, M = P.M;
+    SolveState& st = *P.hst;
+    st = SolveState{};
     st.h = 1;
     st.resume = resume ? 1 : 0;
-    PQP_HIP(hipMemcpyAsync(state.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    PQP_HIP(hipMemcpyAsync(P.state.p, &st, sizeof st, hipMemcpyHostToDevice, s));
     SolveArgs a{};
-    a.QdT = QdT.f();
-    a.Qd = Qd;
-    a.theta = theta.f();
-    a.Fd = Fd;
-    a.Md = Md;
-    a.Qp = Qp;
-    a.Qinv = Qinv;
-    a.Fp = Fp;
-    a.Mp = Mp;
-    a.Gp = Gp;
-    a.Kp = Kp;
-    a.Y = Y;
-    a.U = U;
+    a.QdT = P.QdT.f();
+    a.Qd = P.Qd.f();
+    a.theta = P.theta.f();
+    a.Fd = P.Fd.f();
+    a.Md = P.Md.f();
+    a.Qp = P.Qp.f();
+    a.Qinv = P.Qinv.f();
+    a.Fp = P.Fp.f();
+    a.Mp = P.Mp.f();
+    a.Gp = P.Gp.f();
+    a.Kp = P.Kp.f();
+    a.Y = P.Y.f();
+    a.U = P.U.f();
     a.N = N;
     a.M = M;
-    a.ldq = ldq;
-    a.ldm = ldm;
+    a.ldq = round4(N);
+    a.ldm = round4(M);
     a.mode = mode;
     a.num_iter = num_iter;
     a.max_updates = max_updates;
-    // bound each launch to ~2^26 multiply-adds of work so no launch runs long
-    const double per_update = (double)N * N * 2.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
-    long long chunk = (long long)((double)(1 << 26) / per_update);
+    const double per_update = (double)N * N * 3.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
+    const long long chunk = (long long)((double)(1 << 26) / per_update);
     a.chunk = chunk < 1 ? 1 : chunk;
+    SolveState* dst = static_cast<SolveState*>(P.state.p);
     for (;;) {
-        PQP_HIP(launch_solve_single(a, static_cast<SolveState*>(state.p), s));
-        PQP_HIP(hipMemcpyAsync(&st, state.p, sizeof st, hipMemcpyDeviceToHost, s));
+        if (P.small)
+            PQP_HIP(launch_solve_small(a, dst, s));
+        else
+            PQP_HIP(launch_solve_single(a, dst, s));
+        PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
         if (st.status != kStatusContinue) break;
     }
@@ -287,24 +340,6 @@ int dev_solve(const float* Qd, const float* Fd, const float* Md, const float* Qp
     }
     return PQP_OK;
 }
-
-// Uploaded dual problem + primal data for the host-pointer solve paths.
-struct HostProblem {
-    DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;
-    int upload_all(const float* qd, const float* fd, const float* md, const float* qp, const float* qinv,
-                   const float* fp, const float* mp, const float* gp, const float* kp, int N, int M, hipStream_t s) {
-        PQP_TRY(upload(Qd, qd, (size_t)N * N, s));
-        PQP_TRY(upload(Fd, fd, N, s));
-        PQP_TRY(upload(Md, md, 1, s));
-        PQP_TRY(upload(Qp, qp, (size_t)M * M, s));
-        PQP_TRY(upload(Qinv, qinv, (size_t)M * M, s));
-        PQP_TRY(upload(Fp, fp, M, s));
-        PQP_TRY(upload(Mp, mp, 1, s));
-        PQP_TRY(upload(Gp, gp, (size_t)N * M, s));
-        PQP_TRY(upload(Kp, kp, N, s));
-        return PQP_OK;
-    }
-};
 
 [[noreturn]] void die(const char* fn) {
     std::fprintf(stderr, "libpqp: %s failed: %s\n", fn, t_err.c_str());
@@ -329,30 +364,41 @@ int pqp_version(void) { return 100; }
 // ---------------------------------------------------------------------------
 // 2a. status-returning host API
 // ---------------------------------------------------------------------------
-int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
-                   const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
-                   long long num_iter, long long max_updates, float* Y, float* U, long long* h_out,
-                   float* Jp_out, float* Jd_out) {
+int pqp_problem_create(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
+                       const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M,
+                       pqp_problem** out) {
+    if (!out) return set_error(PQP_ERR_ARG, "pqp_problem_create: null handle pointer");
+    *out = nullptr;
     PQP_TRY(check_dims(N, M));
-    if (!Qd || !Fd || !Md || !Qp || !Qp_inv || !Fp || !Mp || !Gp || !Kp || !Y)
-        return set_error(PQP_ERR_ARG, "pqp_solve_dual: null input");
-    if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
-        return set_error(PQP_ERR_ARG, "pqp_solve_dual: unknown mode %d", mode);
+    if (!Qd || !Fd || !Md || !Qp || !Qp_inv || !Fp || !Mp || !Gp || !Kp)
+        return set_error(PQP_ERR_ARG, "pqp_problem_create: null input");
     std::lock_guard<std::mutex> lk(g_mu);
     PQP_TRY(ensure_device());
     hipStream_t s = lib_stream();
-    HostProblem P;
-    PQP_TRY(P.upload_all(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
-    DevBuf dY, dU;
-    PQP_TRY(dY.floats(N));
-    PQP_TRY(dU.floats(M));
-    PQP_HIP(hipMemsetAsync(dU.p, 0, sizeof(float) * M, s));
+    pqp_problem* P = new pqp_problem();
+    int rc = problem_upload(*P, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s);
+    if (rc == PQP_OK && hipStreamSynchronize(s) != hipSuccess) rc = set_error(PQP_ERR_HIP, "problem setup failed");
+    if (rc != PQP_OK) {
+        delete P;
+        return rc;
+    }
+    *out = P;
+    return PQP_OK;
+}
+
+int pqp_problem_solve(pqp_problem* P, int mode, long long num_iter, long long max_updates, float* Y, float* U,
+                      long long* h_out, float* Jp_out, float* Jd_out) {
+    if (!P || !Y) return set_error(PQP_ERR_ARG, "pqp_problem_solve: null handle or Y");
+    if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
+        return set_error(PQP_ERR_ARG, "pqp_problem_solve: unknown mode %d", mode);
+    std::lock_guard<std::mutex> lk(g_mu);
+    PQP_TRY(ensure_device());
+    hipStream_t s = lib_stream();
     SolveOut o;
-    PQP_TRY(dev_solve(P.Qd.f(), P.Fd.f(), P.Md.f(), P.Qp.f(), P.Qinv.f(), P.Fp.f(), P.Mp.f(), P.Gp.f(), P.Kp.f(), N,
-                      M, mode == PQP_MODE_CONVERGE ? kModeConverge : kModeFixed, num_iter, max_updates, dY.f(),
-                      dU.f(), false, o, s));
-    PQP_TRY(download(Y, dY.p, N, s));
-    if (U && mode == PQP_MODE_CONVERGE) PQP_TRY(download(U, dU.p, M, s));
+    PQP_TRY(problem_run(*P, mode == PQP_MODE_CONVERGE ? kModeConverge : kModeFixed, num_iter, max_updates, false, o,
+                        s));
+    PQP_TRY(download(Y, P->Y.p, P->N, s));
+    if (U && mode == PQP_MODE_CONVERGE) PQP_TRY(download(U, P->U.p, P->M, s));
     PQP_HIP(hipStreamSynchronize(s));
     if (h_out) *h_out = o.h;
     if (Jp_out) *Jp_out = o.Jp;
@@ -360,6 +406,28 @@ int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const floa
     if (o.status == kStatusCapped)
         return set_error(PQP_ERR_NOT_CONVERGED, "no convergence within %lld updates (h=%lld)", max_updates, o.h);
     return PQP_OK;
+}
+
+int pqp_problem_destroy(pqp_problem* P) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    delete P;
+    return PQP_OK;
+}
+
+int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
+                   const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
+                   long long num_iter, long long max_updates, float* Y, float* U, long long* h_out,
+                   float* Jp_out, float* Jd_out) {
+    if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
+        return set_error(PQP_ERR_ARG, "pqp_solve_dual: unknown mode %d", mode);
+    if (!Y) return set_error(PQP_ERR_ARG, "pqp_solve_dual: null Y");
+    pqp_problem* P = nullptr;
+    PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &P));
+    const int rc = pqp_problem_solve(P, mode, num_iter, max_updates, Y, U, h_out, Jp_out, Jd_out);
+    const std::string err = t_err;
+    pqp_problem_destroy(P);
+    t_err = err;
+    return rc;
 }
 
 int pqp_update_host(const float* Qd, const float* theta_diag, const float* Fd, const float* Y, float* Y_next,
@@ -432,32 +500,39 @@ int pqp_run_example(const char* dir, void* out_file) {
     PQP_TRY(upload(Kp, e.Kp.data(), e.Kp.size(), s));
     PQP_TRY(upload(x, e.x.data(), e.x.size(), s));
     PQP_TRY(upload(D, e.D.data(), e.D.size(), s));
-    DevBuf Qp, Fp, Mp, Qd, Fd, Md, Y, U, Jp, Jd;
-    PQP_TRY(Qp.floats((size_t)M * M));
-    PQP_TRY(Fp.floats(M));
-    PQP_TRY(Mp.floats(1));
-    PQP_TRY(Qd.floats((size_t)N * N));
-    PQP_TRY(Fd.floats(N));
-    PQP_TRY(Md.floats(1));
-    PQP_TRY(Y.floats(N));
-    PQP_TRY(U.floats(M));
+    pqp_problem P;
+    P.N = N;
+    P.M = M;
+    DevBuf Jp, Jd;
+    PQP_TRY(P.Qp.floats((size_t)M * M));
+    PQP_TRY(P.Fp.floats(M));
+    PQP_TRY(P.Mp.floats(1));
+    PQP_TRY(P.Qd.floats((size_t)N * N));
+    PQP_TRY(P.Fd.floats(N));
+    PQP_TRY(P.Md.floats(1));
     PQP_TRY(Jp.floats(1));
     PQP_TRY(Jd.floats(1));
-    PQP_TRY(dev_gauss_jordan(Qp.f(), Qinv.f(), M, s));                                                   // :989
-    PQP_TRY(dev_compute_fp(Fp.f(), Fp1.f(), Fp2.f(), Fp3.f(), D.f(), x.f(), m, nd, ns, s));             // :991
-    PQP_TRY(dev_compute_mp(Mp.f(), Mp1.f(), Mp2.f(), Mp3.f(), Mp4.f(), Mp5.f(), Mp6.f(), D.f(), x.f(), nd, ns,
+    std::swap(P.Qinv.p, Qinv.p);
+    std::swap(P.Gp.p, Gp.p);
+    std::swap(P.Kp.p, Kp.p);
+    PQP_TRY(dev_gauss_jordan(P.Qp.f(), P.Qinv.f(), M, s));                                                // :989
+    PQP_TRY(dev_compute_fp(P.Fp.f(), Fp1.f(), Fp2.f(), Fp3.f(), D.f(), x.f(), m, nd, ns, s));            // :991
+    PQP_TRY(dev_compute_mp(P.Mp.f(), Mp1.f(), Mp2.f(), Mp3.f(), Mp4.f(), Mp5.f(), Mp6.f(), D.f(), x.f(), nd, ns,
                            s));                                                                         // :992
-    PQP_TRY(dev_convert_to_dual(Qd.f(), Fd.f(), Md.f(), Qinv.f(), Gp.f(), Kp.f(), Fp.f(), Mp.f(), N, M, s));  // :994
+    PQP_TRY(dev_convert_to_dual(P.Qd.f(), P.Fd.f(), P.Md.f(), P.Qinv.f(), P.Gp.f(), P.Kp.f(), P.Fp.f(), P.Mp.f(), N,
+                                M, s));                                                                 // :994
+    PQP_TRY(problem_finish(P, s));
     SolveOut o;
-    PQP_TRY(dev_solve(Qd.f(), Fd.f(), Md.f(), Qp.f(), Qinv.f(), Fp.f(), Mp.f(), Gp.f(), Kp.f(), N, M, kModeConverge,
-                      0, 0, Y.f(), U.f(), false, o, s));                                                // :996
+    PQP_TRY(problem_run(P, kModeConverge, 0, 0, false, o, s));                                          // :996
     std::fprintf(out, "Printing number of iterations = %ld\n", (long)o.h);                              // :741
-    PQP_TRY(dev_u_from_y(U.f(), Y.f(), Fp.f(), Gp.f(), Qinv.f(), N, M, s));                              // :999
-    PQP_TRY(dev_cost(Jp.f(), U.f(), Qp.f(), Fp.f(), Mp.f(), M, s));                                      // :1002
-    PQP_TRY(dev_cost(Jd.f(), Y.f(), Qd.f(), Fd.f(), Md.f(), N, s));                                      // :1003
+    float* U = P.U.f();
+    float* Y = P.Y.f();
+    PQP_TRY(dev_u_from_y(U, Y, P.Fp.f(), P.Gp.f(), P.Qinv.f(), N, M, s));                                // :999
+    PQP_TRY(dev_cost(Jp.f(), U, P.Qp.f(), P.Fp.f(), P.Mp.f(), M, s));                                    // :1002
+    PQP_TRY(dev_cost(Jd.f(), Y, P.Qd.f(), P.Fd.f(), P.Md.f(), N, s));                                    // :1003
     std::vector<float> hU(M);
     float jp = 0, jd = 0;
-    PQP_TRY(download(hU.data(), U.p, M, s));
+    PQP_TRY(download(hU.data(), U, M, s));
     PQP_TRY(download(&jp, Jp.p, 1, s));
     PQP_TRY(download(&jd, Jd.p, 1, s));
     PQP_HIP(hipStreamSynchronize(s));
@@ -580,15 +655,12 @@ int terminate(float* Y, float* Qd, float* Fd, float* Md, float* U, float* Qp, fl
         std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
-        HostProblem P;
-        PQP_TRY(P.upload_all(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
-        DevBuf dY, dU;
-        PQP_TRY(upload(dY, Y, N, s));
-        PQP_TRY(dU.floats(M));
+        pqp_problem P;
+        PQP_TRY(problem_upload(P, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
+        PQP_HIP(hipMemcpyAsync(P.Y.p, Y, sizeof(float) * N, hipMemcpyHostToDevice, s));
         SolveOut o;
-        PQP_TRY(dev_solve(P.Qd.f(), P.Fd.f(), P.Md.f(), P.Qp.f(), P.Qinv.f(), P.Fp.f(), P.Mp.f(), P.Gp.f(),
-                          P.Kp.f(), N, M, kModeTerminate, 0, 0, dY.f(), dU.f(), true, o, s));
-        PQP_TRY(download(U, dU.p, M, s));
+        PQP_TRY(problem_run(P, kModeTerminate, 0, 0, true, o, s));
+        PQP_TRY(download(U, P.U.p, M, s));
         PQP_HIP(hipStreamSynchronize(s));
         result = o.last_stop;
         return PQP_OK;

@@ -670,6 +670,262 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
 }
 
 // ---------------------------------------------------------------------------
+// k_solve_small: solveQuadraticDual for problems that fit in LDS (the bundled
+// MPC problem: N = 28, M = 7).  One 256-thread workgroup, everything staged in
+// LDS once, and the four waves take fixed ROLES so that the independent pieces
+// of an iteration run concurrently on the CU's four SIMDs:
+//   phase A  wave 0: updateY2 -- 2 lanes per row (even lane: num with the
+//                    stored Qdn_theta, odd lane: den with Qdp_theta), literal
+//                    reference arithmetic, then num/den*y
+//            wave 1: tM = Gp'Y + Fp                 (computeUfromY, :355-356)
+//            wave 2: tq = Y'Qd and s = tq.Y          (computeCost(Y,Qd..), :652-653)
+//            wave 3: lin = Fd'Y                     (:657)
+//   phase B  wave 1: U = -Qp_inv tM, checkFeas, Jp, the three gap tests
+// terminate(Y_h) and the update from Y_h both read only Y_h, so the update is
+// computed speculatively and dropped when terminate() stops -- the arithmetic
+// of every value is exactly the reference's.
+// ---------------------------------------------------------------------------
+struct SmallLayout {
+    int S, Qd, Gp, Qi, Qp, Kp, Fd, Fdp, Fdn, th, Fp, ya, yb, tq, tM, U, tu, nd, total;
+};
+__host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }
+__host__ __device__ inline SmallLayout small_layout(int N, int M) {
+    SmallLayout L;
+    int o = 0;
+    L.S = o;   o += align4(2 * N * N);
+    L.Qd = o;  o += align4(N * N);
+    L.Gp = o;  o += align4(N * M);
+    L.Qi = o;  o += align4(M * M);
+    L.Qp = o;  o += align4(M * M);
+    L.Kp = o;  o += align4(N);
+    L.Fd = o;  o += align4(N);
+    L.Fdp = o; o += align4(N);
+    L.Fdn = o; o += align4(N);
+    L.th = o;  o += align4(N);
+    L.Fp = o;  o += align4(M);
+    L.ya = o;  o += align4(N);
+    L.yb = o;  o += align4(N);
+    L.tq = o;  o += align4(N);
+    L.tM = o;  o += align4(M);
+    L.U = o;   o += align4(M);
+    L.tu = o;  o += align4(M);
+    L.nd = o;  o += align4(2 * N);
+    L.total = o + 8;  // + scalars
+    return L;
+}
+
+__global__ void __launch_bounds__(256) k_solve_small(SolveArgs A, SolveState* __restrict__ st) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int N = A.N, M = A.M;
+    const SmallLayout L = small_layout(N, M);
+    float* S = lds + L.S;      // [k][i][2]: (k*N + i)*2 + side; side 0 = Qdn_theta, 1 = Qdp_theta
+    float* Qd = lds + L.Qd;    // row-major
+    float* Gp = lds + L.Gp;    // row-major N x M
+    float* Qi = lds + L.Qi;    // Qp_inv row-major
+    float* Qp = lds + L.Qp;
+    float* Kp = lds + L.Kp;
+    float* Fd = lds + L.Fd;
+    float* Fdp = lds + L.Fdp;
+    float* Fdn = lds + L.Fdn;
+    float* th = lds + L.th;
+    float* Fp = lds + L.Fp;
+    float* tq = lds + L.tq;
+    float* tM = lds + L.tM;
+    float* Us = lds + L.U;
+    float* tu = lds + L.tu;
+    float* nd = lds + L.nd;
+    float* sc = lds + L.total - 8;  // [0] s_dual [1] lin_dual [2] stop [3] Jp [4] Jd
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool conv = (A.mode != kModeFixed);
+
+    // ---- stage the problem (once per launch) ----
+    for (int e = tid; e < N * N; e += 256) Qd[e] = A.Qd[e];
+    for (int i = tid; i < N; i += 256) {
+        Fd[i] = A.Fd[i];
+        Fdp[i] = max_ref(0.0f, A.Fd[i]);   // matrixPos(Fdp, Fd) :703
+        Fdn[i] = max_ref(0.0f, -A.Fd[i]);  // matrixNeg(Fdn, Fd) :704
+    }
+    if (conv) {
+        for (int e = tid; e < N * M; e += 256) Gp[e] = A.Gp[e];
+        for (int e = tid; e < M * M; e += 256) {
+            Qi[e] = A.Qinv[e];
+            Qp[e] = A.Qp[e];
+        }
+        for (int i = tid; i < N; i += 256) Kp[i] = A.Kp[i];
+        for (int j = tid; j < M; j += 256) Fp[j] = A.Fp[j];
+    }
+    __syncthreads();
+    // computeTheta (:503-519): theta_i = max(sum_k max(0,-Qd[i][k])*1, 5)
+    for (int i = tid; i < N; i += 256) {
+        float s = 0.0f;
+        for (int k = 0; k < N; ++k) s += max_ref(0.0f, -Qd[i * N + k]) * 1.0f;
+        th[i] = max_ref(s, 5.0f);
+    }
+    __syncthreads();
+    // computeQdn_theta / computeQdp_theta (:524-537), stored interleaved
+    for (int e = tid; e < N * N; e += 256) {
+        const int i = e / N, k = e % N;
+        const float q = Qd[e];
+        const float t = (i == k) ? th[i] : 0.0f;
+        S[(k * N + i) * 2 + 0] = max_ref(0.0f, -q) + 1.0f * t;
+        S[(k * N + i) * 2 + 1] = max_ref(0.0f, q) + 1.0f * t;
+    }
+    float* cur = lds + L.ya;
+    float* nxt = lds + L.yb;
+    for (int i = tid; i < N; i += 256) cur[i] = st->resume ? A.Y[i] : 1000.0f;  // initMat(Y,1000) :710
+    const float Md = conv ? A.Md[0] : 0.0f, Mp = conv ? A.Mp[0] : 0.0f;
+    __syncthreads();
+
+    long long h = st->h;
+    long long done_here = 0;
+    int status = kStatusContinue;
+    for (;;) {
+        const bool need_term = conv;
+        const bool may_update = (A.mode != kModeTerminate);
+        // ---------------- phase A ----------------
+        if (wave == 0) {
+            if (may_update) {
+                for (int p = lane; p < 2 * N; p += 64) {
+                    const int i = p >> 1;
+                    float acc = 0.0f;
+                    const float* col = S + 2 * i + (p & 1);
+                    for (int k = 0; k < N; ++k) acc += col[2 * k * N] * cur[k];  // :608-609
+                    nd[p] = acc;
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (int i = lane; i < N; i += 64) {
+                    const float num = nd[2 * i] + 1.0f * Fdn[i];     // :611
+                    const float den = nd[2 * i + 1] + 1.0f * Fdp[i]; // :612
+                    nxt[i] = num / den * cur[i];                     // :594
+                }
+            }
+        } else if (need_term && wave == 1) {
+            for (int j = lane; j < M; j += 64) {
+                float s = 0.0f;
+                for (int k = 0; k < N; ++k) s += Gp[k * M + j] * cur[k];
+                tM[j] = s + 1.0f * Fp[j];
+            }
+        } else if (need_term && wave == 2) {
+            for (int j = lane; j < N; j += 64) {
+                float s = 0.0f;
+                for (int k = 0; k < N; ++k) s += cur[k] * Qd[k * N + j];
+                tq[j] = s;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                float s = 0.0f;
+                for (int j = 0; j < N; ++j) s += tq[j] * cur[j];
+                sc[0] = s;
+            }
+        } else if (need_term && wave == 3) {
+            if (lane == 0) {
+                float s = 0.0f;
+                for (int k = 0; k < N; ++k) s += Fd[k] * cur[k];
+                sc[1] = s;
+            }
+        }
+        __syncthreads();
+        // ---------------- phase B: terminate() decision (wave 1) ----------------
+        if (need_term && wave == 1) {
+            for (int i = lane; i < M; i += 64) {  // U = -(Qp_inv tM)  :357-358
+                float s = 0.0f;
+                for (int j = 0; j < M; ++j) s += Qi[i * M + j] * tM[j];
+                Us[i] = -s;
+            }
+            __builtin_amdgcn_wave_barrier();
+            int bad = 0;  // checkFeas :632-641
+            for (int i = lane; i < N; i += 64) {
+                float s = 0.0f;
+                for (int j = 0; j < M; ++j) s += Gp[i * M + j] * Us[j];
+                const float kp = Kp[i];
+                if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+            }
+            const bool infeasible = __any(bad);
+            int stop = 0;
+            if (!infeasible) {
+                for (int j = lane; j < M; j += 64) {  // U'Qp
+                    float s = 0.0f;
+                    for (int k = 0; k < M; ++k) s += Us[k] * Qp[k * M + j];
+                    tu[j] = s;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) {
+                    float quad = 0.0f, lin = 0.0f;
+                    for (int j = 0; j < M; ++j) quad += tu[j] * Us[j];
+                    for (int k = 0; k < M; ++k) lin += Fp[k] * Us[k];
+                    float Jp = 0.0f;
+                    Jp = (float)((double)Jp + 0.5 * (double)quad);
+                    Jp += lin;
+                    Jp += Mp / 2;
+                    float Jd = 0.0f;
+                    Jd = (float)((double)Jd + 0.5 * (double)sc[0]);
+                    Jd += sc[1];
+                    Jd += Md / 2;
+                    stop = 1;
+                    if (Jp > -Jd) stop = 0;
+                    if ((double)(Jp + Jd) > kTol) stop = 0;
+                    if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                    sc[3] = Jp;
+                    sc[4] = Jd;
+                    st->Jp = Jp;
+                    st->Jd = Jd;
+                    st->have_costs = 1;
+                }
+            }
+            if (lane == 0) sc[2] = (float)stop;
+        }
+        __syncthreads();
+        if (need_term) {
+            const bool stop = sc[2] != 0.0f;
+            if (A.mode == kModeTerminate) {
+                if (tid == 0) st->last_stop = stop ? 1 : 0;
+                status = kStatusDone;
+                break;
+            }
+            if (stop) {
+                status = kStatusDone;
+                break;
+            }
+            if (A.max_updates > 0 && h - 1 >= A.max_updates) {
+                status = kStatusCapped;
+                break;
+            }
+        } else if (h >= A.num_iter) {  // while(h < NUM_ITER)
+            status = kStatusDone;
+            break;
+        }
+        if (done_here >= A.chunk) {
+            status = kStatusContinue;
+            break;
+        }
+        // accept the update computed in phase A
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+        ++h;
+        ++done_here;
+        // no barrier needed: the next phase A reads `cur` (written before the
+        // last __syncthreads) and writes `nxt`, which nobody reads until after
+        // the next __syncthreads
+    }
+    for (int i = tid; i < N; i += 256) A.Y[i] = cur[i];
+    if (conv)
+        for (int i = tid; i < M; i += 256) A.U[i] = Us[i];
+    if (tid == 0) {
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+    }
+}
+
+size_t solve_small_lds_bytes(int N, int M) { return sizeof(float) * (size_t)small_layout(N, M).total; }
+
+hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s) {
+    hipLaunchKernelGGL(k_solve_small, dim3(1), dim3(256), solve_small_lds_bytes(a.N, a.M), s, a, st);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launchers (declared in pqp_launch.h)
 // ---------------------------------------------------------------------------
 static inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
@@ -692,13 +948,16 @@ static void launch_iterate_t(int B, const float* QdT, long long qstride, int ldq
 
 hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
                                 const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
+    // 0 (shipped): 16-deep unroll with non-temporal Qd loads -- 6.88 TB/s at
+    // N=1024, B=4096 vs 7.02 TB/s for a bare read of the same pattern
+    // (profiles/r01/ab_4096.txt).  Others kept for A/B.
     switch (g_variant) {
-        case 1: launch_iterate_t<8, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 2: launch_iterate_t<4, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 3: launch_iterate_t<16, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 4: launch_iterate_t<4, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 5: launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        default: launch_iterate_t<8, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 1: launch_iterate_t<8, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 2: launch_iterate_t<8, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 3: launch_iterate_t<4, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 4: launch_iterate_t<32, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 5: launch_iterate_t<16, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        default: launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
     }
     return hipGetLastError();
 }
@@ -717,12 +976,12 @@ hipError_t launch_batch_update(int B, const float* QdT, long long qstride, int l
     const size_t lds = (size_t)ldq * sizeof(float);
     if (N <= 256) {
         dim3 grid(cdiv(N, 4 * 64), B);
-        hipLaunchKernelGGL(k_batch_update<64>, grid, dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv, Yin,
-                           Yout);
+        hipLaunchKernelGGL((k_batch_update<64, 16, true>), grid, dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd,
+                           ldv, Yin, Yout);
     } else {
         dim3 grid(cdiv(N, 4 * 256), B);
-        hipLaunchKernelGGL(k_batch_update<256>, grid, dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd, ldv, Yin,
-                           Yout);
+        hipLaunchKernelGGL((k_batch_update<256, 16, true>), grid, dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd,
+                           ldv, Yin, Yout);
     }
     return hipGetLastError();
 }

@@ -51,6 +51,8 @@ hipError_t launch_cost_finish(const float* quad, const float* lin, const float* 
 hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStream_t s);
 hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
 size_t solve_single_lds_bytes(int ldq, int ldm);
+size_t solve_small_lds_bytes(int N, int M);
+hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
 void set_variant(int v);
 int get_variant();
 hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,

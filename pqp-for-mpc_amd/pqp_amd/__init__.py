@@ -55,6 +55,10 @@ SIGNATURES = {
     "input": (None, [_fp] * 16),
     "pqp_solve_dual": (C.c_int, [_fp] * 9 + [C.c_int] * 3 + [C.c_longlong] * 2 + [_fp, _fp,
                                                                                    C.POINTER(C.c_longlong), _fp, _fp]),
+    "pqp_problem_create": (C.c_int, [_fp] * 9 + [C.c_int] * 2 + [C.POINTER(C.c_void_p)]),
+    "pqp_problem_solve": (C.c_int, [_vp, C.c_int, C.c_longlong, C.c_longlong, _fp, _fp, C.POINTER(C.c_longlong), _fp,
+                                    _fp]),
+    "pqp_problem_destroy": (C.c_int, [_vp]),
     "pqp_update_host": (C.c_int, [_fp] * 5 + [C.c_int]),
     "pqp_read_example": (C.c_int, [C.c_char_p] + [C.c_int] * 3 + [_fp] * 14),
     "pqp_run_example": (C.c_int, [C.c_char_p, _vp]),
@@ -205,6 +209,47 @@ def solve_dual(P: dict, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_upd
     if rc not in (PQP_OK, PQP_ERR_NOT_CONVERGED):
         _check(rc)
     return dict(h=int(h.value), Y=Y, U=U, Jp=float(jp[0]), Jd=float(jd[0]), converged=(rc == PQP_OK))
+
+
+class Problem:
+    """A dual problem resident in HBM (pqp_problem_*): upload/prepare once,
+    solve repeatedly.  Keys of P: Qd Fd Md Qp Qp_inv Fp Mp Gp Kp N M."""
+
+    KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
+
+    def __init__(self, P: dict):
+        self.N, self.M = int(P["N"]), int(P["M"])
+        a = [_f32(P[k]) for k in self.KEYS]
+        h = C.c_void_p()
+        _check(lib().pqp_problem_create(*[_buf(x) for x in a], self.N, self.M, C.byref(h)))
+        self._h = h
+
+    def solve(self, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0) -> dict:
+        Y, U = np.zeros(self.N, np.float32), np.zeros(self.M, np.float32)
+        h = C.c_longlong(0)
+        jp, jd = np.zeros(1, np.float32), np.zeros(1, np.float32)
+        rc = lib().pqp_problem_solve(self._h, mode, num_iter, max_updates, _buf(Y), _buf(U), C.byref(h), _buf(jp),
+                                     _buf(jd))
+        if rc not in (PQP_OK, PQP_ERR_NOT_CONVERGED):
+            _check(rc)
+        return dict(h=int(h.value), Y=Y, U=U, Jp=float(jp[0]), Jd=float(jd[0]), converged=(rc == PQP_OK))
+
+    def close(self):
+        if self._h:
+            lib().pqp_problem_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def update(Qd, theta_diag, Fd, Y, N) -> np.ndarray:

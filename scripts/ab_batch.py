@@ -16,7 +16,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-VARIANTS = {0: "U8", 1: "U8+nt", 2: "U4", 3: "U16", 4: "U4+nt", 5: "U16+nt"}
+VARIANTS = {0: "U16+nt (default)", 1: "U8", 2: "U8+nt", 3: "U4+nt", 4: "U32+nt", 5: "U16"}
 
 
 def main():
@@ -72,7 +72,7 @@ def main():
         return e0.elapsed_time(e1) / a.launches
 
     arms = [(f"iterate {VARIANTS[v]}", (lambda v=v: t_iter(v))) for v in VARIANTS]
-    arms += [("iterate U8 chunk10", lambda: t_iter(0, 10)), ("stream_read", lambda: t_read(0)),
+    arms += [("iterate default chunk10", lambda: t_iter(0, 10)), ("stream_read", lambda: t_read(0)),
              ("stream_read nt", lambda: t_read(1))]
     res = {name: [] for name, _ in arms}
     for _ in range(a.rounds):

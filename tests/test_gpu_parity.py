@@ -51,6 +51,34 @@ def test_bundled_fixed_k_updates(gpu_lib, golden_bundled, k):
     assert_bitwise(r["Y"], want, f"Y after {k - 1} updates")
 
 
+def test_problem_handle_repeated_solves(gpu_lib, golden_bundled):
+    g = golden_bundled
+    with gpu_lib.Problem(bundled_problem(g)) as prob:
+        for _ in range(3):
+            r = prob.solve()
+            assert r["h"] == 313
+            assert_bitwise(r["Y"], g["Ystar"], "Y*")
+            f = prob.solve(gpu_lib.MODE_FIXED, num_iter=1000)
+            assert_bitwise(f["Y"], g["Y_fixed999"], "fixed-999 Y")
+
+
+@pytest.mark.parametrize("N,M", [(40, 20), (64, 32), (97, 13), (100, 50), (128, 64), (300, 150)])
+def test_single_problem_paths(gpu_lib, orc, N, M):
+    """N <= ~98 runs the LDS-staged wave-specialized k_solve_small (several
+    lane passes per role from N > 32); larger problems take k_solve_single."""
+    P = orc.synth_problem(5, 3, N, M)
+    with gpu_lib.Problem(P) as prob:
+        r = prob.solve(gpu_lib.MODE_FIXED, num_iter=41)
+        h, Y, _ = orc.solve(P, mode=1, num_iter=41)
+        assert r["h"] == h == 41
+        assert_bitwise(r["Y"], Y, f"fixed N={N}")
+        c = prob.solve(max_updates=60)
+    h2, Y2, U2 = orc.solve(P, max_updates=60)
+    assert c["h"] == abs(h2)
+    assert_bitwise(c["Y"], Y2, f"converge-capped N={N}")
+    assert_bitwise(c["U"], U2, f"U N={N}")
+
+
 def test_dropin_solveQuadraticDual_prints_h(gpu_lib, golden_bundled, capfd):
     g = golden_bundled
     P = bundled_problem(g)
