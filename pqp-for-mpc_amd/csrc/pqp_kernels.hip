@@ -511,9 +511,25 @@ __global__ void __launch_bounds__(256) k_gauss_jordan(const float* __restrict__ 
 // round trip per iteration.  Resumable in chunks (state in SolveState) so no
 // single launch runs unbounded.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float seq_dot(const float* x, const float* y, int n) {
+// s = sum_k a[k*astride] * b[k] in the reference's order (k = 0..n-1 from
+// +0.0f, product rounded before each add).  The operands of U consecutive
+// terms are loaded before any of them is used, so LDS/L2 latency overlaps
+// instead of serializing behind the add chain; the add order is unchanged.
+template <int U = 8>
+__device__ __forceinline__ float seq_dot(const float* a, int astride, const float* b, int n) {
     float s = 0.0f;
-    for (int k = 0; k < n; ++k) s += x[k] * y[k];
+    int k = 0;
+    for (; k + U <= n; k += U) {
+        float av[U], bv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            av[j] = a[(size_t)(k + j) * astride];
+            bv[j] = b[k + j];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) s += av[j] * bv[j];
+    }
+    for (; k < n; ++k) s += a[(size_t)k * astride] * b[k];
     return s;
 }
 
@@ -544,23 +560,14 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
         if (A.mode != kModeFixed) {
             // ---- terminate(Y)  PQP_CPU.c:673-687 ----
             // computeUfromY :352-360
-            for (int j = tid; j < M; j += NT) {
-                float s = 0.0f;
-                for (int k = 0; k < N; ++k) s += A.Gp[(size_t)k * M + j] * cur[k];
-                tM[j] = s + 1.0f * A.Fp[j];
-            }
+            for (int j = tid; j < M; j += NT) tM[j] = seq_dot(A.Gp + j, M, cur, N) + 1.0f * A.Fp[j];
             __syncthreads();
-            for (int i = tid; i < M; i += NT) {
-                float s = 0.0f;
-                for (int j = 0; j < M; ++j) s += A.Qinv[(size_t)i * M + j] * tM[j];
-                Us[i] = -s;
-            }
+            for (int i = tid; i < M; i += NT) Us[i] = -seq_dot(A.Qinv + (size_t)i * M, 1, tM, M);
             __syncthreads();
             // checkFeas :632-641
             int bad = 0;
             for (int i = tid; i < N; i += NT) {
-                float s = 0.0f;
-                for (int j = 0; j < M; ++j) s += A.Gp[(size_t)i * M + j] * Us[j];
+                const float s = seq_dot(A.Gp + (size_t)i * M, 1, Us, M);
                 const float kp = A.Kp[i];
                 if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
             }
@@ -568,16 +575,8 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
             int stop = 0;
             if (!infeasible) {
                 // computeCost(Y, Qd, Fd, Md) and computeCost(U, Qp, Fp, Mp) :648-666
-                for (int j = tid; j < N; j += NT) {
-                    float s = 0.0f;
-                    for (int k = 0; k < N; ++k) s += cur[k] * A.Qd[(size_t)k * N + j];
-                    tq[j] = s;
-                }
-                for (int j = tid; j < M; j += NT) {
-                    float s = 0.0f;
-                    for (int k = 0; k < M; ++k) s += Us[k] * A.Qp[(size_t)k * M + j];
-                    tu[j] = s;
-                }
+                for (int j = tid; j < N; j += NT) tq[j] = seq_dot(A.Qd + j, N, cur, N);
+                for (int j = tid; j < M; j += NT) tu[j] = seq_dot(A.Qp + j, M, Us, M);
                 __syncthreads();
                 const int jt = (NT >= 128) ? 64 : 1;  // second scalar chain on another wave
                 if (tid == 0 || tid == jt) {
@@ -586,9 +585,8 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
                     const float* z = dual ? cur : Us;
                     const float* F = dual ? A.Fd : A.Fp;
                     const int n = dual ? N : M;
-                    const float quad = seq_dot(row, z, n);
-                    float lin = 0.0f;
-                    for (int k = 0; k < n; ++k) lin += F[k] * z[k];
+                    const float quad = seq_dot(row, 1, z, n);
+                    const float lin = seq_dot(F, 1, z, n);
                     float J = 0.0f;
                     J = (float)((double)J + 0.5 * (double)quad);
                     J += lin;
@@ -630,22 +628,38 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
             status = kStatusContinue;
             break;
         }
-        // ---- updateY2  PQP_CPU.c:603-618 (one lane per row, literal form) ----
+        // ---- updateY2  PQP_CPU.c:603-618 (one lane per row) ----
+        // Split entries in "max form": (q<0 ? 0 : q)*y and (q>0 ? 0 : -q)*y off
+        // the diagonal (bit-identical to (max(0,+-q)+0.0f)*y),
+        // and the stored literal (max(0,+-q_ii)+theta_i) on it.
         for (int i = tid; i < N; i += NT) {
             float ap = 0.0f, an = 0.0f;
             const float thi = A.theta[i];
+            const float qii = A.QdT[(size_t)i * ldq + i];
+            const float dp = max_ref(0.0f, qii) + 1.0f * thi, dn = max_ref(0.0f, -qii) + 1.0f * thi;
             const float* col = A.QdT + i;
-            for (int k = 0; k < N; ++k) {
-                const float q = col[(size_t)k * ldq];
-                const float yk = cur[k];
-                if (k == i) {
-                    literal1(ap, an, q, yk, thi);
-                } else {
-                    const float z = 0.0f * yk;
-                    const float p = q * yk;
-                    ap += (q < 0.0f) ? z : p;
-                    an += (q > 0.0f) ? z : -p;
+            int k = 0;
+            for (; k + 8 <= N; k += 8) {
+                float q[8], yv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    q[j] = col[(size_t)(k + j) * ldq];
+                    yv[j] = cur[k + j];
                 }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const bool d = (k + j == i);
+                    const float qp = d ? dp : ((q[j] < 0.0f) ? 0.0f : q[j]);
+                    const float qn = d ? dn : ((q[j] > 0.0f) ? 0.0f : -q[j]);
+                    ap += qp * yv[j];
+                    an += qn * yv[j];
+                }
+            }
+            for (; k < N; ++k) {
+                const float q = col[(size_t)k * ldq], yk = cur[k];
+                const bool d = (k == i);
+                ap += (d ? dp : ((q < 0.0f) ? 0.0f : q)) * yk;
+                an += (d ? dn : ((q > 0.0f) ? 0.0f : -q)) * yk;
             }
             const float f = A.Fd[i];
             const float num = an + 1.0f * max_ref(0.0f, -f);
@@ -785,13 +799,7 @@ __global__ void __launch_bounds__(256) k_solve_small(SolveArgs A, SolveState* __
         // ---------------- phase A ----------------
         if (wave == 0) {
             if (may_update) {
-                for (int p = lane; p < 2 * N; p += 64) {
-                    const int i = p >> 1;
-                    float acc = 0.0f;
-                    const float* col = S + 2 * i + (p & 1);
-                    for (int k = 0; k < N; ++k) acc += col[2 * k * N] * cur[k];  // :608-609
-                    nd[p] = acc;
-                }
+                for (int p = lane; p < 2 * N; p += 64) nd[p] = seq_dot(S + p, 2 * N, cur, N);  // :608-609
                 __builtin_amdgcn_wave_barrier();
                 for (int i = lane; i < N; i += 64) {
                     const float num = nd[2 * i] + 1.0f * Fdn[i];     // :611
@@ -800,59 +808,33 @@ __global__ void __launch_bounds__(256) k_solve_small(SolveArgs A, SolveState* __
                 }
             }
         } else if (need_term && wave == 1) {
-            for (int j = lane; j < M; j += 64) {
-                float s = 0.0f;
-                for (int k = 0; k < N; ++k) s += Gp[k * M + j] * cur[k];
-                tM[j] = s + 1.0f * Fp[j];
-            }
+            for (int j = lane; j < M; j += 64) tM[j] = seq_dot(Gp + j, M, cur, N) + 1.0f * Fp[j];
         } else if (need_term && wave == 2) {
-            for (int j = lane; j < N; j += 64) {
-                float s = 0.0f;
-                for (int k = 0; k < N; ++k) s += cur[k] * Qd[k * N + j];
-                tq[j] = s;
-            }
+            for (int j = lane; j < N; j += 64) tq[j] = seq_dot(Qd + j, N, cur, N);
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {
-                float s = 0.0f;
-                for (int j = 0; j < N; ++j) s += tq[j] * cur[j];
-                sc[0] = s;
-            }
+            if (lane == 0) sc[0] = seq_dot(tq, 1, cur, N);
         } else if (need_term && wave == 3) {
-            if (lane == 0) {
-                float s = 0.0f;
-                for (int k = 0; k < N; ++k) s += Fd[k] * cur[k];
-                sc[1] = s;
-            }
+            if (lane == 0) sc[1] = seq_dot(Fd, 1, cur, N);
         }
         __syncthreads();
         // ---------------- phase B: terminate() decision (wave 1) ----------------
         if (need_term && wave == 1) {
-            for (int i = lane; i < M; i += 64) {  // U = -(Qp_inv tM)  :357-358
-                float s = 0.0f;
-                for (int j = 0; j < M; ++j) s += Qi[i * M + j] * tM[j];
-                Us[i] = -s;
-            }
+            for (int i = lane; i < M; i += 64) Us[i] = -seq_dot(Qi + i * M, 1, tM, M);  // :357-358
             __builtin_amdgcn_wave_barrier();
             int bad = 0;  // checkFeas :632-641
             for (int i = lane; i < N; i += 64) {
-                float s = 0.0f;
-                for (int j = 0; j < M; ++j) s += Gp[i * M + j] * Us[j];
+                const float s = seq_dot(Gp + i * M, 1, Us, M);
                 const float kp = Kp[i];
                 if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
             }
             const bool infeasible = __any(bad);
             int stop = 0;
             if (!infeasible) {
-                for (int j = lane; j < M; j += 64) {  // U'Qp
-                    float s = 0.0f;
-                    for (int k = 0; k < M; ++k) s += Us[k] * Qp[k * M + j];
-                    tu[j] = s;
-                }
+                for (int j = lane; j < M; j += 64) tu[j] = seq_dot(Qp + j, M, Us, M);  // U'Qp
                 __builtin_amdgcn_wave_barrier();
                 if (lane == 0) {
-                    float quad = 0.0f, lin = 0.0f;
-                    for (int j = 0; j < M; ++j) quad += tu[j] * Us[j];
-                    for (int k = 0; k < M; ++k) lin += Fp[k] * Us[k];
+                    const float quad = seq_dot(tu, 1, Us, M);
+                    const float lin = seq_dot(Fp, 1, Us, M);
                     float Jp = 0.0f;
                     Jp = (float)((double)Jp + 0.5 * (double)quad);
                     Jp += lin;
