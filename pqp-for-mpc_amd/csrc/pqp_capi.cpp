@@ -244,6 +244,7 @@ namespace pqp {
 namespace {
 
 constexpr size_t kLdsBudget = 150 * 1024;
+bool g_force_small = false;  // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -322,7 +323,9 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
     a.chunk = chunk < 1 ? 1 : chunk;
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     for (;;) {
-        if (P.small)
+        if (P.N <= 32 && P.M <= 32 && !g_force_small)
+            PQP_HIP(launch_solve_tiny(a, dst, s));
+        else if (P.small)
             PQP_HIP(launch_solve_small(a, dst, s));
         else
             PQP_HIP(launch_solve_single(a, dst, s));
@@ -869,8 +872,9 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 #include "../../include/pqp_tuning.h"
 
 extern "C" int pqp_tune_set_variant(int variant) {
-    const int old = pqp::get_variant();
-    pqp::set_variant(variant);
+    const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0);
+    pqp::set_variant(variant & 0xff);
+    pqp::g_force_small = (variant & 0x100) != 0;
     return old;
 }
 

@@ -900,6 +900,221 @@ __global__ void __launch_bounds__(256) k_solve_small(SolveArgs A, SolveState* __
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_solve_tiny<NMAX>: N, M <= NMAX (the bundled problem, N = 28, M = 7).
+// Same roles as k_solve_small, but every lane keeps its slice of the
+// (constant) matrices in VGPRs for the whole solve, cross-lane values move by
+// v_readlane, and one barrier per iteration suffices (per-iteration scalars are
+// double-buffered by parity; every wave evaluates the stop decision from the
+// same LDS words, so control flow stays uniform).  Registers and LDS beyond N/M
+// are zero: an extra term adds exactly +0 to an accumulator that is never -0,
+// so the fully unrolled NMAX-step sums are bit-identical to the N-step ones.
+// Launched with 64 threads (wave 0 only) in fixed mode, 256 otherwise.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float rdl(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __restrict__ st) {
+    __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
+    __shared__ float sc[2][8];  // [parity]: 0 s_dual, 1 lin_dual, 2 infeasible, 3 quad_p, 4 lin_p
+    const int N = A.N, M = A.M;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool conv = (A.mode != kModeFixed);
+
+    // ---- one-time setup: each role loads its slice into registers ----
+    float mat[NMAX];  // wave 0: split row; wave 1: Gp column; wave 2: Qd column; wave 3: unused
+    float mat2[NMAX], mat3[NMAX], mat4[NMAX];  // wave 1: Gp row, Qp_inv row, Qp column
+    float vA = 0.0f, vB = 0.0f;  // per-lane scalars of the role
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) mat[k] = mat2[k] = mat3[k] = mat4[k] = 0.0f;
+    if (wave == 0) {
+        const int i = lane >> 1, side = lane & 1;
+        if (i < N) {
+            float th = 0.0f;  // computeTheta (:503-519)
+            for (int k = 0; k < N; ++k) th += max_ref(0.0f, -A.Qd[i * N + k]) * 1.0f;
+            th = max_ref(th, 5.0f);
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) {
+                if (k < N) {
+                    const float q = A.Qd[i * N + k];
+                    const float t = (i == k) ? th : 0.0f;
+                    // side 0: Qdn_theta (numerator), side 1: Qdp_theta  (:524-537)
+                    mat[k] = (side ? max_ref(0.0f, q) : max_ref(0.0f, -q)) + 1.0f * t;
+                }
+            }
+            const float f = A.Fd[i];
+            vA = side ? max_ref(0.0f, f) : max_ref(0.0f, -f);  // Fdp / Fdn  (:703-704)
+        }
+    } else if (conv && wave == 1) {
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) {
+            if (lane < M && k < N) mat[k] = A.Gp[k * M + lane];      // Gp column  (Gp'Y)
+            if (lane < N && k < M) mat2[k] = A.Gp[lane * M + k];     // Gp row     (Gp U)
+            if (lane < M && k < M) mat3[k] = A.Qinv[lane * M + k];   // Qp_inv row (Qp_inv t)
+            if (lane < M && k < M) mat4[k] = A.Qp[k * M + lane];     // Qp column  (U'Qp)
+        }
+        vA = (lane < M) ? A.Fp[lane] : 0.0f;
+        vB = (lane < N) ? A.Kp[lane] : 0.0f;
+    } else if (conv && wave == 2) {
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k)
+            if (lane < N && k < N) mat[k] = A.Qd[k * N + lane];      // Qd column  (Y'Qd)
+    } else if (conv && wave == 3) {
+        vA = (lane < N) ? A.Fd[lane] : 0.0f;
+    }
+    const float Md = conv ? A.Md[0] : 0.0f, Mp = conv ? A.Mp[0] : 0.0f;
+    for (int k = tid; k < NMAX; k += blockDim.x) {
+        ybuf[0][k] = (k < N) ? (st->resume ? A.Y[k] : 1000.0f) : 0.0f;  // initMat(Y, 1000) :710
+        ybuf[1][k] = 0.0f;
+    }
+    __syncthreads();
+
+    long long h = st->h;
+    long long done_here = 0;
+    int status = kStatusContinue;
+    int cb = 0;  // ybuf index of the current iterate
+    for (int par = 0;; par ^= 1) {
+        const float* cur = ybuf[cb];
+        float* nxt = ybuf[cb ^ 1];
+        float yv[NMAX];
+#pragma unroll
+        for (int k = 0; k < NMAX; k += 4) {
+            const float4 t = *reinterpret_cast<const float4*>(cur + k);
+            yv[k] = t.x;
+            yv[k + 1] = t.y;
+            yv[k + 2] = t.z;
+            yv[k + 3] = t.w;
+        }
+        if (wave == 0) {
+            if (A.mode != kModeTerminate) {  // updateY2 (:603-618)
+                float acc = 0.0f;
+#pragma unroll
+                for (int k = 0; k < NMAX; ++k) acc += mat[k] * yv[k];  // :608-609
+                const float other = __shfl_xor(acc, 1);
+                const int i = lane >> 1;
+                if (!(lane & 1) && i < N) {
+                    const float fdn = vA, fdp = __shfl_xor(vA, 1);
+                    const float num = acc + 1.0f * fdn;    // :611
+                    const float den = other + 1.0f * fdp;  // :612
+                    nxt[i] = num / den * cur[i];           // :594
+                }
+            }
+        } else if (conv && wave == 1) {
+            // computeUfromY (:352-360): t = Gp'Y + Fp ; U = -(Qp_inv t)
+            float t = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) t += mat[k] * yv[k];
+            t = t + 1.0f * vA;
+            if (lane >= M) t = 0.0f;
+            float u = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) u += mat3[j] * rdl(t, j);
+            u = (lane < M) ? -u : 0.0f;
+            // checkFeas (:632-641)
+            float g = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) g += mat2[j] * rdl(u, j);
+            const int bad = (lane < N) && (g > vB + max_ref((float)(kTol * vB), (float)kTol));
+            const bool infeasible = __any(bad);
+            // computeCost(U, Qp, Fp, Mp) (:648-666): row = U'Qp ; quad = row.U ; lin = Fp'U
+            float row = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) row += rdl(u, k) * mat4[k];
+            if (lane >= M) row = 0.0f;
+            float quad = 0.0f, lin = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) {
+                const float uj = rdl(u, j);
+                quad += rdl(row, j) * uj;
+                lin += rdl(vA, j) * uj;
+            }
+            if (lane == 0) {
+                sc[par][2] = infeasible ? 1.0f : 0.0f;
+                sc[par][3] = quad;
+                sc[par][4] = lin;
+            }
+            if (lane < M) A.U[lane] = u;  // computeUfromY writes U on every terminate()
+        } else if (conv && wave == 2) {
+            // computeCost(Y, Qd, Fd, Md): row = Y'Qd ; s = row.Y
+            float row = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) row += yv[k] * mat[k];
+            float s2 = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) s2 += rdl(row, j) * yv[j];
+            if (lane == 0) sc[par][0] = s2;
+        } else if (conv && wave == 3) {
+            float lin = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) lin += rdl(vA, k) * yv[k];
+            if (lane == 0) sc[par][1] = lin;
+        }
+        __syncthreads();
+        if (conv) {
+            int stop = 0;
+            if (sc[par][2] == 0.0f) {
+                float Jp = 0.0f;
+                Jp = (float)((double)Jp + 0.5 * (double)sc[par][3]);
+                Jp += sc[par][4];
+                Jp += Mp / 2;
+                float Jd = 0.0f;
+                Jd = (float)((double)Jd + 0.5 * (double)sc[par][0]);
+                Jd += sc[par][1];
+                Jd += Md / 2;
+                stop = 1;
+                if (Jp > -Jd) stop = 0;
+                if ((double)(Jp + Jd) > kTol) stop = 0;
+                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                if (tid == 0) {
+                    st->Jp = Jp;
+                    st->Jd = Jd;
+                    st->have_costs = 1;
+                }
+            }
+            if (A.mode == kModeTerminate) {
+                if (tid == 0) st->last_stop = stop;
+                status = kStatusDone;
+                break;
+            }
+            if (stop) {
+                status = kStatusDone;
+                break;
+            }
+            if (A.max_updates > 0 && h - 1 >= A.max_updates) {
+                status = kStatusCapped;
+                break;
+            }
+        } else if (h >= A.num_iter) {
+            status = kStatusDone;
+            break;
+        }
+        if (done_here >= A.chunk) {
+            status = kStatusContinue;
+            break;
+        }
+        cb ^= 1;  // accept the update
+        ++h;
+        ++done_here;
+    }
+    for (int i = tid; i < N; i += blockDim.x) A.Y[i] = ybuf[cb][i];
+    if (tid == 0) {
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+    }
+}
+
+hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
+    const int threads = (a.mode == kModeFixed) ? 64 : 256;
+    if (a.N <= 16 && a.M <= 16)
+        hipLaunchKernelGGL(k_solve_tiny<16>, dim3(1), dim3(threads), 0, s, a, st);
+    else
+        hipLaunchKernelGGL(k_solve_tiny<32>, dim3(1), dim3(threads), 0, s, a, st);
+    return hipGetLastError();
+}
+
 size_t solve_small_lds_bytes(int N, int M) { return sizeof(float) * (size_t)small_layout(N, M).total; }
 
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s) {

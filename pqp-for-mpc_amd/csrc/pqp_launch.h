@@ -53,6 +53,7 @@ hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* re
 size_t solve_single_lds_bytes(int ldq, int ldm);
 size_t solve_small_lds_bytes(int N, int M);
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
+hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);  // N, M <= 32
 void set_variant(int v);
 int get_variant();
 hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,

@@ -62,10 +62,28 @@ def test_problem_handle_repeated_solves(gpu_lib, golden_bundled):
             assert_bitwise(f["Y"], g["Y_fixed999"], "fixed-999 Y")
 
 
-@pytest.mark.parametrize("N,M", [(40, 20), (64, 32), (97, 13), (100, 50), (128, 64), (300, 150)])
+def test_lds_staged_solver_on_bundled(gpu_lib, golden_bundled):
+    """Route the bundled problem through k_solve_small (instead of the
+    register-resident k_solve_tiny): same bits, same h."""
+    L = gpu_lib.lib()
+    old = L.pqp_tune_set_variant(0x100)
+    try:
+        r = gpu_lib.solve_dual(bundled_problem(golden_bundled))
+        f = gpu_lib.solve_dual(bundled_problem(golden_bundled), mode=gpu_lib.MODE_FIXED, num_iter=1000)
+    finally:
+        L.pqp_tune_set_variant(old)
+    assert r["h"] == 313
+    assert_bitwise(r["Y"], golden_bundled["Ystar"], "Y*")
+    assert_bitwise(r["U"], golden_bundled["Ustar"], "U")
+    assert_bitwise(f["Y"], golden_bundled["Y_fixed999"], "fixed-999")
+
+
+@pytest.mark.parametrize("N,M", [(5, 3), (16, 16), (17, 9), (32, 32), (40, 20), (64, 32), (97, 13), (100, 50),
+                                 (128, 64), (300, 150)])
 def test_single_problem_paths(gpu_lib, orc, N, M):
-    """N <= ~98 runs the LDS-staged wave-specialized k_solve_small (several
-    lane passes per role from N > 32); larger problems take k_solve_single."""
+    """N, M <= 32: register-resident k_solve_tiny (16- and 32-wide builds);
+    N <= ~98: LDS-staged k_solve_small (several lane passes per role from
+    N > 32); larger problems: k_solve_single."""
     P = orc.synth_problem(5, 3, N, M)
     with gpu_lib.Problem(P) as prob:
         r = prob.solve(gpu_lib.MODE_FIXED, num_iter=41)
