@@ -111,10 +111,10 @@ def bundled_bench(pqp_amd) -> dict:
         for _ in range(reps):
             r = prob.solve(pqp_amd.MODE_FIXED, num_iter=1000)
         fixed_s = (time.perf_counter() - t0) / reps
-        prob.solve()
+        prob.solve(max_updates=200000)
         t0 = time.perf_counter()
         for _ in range(reps):
-            c = prob.solve()
+            c = prob.solve(max_updates=200000)
         conv_s = (time.perf_counter() - t0) / reps
     t0 = time.perf_counter()
     for _ in range(5):

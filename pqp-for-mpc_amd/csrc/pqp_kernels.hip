@@ -992,10 +992,13 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __r
                 float acc = 0.0f;
 #pragma unroll
                 for (int k = 0; k < NMAX; ++k) acc += mat[k] * yv[k];  // :608-609
+                // both shuffles run with the full wave active (a lane-divergent
+                // __shfl would read an inactive partner lane)
                 const float other = __shfl_xor(acc, 1);
+                const float fdp = __shfl_xor(vA, 1);
                 const int i = lane >> 1;
                 if (!(lane & 1) && i < N) {
-                    const float fdn = vA, fdp = __shfl_xor(vA, 1);
+                    const float fdn = vA;
                     const float num = acc + 1.0f * fdn;    // :611
                     const float den = other + 1.0f * fdp;  // :612
                     nxt[i] = num / den * cur[i];           // :594

@@ -18,7 +18,7 @@ def main(reps: int = 50):
     P = pqp_amd.example_problem(ROOT / "tests" / "golden" / "example")
     out = {}
     with pqp_amd.Problem(P) as prob:
-        for name, kw in (("fixed1000", dict(mode=pqp_amd.MODE_FIXED, num_iter=1000)), ("converge", {})):
+        for name, kw in (("fixed1000", dict(mode=pqp_amd.MODE_FIXED, num_iter=1000)), ("converge", dict(max_updates=200000))):
             prob.solve(**kw)
             t0 = time.perf_counter()
             for _ in range(reps):

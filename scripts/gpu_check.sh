@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 echo "start $(date)"
-timeout -k 10 700 python -m pytest tests -m gpu -v -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+PYTHONUNBUFFERED=1 timeout -k 10 700 python -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?

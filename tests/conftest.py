@@ -5,6 +5,7 @@ other tests run on CPU.  ``oracle/`` is imported here strictly as the checker.
 """
 from __future__ import annotations
 
+import os
 import sys
 from pathlib import Path
 
@@ -17,6 +18,13 @@ EXAMPLE_DIR = GOLDEN / "example"
 for p in (ROOT / "pqp-for-mpc_amd", ROOT / "oracle", ROOT):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
+
+
+# A broken converge-mode solve must fail, not hang the GPU box: cap the
+# drop-in solveQuadraticDual (and the CLI / reference-main subprocesses, which
+# inherit the environment).  Correct runs need <= 4524 updates here.
+os.environ.setdefault("PQP_MAX_UPDATES", "200000")
+CAP = 200000
 
 
 def pytest_configure(config):

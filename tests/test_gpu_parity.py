@@ -9,7 +9,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import EXAMPLE_DIR, GOLDEN, assert_bitwise
+from conftest import CAP, EXAMPLE_DIR, GOLDEN, assert_bitwise
 
 pytestmark = pytest.mark.gpu
 
@@ -27,7 +27,7 @@ def bundled_problem(g):
 # ---------------------------------------------------------------------------
 def test_bundled_converge_bit_exact(gpu_lib, golden_bundled):
     g = golden_bundled
-    r = gpu_lib.solve_dual(bundled_problem(g))
+    r = gpu_lib.solve_dual(bundled_problem(g), max_updates=CAP)
     assert r["converged"]
     assert r["h"] == int(g["h"]) == 313
     assert_bitwise(r["Y"], g["Ystar"], "Y*")
@@ -55,7 +55,7 @@ def test_problem_handle_repeated_solves(gpu_lib, golden_bundled):
     g = golden_bundled
     with gpu_lib.Problem(bundled_problem(g)) as prob:
         for _ in range(3):
-            r = prob.solve()
+            r = prob.solve(max_updates=CAP)
             assert r["h"] == 313
             assert_bitwise(r["Y"], g["Ystar"], "Y*")
             f = prob.solve(gpu_lib.MODE_FIXED, num_iter=1000)
@@ -68,7 +68,7 @@ def test_lds_staged_solver_on_bundled(gpu_lib, golden_bundled):
     L = gpu_lib.lib()
     old = L.pqp_tune_set_variant(0x100)
     try:
-        r = gpu_lib.solve_dual(bundled_problem(golden_bundled))
+        r = gpu_lib.solve_dual(bundled_problem(golden_bundled), max_updates=CAP)
         f = gpu_lib.solve_dual(bundled_problem(golden_bundled), mode=gpu_lib.MODE_FIXED, num_iter=1000)
     finally:
         L.pqp_tune_set_variant(old)
@@ -208,7 +208,7 @@ def test_synthetic_converge_cases(gpu_lib, golden_converge, orc):
     for (N, M, seed, h_ref) in cases:
         N, M = int(N), int(M)
         P = orc.synth_problem(int(seed), 0, N, M)
-        r = gpu_lib.solve_dual(P, max_updates=100000)
+        r = gpu_lib.solve_dual(P, max_updates=CAP)
         assert r["converged"] and r["h"] == int(h_ref), (N, M, seed, r["h"])
         assert_bitwise(r["Y"], Ys[yo:yo + N], f"Y {N}/{M}/{seed}")
         yo += N
