@@ -915,7 +915,7 @@ __device__ __forceinline__ float rdl(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-template <int NMAX>
+template <int NMAX, int MMAX>
 __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
     __shared__ float sc[2][8];  // [parity]: 0 s_dual, 1 lin_dual, 2 infeasible, 3 quad_p, 4 lin_p
@@ -925,10 +925,12 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __r
 
     // ---- one-time setup: each role loads its slice into registers ----
     float mat[NMAX];  // wave 0: split row; wave 1: Gp column; wave 2: Qd column; wave 3: unused
-    float mat2[NMAX], mat3[NMAX], mat4[NMAX];  // wave 1: Gp row, Qp_inv row, Qp column
+    float mat2[MMAX], mat3[MMAX], mat4[MMAX];  // wave 1: Gp row, Qp_inv row, Qp column
     float vA = 0.0f, vB = 0.0f;  // per-lane scalars of the role
 #pragma unroll
-    for (int k = 0; k < NMAX; ++k) mat[k] = mat2[k] = mat3[k] = mat4[k] = 0.0f;
+    for (int k = 0; k < NMAX; ++k) mat[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < MMAX; ++k) mat2[k] = mat3[k] = mat4[k] = 0.0f;
     if (wave == 0) {
         const int i = lane >> 1, side = lane & 1;
         if (i < N) {
@@ -949,8 +951,10 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __r
         }
     } else if (conv && wave == 1) {
 #pragma unroll
-        for (int k = 0; k < NMAX; ++k) {
+        for (int k = 0; k < NMAX; ++k)
             if (lane < M && k < N) mat[k] = A.Gp[k * M + lane];      // Gp column  (Gp'Y)
+#pragma unroll
+        for (int k = 0; k < MMAX; ++k) {
             if (lane < N && k < M) mat2[k] = A.Gp[lane * M + k];     // Gp row     (Gp U)
             if (lane < M && k < M) mat3[k] = A.Qinv[lane * M + k];   // Qp_inv row (Qp_inv t)
             if (lane < M && k < M) mat4[k] = A.Qp[k * M + lane];     // Qp column  (U'Qp)
@@ -1013,22 +1017,22 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __r
             if (lane >= M) t = 0.0f;
             float u = 0.0f;
 #pragma unroll
-            for (int j = 0; j < NMAX; ++j) u += mat3[j] * rdl(t, j);
+            for (int j = 0; j < MMAX; ++j) u += mat3[j] * rdl(t, j);
             u = (lane < M) ? -u : 0.0f;
             // checkFeas (:632-641)
             float g = 0.0f;
 #pragma unroll
-            for (int j = 0; j < NMAX; ++j) g += mat2[j] * rdl(u, j);
+            for (int j = 0; j < MMAX; ++j) g += mat2[j] * rdl(u, j);
             const int bad = (lane < N) && (g > vB + max_ref((float)(kTol * vB), (float)kTol));
             const bool infeasible = __any(bad);
             // computeCost(U, Qp, Fp, Mp) (:648-666): row = U'Qp ; quad = row.U ; lin = Fp'U
             float row = 0.0f;
 #pragma unroll
-            for (int k = 0; k < NMAX; ++k) row += rdl(u, k) * mat4[k];
+            for (int k = 0; k < MMAX; ++k) row += rdl(u, k) * mat4[k];
             if (lane >= M) row = 0.0f;
             float quad = 0.0f, lin = 0.0f;
 #pragma unroll
-            for (int j = 0; j < NMAX; ++j) {
+            for (int j = 0; j < MMAX; ++j) {
                 const float uj = rdl(u, j);
                 quad += rdl(row, j) * uj;
                 lin += rdl(vA, j) * uj;
@@ -1109,12 +1113,25 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __r
     }
 }
 
-hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
-    const int threads = (a.mode == kModeFixed) ? 64 : 256;
-    if (a.N <= 16 && a.M <= 16)
-        hipLaunchKernelGGL(k_solve_tiny<16>, dim3(1), dim3(threads), 0, s, a, st);
+template <int NMAX>
+static void launch_tiny_m(const SolveArgs& a, SolveState* st, int threads, hipStream_t s) {
+    if (a.M <= 8)
+        hipLaunchKernelGGL((k_solve_tiny<NMAX, 8>), dim3(1), dim3(threads), 0, s, a, st);
+    else if (a.M <= 16)
+        hipLaunchKernelGGL((k_solve_tiny<NMAX, 16>), dim3(1), dim3(threads), 0, s, a, st);
     else
-        hipLaunchKernelGGL(k_solve_tiny<32>, dim3(1), dim3(threads), 0, s, a, st);
+        hipLaunchKernelGGL((k_solve_tiny<NMAX, 32>), dim3(1), dim3(threads), 0, s, a, st);
+}
+
+hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
+    // the unrolled sums run to the next instantiated width >= N (>= M): the
+    // sequential chain is the critical path, so keep the padding small
+    const int threads = (a.mode == kModeFixed) ? 64 : 256;
+    if (a.N <= 8) launch_tiny_m<8>(a, st, threads, s);
+    else if (a.N <= 16) launch_tiny_m<16>(a, st, threads, s);
+    else if (a.N <= 24) launch_tiny_m<24>(a, st, threads, s);
+    else if (a.N <= 28) launch_tiny_m<28>(a, st, threads, s);
+    else launch_tiny_m<32>(a, st, threads, s);
     return hipGetLastError();
 }
 
