@@ -21,6 +21,8 @@ Extra keys:
                 absent -- single thread on this host, bounded sample
   bundled       the bundled example (configs[0]/[1]) on 1 GPU through the
                 C ABI: fixed 1000-iteration mode and converge mode (h = 313)
+  mpc_batch     16384 MPC problems (bundled plant at perturbed states), one
+                workgroup each, converge mode with device-side terminate()
   gather_ms     RCCL gather of every rank's Y* to rank 0 (outside the timed
                 region)
 
@@ -125,6 +127,35 @@ def bundled_bench(pqp_amd) -> dict:
             "oneshot_fixed1000_ms": oneshot_s * 1e3, "y_fixed_finite": bool(np.all(np.isfinite(r["Y"]))),
             "note": "wall time of one pqp_problem_solve call on an uploaded problem (launch + D2H of Y); "
                     "oneshot = pqp_solve_dual incl. upload/alloc/setup"}
+
+
+def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
+    """Many MPC problems at once: the bundled plant (N=28, M=7) at B states x
+    (x perturbed by 5 %, seed 5), per-problem setup and converge-mode solve on
+    the GPU, one workgroup per problem.  Timed: the batched solve only."""
+    import numpy as np
+    import torch
+
+    ex = pqp_amd.read_example(ROOT / "tests" / "golden" / "example")
+    rng = np.random.default_rng(5)
+    xs = (ex["x"][None, :] * (1.0 + 0.05 * rng.standard_normal((B, ex["ns"])))).astype(np.float32)
+    pb = pqp_amd.mpc_batch(ROOT / "tests" / "golden" / "example", xs)
+    pb.solve(max_updates=200000)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pb.solve(max_updates=200000)
+    dt = time.perf_counter() - t0
+    h = pb.h.cpu().numpy()
+    conv = float((pb.status.cpu().numpy() == 1).mean())
+    t0 = time.perf_counter()
+    pb.solve(pqp_amd.MODE_FIXED, num_iter=1000)
+    dtf = time.perf_counter() - t0
+    return {"problems": B, "n_dual": int(pb.N), "converge_ms": dt * 1e3, "qp_solves_per_s": B / dt,
+            "iterations_per_s": float(h.sum()) / dt, "h_min": int(h.min()), "h_max": int(h.max()),
+            "h_mean": float(h.mean()), "converged_frac": conv, "fixed1000_ms": dtf * 1e3,
+            "fixed1000_instance_iter_per_s": B * 999 / dtf,
+            "note": "bundled plant at B perturbed states; setup (computeFp/Mp, Gauss_Jordan, convertToDual) "
+                    "on device, excluded from the timing; each solve bit-exact with PQP_CPU.c (tests)"}
 
 
 def main():
@@ -238,6 +269,7 @@ def main():
     }
     if world == 1 and not args.no_bundled:
         result["bundled"] = bundled_bench(pqp_amd)
+        result["mpc_batch"] = mpc_batch_bench(pqp_amd)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed)
     print(json.dumps(result), flush=True)

@@ -179,6 +179,40 @@ int pqp_batch_update(int B, int N, const float *d_QdT, int ldq, long long qstrid
 int pqp_batch_iterate(int B, int N, const float *d_QdT, int ldq, long long qstride, const float *d_theta,
                       const float *d_Fd, int ldv, const float *d_Y0, float *d_Y, int updates, void *stream);
 
+/* ----------------------------------------------------------------------
+ * 2c. Batched small problems: many independent MPC problems (batched
+ * horizons / states), one workgroup each.  Every array holds B problems back
+ * to back in the reference's row-major layout (e.g. Qd is [B][N*N], Kp is
+ * [B][N], Md is [B]).  Synchronous: returns when every problem has finished.
+ * -------------------------------------------------------------------- */
+
+/* Gauss_Jordan (PQP_CPU.c:251-326) on B n x n matrices. */
+int pqp_batch_gauss_jordan(int B, int n, const float *d_A, float *d_res, void *stream);
+
+/* convertToDual (PQP_CPU.c:489-498) on B primal problems. */
+int pqp_batch_convert_to_dual(int B, int N, int M, const float *d_Qp_inv, const float *d_Gp, const float *d_Kp,
+                              const float *d_Fp, const float *d_Mp, float *d_Qd, float *d_Fd, float *d_Md,
+                              void *stream);
+
+/* computeFp / computeMp (PQP_CPU.c:373-428) for B (D, x) pairs of one plant:
+ * m = nInput*pHorizon, nd = nDis*pHorizon, ns = nState.  The plant matrices
+ * (Fp1 [m*nd], Fp2 [m*ns], Fp3 [m], Mp1 [ns*ns], Mp2 [nd*ns], Mp3 [nd*nd],
+ * Mp4 [ns], Mp5 [nd], Mp6 [1]) are shared; D is [B][nd], x is [B][ns]. */
+int pqp_batch_compute_fp(int B, int m, int nd, int ns, const float *d_Fp1, const float *d_Fp2, const float *d_Fp3,
+                         const float *d_D, const float *d_x, float *d_Fp, void *stream);
+int pqp_batch_compute_mp(int B, int nd, int ns, const float *d_Mp1, const float *d_Mp2, const float *d_Mp3,
+                         const float *d_Mp4, const float *d_Mp5, const float *d_Mp6, const float *d_D,
+                         const float *d_x, float *d_Mp, void *stream);
+
+/* solveQuadraticDual for B problems at once (converge or fixed mode, as
+ * pqp_solve_dual).  Outputs: Y [B][N], U [B][M] (converge mode), h [B]
+ * (int64, the reference's printed h) and status [B] (1 converged / done,
+ * 2 hit max_updates); h and status may be NULL. */
+int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, const float *d_Md, const float *d_Qp,
+                    const float *d_Qp_inv, const float *d_Fp, const float *d_Mp, const float *d_Gp, const float *d_Kp,
+                    int mode, long long num_iter, long long max_updates, float *d_Y, float *d_U, long long *d_h,
+                    int *d_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -609,6 +609,166 @@ int pqp_batch_iterate(int B, int N, const float* d_QdT, int ldq, long long qstri
 }
 
 // ---------------------------------------------------------------------------
+// 2c. batched small problems
+// ---------------------------------------------------------------------------
+int pqp_batch_gauss_jordan(int B, int n, const float* d_A, float* d_res, void* stream) {
+    if (B <= 0 || n <= 0 || !d_A || !d_res) return set_error(PQP_ERR_ARG, "pqp_batch_gauss_jordan: bad arguments");
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DevBuf aug, fac;
+    PQP_TRY(aug.floats((size_t)B * 2 * n * n));
+    PQP_TRY(fac.floats((size_t)B * n));
+    PQP_HIP(launch_gauss_jordan_b(B, d_A, aug.f(), fac.f(), d_res, n, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+int pqp_batch_convert_to_dual(int B, int N, int M, const float* d_Qp_inv, const float* d_Gp, const float* d_Kp,
+                              const float* d_Fp, const float* d_Mp, float* d_Qd, float* d_Fd, float* d_Md,
+                              void* stream) {
+    if (B <= 0 || N <= 0 || M <= 0 || !d_Qp_inv || !d_Gp || !d_Kp || !d_Fp || !d_Mp || !d_Qd || !d_Fd || !d_Md)
+        return set_error(PQP_ERR_ARG, "pqp_batch_convert_to_dual: bad arguments");
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const long long nm = (long long)N * M, mm = (long long)M * M, nn = (long long)N * N;
+    DevBuf GQ, fq;
+    PQP_TRY(GQ.floats((size_t)B * nm));
+    PQP_TRY(fq.floats((size_t)B * M));
+    // same sequence as dev_convert_to_dual (PQP_CPU.c:489-498), problem-strided
+    PQP_HIP(launch_matmul_seq_b(B, GQ.f(), d_Gp, 0, d_Qp_inv, 0, N, M, M, nm, mm, nm, s));
+    PQP_HIP(launch_matmul_seq_b(B, d_Qd, GQ.f(), 0, d_Gp, 1, N, M, N, nm, nm, nn, s));
+    PQP_HIP(launch_matmul_seq_b(B, d_Fd, GQ.f(), 0, d_Fp, 0, N, M, 1, nm, M, N, s));
+    PQP_HIP(launch_axpy_b(B, d_Fd, d_Kp, 1.0f, N, N, N, s));
+    PQP_HIP(launch_matmul_seq_b(B, fq.f(), d_Fp, 1, d_Qp_inv, 0, 1, M, M, M, mm, M, s));
+    PQP_HIP(launch_matmul_seq_b(B, d_Md, fq.f(), 0, d_Fp, 0, 1, M, 1, M, M, 1, s));
+    PQP_HIP(launch_axpy_b(B, d_Md, d_Mp, -1.0f, 1, 1, 1, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+int pqp_batch_compute_fp(int B, int m, int nd, int ns, const float* d_Fp1, const float* d_Fp2, const float* d_Fp3,
+                         const float* d_D, const float* d_x, float* d_Fp, void* stream) {
+    if (B <= 0 || m <= 0 || nd <= 0 || ns <= 0 || !d_Fp1 || !d_Fp2 || !d_Fp3 || !d_D || !d_x || !d_Fp)
+        return set_error(PQP_ERR_ARG, "pqp_batch_compute_fp: bad arguments");
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DevBuf t;
+    PQP_TRY(t.floats((size_t)B * m));
+    PQP_HIP(launch_matmul_seq_b(B, d_Fp, d_Fp1, 0, d_D, 0, m, nd, 1, 0, nd, m, s));      // Fp1 D
+    PQP_HIP(launch_matmul_seq_b(B, t.f(), d_Fp2, 0, d_x, 0, m, ns, 1, 0, ns, m, s));     // Fp2 x
+    PQP_HIP(launch_axpy_b(B, d_Fp, t.f(), 1.0f, m, m, m, s));
+    PQP_HIP(launch_axpy_b(B, d_Fp, d_Fp3, -1.0f, m, m, 0, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+int pqp_batch_compute_mp(int B, int nd, int ns, const float* d_Mp1, const float* d_Mp2, const float* d_Mp3,
+                         const float* d_Mp4, const float* d_Mp5, const float* d_Mp6, const float* d_D,
+                         const float* d_x, float* d_Mp, void* stream) {
+    if (B <= 0 || nd <= 0 || ns <= 0 || !d_Mp1 || !d_Mp2 || !d_Mp3 || !d_Mp4 || !d_Mp5 || !d_Mp6 || !d_D || !d_x ||
+        !d_Mp)
+        return set_error(PQP_ERR_ARG, "pqp_batch_compute_mp: bad arguments");
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int big = ns > nd ? ns : nd;
+    DevBuf row, T;
+    PQP_TRY(row.floats((size_t)B * big));
+    PQP_TRY(T.floats((size_t)B * 5));
+    float* R = row.f();
+    float* t = T.f();
+    // the five halved terms of PQP_CPU.c:400-423, term s of problem b at t[b*5 + s]
+    PQP_HIP(launch_matmul_seq_b(B, R, d_x, 1, d_Mp1, 0, 1, ns, ns, ns, 0, big, s));       // x' Mp1
+    PQP_HIP(launch_matmul_seq_b(B, t + 0, R, 0, d_x, 0, 1, ns, 1, big, ns, 5, s));        //  . x
+    PQP_HIP(launch_matmul_seq_b(B, R, d_D, 1, d_Mp2, 0, 1, nd, ns, nd, 0, big, s));       // D' Mp2
+    PQP_HIP(launch_matmul_seq_b(B, t + 1, R, 0, d_x, 0, 1, ns, 1, big, ns, 5, s));        //  . x
+    PQP_HIP(launch_matmul_seq_b(B, t + 2, d_Mp4, 1, d_x, 0, 1, ns, 1, 0, ns, 5, s));      // Mp4' x
+    PQP_HIP(launch_matmul_seq_b(B, R, d_D, 1, d_Mp3, 0, 1, nd, nd, nd, 0, big, s));       // D' Mp3
+    PQP_HIP(launch_matmul_seq_b(B, t + 3, R, 0, d_D, 0, 1, nd, 1, big, nd, 5, s));        //  . D
+    PQP_HIP(launch_matmul_seq_b(B, t + 4, d_Mp5, 1, d_D, 0, 1, nd, 1, 0, nd, 5, s));      // Mp5' D
+    PQP_HIP(launch_mp_finish_b(B, t, d_Mp6, d_Mp, 0, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, const float* d_Md, const float* d_Qp,
+                    const float* d_Qp_inv, const float* d_Fp, const float* d_Mp, const float* d_Gp, const float* d_Kp,
+                    int mode, long long num_iter, long long max_updates, float* d_Y, float* d_U, long long* d_h,
+                    int* d_status, void* stream) {
+    if (B <= 0 || N <= 0 || M <= 0 || !d_Qd || !d_Fd || !d_Y)
+        return set_error(PQP_ERR_ARG, "pqp_batch_solve: bad arguments");
+    if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
+        return set_error(PQP_ERR_ARG, "pqp_batch_solve: unknown mode %d", mode);
+    if (mode == PQP_MODE_CONVERGE && (!d_Md || !d_Qp || !d_Qp_inv || !d_Fp || !d_Mp || !d_Gp || !d_Kp || !d_U))
+        return set_error(PQP_ERR_ARG, "pqp_batch_solve: converge mode needs every primal/dual array and U");
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int ldq = round4(N), ldm = round4(M);
+    int path = 2;
+    if (N <= 32 && M <= 32 && !g_force_small)
+        path = 0;
+    else if (solve_small_lds_bytes(N, M) <= kLdsBudget)
+        path = 1;
+    else if (solve_single_lds_bytes(ldq, ldm) > kLdsBudget)
+        return set_error(PQP_ERR_ARG, "pqp_batch_solve: N=%d, M=%d exceeds the LDS budget", N, M);
+    DevBuf QdT, theta, state, pending, Udummy;
+    if (path == 2) {
+        PQP_TRY(QdT.floats((size_t)B * N * ldq));
+        PQP_TRY(theta.floats((size_t)B * N));
+        PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, QdT.f(), ldq, (long long)N * ldq, s));
+        PQP_HIP(launch_theta(B, QdT.f(), ldq, (long long)N * ldq, N, theta.f(), N, s));
+    }
+    if (!d_U) {
+        PQP_TRY(Udummy.floats((size_t)B * M));
+        d_U = Udummy.f();
+    }
+    PQP_TRY(state.alloc(sizeof(SolveState) * (size_t)B));
+    PQP_TRY(pending.alloc(sizeof(int)));
+    std::vector<SolveState> init((size_t)B);
+    for (auto& st : init) {
+        st = SolveState{};
+        st.h = 1;
+    }
+    PQP_HIP(hipMemcpyAsync(state.p, init.data(), sizeof(SolveState) * (size_t)B, hipMemcpyHostToDevice, s));
+    SolveArgs a{};
+    a.QdT = QdT.f();
+    a.Qd = d_Qd;
+    a.theta = theta.f();
+    a.Fd = d_Fd;
+    a.Md = d_Md;
+    a.Qp = d_Qp;
+    a.Qinv = d_Qp_inv;
+    a.Fp = d_Fp;
+    a.Mp = d_Mp;
+    a.Gp = d_Gp;
+    a.Kp = d_Kp;
+    a.Y = d_Y;
+    a.U = d_U;
+    a.N = N;
+    a.M = M;
+    a.ldq = ldq;
+    a.ldm = ldm;
+    a.mode = (mode == PQP_MODE_CONVERGE) ? kModeConverge : kModeFixed;
+    a.num_iter = num_iter;
+    a.max_updates = max_updates;
+    const double per_update = (double)N * N * 3.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
+    const long long chunk = (long long)((double)(1 << 26) / per_update);
+    a.chunk = chunk < 1 ? 1 : chunk;
+    a.pending = static_cast<int*>(pending.p);
+    SolveState* st = static_cast<SolveState*>(state.p);
+    for (;;) {
+        int left = 0;
+        PQP_HIP(hipMemsetAsync(pending.p, 0, sizeof(int), s));
+        PQP_HIP(launch_solve_batch(B, path, a, st, s));
+        PQP_HIP(hipMemcpyAsync(&left, pending.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (left == 0) break;
+    }
+    PQP_HIP(launch_extract_state(B, st, d_h, d_status, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    return PQP_OK;
+}
+
+// ---------------------------------------------------------------------------
 // 1. drop-in entry points (reference signatures)
 // ---------------------------------------------------------------------------
 void solveQuadraticDual(float* Y, float* Qd, float* Fd, float* Md, float* U, float* Qp, float* Qp_inv, float* Fp,

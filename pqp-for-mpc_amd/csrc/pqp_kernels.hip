@@ -403,9 +403,13 @@ __global__ void k_zero_pad(float* __restrict__ QdT, int N, int ldq, long long qs
 // for setup and for the drop-in helpers, not on the iteration path.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_matmul_seq(float* __restrict__ out, const float* __restrict__ A, int tA,
-                                                    const float* __restrict__ B, int tB, int a, int bdim, int c) {
+                                                    const float* __restrict__ B, int tB, int a, int bdim, int c,
+                                                    long long sA = 0, long long sB = 0, long long sO = 0) {
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
     if (e >= (long long)a * c) return;
+    A += blockIdx.y * sA;  // problem blockIdx.y of a batch (strides 0 = shared operand)
+    B += blockIdx.y * sB;
+    out += blockIdx.y * sO;
     const int i = (int)(e / c), j = (int)(e % c);
     float s = 0.0f;
     for (int k = 0; k < bdim; ++k) {
@@ -417,13 +421,17 @@ __global__ void __launch_bounds__(256) k_matmul_seq(float* __restrict__ out, con
 }
 
 // A[i] += sign * B[i]   (matrixAdd, PQP_CPU.c:157-163)
-__global__ void k_axpy(float* __restrict__ A, const float* __restrict__ B, float sign, int n) {
+__global__ void k_axpy(float* __restrict__ A, const float* __restrict__ B, float sign, int n, long long sA = 0,
+                       long long sB = 0) {
     const int i = blockIdx.x * 256 + threadIdx.x;
+    A += blockIdx.y * sA;
+    B += blockIdx.y * sB;
     if (i < n) A[i] += sign * B[i];
 }
 // A[i] = -A[i]   (negateMatrix, PQP_CPU.c:171-177)
-__global__ void k_negate(float* __restrict__ A, int n) {
+__global__ void k_negate(float* __restrict__ A, int n, long long sA = 0) {
     const int i = blockIdx.x * 256 + threadIdx.x;
+    A += blockIdx.y * sA;
     if (i < n) A[i] = -A[i];
 }
 // flag = all(GpU <= Kp + max(erc*Kp, eac))   (compare, PQP_CPU.c:334-343); flag preset to 1
@@ -452,7 +460,11 @@ __global__ void k_cost_finish(const float* __restrict__ quad, const float* __res
     J[0] = j;
 }
 // computeMp's accumulation (PQP_CPU.c:397-425): terms t[0..4] then Mp6, each halved
-__global__ void k_mp_finish(const float* __restrict__ t, const float* __restrict__ Mp6, float* __restrict__ Mp) {
+__global__ void k_mp_finish(const float* __restrict__ t, const float* __restrict__ Mp6, float* __restrict__ Mp,
+                            long long sMp6 = 0) {
+    t += (size_t)blockIdx.x * 5;  // problem blockIdx.x of a batch
+    Mp6 += blockIdx.x * sMp6;
+    Mp += blockIdx.x;
     float m = 0.0f;
     for (int s = 0; s < 5; ++s) m += t[s] / 2;
     m += Mp6[0] / 2;
@@ -466,6 +478,13 @@ __global__ void k_mp_finish(const float* __restrict__ t, const float* __restrict
 __global__ void __launch_bounds__(256) k_gauss_jordan(const float* __restrict__ A, float* __restrict__ aug,
                                                       float* __restrict__ fac, float* __restrict__ res, int n) {
     const int tid = threadIdx.x, w = 2 * n;
+    {  // problem blockIdx.x of a batch
+        const size_t b = blockIdx.x;
+        A += b * n * n;
+        res += b * n * n;
+        aug += b * n * w;
+        fac += b * n;
+    }
     for (int e = tid; e < n * w; e += 256) {
         const int r = e / w, c = e % w;
         aug[e] = (c < n) ? A[(size_t)r * n + c] : ((c == n + r) ? 1.0f : 0.0f);
@@ -505,6 +524,25 @@ __global__ void __launch_bounds__(256) k_gauss_jordan(const float* __restrict__ 
     }
 }
 
+// Problem b of a batched SolveArgs (contiguous per-problem arrays).
+__device__ __forceinline__ SolveArgs problem_at(SolveArgs A, int b) {
+    const size_t N = A.N, M = A.M;
+    A.QdT = A.QdT ? A.QdT + b * N * A.ldq : nullptr;
+    A.theta = A.theta ? A.theta + b * N : nullptr;
+    A.Qd += b * N * N;
+    A.Fd += b * N;
+    A.Md = A.Md ? A.Md + b : nullptr;
+    A.Qp = A.Qp ? A.Qp + b * M * M : nullptr;
+    A.Qinv = A.Qinv ? A.Qinv + b * M * M : nullptr;
+    A.Fp = A.Fp ? A.Fp + b * M : nullptr;
+    A.Mp = A.Mp ? A.Mp + b : nullptr;
+    A.Gp = A.Gp ? A.Gp + b * N * M : nullptr;
+    A.Kp = A.Kp ? A.Kp + b * N : nullptr;
+    A.Y += b * N;
+    A.U = A.U ? A.U + b * M : nullptr;
+    return A;
+}
+
 // ---------------------------------------------------------------------------
 // k_solve_single: the whole solveQuadraticDual (PQP_CPU.c:694-750) in ONE
 // persistent workgroup: terminate() before every update, bit-exact, no host
@@ -534,8 +572,11 @@ __device__ __forceinline__ float seq_dot(const float* a, int astride, const floa
 }
 
 template <int NT>
-__global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __restrict__ st) {
+__global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;  // finished in an earlier launch
     const int N = A.N, M = A.M, ldq = A.ldq;
     float* ya = lds;              // ldq
     float* yb = ya + ldq;         // ldq
@@ -680,6 +721,7 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A, SolveState* __
         st->h = h;
         st->status = status;
         st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
     }
 }
 
@@ -728,8 +770,11 @@ __host__ __device__ inline SmallLayout small_layout(int N, int M) {
     return L;
 }
 
-__global__ void __launch_bounds__(256) k_solve_small(SolveArgs A, SolveState* __restrict__ st) {
+__global__ void __launch_bounds__(256) k_solve_small(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;
     const int N = A.N, M = A.M;
     const SmallLayout L = small_layout(N, M);
     float* S = lds + L.S;      // [k][i][2]: (k*N + i)*2 + side; side 0 = Qdn_theta, 1 = Qdp_theta
@@ -897,6 +942,7 @@ __global__ void __launch_bounds__(256) k_solve_small(SolveArgs A, SolveState* __
         st->h = h;
         st->status = status;
         st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
     }
 }
 
@@ -916,7 +962,10 @@ __device__ __forceinline__ float rdl(float v, int lane) {
 }
 
 template <int NMAX, int MMAX>
-__global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __restrict__ st) {
+__global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A0, SolveState* __restrict__ st0) {
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;
     __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
     __shared__ float sc[2][8];  // [parity]: 0 s_dual, 1 lin_dual, 2 infeasible, 3 quad_p, 4 lin_p
     const int N = A.N, M = A.M;
@@ -1110,37 +1159,40 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A, SolveState* __r
         st->h = h;
         st->status = status;
         st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
     }
 }
 
 template <int NMAX>
-static void launch_tiny_m(const SolveArgs& a, SolveState* st, int threads, hipStream_t s) {
+static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads, hipStream_t s) {
     if (a.M <= 8)
-        hipLaunchKernelGGL((k_solve_tiny<NMAX, 8>), dim3(1), dim3(threads), 0, s, a, st);
+        hipLaunchKernelGGL((k_solve_tiny<NMAX, 8>), dim3(B), dim3(threads), 0, s, a, st);
     else if (a.M <= 16)
-        hipLaunchKernelGGL((k_solve_tiny<NMAX, 16>), dim3(1), dim3(threads), 0, s, a, st);
+        hipLaunchKernelGGL((k_solve_tiny<NMAX, 16>), dim3(B), dim3(threads), 0, s, a, st);
     else
-        hipLaunchKernelGGL((k_solve_tiny<NMAX, 32>), dim3(1), dim3(threads), 0, s, a, st);
+        hipLaunchKernelGGL((k_solve_tiny<NMAX, 32>), dim3(B), dim3(threads), 0, s, a, st);
 }
 
-hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
+static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the
     // sequential chain is the critical path, so keep the padding small
     const int threads = (a.mode == kModeFixed) ? 64 : 256;
-    if (a.N <= 8) launch_tiny_m<8>(a, st, threads, s);
-    else if (a.N <= 16) launch_tiny_m<16>(a, st, threads, s);
-    else if (a.N <= 24) launch_tiny_m<24>(a, st, threads, s);
-    else if (a.N <= 28) launch_tiny_m<28>(a, st, threads, s);
-    else launch_tiny_m<32>(a, st, threads, s);
+    if (a.N <= 8) launch_tiny_m<8>(B, a, st, threads, s);
+    else if (a.N <= 16) launch_tiny_m<16>(B, a, st, threads, s);
+    else if (a.N <= 24) launch_tiny_m<24>(B, a, st, threads, s);
+    else if (a.N <= 28) launch_tiny_m<28>(B, a, st, threads, s);
+    else launch_tiny_m<32>(B, a, st, threads, s);
     return hipGetLastError();
 }
+hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) { return launch_tiny_grid(1, a, st, s); }
 
 size_t solve_small_lds_bytes(int N, int M) { return sizeof(float) * (size_t)small_layout(N, M).total; }
 
-hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s) {
-    hipLaunchKernelGGL(k_solve_small, dim3(1), dim3(256), solve_small_lds_bytes(a.N, a.M), s, a, st);
+static hipError_t launch_small_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    hipLaunchKernelGGL(k_solve_small, dim3(B), dim3(256), solve_small_lds_bytes(a.N, a.M), s, a, st);
     return hipGetLastError();
 }
+hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s) { return launch_small_grid(1, a, st, s); }
 
 // ---------------------------------------------------------------------------
 // Host-side launchers (declared in pqp_launch.h)
@@ -1243,6 +1295,30 @@ hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B,
     hipLaunchKernelGGL(k_matmul_seq, dim3(cdiv(n, 256)), dim3(256), 0, s, out, A, tA, B, tB, a, b, c);
     return hipGetLastError();
 }
+hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const float* Bm, int tB, int a, int b,
+                               int c, long long sA, long long sB, long long sO, hipStream_t s) {
+    const long long n = (long long)a * c;
+    if (n == 0 || B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_matmul_seq, dim3(cdiv(n, 256), B), dim3(256), 0, s, out, A, tA, Bm, tB, a, b, c, sA, sB, sO);
+    return hipGetLastError();
+}
+hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, long long sA, long long sB,
+                         hipStream_t s) {
+    if (n > 0 && B > 0) hipLaunchKernelGGL(k_axpy, dim3(cdiv(n, 256), B), dim3(256), 0, s, A, Bv, sign, n, sA, sB);
+    return hipGetLastError();
+}
+hipError_t launch_negate_b(int B, float* A, int n, long long sA, hipStream_t s) {
+    if (n > 0 && B > 0) hipLaunchKernelGGL(k_negate, dim3(cdiv(n, 256), B), dim3(256), 0, s, A, n, sA);
+    return hipGetLastError();
+}
+hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp, long long sMp6, hipStream_t s) {
+    if (B > 0) hipLaunchKernelGGL(k_mp_finish, dim3(B), dim3(1), 0, s, t, Mp6, Mp, sMp6);
+    return hipGetLastError();
+}
+hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s) {
+    if (B > 0) hipLaunchKernelGGL(k_gauss_jordan, dim3(B), dim3(256), 0, s, A, aug, fac, res, n);
+    return hipGetLastError();
+}
 hipError_t launch_axpy(float* A, const float* B, float sign, int n, hipStream_t s) {
     if (n > 0) hipLaunchKernelGGL(k_axpy, dim3(cdiv(n, 256)), dim3(256), 0, s, A, B, sign, n);
     return hipGetLastError();
@@ -1274,12 +1350,34 @@ hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* re
 
 size_t solve_single_lds_bytes(int ldq, int ldm) { return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm); }
 
-hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s) {
+static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm);
     if (a.N <= 64)
-        hipLaunchKernelGGL(k_solve_single<64>, dim3(1), dim3(64), lds, s, a, st);
+        hipLaunchKernelGGL(k_solve_single<64>, dim3(B), dim3(64), lds, s, a, st);
     else
-        hipLaunchKernelGGL(k_solve_single<256>, dim3(1), dim3(256), lds, s, a, st);
+        hipLaunchKernelGGL(k_solve_single<256>, dim3(B), dim3(256), lds, s, a, st);
+    return hipGetLastError();
+}
+hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s) {
+    return launch_single_grid(1, a, st, s);
+}
+
+// path: 0 tiny (N, M <= 32), 1 LDS-staged small, 2 global-memory single
+hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    if (path == 0) return launch_tiny_grid(B, a, st, s);
+    if (path == 1) return launch_small_grid(B, a, st, s);
+    return launch_single_grid(B, a, st, s);
+}
+
+__global__ void k_extract_state(int B, const SolveState* __restrict__ st, long long* __restrict__ h,
+                                int* __restrict__ status) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    if (h) h[b] = st[b].h;
+    if (status) status[b] = st[b].status;
+}
+hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s) {
+    hipLaunchKernelGGL(k_extract_state, dim3(cdiv(B, 256)), dim3(256), 0, s, B, st, h, status);
     return hipGetLastError();
 }
 

@@ -22,11 +22,14 @@ struct SolveState {
 
 // All device pointers.  Qd row-major N x N (Jd's Y'Qd row), QdT column-major
 // (ldq) for the update, Gp row-major N x M, Qinv/Qp row-major M x M.
+// Batched: workgroup b solves problem b; every array holds B problems back to
+// back (row-major per problem, strides N*N, N, 1, M*M, ... ; QdT N*ldq).
 struct SolveArgs {
     const float *QdT, *Qd, *theta, *Fd, *Md, *Qp, *Qinv, *Fp, *Mp, *Gp, *Kp;
     float *Y, *U;
     int N, M, ldq, ldm, mode;
     long long num_iter, max_updates, chunk;
+    int* pending;  // optional: +1 per problem still running when a launch ends
 };
 
 hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
@@ -54,6 +57,16 @@ size_t solve_single_lds_bytes(int ldq, int ldm);
 size_t solve_small_lds_bytes(int N, int M);
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);  // N, M <= 32
+// batched forms: grid = B problems (states st[0..B-1])
+hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
+hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);
+hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const float* Bm, int tB, int a, int b,
+                               int c, long long sA, long long sB, long long sO, hipStream_t s);
+hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, long long sA, long long sB,
+                         hipStream_t s);
+hipError_t launch_negate_b(int B, float* A, int n, long long sA, hipStream_t s);
+hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp, long long sMp6, hipStream_t s);
+hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
 void set_variant(int v);
 int get_variant();
 hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,

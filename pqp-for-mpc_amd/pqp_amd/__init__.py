@@ -69,6 +69,12 @@ SIGNATURES = {
     "pqp_batch_update": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp, _vp]),
     "pqp_batch_iterate": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp,
                                     C.c_int, _vp]),
+    "pqp_batch_gauss_jordan": (C.c_int, [C.c_int, C.c_int, _vp, _vp, _vp]),
+    "pqp_batch_convert_to_dual": (C.c_int, [C.c_int] * 3 + [_vp] * 8 + [_vp]),
+    "pqp_batch_compute_fp": (C.c_int, [C.c_int] * 4 + [_vp] * 6 + [_vp]),
+    "pqp_batch_compute_mp": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [_vp]),
+    "pqp_batch_solve": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [C.c_int, C.c_longlong, C.c_longlong] + [_vp] * 4
+                        + [_vp]),
     # include/pqp_tuning.h
     "pqp_tune_set_variant": (C.c_int, [C.c_int]),
     "pqp_tune_stream_read": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, C.c_int, _vp]),
@@ -398,3 +404,103 @@ class Batch:
         """Problem b's Qd back in the reference's row-major layout (host)."""
         qt = self.QdT[b * self.qstride:(b + 1) * self.qstride].reshape(self.N, self.ldq)[:, : self.N]
         return qt.t().contiguous().cpu().numpy().reshape(-1)
+
+
+class ProblemBatch:
+    """B independent dual problems of sizes (N, M) resident in HBM, solved one
+    workgroup per problem (pqp_batch_* of include/pqp.h).  Arrays follow the
+    reference's row-major layout per problem, stacked: Qd [B, N*N], Fd [B, N],
+    Md [B], Qp / Qp_inv [B, M*M], Fp [B, M], Mp [B], Gp [B, N*M], Kp [B, N]."""
+
+    PRIMAL = ("Qp_inv", "Gp", "Kp", "Fp", "Mp")
+    DUAL = ("Qd", "Fd", "Md")
+
+    def __init__(self, B: int, N: int, M: int, device=None):
+        import torch
+
+        self.torch = torch
+        self.B, self.N, self.M = int(B), int(N), int(M)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        f = dict(dtype=torch.float32, device=self.device)
+        B, N, M = self.B, self.N, self.M
+        self.Qd, self.Fd, self.Md = torch.zeros(B, N * N, **f), torch.zeros(B, N, **f), torch.zeros(B, **f)
+        self.Qp, self.Qp_inv = torch.zeros(B, M * M, **f), torch.zeros(B, M * M, **f)
+        self.Fp, self.Mp = torch.zeros(B, M, **f), torch.zeros(B, **f)
+        self.Gp, self.Kp = torch.zeros(B, N * M, **f), torch.zeros(B, N, **f)
+        self.Y, self.U = torch.zeros(B, N, **f), torch.zeros(B, M, **f)
+        self.h = torch.zeros(B, dtype=torch.int64, device=self.device)
+        self.status = torch.zeros(B, dtype=torch.int32, device=self.device)
+
+    def _s(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def _p(t):
+        return C.c_void_p(t.data_ptr())
+
+    @classmethod
+    def replicate(cls, P: dict, B: int, device=None) -> "ProblemBatch":
+        """B copies of one problem dict (keys of solve_dual)."""
+        pb = cls(B, int(P["N"]), int(P["M"]), device)
+        for k in cls.PRIMAL + cls.DUAL + ("Qp",):
+            if k in P:
+                v = pb.torch.as_tensor(np.asarray(P[k], np.float32).reshape(-1), device=pb.device)
+                getattr(pb, k).copy_(v.expand(B, -1) if getattr(pb, k).dim() == 2 else v.expand(B))
+        return pb
+
+    def set(self, name: str, values):
+        """Per-problem values for one array ([B, ...] numpy/torch)."""
+        t = getattr(self, name)
+        t.copy_(self.torch.as_tensor(np.asarray(values, np.float32) if not self.torch.is_tensor(values) else values,
+                                     device=self.device).reshape(t.shape))
+        return self
+
+    def gauss_jordan(self):
+        """Qp = inverse(Qp_inv) per problem (Gauss_Jordan, PQP_CPU.c:251)."""
+        _check(lib().pqp_batch_gauss_jordan(self.B, self.M, self._p(self.Qp_inv), self._p(self.Qp), self._s()))
+        return self
+
+    def convert_to_dual(self):
+        """Qd, Fd, Md from the primal data (convertToDual, PQP_CPU.c:489)."""
+        _check(lib().pqp_batch_convert_to_dual(self.B, self.N, self.M, *[self._p(getattr(self, k)) for k in
+                                                                         self.PRIMAL + self.DUAL], self._s()))
+        return self
+
+    def solve(self, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0):
+        """solveQuadraticDual for every problem; fills Y, U, h, status."""
+        _check(lib().pqp_batch_solve(self.B, self.N, self.M, *[self._p(getattr(self, k)) for k in
+                                                              ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp",
+                                                               "Kp")],
+                                     mode, num_iter, max_updates, self._p(self.Y), self._p(self.U), self._p(self.h),
+                                     self._p(self.status), self._s()))
+        return self
+
+
+def mpc_batch(directory, states, device=None) -> ProblemBatch:
+    """The bundled plant (example/*.txt) at B different states x (and the
+    file's disturbance D): per-problem Fp = Fp1 D + Fp2 x - Fp3 and Mp
+    (computeFp / computeMp), shared Qp_inv, Gp, Kp, then Qp and the duals --
+    all on the GPU.  `states` is [B, nState]."""
+    import torch
+
+    E = read_example(directory)
+    xs = np.ascontiguousarray(np.asarray(states, np.float32).reshape(len(states), -1))
+    B, ns = xs.shape
+    if ns != E["ns"]:
+        raise ValueError(f"states must have {E['ns']} columns")
+    pb = ProblemBatch(B, E["N"], E["M"], device)
+    dev = pb.device
+    T = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=dev).contiguous()  # noqa: E731
+    plant = {k: T(E[k]) for k in ("Fp1", "Fp2", "Fp3", "Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6")}
+    x = T(xs)
+    D = T(np.tile(E["D"], (B, 1)))
+    for k in ("Qp_inv", "Gp", "Kp"):
+        getattr(pb, k).copy_(T(E[k]).reshape(1, -1).expand(B, -1))
+    p = ProblemBatch._p
+    s = pb._s()
+    _check(lib().pqp_batch_compute_fp(B, E["M"], E["nd"], ns, p(plant["Fp1"]), p(plant["Fp2"]), p(plant["Fp3"]),
+                                      p(D), p(x), p(pb.Fp), s))
+    _check(lib().pqp_batch_compute_mp(B, E["nd"], ns, *[p(plant[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5",
+                                                                                "Mp6")], p(D), p(x), p(pb.Mp), s))
+    pb.gauss_jordan().convert_to_dual()
+    return pb

@@ -339,3 +339,109 @@ def test_reference_main_linked_against_libpqp(tmp_path):
     out = subprocess.run([str(exe)], cwd=tmp_path, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout == (GOLDEN / "bundled_stdout.txt").read_text()
+
+
+# ---------------------------------------------------------------------------
+# batched small problems (one workgroup per problem): F1 setup + F2 solve
+# ---------------------------------------------------------------------------
+def test_problem_batch_replicated_bundled(gpu_lib, golden_bundled):
+    g = golden_bundled
+    pb = gpu_lib.ProblemBatch.replicate(bundled_problem(g), 300)
+    pb.solve(max_updates=CAP)
+    h = pb.h.cpu().numpy()
+    assert np.all(h == 313) and np.all(pb.status.cpu().numpy() == 1)
+    Y, U = pb.Y.cpu().numpy(), pb.U.cpu().numpy()
+    for b in (0, 1, 150, 299):
+        assert_bitwise(Y[b], g["Ystar"], f"Y* problem {b}")
+        assert_bitwise(U[b], g["Ustar"], f"U problem {b}")
+    pb.solve(gpu_lib.MODE_FIXED, num_iter=1000)
+    assert np.all(pb.h.cpu().numpy() == 1000)
+    assert_bitwise(pb.Y.cpu().numpy()[299], g["Y_fixed999"], "fixed-999")
+
+
+def test_batched_setup_from_primal(gpu_lib, golden_bundled):
+    """Batched Gauss_Jordan + convertToDual on device reproduce the reference's
+    dual of the bundled problem."""
+    g = golden_bundled
+    pb = gpu_lib.ProblemBatch.replicate({k: g[k] for k in ("Qp_inv", "Gp", "Kp", "Fp", "Mp")} |
+                                        dict(N=int(g["N"]), M=int(g["M"])), 5)
+    pb.gauss_jordan().convert_to_dual()
+    for name in ("Qd", "Fd", "Qp"):
+        assert_bitwise(getattr(pb, name).cpu().numpy()[4], g[name], name)
+    assert_bitwise(pb.Md.cpu().numpy()[4:5], g["Md"], "Md")
+
+
+def _oracle_example_at_state(orc, x):
+    """main()'s setup (PQP_CPU.c:988-994) with the state x replaced."""
+    import ctypes as C
+
+    from oracle import _p, f32
+
+    E = orc.load_example(EXAMPLE_DIR)
+    N, M, nd, ns = E["N"], E["M"], E["nd"], E["ns"]
+    x = f32(x)
+    Fp, Mp = np.zeros(M, np.float32), np.zeros(1, np.float32)
+    orc.lib.orc_compute_fp(_p(Fp), _p(E["Fp1"]), _p(E["Fp2"]), _p(E["Fp3"]), _p(E["D"]), _p(x), M, nd, ns)
+    orc.lib.orc_compute_mp(_p(Mp), *[_p(E[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "D")], _p(x), nd, ns)
+    Qd, Fd, Md = orc.convert_to_dual(E["Qp_inv"], E["Gp"], E["Kp"], Fp, Mp, N, M)
+    return dict(Qd=Qd, Fd=Fd, Md=Md, Qp=orc.gauss_jordan(E["Qp_inv"], M), Qp_inv=E["Qp_inv"], Fp=Fp, Mp=Mp,
+                Gp=E["Gp"], Kp=E["Kp"], N=N, M=M)
+
+
+def test_mpc_batch_of_states_vs_oracle(gpu_lib, orc):
+    """The bundled plant at 64 different states x: per-problem computeFp /
+    computeMp / convertToDual / solve on the GPU == the oracle, including h."""
+    E = orc.load_example(EXAMPLE_DIR)
+    rng = np.random.default_rng(5)
+    xs = (E["x"][None, :] * (1.0 + 0.05 * rng.standard_normal((64, E["ns"])))).astype(np.float32)
+    pb = gpu_lib.mpc_batch(EXAMPLE_DIR, xs)
+    pb.solve(max_updates=CAP)
+    h, st = pb.h.cpu().numpy(), pb.status.cpu().numpy()
+    Y, Fp, Mp = pb.Y.cpu().numpy(), pb.Fp.cpu().numpy(), pb.Mp.cpu().numpy()
+    for b in (0, 7, 33, 63):
+        P = _oracle_example_at_state(orc, xs[b])
+        assert_bitwise(Fp[b], P["Fp"], f"Fp {b}")
+        assert_bitwise(Mp[b:b + 1], P["Mp"], f"Mp {b}")
+        hr, Yr, _ = orc.solve(P, max_updates=CAP)
+        assert st[b] == (1 if hr > 0 else 2) and h[b] == abs(hr), (b, h[b], hr)
+        assert_bitwise(Y[b], Yr, f"Y {b}")
+
+
+def test_batched_synthetic_converge_groups(gpu_lib, golden_converge, orc):
+    cases, Ys = golden_converge["cases"], golden_converge["Y"]
+    offs = np.concatenate([[0], np.cumsum(cases[:, 0])])
+    groups = {}
+    for idx, (N, M, seed, h) in enumerate(cases):
+        groups.setdefault((int(N), int(M)), []).append((idx, int(seed), int(h)))
+    for (N, M), items in groups.items():
+        pb = gpu_lib.ProblemBatch(len(items), N, M)
+        for j, (idx, seed, _) in enumerate(items):
+            P = orc.synth_problem(seed, 0, N, M)
+            for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
+                getattr(pb, k)[j] = pb.torch.as_tensor(P[k].reshape(-1), device=pb.device)
+        pb.solve(max_updates=CAP)
+        for j, (idx, seed, h) in enumerate(items):
+            assert int(pb.h[j]) == h, (N, M, seed)
+            assert_bitwise(pb.Y[j].cpu().numpy(), Ys[offs[idx]:offs[idx] + N], f"{N}/{M}/{seed}")
+
+
+@pytest.mark.parametrize("N,M", [(48, 24), (120, 60)])
+def test_batched_larger_paths(gpu_lib, orc, N, M):
+    """LDS-staged (N=48) and global-memory (N=120) batched paths, fixed and
+    capped-converge modes, vs the oracle."""
+    B = 6
+    pb = gpu_lib.ProblemBatch(B, N, M)
+    Ps = [orc.synth_problem(21, j, N, M) for j in range(B)]
+    for j, P in enumerate(Ps):
+        for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
+            getattr(pb, k)[j] = pb.torch.as_tensor(P[k].reshape(-1), device=pb.device)
+    pb.solve(gpu_lib.MODE_FIXED, num_iter=30)
+    for j in (0, B - 1):
+        _, Yr, _ = orc.solve(Ps[j], mode=1, num_iter=30)
+        assert_bitwise(pb.Y[j].cpu().numpy(), Yr, f"fixed {j}")
+    pb.solve(max_updates=40)
+    for j in (0, B - 1):
+        hr, Yr, Ur = orc.solve(Ps[j], max_updates=40)
+        assert int(pb.h[j]) == abs(hr)
+        assert_bitwise(pb.Y[j].cpu().numpy(), Yr, f"capped {j}")
+        assert_bitwise(pb.U[j].cpu().numpy(), Ur, f"U {j}")
