@@ -146,6 +146,18 @@ int pqp_read_example(const char *dir, int m, int nd, int ns, float *Qp_inv, floa
                      float *Fp3, float *Mp1, float *Mp2, float *Mp3, float *Mp4, float *Mp5, float *Mp6,
                      float *Gp, float *Kp, float *x, float *D);
 
+/* The testing/ sample-test format ("testing/sample test/test*.txt"; reader at
+ * testing/GPU unoptimized version/PQP_GPU_unoptimized.cu:751-794 and
+ * testing/CPU version/PQP_CPU_test.c:936-978): header "M N", M diagonal
+ * entries of Qp_inv, M of Fp, Mp, N of Kp, N x M integers for Gp mapped by C's
+ * `v % 3` (0 -> 0, 2 -> -1, otherwise +1, so a file -1 becomes +1).  With
+ * glibc_kp != 0 the file's Kp is replaced, as the harness does, by
+ * fabs(10.0*rand()/RAND_MAX) from glibc's unseeded rand() sequence.
+ * Call with NULL arrays to get (*M_out, *N_out) first; Qp_inv is M x M dense.
+ * (Host I/O; no GPU work.) */
+int pqp_read_testfile(const char *path, int glibc_kp, int *M_out, int *N_out, float *Qp_inv, float *Fp, float *Mp,
+                      float *Gp, float *Kp);
+
 /* main() of PQP_CPU.c:935-1013 on the GPU: read `dir`, build the dual, solve,
  * recompute U, print the reference's stdout to `out` (a FILE*; NULL = stdout). */
 int pqp_run_example(const char *dir, void *out);

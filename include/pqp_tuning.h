@@ -21,6 +21,10 @@ int pqp_tune_set_variant(int variant);
 int pqp_tune_stream_read(int B, int N, const float *d_QdT, int ldq, long long qstride, float *d_out, int nontemporal,
                          void *stream);
 
+/* The first n values of glibc's unseeded rand() as reproduced by the
+ * testing/ reader (for checking the emulation against the C library). */
+int pqp_tune_glibc_rand(int n, int *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,7 @@ HERE = Path(__file__).resolve().parent
 ORACLE_SO = HERE / "_build" / "liboracle.so"
 REF_SO = HERE / "_ref" / "libpqp_ref.so"
 REF_BIN = HERE / "_ref" / "pqp_cpu_ref"
+REF_TEST_SO = HERE / "_ref" / "libpqp_ref_test.so"
 
 # Bundled-example dimensions: PQP_CPU.c:13-17 (pHorizon=1, nState=29, nInput=7,
 # nOutput=7, nDis=1) -> M = 7 primal, N = 28 dual (PQP_CPU.c:940-941).
@@ -341,3 +342,38 @@ class Reference:
             text = tf.read().decode()
         h = int(text.strip().split("=")[-1])
         return h, Y, U
+
+
+class ReferenceTesting:
+    """testing/CPU version/PQP_CPU_test.c compiled unmodified (main renamed):
+    its input() is the reference reader of the testing/ sample files
+    (PQP_CPU_test.c:936-978), including the glibc-rand Kp overwrite."""
+
+    def __init__(self, path: Path = REF_TEST_SO):
+        if not Path(path).exists():
+            raise FileNotFoundError(f"{path} not built (needs /root/reference)")
+        self.lib = C.CDLL(str(path))
+        self.lib.input.argtypes = [_fp] * 9 + [C.c_int, C.c_int, C.c_void_p]
+        self.libc = C.CDLL(None)
+        self.libc.fopen.restype = C.c_void_p
+        self.libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+        self.libc.fclose.argtypes = [C.c_void_p]
+
+    def read_testfile(self, path) -> dict:
+        fp = self.libc.fopen(str(path).encode(), b"r")
+        if not fp:
+            raise FileNotFoundError(path)
+        try:
+            M, N = C.c_int(0), C.c_int(0)
+            self.libc.fscanf(C.c_void_p(fp), b"%d%d", C.byref(M), C.byref(N))  # the commented-out main's header read
+            M, N = M.value, N.value
+            z = lambda n: np.zeros(n, np.float32)  # noqa: E731
+            P = dict(Qp_inv=z(M * M), Fp=z(M), Mp=z(1), Gp=z(N * M), Kp=z(N))
+            dummy = [z(64) for _ in range(4)]
+            self.libc.srand(1)  # a fresh process's rand() state (the harness never seeds)
+            self.lib.input(_p(P["Qp_inv"]), _p(P["Fp"]), _p(P["Mp"]), _p(P["Gp"]), _p(P["Kp"]),
+                           *[_p(d) for d in dummy], N, M, C.c_void_p(fp))
+        finally:
+            self.libc.fclose(fp)
+        P.update(N=N, M=M)
+        return P

@@ -479,6 +479,24 @@ int pqp_read_example(const char* dir, int m, int nd, int ns, float* Qp_inv, floa
     return PQP_OK;
 }
 
+int pqp_read_testfile(const char* path, int glibc_kp, int* M_out, int* N_out, float* Qp_inv, float* Fp, float* Mp,
+                      float* Gp, float* Kp) {
+    if (!path) return set_error(PQP_ERR_ARG, "pqp_read_testfile: null path");
+    TestfileData t;
+    PQP_TRY(read_testfile(path, glibc_kp != 0, t));
+    if (M_out) *M_out = t.M;
+    if (N_out) *N_out = t.N;
+    auto put = [](float* dst, const std::vector<float>& v) {
+        if (dst) std::memcpy(dst, v.data(), v.size() * sizeof(float));
+    };
+    put(Qp_inv, t.Qp_inv);
+    put(Fp, t.Fp);
+    put(Mp, t.Mp);
+    put(Gp, t.Gp);
+    put(Kp, t.Kp);
+    return PQP_OK;
+}
+
 int pqp_run_example(const char* dir, void* out_file) {
     FILE* out = out_file ? static_cast<FILE*>(out_file) : stdout;
     ExampleData e;
@@ -1036,6 +1054,11 @@ extern "C" int pqp_tune_set_variant(int variant) {
     pqp::set_variant(variant & 0xff);
     pqp::g_force_small = (variant & 0x100) != 0;
     return old;
+}
+
+extern "C" int pqp_tune_glibc_rand(int n, int* out) {
+    if (n < 0 || (n > 0 && !out)) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_glibc_rand: bad arguments");
+    return pqp::glibc_rand_sequence(n, out);
 }
 
 extern "C" int pqp_tune_stream_read(int B, int N, const float* d_QdT, int ldq, long long qstride, float* d_out,

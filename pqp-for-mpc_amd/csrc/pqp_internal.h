@@ -34,6 +34,14 @@ struct ExampleData {
 int read_example(const char* dir, int m, int nd, int ns, ExampleData& e);
 int read_unused_example(const char* dir, int ns, int no, int nd, float* Z, float* theta7);
 
+// testing/ sample-test file (see pqp_io.cpp).
+struct TestfileData {
+    int M = 0, N = 0;
+    std::vector<float> Qp_inv, Fp, Mp, Kp, Gp;
+};
+int read_testfile(const char* path, bool glibc_kp, TestfileData& t);
+int glibc_rand_sequence(int n, int* out);
+
 // Reference compile-time dimensions (PQP_CPU.c:13-17).
 constexpr int kRefPHorizon = 1, kRefNState = 29, kRefNInput = 7, kRefNOutput = 7, kRefNDis = 1;
 

@@ -3,6 +3,8 @@
 // example/*.txt (PQP_CPU.c:757-930): each file is one line of `%f` tokens;
 // matrices are listed transposed, i.e. the file's (outer, inner) listing puts
 // token o*inner + in at element [in][o] of the row-major matrix.
+#include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -79,6 +81,86 @@ int read_unused_example(const char* dir, int ns, int no, int nd, float* Z, float
     int rc;
     if (Z && (rc = read_transposed(d + "/Z.txt", Z, ns, no))) return rc;
     if (theta7 && (rc = read_transposed(d + "/Theta.txt", theta7, nd, no))) return rc;
+    return PQP_OK;
+}
+
+// glibc rand() from its default seed (srand(1)): the TYPE_3 additive-feedback
+// generator, r[i] = r[i-3] + r[i-31] (mod 2^32), output r[i] >> 1, with the
+// first 310 outputs discarded.  The testing/ harness overwrites Kp with
+// fabs(10.0*rand()/RAND_MAX) (testing/GPU unoptimized version/
+// PQP_GPU_unoptimized.cu:775) without seeding, i.e. this sequence.
+class GlibcRand {
+   public:
+    explicit GlibcRand(uint32_t seed = 1) {
+        int32_t r[34];
+        r[0] = (int32_t)(seed ? seed : 1);
+        for (int i = 1; i < 31; ++i) {
+            const int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+            int64_t w = 16807 * lo - 2836 * hi;
+            if (w < 0) w += 2147483647;
+            r[i] = (int32_t)w;
+        }
+        for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+        for (int i = 0; i < 34; ++i) ring_[i] = (uint32_t)r[i];
+        n_ = 34;
+        for (int i = 0; i < 310; ++i) next();
+    }
+    int next() {
+        const uint32_t v = ring_[(n_ - 31) % 34] + ring_[(n_ - 3) % 34];
+        ring_[n_ % 34] = v;
+        ++n_;
+        return (int)(v >> 1);
+    }
+
+   private:
+    uint32_t ring_[34];
+    uint64_t n_;
+};
+
+// testing/ sample-test file (written by testing/test_generator.c:936-987, read
+// by testing/GPU unoptimized version/PQP_GPU_unoptimized.cu:751-794 and
+// testing/CPU version/PQP_CPU_test.c:936-978): "M N", M diagonal entries of
+// Qp_inv, M of Fp, Mp, N of Kp, then N x M integers for Gp.
+int read_testfile(const char* path, bool glibc_kp, TestfileData& t) {
+    FILE* f = std::fopen(path, "r");
+    if (!f) return set_error(PQP_ERR_IO, "cannot open %s", path);
+    auto fail = [&](const char* what) {
+        std::fclose(f);
+        return set_error(PQP_ERR_IO, "%s: short or malformed file (%s)", path, what);
+    };
+    int M = 0, N = 0;
+    if (std::fscanf(f, "%d%d", &M, &N) != 2 || M <= 0 || N <= 0) return fail("header");
+    t.M = M;
+    t.N = N;
+    t.Qp_inv.assign((size_t)M * M, 0.0f);
+    t.Fp.assign(M, 0.0f);
+    t.Mp.assign(1, 0.0f);
+    t.Kp.assign(N, 0.0f);
+    t.Gp.assign((size_t)N * M, 0.0f);
+    for (int i = 0; i < M; ++i)
+        if (std::fscanf(f, "%f", &t.Qp_inv[(size_t)i * M + i]) != 1) return fail("Qp_inv");
+    for (int i = 0; i < M; ++i)
+        if (std::fscanf(f, "%f", &t.Fp[i]) != 1) return fail("Fp");
+    if (std::fscanf(f, "%f", &t.Mp[0]) != 1) return fail("Mp");
+    for (int i = 0; i < N; ++i)
+        if (std::fscanf(f, "%f", &t.Kp[i]) != 1) return fail("Kp");
+    GlibcRand rng(1);
+    for (int i = 0; i < N; ++i) {
+        if (glibc_kp) t.Kp[i] = (float)std::fabs(10.0 * rng.next() / 2147483647.0);  // RAND_MAX
+        for (int j = 0; j < M; ++j) {
+            int v = 0;
+            if (std::fscanf(f, "%d", &v) != 1) return fail("Gp");
+            // C remainder: -1 % 3 == -1, so a file value of -1 maps to +1 (the quirk)
+            t.Gp[(size_t)i * M + j] = (v % 3 == 0) ? 0.0f : ((v % 3 == 2) ? -1.0f : 1.0f);
+        }
+    }
+    std::fclose(f);
+    return PQP_OK;
+}
+
+int glibc_rand_sequence(int n, int* out) {
+    GlibcRand rng(1);
+    for (int i = 0; i < n; ++i) out[i] = rng.next();
     return PQP_OK;
 }
 

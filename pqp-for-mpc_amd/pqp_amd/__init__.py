@@ -62,6 +62,7 @@ SIGNATURES = {
     "pqp_update_host": (C.c_int, [_fp] * 5 + [C.c_int]),
     "pqp_read_example": (C.c_int, [C.c_char_p] + [C.c_int] * 3 + [_fp] * 14),
     "pqp_run_example": (C.c_int, [C.c_char_p, _vp]),
+    "pqp_read_testfile": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)] + [_fp] * 5),
     "pqp_batch_generate": (C.c_int, [C.c_uint32, C.c_longlong, C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_longlong,
                                      _vp, _vp, _vp, C.c_int, _vp]),
     "pqp_batch_pack": (C.c_int, [C.c_int, C.c_int, _vp, _vp, C.c_int, C.c_longlong, _vp]),
@@ -77,6 +78,7 @@ SIGNATURES = {
                         + [_vp]),
     # include/pqp_tuning.h
     "pqp_tune_set_variant": (C.c_int, [C.c_int]),
+    "pqp_tune_glibc_rand": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
     "pqp_tune_stream_read": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, C.c_int, _vp]),
 }
 
@@ -276,6 +278,33 @@ def read_example(directory, m=N_INPUT * P_HORIZON, nd=N_DIS * P_HORIZON, ns=N_ST
     _check(lib().pqp_read_example(str(directory).encode(), m, nd, ns, *[_buf(arr[k]) for k in order]))
     arr.update(N=N, M=m, nd=nd, ns=ns)
     return arr
+
+
+def read_testfile(path, glibc_kp: bool = True) -> dict:
+    """testing/ sample-test file (pqp_read_testfile).  No GPU work."""
+    M, N = C.c_int(0), C.c_int(0)
+    _check(lib().pqp_read_testfile(str(path).encode(), int(glibc_kp), C.byref(M), C.byref(N), None, None, None, None,
+                                   None))
+    M, N = M.value, N.value
+    arr = dict(Qp_inv=np.zeros(M * M, np.float32), Fp=np.zeros(M, np.float32), Mp=np.zeros(1, np.float32),
+               Gp=np.zeros(N * M, np.float32), Kp=np.zeros(N, np.float32))
+    _check(lib().pqp_read_testfile(str(path).encode(), int(glibc_kp), None, None,
+                                   *[_buf(arr[k]) for k in ("Qp_inv", "Fp", "Mp", "Gp", "Kp")]))
+    arr.update(N=N, M=M)
+    return arr
+
+
+def testfile_problem(path, glibc_kp: bool = True) -> dict:
+    """A testing/ sample-test file as a dual problem, setup on the GPU
+    (Gauss_Jordan, convertToDual)."""
+    P = read_testfile(path, glibc_kp)
+    N, M = P["N"], P["M"]
+    Qp = np.zeros(M * M, np.float32)
+    Gauss_Jordan(P["Qp_inv"], Qp, M)
+    Qd, Fd, Md = np.zeros(N * N, np.float32), np.zeros(N, np.float32), np.zeros(1, np.float32)
+    convertToDual(Qd, Fd, Md, P["Qp_inv"], P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+    P.update(Qp=Qp, Qd=Qd, Fd=Fd, Md=Md)
+    return P
 
 
 def example_problem(directory) -> dict:

@@ -28,7 +28,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "oracle"))
-from oracle import Oracle, Reference, REF_BIN, build  # noqa: E402
+from oracle import Oracle, Reference, ReferenceTesting, REF_BIN, build  # noqa: E402
 
 OUT = Path(__file__).resolve().parent
 REFERENCE_DIR = Path("/root/reference")
@@ -136,12 +136,31 @@ def synth_large(ref: Reference, orc: Oracle):
     np.savez(OUT / "synth_large.npz", **out)
 
 
+def testing_files(ref: Reference):
+    """testing/ sample file test2.txt (M=100, N=400) read by the reference's own
+    reader (PQP_CPU_test.c input()), converted and iterated by PQP_CPU.c."""
+    rt = ReferenceTesting()
+    P = rt.read_testfile(OUT / "testing" / "test2.txt")
+    N, M = P["N"], P["M"]
+    Qd, Fd, Md = ref.convert_to_dual(P["Qp_inv"], P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+    Qp = ref.gauss_jordan(P["Qp_inv"], M)
+    S = ref.split(Qd, Fd, N)
+    Y = np.full(N, 1000.0, np.float32)
+    for _ in range(20):
+        Y = ref.update(Y, S, Fd, N)
+    np.savez_compressed(OUT / "testing_test2.npz", N=np.int64(N), M=np.int64(M), Qp_inv=P["Qp_inv"], Fp=P["Fp"], Mp=P["Mp"],
+             Gp=P["Gp"], Kp=P["Kp"], Qd_sha256=np.frombuffer(bytes.fromhex(digest(Qd)), np.uint8), Fd=Fd, Md=Md,
+             Qp=Qp, theta=S["theta"].reshape(N, N).diagonal().copy(), Y20=Y)
+    print("testing/test2.txt: M", M, "N", N)
+
+
 def main():
     build()
     ref, orc = Reference(), Oracle()
     bundled(ref)
     synth_converge(ref, orc)
     synth_large(ref, orc)
+    testing_files(ref)
 
 
 if __name__ == "__main__":

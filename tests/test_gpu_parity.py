@@ -445,3 +445,26 @@ def test_batched_larger_paths(gpu_lib, orc, N, M):
         assert int(pb.h[j]) == abs(hr)
         assert_bitwise(pb.Y[j].cpu().numpy(), Yr, f"capped {j}")
         assert_bitwise(pb.U[j].cpu().numpy(), Ur, f"U {j}")
+
+
+# ---------------------------------------------------------------------------
+# testing/ sample file (F3): reader -> GPU setup -> GPU iterations
+# ---------------------------------------------------------------------------
+def test_testfile_problem_vs_reference(gpu_lib, orc):
+    g = dict(np.load(GOLDEN / "testing_test2.npz"))
+    P = gpu_lib.testfile_problem(GOLDEN / "testing" / "test2.txt")
+    N, M = P["N"], P["M"]
+    assert hashlib.sha256(P["Qd"].tobytes()).digest() == g["Qd_sha256"].tobytes()
+    for k in ("Fd", "Md", "Qp"):
+        assert_bitwise(P[k], g[k], k)
+    with gpu_lib.Problem(P) as prob:
+        r = prob.solve(gpu_lib.MODE_FIXED, num_iter=21)
+        assert_bitwise(r["Y"], g["Y20"], "Y after 20 updates (solver)")
+        c = prob.solve(max_updates=150)
+    b = gpu_lib.Batch(1, N).load(P["Qd"][None, :], P["Fd"][None, :])
+    assert_bitwise(b.theta[0, :N].cpu().numpy(), g["theta"], "theta")
+    assert_bitwise(b.iterate(20).result()[0], g["Y20"], "Y after 20 updates (batched kernel)")
+    hr, Yr, Ur = orc.solve(P, max_updates=150)
+    assert c["h"] == abs(hr)
+    assert_bitwise(c["Y"], Yr, "converge-capped Y")
+    assert_bitwise(c["U"], Ur, "converge-capped U")
