@@ -233,6 +233,7 @@ struct pqp_problem {
     bool small = false;  // fits k_solve_small (everything staged in LDS)
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
+    pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     ~pqp_problem() {
@@ -244,7 +245,8 @@ namespace pqp {
 namespace {
 
 constexpr size_t kLdsBudget = 150 * 1024;
-bool g_force_small = false;  // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
+bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
+bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -289,9 +291,35 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 // Run the persistent solve kernel until it reports Done/Capped.  Each launch
 // is bounded (chunk updates) so no launch runs unbounded.  `resume` = start
 // from P.Y instead of Y = 1000 (used by the terminate() drop-in, mode 2).
+// Fixed mode of a large problem: one multi-workgroup launch per update
+// (k_split_update), the stored split matrices built once per problem.
+int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
+    const int N = P.N;
+    if (!P.SP.p) {
+        PQP_TRY(P.SP.floats((size_t)2 * N * N));
+        PQP_TRY(P.fdpn.floats((size_t)2 * N));
+        PQP_TRY(P.Yb.floats(N));
+        PQP_HIP(launch_build_split(P.Qd.f(), P.theta.f(), P.Fd.f(), N, P.SP.f(), P.fdpn.f(), s));
+    }
+    float* a = P.Y.f();
+    float* b = P.Yb.f();
+    PQP_HIP(launch_fill(a, 1000.0f, N, s));  // initMat(Y, 1000) :710
+    const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
+    for (long long u = 0; u < updates; ++u) {
+        PQP_HIP(launch_split_update(P.SP.f(), P.fdpn.f(), N, a, b, s));
+        std::swap(a, b);
+    }
+    if (a != P.Y.f()) PQP_HIP(hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    out.h = updates + 1;
+    out.status = kStatusDone;
+    return PQP_OK;
+}
+
 int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_updates, bool resume, SolveOut& out,
                 hipStream_t s) {
     const int N = P.N, M = P.M;
+    if (mode == kModeFixed && !P.small && !g_force_single && !resume) return problem_run_fixed_split(P, num_iter, out, s);
     SolveState& st = *P.hst;
     st = SolveState{};
     st.h = 1;
@@ -1050,9 +1078,10 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 #include "../../include/pqp_tuning.h"
 
 extern "C" int pqp_tune_set_variant(int variant) {
-    const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0);
+    const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0);
     pqp::set_variant(variant & 0xff);
     pqp::g_force_small = (variant & 0x100) != 0;
+    pqp::g_force_single = (variant & 0x200) != 0;
     return old;
 }
 

@@ -25,6 +25,8 @@
 
 namespace pqp {
 
+static inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
 // ---------------------------------------------------------------------------
 // Row-update building blocks
 // ---------------------------------------------------------------------------
@@ -267,6 +269,85 @@ __global__ void __launch_bounds__(256) k_update_split(const float* __restrict__ 
     num = num + 1.0f * Fdn[i];
     den = den + 1.0f * Fdp[i];
     Ynext[i] = num / den * Y[i];
+}
+
+// ---------------------------------------------------------------------------
+// Single large problem, fixed mode, spread over many workgroups (BASELINE
+// configs[2]).  The reference's two stored split matrices are kept (8 N^2 B),
+// interleaved so lane p = 2i + side owns row i's numerator (side 0,
+// Qdn_theta) or denominator (side 1, Qdp_theta): SP[k][2N] holds
+// (max(0,-q_ik)+t, max(0,q_ik)+t) for every row i.  At a fixed k a wave reads
+// 256 contiguous bytes; each lane's k order is the reference's.  The
+// per-iteration floor is one lane's N-long mul/add chain, so rows are spread
+// over ceil(2N/64) single-wave workgroups (32 CUs at N = 1024).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Qd, const float* __restrict__ theta,
+                                                     const float* __restrict__ Fd, int N, float* __restrict__ SP,
+                                                     float* __restrict__ fdpn) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e < (long long)N * N) {
+        const int i = (int)(e / N), k = (int)(e % N);
+        const float q = Qd[e];
+        const float t = (i == k) ? theta[i] : 0.0f;
+        SP[(size_t)k * 2 * N + 2 * i + 0] = max_ref(0.0f, -q) + 1.0f * t;  // computeQdn_theta :533-537
+        SP[(size_t)k * 2 * N + 2 * i + 1] = max_ref(0.0f, q) + 1.0f * t;   // computeQdp_theta :524-528
+    }
+    if (e < N) {
+        fdpn[2 * e + 0] = max_ref(0.0f, -Fd[e]);  // Fdn :704
+        fdpn[2 * e + 1] = max_ref(0.0f, Fd[e]);   // Fdp :703
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
+                                                     int N, const float* __restrict__ Yin, float* __restrict__ Yout) {
+    extern __shared__ __attribute__((aligned(16))) float ys[];
+    for (int k = threadIdx.x; k < N; k += 64) ys[k] = Yin[k];
+    __syncthreads();
+    const int twoN = 2 * N;
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    float acc = 0.0f;
+    if (p < twoN) {
+        const float* col = SP + p;
+        int k = 0;
+        for (; k + U <= N; k += U) {
+            float q[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) q[j] = col[(size_t)(k + j) * twoN];
+#pragma unroll
+            for (int j = 0; j < U; ++j) acc += q[j] * ys[k + j];  // :608-609, k in order
+        }
+        for (; k < N; ++k) acc += col[(size_t)k * twoN] * ys[k];
+    }
+    const float other = __shfl_xor(acc, 1);  // full wave active
+    if (!(p & 1) && p < twoN) {
+        const int i = p >> 1;
+        const float num = acc + 1.0f * fdpn[p];        // :611
+        const float den = other + 1.0f * fdpn[p + 1];  // :612
+        Yout[i] = num / den * ys[i];                   // :594
+    }
+}
+
+hipError_t launch_build_split(const float* Qd, const float* theta, const float* Fd, int N, float* SP, float* fdpn,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_build_split, dim3(cdiv((long long)N * N, 256)), dim3(256), 0, s, Qd, theta, Fd, N, SP, fdpn);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
+                               hipStream_t s) {
+    const size_t lds = sizeof(float) * (size_t)((N + 3) & ~3);
+    hipLaunchKernelGGL((k_split_update<16>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
+    return hipGetLastError();
+}
+
+__global__ void k_fill(float* __restrict__ a, float v, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) a[i] = v;
+}
+hipError_t launch_fill(float* a, float v, int n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_fill, dim3(cdiv(n, 256)), dim3(256), 0, s, a, v, n);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -1197,7 +1278,6 @@ hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s)
 // ---------------------------------------------------------------------------
 // Host-side launchers (declared in pqp_launch.h)
 // ---------------------------------------------------------------------------
-static inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
 static int g_variant = 0;  // tuning knob (include/pqp_tuning.h); 0 = shipped default
 void set_variant(int v) { g_variant = v; }

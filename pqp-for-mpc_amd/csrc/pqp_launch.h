@@ -57,6 +57,12 @@ size_t solve_single_lds_bytes(int ldq, int ldm);
 size_t solve_small_lds_bytes(int N, int M);
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);  // N, M <= 32
+// single large problem, fixed mode, multi-workgroup (stored split matrices)
+hipError_t launch_build_split(const float* Qd, const float* theta, const float* Fd, int N, float* SP, float* fdpn,
+                              hipStream_t s);
+hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
+                               hipStream_t s);
+hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
 // batched forms: grid = B problems (states st[0..B-1])
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);

@@ -97,6 +97,28 @@ def test_single_problem_paths(gpu_lib, orc, N, M):
     assert_bitwise(c["U"], U2, f"U N={N}")
 
 
+@pytest.mark.parametrize("N", [99, 257, 1000])
+def test_large_fixed_split_vs_single_workgroup(gpu_lib, orc, N):
+    """Fixed mode of a large problem: the multi-workgroup split-matrix path
+    (default) and the one-workgroup solver (tuning bit 0x200) give the same
+    bits as the oracle."""
+    M = N // 2
+    P = orc.synth_problem(8, 1, N, M, with_qp=False)
+    P.update(Qp=np.zeros(M * M, np.float32))
+    _, Yr, _ = orc.solve(P, mode=1, num_iter=12)
+    L = gpu_lib.lib()
+    with gpu_lib.Problem(P) as prob:
+        a = prob.solve(gpu_lib.MODE_FIXED, num_iter=12)
+        old = L.pqp_tune_set_variant(0x200)
+        try:
+            b = prob.solve(gpu_lib.MODE_FIXED, num_iter=12)
+        finally:
+            L.pqp_tune_set_variant(old)
+    assert a["h"] == b["h"] == 12
+    assert_bitwise(a["Y"], Yr, "split path")
+    assert_bitwise(b["Y"], Yr, "single-workgroup path")
+
+
 def test_dropin_solveQuadraticDual_prints_h(gpu_lib, golden_bundled, capfd):
     g = golden_bundled
     P = bundled_problem(g)
