@@ -234,9 +234,12 @@ struct pqp_problem {
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
+    hipGraphExec_t graph = nullptr;                  // captured fixed-mode launch sequence
+    long long graph_updates = -1;
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     ~pqp_problem() {
+        if (graph) (void)hipGraphExecDestroy(graph);
         if (hst) (void)hipHostFree(hst);
     }
 };
@@ -301,15 +304,37 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
         PQP_TRY(P.Yb.floats(N));
         PQP_HIP(launch_build_split(P.Qd.f(), P.theta.f(), P.Fd.f(), N, P.SP.f(), P.fdpn.f(), s));
     }
-    float* a = P.Y.f();
-    float* b = P.Yb.f();
-    PQP_HIP(launch_fill(a, 1000.0f, N, s));  // initMat(Y, 1000) :710
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
-    for (long long u = 0; u < updates; ++u) {
-        PQP_HIP(launch_split_update(P.SP.f(), P.fdpn.f(), N, a, b, s));
-        std::swap(a, b);
+    // The whole launch sequence (fill, `updates` dependent updates, final copy)
+    // is captured once into a hipGraph and replayed: per-update host launch
+    // overhead would otherwise exceed the kernel itself.
+    if (!P.graph || P.graph_updates != updates) {
+        if (P.graph) {
+            (void)hipGraphExecDestroy(P.graph);
+            P.graph = nullptr;
+        }
+        hipGraph_t g = nullptr;
+        PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        float* a = P.Y.f();
+        float* b = P.Yb.f();
+        hipError_t e = launch_fill(a, 1000.0f, N, s);  // initMat(Y, 1000) :710
+        for (long long u = 0; u < updates && e == hipSuccess; ++u) {
+            e = launch_split_update(P.SP.f(), P.fdpn.f(), N, a, b, s);
+            std::swap(a, b);
+        }
+        if (e == hipSuccess && a != P.Y.f())
+            e = hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s);
+        const hipError_t e2 = hipStreamEndCapture(s, &g);
+        if (e != hipSuccess || e2 != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            PQP_HIP(e != hipSuccess ? e : e2);
+        }
+        const hipError_t e3 = hipGraphInstantiate(&P.graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        PQP_HIP(e3);
+        P.graph_updates = updates;
     }
-    if (a != P.Y.f()) PQP_HIP(hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+    PQP_HIP(hipGraphLaunch(P.graph, s));
     PQP_HIP(hipStreamSynchronize(s));
     out.h = updates + 1;
     out.status = kStatusDone;
