@@ -308,16 +308,35 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
     const int p = blockIdx.x * 64 + threadIdx.x;
     float acc = 0.0f;
     if (p < twoN) {
+        // two register stages of U loads: the next stage's loads are in flight
+        // while the current one is consumed (the operands come from L2/MALL
+        // at ~0.5k-cycle latency; the add order stays k = 0..N-1)
         const float* col = SP + p;
+        const size_t step = (size_t)twoN;
+        float qa[U], qb[U];
         int k = 0;
-        for (; k + U <= N; k += U) {
-            float q[U];
+        if (N >= U) {
 #pragma unroll
-            for (int j = 0; j < U; ++j) q[j] = col[(size_t)(k + j) * twoN];
-#pragma unroll
-            for (int j = 0; j < U; ++j) acc += q[j] * ys[k + j];  // :608-609, k in order
+            for (int j = 0; j < U; ++j) qa[j] = col[(size_t)j * step];
         }
-        for (; k < N; ++k) acc += col[(size_t)k * twoN] * ys[k];
+        for (; k + 2 * U <= N; k += 2 * U) {
+#pragma unroll
+            for (int j = 0; j < U; ++j) qb[j] = col[(size_t)(k + U + j) * step];
+#pragma unroll
+            for (int j = 0; j < U; ++j) acc += qa[j] * ys[k + j];
+            if (k + 3 * U <= N) {
+#pragma unroll
+                for (int j = 0; j < U; ++j) qa[j] = col[(size_t)(k + 2 * U + j) * step];
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) acc += qb[j] * ys[k + U + j];
+        }
+        if (k + U <= N) {  // one staged block left (qa holds k..k+U-1)
+#pragma unroll
+            for (int j = 0; j < U; ++j) acc += qa[j] * ys[k + j];
+            k += U;
+        }
+        for (; k < N; ++k) acc += col[(size_t)k * step] * ys[k];
     }
     const float other = __shfl_xor(acc, 1);  // full wave active
     if (!(p & 1) && p < twoN) {
@@ -337,7 +356,7 @@ hipError_t launch_build_split(const float* Qd, const float* theta, const float* 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
                                hipStream_t s) {
     const size_t lds = sizeof(float) * (size_t)((N + 3) & ~3);
-    hipLaunchKernelGGL((k_split_update<16>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
+    hipLaunchKernelGGL((k_split_update<32>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
     return hipGetLastError();
 }
 
