@@ -308,25 +308,29 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
     const int p = blockIdx.x * 64 + threadIdx.x;
     float acc = 0.0f;
     if (p < twoN) {
-        // two register stages of U loads: the next stage's loads are in flight
-        // while the current one is consumed (the operands come from L2/MALL
-        // at ~0.5k-cycle latency; the add order stays k = 0..N-1)
-        const float* col = SP + p;
-        const size_t step = (size_t)twoN;
+        // Buffer loads: wave-uniform descriptor, the lane's column in voffset
+        // and the row k's byte offset in an SGPR (soffset), so the 64-bit
+        // per-load address chain of a flat load disappears from the VALU.
+        // Two register stages of U loads keep ~2U loads in flight.
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(SP), (short)0, 0x7fffffff, 0x00020000);
+        const int vo = p * 4;
+        const int rowb = twoN * 4;
         float qa[U], qb[U];
         int k = 0;
         if (N >= U) {
 #pragma unroll
-            for (int j = 0; j < U; ++j) qa[j] = col[(size_t)j * step];
+            for (int j = 0; j < U; ++j) qa[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * rowb, 0);
         }
         for (; k + 2 * U <= N; k += 2 * U) {
 #pragma unroll
-            for (int j = 0; j < U; ++j) qb[j] = col[(size_t)(k + U + j) * step];
+            for (int j = 0; j < U; ++j) qb[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (k + U + j) * rowb, 0);
 #pragma unroll
             for (int j = 0; j < U; ++j) acc += qa[j] * ys[k + j];
             if (k + 3 * U <= N) {
 #pragma unroll
-                for (int j = 0; j < U; ++j) qa[j] = col[(size_t)(k + 2 * U + j) * step];
+                for (int j = 0; j < U; ++j)
+                    qa[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (k + 2 * U + j) * rowb, 0);
             }
 #pragma unroll
             for (int j = 0; j < U; ++j) acc += qb[j] * ys[k + U + j];
@@ -336,7 +340,7 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
             for (int j = 0; j < U; ++j) acc += qa[j] * ys[k + j];
             k += U;
         }
-        for (; k < N; ++k) acc += col[(size_t)k * step] * ys[k];
+        for (; k < N; ++k) acc += __builtin_amdgcn_raw_buffer_load_b32(rs, vo, k * rowb, 0) * ys[k];
     }
     const float other = __shfl_xor(acc, 1);  // full wave active
     if (!(p & 1) && p < twoN) {
