@@ -299,7 +299,7 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     if (!P.SP.p) {
-        PQP_TRY(P.SP.floats((size_t)2 * N * N));
+        PQP_TRY(P.SP.floats(split_floats(N)));
         PQP_TRY(P.fdpn.floats((size_t)2 * N));
         PQP_TRY(P.Yb.floats(N));
         PQP_HIP(launch_build_split(P.Qd.f(), P.theta.f(), P.Fd.f(), N, P.SP.f(), P.fdpn.f(), s));

@@ -273,24 +273,34 @@ __global__ void __launch_bounds__(256) k_update_split(const float* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // Single large problem, fixed mode, spread over many workgroups (BASELINE
-// configs[2]).  The reference's two stored split matrices are kept (8 N^2 B),
-// interleaved so lane p = 2i + side owns row i's numerator (side 0,
-// Qdn_theta) or denominator (side 1, Qdp_theta): SP[k][2N] holds
-// (max(0,-q_ik)+t, max(0,q_ik)+t) for every row i.  At a fixed k a wave reads
-// 256 contiguous bytes; each lane's k order is the reference's.  The
-// per-iteration floor is one lane's N-long mul/add chain, so rows are spread
-// over ceil(2N/64) single-wave workgroups (32 CUs at N = 1024).
+// configs[2]).  The reference's two stored split matrices are kept (8 N^2 B):
+// lane p = 2i + side owns row i's numerator (side 0, Qdn_theta) or
+// denominator (side 1, Qdp_theta).  Layout: 4-k packets, SP[kb][p][4] =
+// row-i side-s entries for k = 4kb..4kb+3, so each lane loads one dwordx4 per
+// four k and a wave reads 1 KiB contiguous per load (k >= N padded with +0,
+// an exact no-op).  The per-iteration floor is one lane's N-long mul/add chain
+// plus the bytes one CU can pull from L2/MALL, so rows are spread over
+// ceil(2N/64) single-wave workgroups (32 CUs at N = 1024).
 // ---------------------------------------------------------------------------
+__host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
+
 __global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Qd, const float* __restrict__ theta,
                                                      const float* __restrict__ Fd, int N, float* __restrict__ SP,
                                                      float* __restrict__ fdpn) {
-    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (e < (long long)N * N) {
-        const int i = (int)(e / N), k = (int)(e % N);
-        const float q = Qd[e];
-        const float t = (i == k) ? theta[i] : 0.0f;
-        SP[(size_t)k * 2 * N + 2 * i + 0] = max_ref(0.0f, -q) + 1.0f * t;  // computeQdn_theta :533-537
-        SP[(size_t)k * 2 * N + 2 * i + 1] = max_ref(0.0f, q) + 1.0f * t;   // computeQdp_theta :524-528
+    const int KB = split_kblocks(N);
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (i, k) with k < 4*KB
+    if (e < (long long)N * 4 * KB) {
+        const int i = (int)(e / (4 * KB)), k = (int)(e % (4 * KB));
+        float qn = 0.0f, qp = 0.0f;
+        if (k < N) {
+            const float q = Qd[(size_t)i * N + k];
+            const float t = (i == k) ? theta[i] : 0.0f;
+            qn = max_ref(0.0f, -q) + 1.0f * t;  // computeQdn_theta :533-537
+            qp = max_ref(0.0f, q) + 1.0f * t;   // computeQdp_theta :524-528
+        }
+        const size_t base = ((size_t)(k >> 2) * 2 * N + 2 * i) * 4 + (k & 3);
+        SP[base] = qn;      // lane 2i
+        SP[base + 4] = qp;  // lane 2i + 1
     }
     if (e < N) {
         fdpn[2 * e + 0] = max_ref(0.0f, -Fd[e]);  // Fdn :704
@@ -302,45 +312,52 @@ template <int U>
 __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                      int N, const float* __restrict__ Yin, float* __restrict__ Yout) {
     extern __shared__ __attribute__((aligned(16))) float ys[];
-    for (int k = threadIdx.x; k < N; k += 64) ys[k] = Yin[k];
+    const int KB = split_kblocks(N);
+    for (int k = threadIdx.x; k < 4 * KB; k += 64) ys[k] = (k < N) ? Yin[k] : 0.0f;
     __syncthreads();
     const int twoN = 2 * N;
     const int p = blockIdx.x * 64 + threadIdx.x;
     float acc = 0.0f;
     if (p < twoN) {
-        // Buffer loads: wave-uniform descriptor, the lane's column in voffset
-        // and the row k's byte offset in an SGPR (soffset), so the 64-bit
-        // per-load address chain of a flat load disappears from the VALU.
-        // Two register stages of U loads keep ~2U loads in flight.
+        // buffer loads: wave-uniform descriptor, lane offset in voffset, the
+        // k-block offset in an SGPR; two register stages of U packets in flight
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(SP), (short)0, 0x7fffffff, 0x00020000);
-        const int vo = p * 4;
-        const int rowb = twoN * 4;
-        float qa[U], qb[U];
-        int k = 0;
-        if (N >= U) {
+        const int vo = p * 16;
+        const int blkb = twoN * 16;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * blkb, 0); };
+        auto use = [&](f4v q, int kb) {
+            const float4 y = *reinterpret_cast<const float4*>(ys + 4 * kb);
+            acc += q.x * y.x;  // :608-609, k in order
+            acc += q.y * y.y;
+            acc += q.z * y.z;
+            acc += q.w * y.w;
+        };
+        f4v qa[U], qb[U];
+        int kb = 0;
+        if (KB >= U) {
 #pragma unroll
-            for (int j = 0; j < U; ++j) qa[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * rowb, 0);
+            for (int j = 0; j < U; ++j) qa[j] = ld(j);
         }
-        for (; k + 2 * U <= N; k += 2 * U) {
+        for (; kb + 2 * U <= KB; kb += 2 * U) {
 #pragma unroll
-            for (int j = 0; j < U; ++j) qb[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (k + U + j) * rowb, 0);
+            for (int j = 0; j < U; ++j) qb[j] = ld(kb + U + j);
 #pragma unroll
-            for (int j = 0; j < U; ++j) acc += qa[j] * ys[k + j];
-            if (k + 3 * U <= N) {
+            for (int j = 0; j < U; ++j) use(qa[j], kb + j);
+            if (kb + 3 * U <= KB) {
 #pragma unroll
-                for (int j = 0; j < U; ++j)
-                    qa[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (k + 2 * U + j) * rowb, 0);
+                for (int j = 0; j < U; ++j) qa[j] = ld(kb + 2 * U + j);
             }
 #pragma unroll
-            for (int j = 0; j < U; ++j) acc += qb[j] * ys[k + U + j];
+            for (int j = 0; j < U; ++j) use(qb[j], kb + U + j);
         }
-        if (k + U <= N) {  // one staged block left (qa holds k..k+U-1)
+        if (kb + U <= KB) {  // one staged block left
 #pragma unroll
-            for (int j = 0; j < U; ++j) acc += qa[j] * ys[k + j];
-            k += U;
+            for (int j = 0; j < U; ++j) use(qa[j], kb + j);
+            kb += U;
         }
-        for (; k < N; ++k) acc += __builtin_amdgcn_raw_buffer_load_b32(rs, vo, k * rowb, 0) * ys[k];
+        for (; kb < KB; ++kb) use(ld(kb), kb);
     }
     const float other = __shfl_xor(acc, 1);  // full wave active
     if (!(p & 1) && p < twoN) {
@@ -351,16 +368,19 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
     }
 }
 
+size_t split_floats(int N) { return (size_t)split_kblocks(N) * 4 * 2 * N; }
+
 hipError_t launch_build_split(const float* Qd, const float* theta, const float* Fd, int N, float* SP, float* fdpn,
                               hipStream_t s) {
-    hipLaunchKernelGGL(k_build_split, dim3(cdiv((long long)N * N, 256)), dim3(256), 0, s, Qd, theta, Fd, N, SP, fdpn);
+    hipLaunchKernelGGL(k_build_split, dim3(cdiv((long long)N * 4 * split_kblocks(N), 256)), dim3(256), 0, s, Qd,
+                       theta, Fd, N, SP, fdpn);
     return hipGetLastError();
 }
 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
                                hipStream_t s) {
-    const size_t lds = sizeof(float) * (size_t)((N + 3) & ~3);
-    hipLaunchKernelGGL((k_split_update<32>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
+    const size_t lds = sizeof(float) * (size_t)4 * split_kblocks(N);
+    hipLaunchKernelGGL((k_split_update<8>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
     return hipGetLastError();
 }
 
