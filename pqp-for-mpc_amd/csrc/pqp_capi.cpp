@@ -233,7 +233,7 @@ struct pqp_problem {
     bool small = false;  // fits k_solve_small (everything staged in LDS)
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
-    pqp::DevBuf SP, fdpn, Ysp, Yb;                   // large path, fixed mode (built on first use)
+    pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
     hipGraphExec_t graph = nullptr;                  // captured fixed-mode launch sequence
     long long graph_updates = -1;
     pqp::DevBuf Y, U, state;
@@ -301,11 +301,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     if (!P.SP.p) {
         PQP_TRY(P.SP.floats(split_floats(N)));
         PQP_TRY(P.fdpn.floats((size_t)2 * N));
-        const size_t npad = (size_t)round4(N);  // the update reads y in 4-k packets: tail must be +0
-        PQP_TRY(P.Yb.floats(npad));
-        PQP_TRY(P.Ysp.floats(npad));
-        PQP_HIP(hipMemsetAsync(P.Yb.p, 0, sizeof(float) * npad, s));
-        PQP_HIP(hipMemsetAsync(P.Ysp.p, 0, sizeof(float) * npad, s));
+        PQP_TRY(P.Yb.floats(N));
         PQP_HIP(launch_build_split(P.Qd.f(), P.theta.f(), P.Fd.f(), N, P.SP.f(), P.fdpn.f(), s));
     }
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
@@ -319,14 +315,15 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
         }
         hipGraph_t g = nullptr;
         PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        float* a = P.Ysp.f();
+        float* a = P.Y.f();
         float* b = P.Yb.f();
         hipError_t e = launch_fill(a, 1000.0f, N, s);  // initMat(Y, 1000) :710
         for (long long u = 0; u < updates && e == hipSuccess; ++u) {
             e = launch_split_update(P.SP.f(), P.fdpn.f(), N, a, b, s);
             std::swap(a, b);
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess && a != P.Y.f())
+            e = hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s);
         const hipError_t e2 = hipStreamEndCapture(s, &g);
         if (e != hipSuccess || e2 != hipSuccess) {
             if (g) (void)hipGraphDestroy(g);

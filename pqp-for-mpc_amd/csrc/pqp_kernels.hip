@@ -311,15 +311,16 @@ __global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Q
 template <int U>
 __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                      int N, const float* __restrict__ Yin, float* __restrict__ Yout) {
+    extern __shared__ __attribute__((aligned(16))) float ys[];
     const int KB = split_kblocks(N);
+    for (int k = threadIdx.x; k < 4 * KB; k += 64) ys[k] = (k < N) ? Yin[k] : 0.0f;
+    __syncthreads();
     const int twoN = 2 * N;
     const int p = blockIdx.x * 64 + threadIdx.x;
     float acc = 0.0f;
-    // y[k] is wave-uniform: it is read with scalar loads straight into SGPRs
-    // (VALU operands), so there is no LDS staging, no barrier, and the Qd
-    // packet stream starts at kernel entry.  Yin must hold 4*KB floats with
-    // the tail (k >= N) zero.
     if (p < twoN) {
+        // buffer loads: wave-uniform descriptor, lane offset in voffset, the
+        // k-block offset in an SGPR; two register stages of U packets in flight
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(SP), (short)0, 0x7fffffff, 0x00020000);
         const int vo = p * 16;
@@ -327,7 +328,7 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
         typedef float f4v __attribute__((ext_vector_type(4)));
         auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * blkb, 0); };
         auto use = [&](f4v q, int kb) {
-            const float4 y = *reinterpret_cast<const float4*>(Yin + 4 * kb);
+            const float4 y = *reinterpret_cast<const float4*>(ys + 4 * kb);
             acc += q.x * y.x;  // :608-609, k in order
             acc += q.y * y.y;
             acc += q.z * y.z;
@@ -363,7 +364,7 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
         const int i = p >> 1;
         const float num = acc + 1.0f * fdpn[p];        // :611
         const float den = other + 1.0f * fdpn[p + 1];  // :612
-        Yout[i] = num / den * Yin[i];                  // :594
+        Yout[i] = num / den * ys[i];                   // :594
     }
 }
 
@@ -378,7 +379,8 @@ hipError_t launch_build_split(const float* Qd, const float* theta, const float* 
 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
                                hipStream_t s) {
-    hipLaunchKernelGGL((k_split_update<8>), dim3(cdiv(2LL * N, 64)), dim3(64), 0, s, SP, fdpn, N, Yin, Yout);
+    const size_t lds = sizeof(float) * (size_t)4 * split_kblocks(N);
+    hipLaunchKernelGGL((k_split_update<8>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
     return hipGetLastError();
 }
 
