@@ -16,7 +16,8 @@ extern "C" {
  * launch_batch_iterate).  Bit 0x100: solve N, M <= 32 problems with the
  * LDS-staged k_solve_small instead of k_solve_tiny.  Bit 0x200: fixed-mode
  * solves of large single problems on one workgroup (k_solve_single) instead
- * of the multi-workgroup k_split_update.  Returns the previous value. */
+ * of the multi-workgroup k_split_update.  Bits 12-13: k_split_update load
+ * stage depth (0: 16 packets, 1: 8, 2: 24).  Returns the previous value. */
 int pqp_tune_set_variant(int variant);
 
 /* Stream B problems' QdT with the hot kernel's exact access pattern and no

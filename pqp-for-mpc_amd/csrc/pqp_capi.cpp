@@ -1103,8 +1103,10 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 #include "../../include/pqp_tuning.h"
 
 extern "C" int pqp_tune_set_variant(int variant) {
-    const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0);
+    const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0) |
+                    (pqp::g_split_u << 12);
     pqp::set_variant(variant & 0xff);
+    pqp::g_split_u = (variant >> 12) & 3;
     pqp::g_force_small = (variant & 0x100) != 0;
     pqp::g_force_single = (variant & 0x200) != 0;
     return old;

@@ -309,7 +309,7 @@ __global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Q
 }
 
 template <int U>
-__global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
+__global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                      int N, const float* __restrict__ Yin, float* __restrict__ Yout) {
     extern __shared__ __attribute__((aligned(16))) float ys[];
     const int KB = split_kblocks(N);
@@ -368,6 +368,7 @@ __global__ void __launch_bounds__(64) k_split_update(const float* __restrict__ S
     }
 }
 
+int g_split_u = 0;  // tuning: k_split_update stage depth (0: 16, 1: 8, 2: 24)
 size_t split_floats(int N) { return (size_t)split_kblocks(N) * 4 * 2 * N; }
 
 hipError_t launch_build_split(const float* Qd, const float* theta, const float* Fd, int N, float* SP, float* fdpn,
@@ -380,7 +381,14 @@ hipError_t launch_build_split(const float* Qd, const float* theta, const float* 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
                                hipStream_t s) {
     const size_t lds = sizeof(float) * (size_t)4 * split_kblocks(N);
-    hipLaunchKernelGGL((k_split_update<8>), dim3(cdiv(2LL * N, 64)), dim3(64), lds, s, SP, fdpn, N, Yin, Yout);
+    // one wave per CU with most of the register file as a 2-stage load buffer:
+    // a lane's packet stream is latency-bound (Little's law) with few in flight
+    const dim3 grid(cdiv(2LL * N, 64));
+    switch (g_split_u) {
+        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, Yin, Yout); break;
+        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, Yin, Yout); break;
+        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, Yin, Yout); break;
+    }
     return hipGetLastError();
 }
 

@@ -64,6 +64,7 @@ hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const 
                                hipStream_t s);
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
 size_t split_floats(int N);  // size of the packed split matrices
+extern int g_split_u;        // tuning: k_split_update stage depth selector
 // batched forms: grid = B problems (states st[0..B-1])
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);

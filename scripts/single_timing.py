@@ -29,7 +29,7 @@ def main(N: int = 1024, iters: int = 1000, reps: int = 5):
     out = {"n_dual": N, "iterations": iters}
     with pqp_amd.Problem(P) as prob:
         ys = {}
-        for name, var in (("split_multi_wg", 0), ("single_wg", 0x200)):
+        for name, var in (("split_multi_wg", 0), ("split_u8", 0x1000), ("split_u24", 0x2000), ("single_wg", 0x200)):
             L.pqp_tune_set_variant(var)
             prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
             t0 = time.perf_counter()
