@@ -23,6 +23,7 @@ Extra keys:
                 C ABI: fixed 1000-iteration mode and converge mode (h = 313)
   mpc_batch     16384 MPC problems (bundled plant at perturbed states), one
                 workgroup each, converge mode with device-side terminate()
+  single_n1024  configs[2]: one n_dual=1024 problem, 1000 fixed iterations
   gather_ms     RCCL gather of every rank's Y* to rank 0 (outside the timed
                 region)
 
@@ -158,6 +159,31 @@ def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
                     "on device, excluded from the timing; each solve bit-exact with PQP_CPU.c (tests)"}
 
 
+def single_bench(pqp_amd, N: int = 1024, iters: int = 1000) -> dict:
+    """configs[2]: ONE synthetic n_dual=1024 problem, 1000 fixed-mode
+    iterations, through pqp_problem_solve (multi-workgroup k_split_update,
+    graph-replayed).  The 8 MB of stored split matrices stay in L2/MALL, so
+    this is latency- not HBM-bound (single-instance caveat)."""
+    import numpy as np
+
+    M = N // 2
+    b = pqp_amd.Batch(1, N).generate(seed=1, inst0=0, M=M)
+    P = dict(Qd=b.qd_rowmajor(0), Fd=b.Fd[0, :N].cpu().numpy(), Md=b.Md[:1].cpu().numpy(),
+             Qp=np.zeros(M * M, np.float32), Qp_inv=np.zeros(M * M, np.float32), Fp=np.zeros(M, np.float32),
+             Mp=np.zeros(1, np.float32), Gp=np.zeros(N * M, np.float32), Kp=np.zeros(N, np.float32), N=N, M=M)
+    del b
+    with pqp_amd.Problem(P) as prob:
+        prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
+        dt = (time.perf_counter() - t0) / reps
+    return {"n_dual": N, "iterations": iters, "ms_per_solve": dt * 1e3, "iter_per_s": (iters - 1) / dt,
+            "alg_GBps_split_matrices": 8.0 * N * N * (iters - 1) / dt / 1e9,
+            "note": "1 problem, fixed mode; per-iteration floor = one lane's N-long sequential sum"}
+
+
 def main():
     args = parse()
     import torch
@@ -270,6 +296,7 @@ def main():
     if world == 1 and not args.no_bundled:
         result["bundled"] = bundled_bench(pqp_amd)
         result["mpc_batch"] = mpc_batch_bench(pqp_amd)
+        result["single_n1024"] = single_bench(pqp_amd)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed)
     print(json.dumps(result), flush=True)

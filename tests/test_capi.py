@@ -134,3 +134,24 @@ def test_reference_main_driver_links_libpqp_first():
                       "computeUfromY", "computeCost"}
     assert called_by_main <= ours
     assert all(f" {n}\n" in ref_syms for n in called_by_main)
+
+
+def test_dropin_input_reads_example_from_cwd(tmp_path, monkeypatch, orc):
+    """input() (PQP_CPU.c:757) reads ./example relative to the CWD; host I/O."""
+    import shutil
+
+    import pqp_amd
+
+    shutil.copytree(EXAMPLE_DIR, tmp_path / "example")
+    monkeypatch.chdir(tmp_path)
+    m, nd, ns, no = 7, 1, 29, 7
+    z = lambda n: np.zeros(n, np.float32)  # noqa: E731
+    A = dict(qp_inv=z(m * m), Fp1=z(m * nd), Fp2=z(m * ns), Fp3=z(m), Mp1=z(ns * ns), Mp2=z(nd * ns), Mp3=z(nd * nd),
+             Mp4=z(ns), Mp5=z(nd), Mp6=z(1), Gp=z(4 * m * m), Kp=z(4 * m), x=z(ns), D=z(nd), theta=z(no * nd),
+             Z=z(no * ns))
+    pqp_amd.lib().input(*[pqp_amd._buf(v) for v in A.values()])
+    exp = orc.load_example(tmp_path / "example")
+    assert_bitwise(A["qp_inv"], exp["Qp_inv"], "Qp_inv")
+    for k in ("Fp1", "Fp2", "Fp3", "Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "Gp", "Kp", "x", "D"):
+        assert_bitwise(A[k], exp[k], k)
+    assert A["Z"].any()  # read although unused by the solver (PQP_CPU.c:889-899)

@@ -490,3 +490,49 @@ def test_testfile_problem_vs_reference(gpu_lib, orc):
     assert c["h"] == abs(hr)
     assert_bitwise(c["Y"], Yr, "converge-capped Y")
     assert_bitwise(c["U"], Ur, "converge-capped U")
+
+
+# ---------------------------------------------------------------------------
+# non-finite and signed-zero propagation: the lean form must match the
+# reference's literal (max(0,+-q)+0.0f)*y arithmetic bit for bit
+# ---------------------------------------------------------------------------
+def _same_bits_or_both_nan(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all(nan | (a.view(np.uint32) == b.view(np.uint32))))
+
+
+@pytest.mark.parametrize("N", [7, 300, 1030])
+def test_update_special_values_vs_oracle(gpu_lib, orc, N):
+    rng = np.random.default_rng(N)
+    Qd = rng.standard_normal((N, N)).astype(np.float32)
+    Qd[rng.random((N, N)) < 0.1] = 0.0
+    Qd[rng.random((N, N)) < 0.05] = -0.0
+    Qd[rng.random((N, N)) < 0.002] = np.nan
+    Qd = Qd.reshape(-1)
+    Fd = rng.standard_normal(N).astype(np.float32)
+    Fd[::7] = -0.0
+    th = orc.theta(Qd, N)
+    for trial in range(3):
+        Y = (rng.random(N) * 100).astype(np.float32)
+        if trial >= 1:
+            Y[rng.integers(0, N, 3)] = np.inf
+            Y[rng.integers(0, N, 2)] = 0.0
+        if trial == 2:
+            Y[rng.integers(0, N, 2)] = np.nan
+        want = orc.update(Y, Qd, th, Fd, N)
+        got = gpu_lib.update(Qd, th, Fd, Y, N)  # k_batch_update (lean + literal window)
+        assert _same_bits_or_both_nan(got, want), f"N={N} trial={trial}"
+        b = gpu_lib.Batch(1, N).load(Qd[None, :], Fd[None, :])
+        b.Y[0, :N] = b.torch.as_tensor(Y, device=b.device)
+        b.iterate(1, from_start=False)
+        assert _same_bits_or_both_nan(b.result()[0], want), f"iterate N={N} trial={trial}"
+
+
+def test_pqp_update_host_vs_golden(gpu_lib, golden_bundled):
+    g = golden_bundled
+    N = int(g["N"])
+    Y = g["Y_h1"]
+    for h in range(1, 10):
+        Y = gpu_lib.update(g["Qd"], g["theta"], g["Fd"], Y, N)
+    assert_bitwise(Y, g["Y_h10"], "9 updates via pqp_update_host")
