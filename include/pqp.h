@@ -225,6 +225,40 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
                     int mode, long long num_iter, long long max_updates, float *d_Y, float *d_U, long long *d_h,
                     int *d_status, void *stream);
 
+/* ----------------------------------------------------------------------
+ * 2d. Row blocks of one large problem (a single problem
+ * row-sharded across GPUs).  A pqp_rowblock holds rows [row0, row0+rows) of
+ * updateY2's stored split matrices (PQP_CPU.c:524-537 Qdp_theta/Qdn_theta
+ * rows, :703-704 Fdp/Fdn) on the current device.  One step reads the FULL
+ * iterate Y (N, device) and writes the block's rows of Y_next
+ * (PQP_CPU.c:603-618 restricted to those rows); between steps the caller
+ * assembles Y_next from every block (e.g. an RCCL all-gather).  Every row's
+ * sums still run over k = 0..N-1 in order, so the assembled Y_next is
+ * bit-identical to updateY2's whatever the partition.  N <= 38400 (the full
+ * y is staged in LDS).
+ * -------------------------------------------------------------------- */
+typedef struct pqp_rowblock pqp_rowblock;
+
+/* d_Qd_rows: the block's rows of Qd, row-major with leading dimension ld >= N
+ * (a pointer into a full row-major Qd works); d_Fd: the full Fd (N).  Theta_ii
+ * of the block's rows is computed from them (computeTheta, PQP_CPU.c:503-519).
+ * The inputs may be freed once this returns.  rows == 0 gives an empty block
+ * whose update is a no-op. */
+int pqp_rowblock_create(const float *d_Qd_rows, int ld, const float *d_Fd, int N, int row0, int rows, void *stream,
+                        pqp_rowblock **out);
+/* d_Y_rows[i] = updateY2(Y)[row0 + i] for i < rows.  d_Y must hold N floats
+ * (more is allowed and ignored).  Async on `stream`. */
+int pqp_rowblock_update(pqp_rowblock *b, const float *d_Y, float *d_Y_rows, void *stream);
+int pqp_rowblock_destroy(pqp_rowblock *b);
+
+/* Rows [row0, row0+rows) of synthetic problem `inst` of `seed` (the
+ * generator of pqp_batch_generate), row-major with leading dimension ld >= N
+ * (columns N..ld-1 zeroed), so that a rank can build its row block without
+ * materialising the whole N x N matrix.  d_Fd (N) and d_Md (1) receive the
+ * full Fd / Md when not NULL. */
+int pqp_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float *d_Qd_rows, int ld,
+                   float *d_Fd, float *d_Md, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

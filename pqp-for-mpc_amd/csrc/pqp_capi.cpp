@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -244,6 +245,12 @@ struct pqp_problem {
     }
 };
 
+// One row block of a large problem's stored split matrices (pqp_rowblock_*).
+struct pqp_rowblock {
+    int N = 0, row0 = 0, rows = 0;
+    pqp::DevBuf SP, fdpn;
+};
+
 namespace pqp {
 namespace {
 
@@ -299,10 +306,13 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     if (!P.SP.p) {
-        PQP_TRY(P.SP.floats(split_floats(N)));
+        if (split_lds_bytes(N) > kLdsBudget)
+            return set_error(PQP_ERR_ARG, "fixed-mode solve: N=%d needs more than %zu B of LDS", N, kLdsBudget);
+        PQP_TRY(P.SP.floats(split_floats(N, N)));
         PQP_TRY(P.fdpn.floats((size_t)2 * N));
         PQP_TRY(P.Yb.floats(N));
-        PQP_HIP(launch_build_split(P.Qd.f(), P.theta.f(), P.Fd.f(), N, P.SP.f(), P.fdpn.f(), s));
+        PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N), s));
+        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, P.SP.f(), P.fdpn.f(), s));
     }
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
     // The whole launch sequence (fill, `updates` dependent updates, final copy)
@@ -319,7 +329,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
         float* b = P.Yb.f();
         hipError_t e = launch_fill(a, 1000.0f, N, s);  // initMat(Y, 1000) :710
         for (long long u = 0; u < updates && e == hipSuccess; ++u) {
-            e = launch_split_update(P.SP.f(), P.fdpn.f(), N, a, b, s);
+            e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, a, b, s);
             std::swap(a, b);
         }
         if (e == hipSuccess && a != P.Y.f())
@@ -676,6 +686,61 @@ int pqp_batch_iterate(int B, int N, const float* d_QdT, int ldq, long long qstri
         return set_error(PQP_ERR_ARG, "pqp_batch_iterate: ldq=%d needs more than 160 KiB of LDS", ldq);
     PQP_HIP(launch_batch_iterate(B, d_QdT, qstride, ldq, N, d_theta, d_Fd, ldv, d_Y0, d_Y, updates,
                                  static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// 2d. row blocks of one large problem (row-sharded solve)
+// ---------------------------------------------------------------------------
+int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N, int row0, int rows, void* stream,
+                        pqp_rowblock** out) {
+    if (!out) return set_error(PQP_ERR_ARG, "pqp_rowblock_create: null out");
+    *out = nullptr;
+    if (N <= 0 || ld < N || row0 < 0 || rows < 0 || row0 + (long long)rows > N || !d_Fd || (rows > 0 && !d_Qd_rows))
+        return set_error(PQP_ERR_ARG, "pqp_rowblock_create: bad arguments (N=%d ld=%d row0=%d rows=%d)", N, ld, row0,
+                         rows);
+    if (split_lds_bytes(N) > kLdsBudget)
+        return set_error(PQP_ERR_ARG, "pqp_rowblock_create: N=%d needs more than %zu B of LDS", N, kLdsBudget);
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::unique_ptr<pqp_rowblock> b(new pqp_rowblock);
+    b->N = N;
+    b->row0 = row0;
+    b->rows = rows;
+    if (rows > 0) {
+        DevBuf theta;
+        PQP_TRY(theta.floats(rows));
+        PQP_TRY(b->SP.floats(split_floats(N, rows)));
+        PQP_TRY(b->fdpn.floats((size_t)2 * rows));
+        PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * split_floats(N, rows), s));
+        PQP_HIP(launch_theta_rows(d_Qd_rows, ld, N, rows, theta.f(), s));
+        PQP_HIP(launch_build_split(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->SP.f(), b->fdpn.f(), s));
+        PQP_HIP(hipStreamSynchronize(s));  // theta is freed on return
+    }
+    *out = b.release();
+    return PQP_OK;
+}
+
+int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void* stream) {
+    if (!b || !d_Y || (b->rows > 0 && !d_Y_rows)) return set_error(PQP_ERR_ARG, "pqp_rowblock_update: null argument");
+    PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, d_Y, d_Y_rows,
+                                static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
+int pqp_rowblock_destroy(pqp_rowblock* b) {
+    delete b;
+    return PQP_OK;
+}
+
+int pqp_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float* d_Qd_rows, int ld,
+                   float* d_Fd, float* d_Md, void* stream) {
+    if (N <= 0 || M <= 0 || ld < N || row0 < 0 || rows < 0 || row0 + (long long)rows > N || (rows > 0 && !d_Qd_rows))
+        return set_error(PQP_ERR_ARG, "pqp_synth_rows: bad arguments (N=%d M=%d ld=%d row0=%d rows=%d)", N, M, ld,
+                         row0, rows);
+    PQP_TRY(ensure_device());
+    PQP_HIP(launch_synth_rows(seed, inst, N, M, row0, rows, d_Qd_rows, ld, d_Fd, d_Md,
+                              static_cast<hipStream_t>(stream)));
     return PQP_OK;
 }
 

@@ -273,60 +273,80 @@ __global__ void __launch_bounds__(256) k_update_split(const float* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // Single large problem, fixed mode, spread over many workgroups (BASELINE
-// configs[2]).  The reference's two stored split matrices are kept (8 N^2 B):
-// lane p = 2i + side owns row i's numerator (side 0, Qdn_theta) or
-// denominator (side 1, Qdp_theta).  Layout: 4-k packets, SP[kb][p][4] =
-// row-i side-s entries for k = 4kb..4kb+3, so each lane loads one dwordx4 per
-// four k and a wave reads 1 KiB contiguous per load (k >= N padded with +0,
-// an exact no-op).  The per-iteration floor is one lane's N-long mul/add chain
-// plus the bytes one CU can pull from L2/MALL, so rows are spread over
-// ceil(2N/64) single-wave workgroups (32 CUs at N = 1024).
+// configs[2]), and the row blocks of a row-sharded problem.
+// The reference's two stored split matrices are kept (8 B per entry): lane
+// p = 2i + side owns local row i's numerator (side 0, Qdn_theta) or
+// denominator (side 1, Qdp_theta).  A block of `rows` rows starting at global
+// row `row0` is spread over ceil(2 rows / 64) single-wave workgroups.
+// Layout: workgroup-major 4-k packets, SP[wg][kb][lane][4] = the entries for
+// k = 4kb..4kb+3, so each workgroup streams its own contiguous region
+// (KB KiB) with one dwordx4 per lane per four k, and a wave reads 1 KiB
+// contiguous per load.  k >= N is padded with +0 (an exact no-op) and the
+// padding lanes of the last workgroup hold zeros.  The per-update floor is
+// one lane's N-long mul/add chain plus the bytes one CU can pull.
 // ---------------------------------------------------------------------------
 __host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
+__host__ __device__ inline int split_wgs(int rows) { return (2 * rows + 63) / 64; }
 
-__global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Qd, const float* __restrict__ theta,
-                                                     const float* __restrict__ Fd, int N, float* __restrict__ SP,
+// Qd: the block's rows, row-major with leading dimension ld (row i local =
+// global row row0 + i); theta: the block's Theta_ii (rows); Fd: full N-vector.
+__global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Qd, int ld,
+                                                     const float* __restrict__ theta, const float* __restrict__ Fd,
+                                                     int N, int rows, int row0, float* __restrict__ SP,
                                                      float* __restrict__ fdpn) {
     const int KB = split_kblocks(N);
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (i, k) with k < 4*KB
-    if (e < (long long)N * 4 * KB) {
+    if (e < (long long)rows * 4 * KB) {
         const int i = (int)(e / (4 * KB)), k = (int)(e % (4 * KB));
         float qn = 0.0f, qp = 0.0f;
         if (k < N) {
-            const float q = Qd[(size_t)i * N + k];
-            const float t = (i == k) ? theta[i] : 0.0f;
+            const float q = Qd[(size_t)i * ld + k];
+            const float t = (row0 + i == k) ? theta[i] : 0.0f;
             qn = max_ref(0.0f, -q) + 1.0f * t;  // computeQdn_theta :533-537
             qp = max_ref(0.0f, q) + 1.0f * t;   // computeQdp_theta :524-528
         }
-        const size_t base = ((size_t)(k >> 2) * 2 * N + 2 * i) * 4 + (k & 3);
+        const int p = 2 * i;  // even, so lane p + 1 is in the same workgroup
+        const size_t base = (((size_t)(p >> 6) * KB + (k >> 2)) * 64 + (p & 63)) * 4 + (k & 3);
         SP[base] = qn;      // lane 2i
         SP[base + 4] = qp;  // lane 2i + 1
     }
-    if (e < N) {
-        fdpn[2 * e + 0] = max_ref(0.0f, -Fd[e]);  // Fdn :704
-        fdpn[2 * e + 1] = max_ref(0.0f, Fd[e]);   // Fdp :703
+    if (e < rows) {
+        const float fd = Fd[row0 + e];
+        fdpn[2 * e + 0] = max_ref(0.0f, -fd);  // Fdn :704
+        fdpn[2 * e + 1] = max_ref(0.0f, fd);   // Fdp :703
     }
+}
+
+// Theta_ii = max(sum_k max(0, -Qd_ik) * 1.0, 5) for the block's rows
+// (computeTheta, PQP_CPU.c:503-519; k sequential).
+__global__ void __launch_bounds__(256) k_theta_rows(const float* __restrict__ Qd, int ld, int N, int rows,
+                                                    float* __restrict__ theta) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= rows) return;
+    float s = 0.0f;
+    for (int k = 0; k < N; ++k) s += max_ref(0.0f, -Qd[(size_t)i * ld + k]) * 1.0f;
+    theta[i] = max_ref(s, 5.0f);
 }
 
 template <int U>
 __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
-                                                     int N, const float* __restrict__ Yin, float* __restrict__ Yout) {
+                                                     int N, int rows, int row0, const float* __restrict__ Yin,
+                                                     float* __restrict__ Yout) {
     extern __shared__ __attribute__((aligned(16))) float ys[];
     const int KB = split_kblocks(N);
     for (int k = threadIdx.x; k < 4 * KB; k += 64) ys[k] = (k < N) ? Yin[k] : 0.0f;
     __syncthreads();
-    const int twoN = 2 * N;
-    const int p = blockIdx.x * 64 + threadIdx.x;
     float acc = 0.0f;
-    if (p < twoN) {
-        // buffer loads: wave-uniform descriptor, lane offset in voffset, the
-        // k-block offset in an SGPR; two register stages of U packets in flight
+    {
+        // buffer loads over this workgroup's region: wave-uniform descriptor,
+        // lane offset in voffset, the k-block offset in an SGPR; two register
+        // stages of U packets in flight
+        const float* region = SP + (size_t)blockIdx.x * KB * 256;
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(SP), (short)0, 0x7fffffff, 0x00020000);
-        const int vo = p * 16;
-        const int blkb = twoN * 16;
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * 1024, 0x00020000);
+        const int vo = threadIdx.x * 16;
         typedef float f4v __attribute__((ext_vector_type(4)));
-        auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * blkb, 0); };
+        auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * 1024, 0); };
         auto use = [&](f4v q, int kb) {
             const float4 y = *reinterpret_cast<const float4*>(ys + 4 * kb);
             acc += q.x * y.x;  // :608-609, k in order
@@ -360,34 +380,44 @@ __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict_
         for (; kb < KB; ++kb) use(ld(kb), kb);
     }
     const float other = __shfl_xor(acc, 1);  // full wave active
-    if (!(p & 1) && p < twoN) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (!(p & 1) && p < 2 * rows) {
         const int i = p >> 1;
         const float num = acc + 1.0f * fdpn[p];        // :611
         const float den = other + 1.0f * fdpn[p + 1];  // :612
-        Yout[i] = num / den * ys[i];                   // :594
+        Yout[i] = num / den * ys[row0 + i];            // :594
     }
 }
 
 int g_split_u = 0;  // tuning: k_split_update stage depth (0: 16, 1: 8, 2: 24)
-size_t split_floats(int N) { return (size_t)split_kblocks(N) * 4 * 2 * N; }
+size_t split_floats(int N, int rows) { return (size_t)split_wgs(rows) * split_kblocks(N) * 256; }
+size_t split_lds_bytes(int N) { return sizeof(float) * (size_t)4 * split_kblocks(N); }
 
-hipError_t launch_build_split(const float* Qd, const float* theta, const float* Fd, int N, float* SP, float* fdpn,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(k_build_split, dim3(cdiv((long long)N * 4 * split_kblocks(N), 256)), dim3(256), 0, s, Qd,
-                       theta, Fd, N, SP, fdpn);
+hipError_t launch_build_split(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows,
+                              int row0, float* SP, float* fdpn, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_build_split, dim3(cdiv((long long)rows * 4 * split_kblocks(N), 256)), dim3(256), 0, s, Qd,
+                       ld, theta, Fd, N, rows, row0, SP, fdpn);
     return hipGetLastError();
 }
 
-hipError_t launch_split_update(const float* SP, const float* fdpn, int N, const float* Yin, float* Yout,
-                               hipStream_t s) {
-    const size_t lds = sizeof(float) * (size_t)4 * split_kblocks(N);
+hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* theta, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_theta_rows, dim3(cdiv(rows, 256)), dim3(256), 0, s, Qd, ld, N, rows, theta);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, const float* Yin,
+                               float* Yout, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    const size_t lds = split_lds_bytes(N);
     // one wave per CU with most of the register file as a 2-stage load buffer:
     // a lane's packet stream is latency-bound (Little's law) with few in flight
-    const dim3 grid(cdiv(2LL * N, 64));
+    const dim3 grid(split_wgs(rows));
     switch (g_split_u) {
-        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, Yin, Yout); break;
-        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, Yin, Yout); break;
-        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, Yin, Yout); break;
+        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, Yin, Yout); break;
+        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, Yin, Yout); break;
+        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, Yin, Yout); break;
     }
     return hipGetLastError();
 }
@@ -444,12 +474,16 @@ __global__ void __launch_bounds__(256) k_theta(const float* __restrict__ QdT, in
 // counter hash into LDS per 32-deep k chunk.
 constexpr int SYN_T = 64, SYN_K = 32;
 __global__ void __launch_bounds__(256) k_synth_qd(uint32_t seed, long long inst0, int N, int M,
-                                                  float* __restrict__ QdT, int ldq, long long qstride) {
+                                                  float* __restrict__ QdT, int ldq, long long qstride, int c0,
+                                                  int cols) {
     __shared__ float gq[SYN_K][SYN_T + 4];  // (Gp Qinv)(i0+ii, k0+kk) stored [kk][ii]
     __shared__ float gj[SYN_K][SYN_T + 4];  // Gp(j0+jj, k0+kk) stored [kk][jj]
     const int b = blockIdx.z;
     const SynthKeys K = synth_keys(seed, (uint32_t)(inst0 + b));
-    const int i0 = blockIdx.x * SYN_T, j0 = blockIdx.y * SYN_T;
+    // columns j in [c0, c0 + cols) only (stored at column j - c0): a column
+    // block of the exactly symmetric Qd is the row-major block of its rows
+    const int i0 = blockIdx.x * SYN_T, j0 = c0 + blockIdx.y * SYN_T;
+    const int jend = (c0 + cols < N) ? c0 + cols : N;
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     float acc[4][4];
 #pragma unroll
@@ -466,7 +500,7 @@ __global__ void __launch_bounds__(256) k_synth_qd(uint32_t seed, long long inst0
                 const int rr = (tid >> 5) + 8 * s;
                 const int i = i0 + rr, j = j0 + rr;
                 gq[kk][rr] = (k < M && i < N) ? synth_gp(K, i, k, M) * q : 0.0f;
-                gj[kk][rr] = (k < M && j < N) ? synth_gp(K, j, k, M) : 0.0f;
+                gj[kk][rr] = (k < M && j < jend) ? synth_gp(K, j, k, M) : 0.0f;
             }
         }
         __syncthreads();
@@ -488,11 +522,11 @@ __global__ void __launch_bounds__(256) k_synth_qd(uint32_t seed, long long inst0
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int j = j0 + ty + 16 * c;
-        if (j >= N) continue;
+        if (j >= jend) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = i0 + tx + 16 * r;
-            if (i < ldq) dst[(size_t)j * ldq + i] = (i < N) ? acc[r][c] : 0.0f;  // Qd(i,j) at col j
+            if (i < ldq) dst[(size_t)(j - c0) * ldq + i] = (i < N) ? acc[r][c] : 0.0f;  // Qd(i,j) at col j
         }
     }
 }
@@ -1399,6 +1433,17 @@ hipError_t launch_pack_colmajor(int B, const float* Qd, int N, long long in_stri
     return hipGetLastError();
 }
 
+hipError_t launch_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float* Qrows, int ld,
+                             float* Fd, float* Md, hipStream_t s) {
+    if (rows > 0) {
+        dim3 grid(cdiv(ld, SYN_T), cdiv(rows, SYN_T), 1);
+        hipLaunchKernelGGL(k_synth_qd, grid, dim3(256), 0, s, seed, inst, N, M, Qrows, ld, (long long)rows * ld, row0,
+                           rows);
+    }
+    if (Fd) hipLaunchKernelGGL(k_synth_fd, dim3(cdiv(N, 256), 1), dim3(256), 0, s, seed, inst, N, M, Fd, N, Md);
+    return hipGetLastError();
+}
+
 hipError_t launch_theta(int B, const float* QdT, int ldq, long long qstride, int N, float* theta, int ldv,
                         hipStream_t s) {
     hipLaunchKernelGGL(k_theta, dim3(cdiv(N, 256), B), dim3(256), 0, s, QdT, ldq, qstride, N, theta, ldv);
@@ -1412,7 +1457,7 @@ hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, flo
         const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
         dim3 grid(cdiv(ldq, SYN_T), cdiv(N, SYN_T), nb);
         hipLaunchKernelGGL(k_synth_qd, grid, dim3(256), 0, s, seed, inst0 + b0, N, M, QdT + (size_t)b0 * qstride,
-                           ldq, qstride);
+                           ldq, qstride, 0, N);
         hipLaunchKernelGGL(k_synth_fd, dim3(cdiv(N, 256), nb), dim3(256), 0, s, seed, inst0 + b0, N, M,
                            Fd + (size_t)b0 * ldv, ldv, Md ? Md + b0 : nullptr);
     }

@@ -12,7 +12,10 @@ Layers
     computeUfromY, computeCost, checkFeas, computeTheta, matrixMultiply,
     Gauss_Jordan, computeFp, computeMp
   * status API: solve_dual, update, read_example, run_example
-  * batched device API (torch tensors as device memory): :class:`Batch`
+  * batched device API (torch tensors as device memory): :class:`Batch`,
+    :class:`ProblemBatch`, :func:`mpc_batch`
+  * row blocks of one large problem (row-sharded solve): :class:`RowBlock`
+    (driver in :mod:`pqp_amd.rowshard`)
 """
 from __future__ import annotations
 
@@ -76,6 +79,10 @@ SIGNATURES = {
     "pqp_batch_compute_mp": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [_vp]),
     "pqp_batch_solve": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [C.c_int, C.c_longlong, C.c_longlong] + [_vp] * 4
                         + [_vp]),
+    "pqp_rowblock_create": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(C.c_void_p)]),
+    "pqp_rowblock_update": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "pqp_rowblock_destroy": (C.c_int, [_vp]),
+    "pqp_synth_rows": (C.c_int, [C.c_uint32, C.c_longlong] + [C.c_int] * 4 + [_vp, C.c_int, _vp, _vp, _vp]),
     # include/pqp_tuning.h
     "pqp_tune_set_variant": (C.c_int, [C.c_int]),
     "pqp_tune_glibc_rand": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
@@ -533,3 +540,73 @@ def mpc_batch(directory, states, device=None) -> ProblemBatch:
                                                                                 "Mp6")], p(D), p(x), p(pb.Mp), s))
     pb.gauss_jordan().convert_to_dual()
     return pb
+
+
+class RowBlock:
+    """Rows [row0, row0+rows) of one large dual problem's updateY2
+    (pqp_rowblock_* of include/pqp.h).
+
+    ``update(Y, Y_rows)`` reads the full iterate Y (N floats, device) and
+    writes the block's rows of Y_next, bit-identical to the corresponding rows
+    of PQP_CPU.c:603-618.  Launches go to torch's current stream of `device`.
+    """
+
+    def __init__(self, Qd_rows, Fd, N: int, row0: int, rows: int, ld: int | None = None, device=None):
+        import torch
+
+        self.torch = torch
+        self.N, self.row0, self.rows = int(N), int(row0), int(rows)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.ld = int(ld) if ld else self.N
+        dev = lambda a: (a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a, np.float32))).to(  # noqa: E731
+            self.device, torch.float32).contiguous()
+        Fd = dev(Fd)
+        if self.rows > 0:
+            Qd_rows = dev(Qd_rows)
+            if Qd_rows.numel() < (self.rows - 1) * self.ld + self.N:
+                raise ValueError("Qd_rows is smaller than rows x ld")
+        h = C.c_void_p()
+        _check(lib().pqp_rowblock_create(C.c_void_p(Qd_rows.data_ptr()) if self.rows > 0 else None, self.ld,
+                                         C.c_void_p(Fd.data_ptr()), self.N, self.row0, self.rows, self._s(),
+                                         C.byref(h)))
+        self._h = h
+
+    def _s(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    @classmethod
+    def synthetic(cls, seed: int, inst: int, N: int, row0: int, rows: int, M: int | None = None, device=None):
+        """The block of synthetic problem `inst` of `seed` (pqp_synth_rows,
+        the generator of :meth:`Batch.generate`), generated on the device
+        without the full N x N matrix.  Returns (block, Fd, Md) with Fd/Md
+        the full problem's (device tensors)."""
+        import torch
+
+        device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        M = int(M) if M else max(1, int(N) // 2)
+        ld = round_up(int(N), 4)
+        kw = dict(dtype=torch.float32, device=device)
+        Q = torch.empty(max(1, int(rows)) * ld, **kw)
+        Fd = torch.empty(int(N), **kw)
+        Md = torch.empty(1, **kw)
+        s = C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+        _check(lib().pqp_synth_rows(seed, inst, int(N), M, int(row0), int(rows), C.c_void_p(Q.data_ptr()), ld,
+                                    C.c_void_p(Fd.data_ptr()), C.c_void_p(Md.data_ptr()), s))
+        blk = cls(Q, Fd, N, row0, rows, ld=ld, device=device)
+        return blk, Fd, Md
+
+    def update(self, Y, Y_rows):
+        """Y_rows[:rows] = updateY2(Y)[row0:row0+rows] (async)."""
+        _check(lib().pqp_rowblock_update(self._h, C.c_void_p(Y.data_ptr()),
+                                         C.c_void_p(Y_rows.data_ptr()) if self.rows > 0 else None, self._s()))
+
+    def close(self):
+        if getattr(self, "_h", None) and _LIB is not None:
+            _LIB.pqp_rowblock_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
