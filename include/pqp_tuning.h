@@ -16,8 +16,14 @@ extern "C" {
  * launch_batch_iterate).  Bit 0x100: solve N, M <= 32 problems with the
  * LDS-staged k_solve_small instead of k_solve_tiny.  Bit 0x200: fixed-mode
  * solves of large single problems on one workgroup (k_solve_single) instead
- * of the multi-workgroup k_split_update.  Bits 12-13: k_split_update load
- * stage depth (0: 16 packets, 1: 8, 2: 24).  Returns the previous value. */
+ * of the multi-workgroup split-matrix update.  Bits 12-13: k_split_update
+ * load stage depth (0: 16 packets, 1: 8, 2: 24).  Bits 14-16: the kernel
+ * behind pqp_rowblock_update and large fixed-mode solves (0: default =
+ * k_split_relay with 8 waves x 16-packet segments, 1: streaming
+ * k_split_update, 2: relay 4 x 64, 3: relay 8 x 32, 4: relay 16 x 16,
+ * 5: relay 8 x 16).  Bits 17-19: row sides per workgroup of blocks built
+ * afterwards (0: auto, about one workgroup per CU; 1: 8, 2: 16, 3: 32,
+ * 4: 64).  Returns the previous value. */
 int pqp_tune_set_variant(int variant);
 
 /* Stream B problems' QdT with the hot kernel's exact access pattern and no

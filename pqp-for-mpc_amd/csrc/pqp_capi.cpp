@@ -235,8 +235,10 @@ struct pqp_problem {
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
+    int split_lw = 0;                                // lanes per workgroup SP was built with
     hipGraphExec_t graph = nullptr;                  // captured fixed-mode launch sequence
     long long graph_updates = -1;
+    int graph_variant = -1;                          // g_split_u the graph was captured with
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     ~pqp_problem() {
@@ -247,7 +249,7 @@ struct pqp_problem {
 
 // One row block of a large problem's stored split matrices (pqp_rowblock_*).
 struct pqp_rowblock {
-    int N = 0, row0 = 0, rows = 0;
+    int N = 0, row0 = 0, rows = 0, lw = 64;
     pqp::DevBuf SP, fdpn;
 };
 
@@ -305,20 +307,22 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 // (k_split_update), the stored split matrices built once per problem.
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
-    if (!P.SP.p) {
+    const int lw = split_pick_lw(N);
+    if (!P.SP.p || P.split_lw != lw) {
         if (split_lds_bytes(N) > kLdsBudget)
             return set_error(PQP_ERR_ARG, "fixed-mode solve: N=%d needs more than %zu B of LDS", N, kLdsBudget);
-        PQP_TRY(P.SP.floats(split_floats(N, N)));
+        PQP_TRY(P.SP.floats(split_floats(N, N, lw)));
         PQP_TRY(P.fdpn.floats((size_t)2 * N));
         PQP_TRY(P.Yb.floats(N));
-        PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N), s));
-        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, P.SP.f(), P.fdpn.f(), s));
+        PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N, lw), s));
+        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
+        P.split_lw = lw;
     }
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
     // The whole launch sequence (fill, `updates` dependent updates, final copy)
     // is captured once into a hipGraph and replayed: per-update host launch
     // overhead would otherwise exceed the kernel itself.
-    if (!P.graph || P.graph_updates != updates) {
+    if (!P.graph || P.graph_updates != updates || P.graph_variant != (g_split_u | (g_split_kind << 4) | (lw << 8))) {
         if (P.graph) {
             (void)hipGraphExecDestroy(P.graph);
             P.graph = nullptr;
@@ -329,7 +333,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
         float* b = P.Yb.f();
         hipError_t e = launch_fill(a, 1000.0f, N, s);  // initMat(Y, 1000) :710
         for (long long u = 0; u < updates && e == hipSuccess; ++u) {
-            e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, a, b, s);
+            e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, a, b, s);
             std::swap(a, b);
         }
         if (e == hipSuccess && a != P.Y.f())
@@ -343,6 +347,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
         (void)hipGraphDestroy(g);
         PQP_HIP(e3);
         P.graph_updates = updates;
+        P.graph_variant = g_split_u | (g_split_kind << 4) | (lw << 8);
     }
     PQP_HIP(hipGraphLaunch(P.graph, s));
     PQP_HIP(hipStreamSynchronize(s));
@@ -710,11 +715,12 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
     if (rows > 0) {
         DevBuf theta;
         PQP_TRY(theta.floats(rows));
-        PQP_TRY(b->SP.floats(split_floats(N, rows)));
+        b->lw = split_pick_lw(rows);
+        PQP_TRY(b->SP.floats(split_floats(N, rows, b->lw)));
         PQP_TRY(b->fdpn.floats((size_t)2 * rows));
-        PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * split_floats(N, rows), s));
+        PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * split_floats(N, rows, b->lw), s));
         PQP_HIP(launch_theta_rows(d_Qd_rows, ld, N, rows, theta.f(), s));
-        PQP_HIP(launch_build_split(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->SP.f(), b->fdpn.f(), s));
+        PQP_HIP(launch_build_split(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->lw, b->SP.f(), b->fdpn.f(), s));
         PQP_HIP(hipStreamSynchronize(s));  // theta is freed on return
     }
     *out = b.release();
@@ -723,7 +729,7 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
 
 int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void* stream) {
     if (!b || !d_Y || (b->rows > 0 && !d_Y_rows)) return set_error(PQP_ERR_ARG, "pqp_rowblock_update: null argument");
-    PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, d_Y, d_Y_rows,
+    PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows,
                                 static_cast<hipStream_t>(stream)));
     return PQP_OK;
 }
@@ -1169,9 +1175,13 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 
 extern "C" int pqp_tune_set_variant(int variant) {
     const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0) |
-                    (pqp::g_split_u << 12);
+                    (pqp::g_split_u << 12) | (pqp::g_split_kind << 14) |
+                    ((pqp::g_split_lw ? __builtin_ctz(pqp::g_split_lw) - 2 : 0) << 17);
     pqp::set_variant(variant & 0xff);
     pqp::g_split_u = (variant >> 12) & 3;
+    pqp::g_split_kind = (variant >> 14) & 7;
+    const int lwsel = (variant >> 17) & 7;  // 0 auto, 1: 8, 2: 16, 3: 32, 4: 64 lanes per workgroup
+    pqp::g_split_lw = (lwsel >= 1 && lwsel <= 4) ? (4 << lwsel) : 0;
     pqp::g_force_small = (variant & 0x100) != 0;
     pqp::g_force_single = (variant & 0x200) != 0;
     return old;

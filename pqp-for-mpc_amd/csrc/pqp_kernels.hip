@@ -278,21 +278,24 @@ __global__ void __launch_bounds__(256) k_update_split(const float* __restrict__ 
 // p = 2i + side owns local row i's numerator (side 0, Qdn_theta) or
 // denominator (side 1, Qdp_theta).  A block of `rows` rows starting at global
 // row `row0` is spread over ceil(2 rows / 64) single-wave workgroups.
-// Layout: workgroup-major 4-k packets, SP[wg][kb][lane][4] = the entries for
-// k = 4kb..4kb+3, so each workgroup streams its own contiguous region
-// (KB KiB) with one dwordx4 per lane per four k, and a wave reads 1 KiB
-// contiguous per load.  k >= N is padded with +0 (an exact no-op) and the
+// Layout: workgroup-major 4-k packets, SP[wg][kb][lane < lw][4] = the entries
+// for k = 4kb..4kb+3, so each workgroup streams its own contiguous region
+// (KB * lw * 16 B) with one dwordx4 per lane per four k, and a wave reads
+// lw * 16 B contiguous per load.  k >= N is padded with +0 (an exact no-op) and the
 // padding lanes of the last workgroup hold zeros.  The per-update floor is
 // one lane's N-long mul/add chain plus the bytes one CU can pull.
 // ---------------------------------------------------------------------------
 __host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
-__host__ __device__ inline int split_wgs(int rows) { return (2 * rows + 63) / 64; }
+// lw = lanes (row sides) per workgroup: 64, 32, 16 or 8.  Fewer rows per
+// workgroup spread a block over more CUs (each CU then pulls fewer bytes per
+// update; the per-CU fetch rate, not HBM, bounds a single small problem).
+__host__ __device__ inline int split_wgs(int rows, int lw) { return (2 * rows + lw - 1) / lw; }
 
 // Qd: the block's rows, row-major with leading dimension ld (row i local =
 // global row row0 + i); theta: the block's Theta_ii (rows); Fd: full N-vector.
 __global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Qd, int ld,
                                                      const float* __restrict__ theta, const float* __restrict__ Fd,
-                                                     int N, int rows, int row0, float* __restrict__ SP,
+                                                     int N, int rows, int row0, int lw, float* __restrict__ SP,
                                                      float* __restrict__ fdpn) {
     const int KB = split_kblocks(N);
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (i, k) with k < 4*KB
@@ -306,7 +309,7 @@ __global__ void __launch_bounds__(256) k_build_split(const float* __restrict__ Q
             qp = max_ref(0.0f, q) + 1.0f * t;   // computeQdp_theta :524-528
         }
         const int p = 2 * i;  // even, so lane p + 1 is in the same workgroup
-        const size_t base = (((size_t)(p >> 6) * KB + (k >> 2)) * 64 + (p & 63)) * 4 + (k & 3);
+        const size_t base = (((size_t)(p / lw) * KB + (k >> 2)) * lw + (p % lw)) * 4 + (k & 3);
         SP[base] = qn;      // lane 2i
         SP[base + 4] = qp;  // lane 2i + 1
     }
@@ -328,25 +331,69 @@ __global__ void __launch_bounds__(256) k_theta_rows(const float* __restrict__ Qd
     theta[i] = max_ref(s, 5.0f);
 }
 
+// Stage y[0..N) (zero-padded to n_lds) in LDS with one wave.  Each batch
+// issues all of its loads before the LDS stores, so their latencies overlap;
+// a plain load-store loop would pay one L2 round trip per 64 elements, which
+// dominated the single-problem update.
+__device__ inline void stage_y_lds(const float* __restrict__ Y, int N, int n_lds, float* ys) {
+    const int t = threadIdx.x;
+    int done = 0;
+    if ((reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
+        const int N4 = N >> 2;
+        const float4* Y4 = reinterpret_cast<const float4*>(Y);
+        for (int b = 0; b < N4; b += 64 * 8) {
+            float4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = b + 64 * j + t;
+                v[j] = (i < N4) ? Y4[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = b + 64 * j + t;
+                if (i < N4) reinterpret_cast<float4*>(ys)[i] = v[j];
+            }
+        }
+        done = 4 * N4;
+    }
+    for (int b = done; b < n_lds; b += 64 * 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int k = b + 64 * j + t;
+            v[j] = (k < N) ? Y[k] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int k = b + 64 * j + t;
+            if (k < n_lds) ys[k] = v[j];
+        }
+    }
+    __syncthreads();
+}
+
 template <int U>
 __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
-                                                     int N, int rows, int row0, const float* __restrict__ Yin,
+                                                     int N, int rows, int row0, int lw, const float* __restrict__ Yin,
                                                      float* __restrict__ Yout) {
     extern __shared__ __attribute__((aligned(16))) float ys[];
     const int KB = split_kblocks(N);
-    for (int k = threadIdx.x; k < 4 * KB; k += 64) ys[k] = (k < N) ? Yin[k] : 0.0f;
-    __syncthreads();
+    // lanes >= lw repeat lane % lw's loads (same cache lines) and are discarded
+    const int lane = threadIdx.x, ll = lane % lw;
+    const int p = blockIdx.x * lw + ll;
+    const bool live = lane < lw && p < 2 * rows;
+    const float fd = live ? fdpn[p] : 0.0f;  // this lane's Fdn / Fdp, fetched early
     float acc = 0.0f;
     {
         // buffer loads over this workgroup's region: wave-uniform descriptor,
         // lane offset in voffset, the k-block offset in an SGPR; two register
         // stages of U packets in flight
-        const float* region = SP + (size_t)blockIdx.x * KB * 256;
+        const float* region = SP + (size_t)blockIdx.x * KB * lw * 4;
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * 1024, 0x00020000);
-        const int vo = threadIdx.x * 16;
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * lw * 16, 0x00020000);
+        const int vo = ll * 16, kstride = lw * 16;
         typedef float f4v __attribute__((ext_vector_type(4)));
-        auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * 1024, 0); };
+        auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * kstride, 0); };
         auto use = [&](f4v q, int kb) {
             const float4 y = *reinterpret_cast<const float4*>(ys + 4 * kb);
             acc += q.x * y.x;  // :608-609, k in order
@@ -356,10 +403,12 @@ __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict_
         };
         f4v qa[U], qb[U];
         int kb = 0;
+        // the first stage does not depend on y: issue it before staging y
         if (KB >= U) {
 #pragma unroll
             for (int j = 0; j < U; ++j) qa[j] = ld(j);
         }
+        stage_y_lds(Yin, N, 4 * KB, ys);
         for (; kb + 2 * U <= KB; kb += 2 * U) {
 #pragma unroll
             for (int j = 0; j < U; ++j) qb[j] = ld(kb + U + j);
@@ -379,25 +428,144 @@ __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict_
         }
         for (; kb < KB; ++kb) use(ld(kb), kb);
     }
-    const float other = __shfl_xor(acc, 1);  // full wave active
-    const int p = blockIdx.x * 64 + threadIdx.x;
-    if (!(p & 1) && p < 2 * rows) {
+    const float v = acc + 1.0f * fd;       // even lane: num (:611), odd lane: den (:612)
+    const float den = __shfl_xor(v, 1);  // full wave active
+    if (!(p & 1) && live) {
         const int i = p >> 1;
-        const float num = acc + 1.0f * fdpn[p];        // :611
-        const float den = other + 1.0f * fdpn[p + 1];  // :612
-        Yout[i] = num / den * ys[row0 + i];            // :594
+        Yout[i] = v / den * ys[row0 + i];  // :594
+    }
+}
+
+// Relay form of the same update: W waves per workgroup share the workgroup's
+// 32 rows (same layout and lanes as k_split_update) and split the k range
+// into segments of S packets (4S values of k).  Segment g belongs to wave
+// g % W.  A wave loads its segment into registers as early as it can and
+// multiplies it by y while earlier segments are being summed; only the
+// additions form the sequential chain, and they run segment after segment,
+// the running sums handed from wave to wave through LDS (a turn counter
+// orders the hand-off).  Each row's sum therefore still runs over k = 0..N-1
+// in order from +0.0f, bit-identical to the reference and to
+// k_split_update, while a workgroup keeps W*S KiB of packets in flight
+// instead of one wave's pipeline, and the chain issues 4 cycles per k
+// (an add) instead of 8 (a multiply and an add).
+template <int W, int S>
+__global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict__ SP, const float* __restrict__ fdpn,
+                                                        int N, int rows, int row0, int lw,
+                                                        const float* __restrict__ Yin, float* __restrict__ Yout) {
+    // LDS: [64] hand-off words, then y [4*KB]
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds);  // per lane: (seq << 32) | bits(sum)
+    float* ys = lds + 128;
+    const int KB = split_kblocks(N);
+    // w is wave-uniform; readfirstlane tells the compiler so (segment offsets
+    // then live in SGPRs instead of forcing waterfall loops around the loads)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // lanes >= lw repeat lane % lw's loads (same cache lines) and are discarded
+    const int ll = lane % lw;
+    const int p = blockIdx.x * lw + ll;
+    const bool live = lane < lw && p < 2 * rows;
+    const int G = (KB + S - 1) / S;  // segments
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const float* region = SP + (size_t)blockIdx.x * KB * lw * 4;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * lw * 16, 0x00020000);
+    const int vo = ll * 16, kstride = lw * 16;
+    f4v q[S];
+    auto load_seg = [&](int g) {
+        // packets past KB (the last segment's tail) are +0, an exact no-op;
+        // they are not loaded (the SGPR offset is not range-checked)
+        const int nj = KB - g * S;  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+            q[j] = (j < nj) ? __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (g * S + j) * kstride, 0)
+                            : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    };
+    if (w < G) load_seg(w);  // independent of y: in flight while y is staged
+    const float fd = live ? fdpn[p] : 0.0f;
+    // y staged by all W waves (loads issued before the LDS stores)
+    {
+        const int t = threadIdx.x, n_lds = 4 * KB;
+        for (int b = 0; b < n_lds; b += 64 * W * 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = b + 64 * W * j + t;
+                v[j] = (k < N) ? Yin[k] : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = b + 64 * W * j + t;
+                if (k < n_lds) ys[k] = v[j];
+            }
+        }
+        if (w == 0) slot[lane] = 0ull;  // segment 0 starts from +0.0f
+    }
+    __syncthreads();
+    float acc = 0.0f;
+    for (int g = w; g < G; g += W) {
+        // products of this segment (packed multiplies, each product rounded
+        // exactly as q * y), overwriting the packets
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const f4v y = *reinterpret_cast<const f4v*>(ys + 4 * (g * S + j));
+            f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
+            f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
+            q[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+            // pin the products here, before the wait below: otherwise the
+            // compiler sinks the multiplies into the add chain
+            asm volatile("" : "+v"(q[j]));
+        }
+        // wait until every lane's hand-off word carries sequence g (the sum
+        // and its sequence number travel in one 64-bit LDS word).  Bounded:
+        // a broken hand-off ends with wrong sums instead of a hang.
+        unsigned long long h;
+        for (int spin = 0;; ++spin) {
+            h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
+        }
+        __builtin_amdgcn_s_setprio(3);
+        acc = __uint_as_float((unsigned)h);
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            acc += q[j].x;  // :608-609, k in order
+            acc += q[j].y;
+            acc += q[j].z;
+            acc += q[j].w;
+        }
+        __hip_atomic_store(slot + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_s_setprio(0);
+        if (g + W < G) load_seg(g + W);
+    }
+    if (w == (G - 1) % W) {  // the wave that summed the last segment
+        const float v = acc + 1.0f * fd;     // even lane: num (:611), odd lane: den (:612)
+        const float den = __shfl_xor(v, 1);  // the whole wave is here
+        if (!(p & 1) && live) {
+            const int i = p >> 1;
+            Yout[i] = v / den * ys[row0 + i];  // :594
+        }
     }
 }
 
 int g_split_u = 0;  // tuning: k_split_update stage depth (0: 16, 1: 8, 2: 24)
-size_t split_floats(int N, int rows) { return (size_t)split_wgs(rows) * split_kblocks(N) * 256; }
-size_t split_lds_bytes(int N) { return sizeof(float) * (size_t)4 * split_kblocks(N); }
+size_t split_floats(int N, int rows, int lw) { return (size_t)split_wgs(rows, lw) * split_kblocks(N) * lw * 4; }
+size_t split_lds_bytes(int N) { return sizeof(float) * ((size_t)4 * split_kblocks(N) + 128); }
+
+int g_split_lw = 0;  // tuning: lanes per workgroup (0 auto, else 8/16/32/64)
+int split_pick_lw(int rows) {
+    if (g_split_lw == 8 || g_split_lw == 16 || g_split_lw == 32 || g_split_lw == 64) return g_split_lw;
+    // about one workgroup per CU: 2 rows / lw ~ 256
+    int lw = 8;
+    while (lw < 64 && 2LL * rows > 256LL * lw) lw *= 2;
+    return lw;
+}
 
 hipError_t launch_build_split(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows,
-                              int row0, float* SP, float* fdpn, hipStream_t s) {
+                              int row0, int lw, float* SP, float* fdpn, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_build_split, dim3(cdiv((long long)rows * 4 * split_kblocks(N), 256)), dim3(256), 0, s, Qd,
-                       ld, theta, Fd, N, rows, row0, SP, fdpn);
+                       ld, theta, Fd, N, rows, row0, lw, SP, fdpn);
     return hipGetLastError();
 }
 
@@ -407,17 +575,33 @@ hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* th
     return hipGetLastError();
 }
 
-hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, const float* Yin,
-                               float* Yout, hipStream_t s) {
+int g_split_kind = 0;  // tuning: 0 auto (relay W8 S16), 1 k_split_update, 2 relay W4 S64, 3 W8 S32, 4 W16 S16, 5 W8 S16
+
+template <int W, int S>
+static void launch_relay(const float* SP, const float* fdpn, int N, int rows, int row0, int lw, const float* Yin,
+                         float* Yout, hipStream_t s) {
+    hipLaunchKernelGGL((k_split_relay<W, S>), dim3(split_wgs(rows, lw)), dim3(64 * W), split_lds_bytes(N), s, SP,
+                       fdpn, N, rows, row0, lw, Yin, Yout);
+}
+
+hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
+                               const float* Yin, float* Yout, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
+    switch (g_split_kind) {
+        case 1: break;
+        case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
+        case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
+        case 4: launch_relay<16, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
+        default: launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
+    }
     const size_t lds = split_lds_bytes(N);
     // one wave per CU with most of the register file as a 2-stage load buffer:
     // a lane's packet stream is latency-bound (Little's law) with few in flight
-    const dim3 grid(split_wgs(rows));
+    const dim3 grid(split_wgs(rows, lw));
     switch (g_split_u) {
-        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, Yin, Yout); break;
-        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, Yin, Yout); break;
-        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, Yin, Yout); break;
+        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout); break;
+        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout); break;
+        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout); break;
     }
     return hipGetLastError();
 }

@@ -60,18 +60,21 @@ hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);
 // row block [row0, row0 + rows) of one large problem, fixed mode,
 // multi-workgroup (stored split matrices); rows = N, row0 = 0 for a whole problem
 hipError_t launch_build_split(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows,
-                              int row0, float* SP, float* fdpn, hipStream_t s);
+                              int row0, int lw, float* SP, float* fdpn, hipStream_t s);
 hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* theta, hipStream_t s);
-hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, const float* Yin,
-                               float* Yout, hipStream_t s);
+hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
+                               const float* Yin, float* Yout, hipStream_t s);
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
-size_t split_floats(int N, int rows);  // size of a row block's packed split matrices
+size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
+int split_pick_lw(int rows);                   // lanes per workgroup for a block of `rows`
 size_t split_lds_bytes(int N);         // k_split_update's LDS (the full y)
 // rows [row0, row0 + rows) of synthetic problem `inst` (row-major, ld >= N,
 // columns [N, ld) zeroed) and, if Fd, its full Fd (and Md)
 hipError_t launch_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float* Qrows, int ld,
                              float* Fd, float* Md, hipStream_t s);
 extern int g_split_u;        // tuning: k_split_update stage depth selector
+extern int g_split_kind;     // tuning: relay / stream kernel selector
+extern int g_split_lw;       // tuning: lanes per workgroup override (0 = auto)
 // batched forms: grid = B problems (states st[0..B-1])
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);

@@ -18,13 +18,16 @@ def main():
     ap.add_argument("--sizes", default="1024,4096,8192,16384,32768")
     ap.add_argument("--blocks", type=int, default=1)
     ap.add_argument("--updates", type=int, default=50)
+    ap.add_argument("--variants", default="0", help="pqp_tune_set_variant values to time (comma separated)")
     a = ap.parse_args()
     import torch
 
     import pqp_amd
     from pqp_amd.rowshard import row_plan
 
-    for N in (int(s) for s in a.sizes.split(",")):
+    L = pqp_amd.lib()
+    for N, var in ((int(s), int(v, 0)) for s in a.sizes.split(",") for v in a.variants.split(",")):
+        L.pqp_tune_set_variant(var)
         R, plan = row_plan(N, a.blocks)
         blocks = [pqp_amd.RowBlock.synthetic(1, 0, N, r0, rows)[0] for r0, rows in plan]
         Y = torch.full((N,), 1000.0, device="cuda")
@@ -46,7 +49,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / a.updates * 1e3
-        print(json.dumps({"n_dual": N, "blocks": a.blocks, "us_per_update": us,
+        print(json.dumps({"n_dual": N, "variant": hex(var), "blocks": a.blocks, "us_per_update": us,
                           "alg_split_GBps": 8.0 * N * N / (us * 1e-6) / 1e9,
                           "finite": bool(torch.isfinite(Y[:N]).all().item())}), flush=True)
         del blocks

@@ -29,7 +29,13 @@ def main(N: int = 1024, iters: int = 1000, reps: int = 5):
     out = {"n_dual": N, "iterations": iters}
     with pqp_amd.Problem(P) as prob:
         ys = {}
-        for name, var in (("split_multi_wg", 0), ("split_u8", 0x1000), ("split_u24", 0x2000), ("single_wg", 0x200)):
+        variants = [("split_multi_wg", 0), ("stream_u16_lw64", (1 << 14) | (4 << 17)),
+                    ("stream_u16_lw8", (1 << 14) | (1 << 17))]
+        for kind, kn in ((2, "w4s64"), (3, "w8s32"), (4, "w16s16"), (5, "w8s16")):
+            for lwsel, lw in ((1, 8), (2, 16), (4, 64)):
+                variants.append((f"relay_{kn}_lw{lw}", (kind << 14) | (lwsel << 17)))
+        variants.append(("single_wg", 0x200))
+        for name, var in variants:
             L.pqp_tune_set_variant(var)
             prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
             t0 = time.perf_counter()
@@ -40,7 +46,8 @@ def main(N: int = 1024, iters: int = 1000, reps: int = 5):
             out[name] = {"ms_per_solve": dt * 1e3, "us_per_iter": dt / (iters - 1) * 1e6,
                          "iter_per_s": (iters - 1) / dt}
         L.pqp_tune_set_variant(0)
-    out["bit_identical"] = bool(np.array_equal(ys["split_multi_wg"].view(np.uint32), ys["single_wg"].view(np.uint32)))
+    out["bit_identical"] = all(bool(np.array_equal(y.view(np.uint32), ys["single_wg"].view(np.uint32)))
+                               for y in ys.values())
     out["split_alg_GBps"] = 8 * N * N / (out["split_multi_wg"]["us_per_iter"] * 1e-6) / 1e9
     bb = pqp_amd.Batch(1, N).generate(seed=1, inst0=0, M=M)
     bb.iterate(3)
