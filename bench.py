@@ -24,6 +24,9 @@ Extra keys:
   mpc_batch     16384 MPC problems (bundled plant at perturbed states), one
                 workgroup each, converge mode with device-side terminate()
   single_n1024  configs[2]: one n_dual=1024 problem, 1000 fixed iterations
+  rowshard      one large problem (n_dual = 16384) row-sharded over the job's
+                ranks: per update, every rank updates its
+                rows and an RCCL all-gather assembles y (all ranks take part)
   gather_ms     RCCL gather of every rank's Y* to rank 0 (outside the timed
                 region)
 
@@ -64,6 +67,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bundled", action="store_true")
+    ap.add_argument("--rowshard-n", type=int, default=16384, help="n_dual of the row-sharded leg (0: skip)")
+    ap.add_argument("--rowshard-updates", type=int, default=100)
     return ap.parse_args()
 
 
@@ -184,6 +189,44 @@ def single_bench(pqp_amd, N: int = 1024, iters: int = 1000) -> dict:
             "note": "1 problem, fixed mode; per-iteration floor = one lane's N-long sequential sum"}
 
 
+def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: int) -> dict:
+    """One synthetic problem of n_dual = N whose rows are spread over the
+    ranks (pqp_amd.rowshard); fixed-mode updates, timed as the max over
+    ranks.  Every rank ends with the whole iterate."""
+    import torch
+
+    from pqp_amd.rowshard import RowShardedSolver, row_plan
+
+    R, plan = row_plan(N, world)
+    row0, rows = plan[rank]
+    blk, _, _ = pqp_amd.RowBlock.synthetic(7, 0, N, row0, rows, device=dev)
+    solver = RowShardedSolver(blk, N, dev, dist=dist)
+    solver.Y.fill_(1000.0)
+    for _ in range(5):
+        solver.step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(updates):
+        solver.step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t[0]) / updates
+    y = solver.Y[:N]
+    out = {"n_dual": N, "ranks": world, "rows_per_rank": R, "updates": updates, "us_per_update": dt * 1e6,
+           "iter_per_s": 1.0 / dt, "alg_GBps_split_matrices": 8.0 * N * N / dt / 1e9,
+           "finite_nonneg": bool(torch.isfinite(y).all().item()) and bool((y >= 0).all().item()),
+           "note": "eager launches (pqp_rowblock_update + RCCL all_gather_into_tensor per update at N>1 ranks)"}
+    del solver, blk
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -256,6 +299,10 @@ def main():
     Yh = batch.Y[:, :N]
     finite = bool(torch.isfinite(Yh).all().item()) and bool((Yh >= 0).all().item())
 
+    rowshard = None
+    if args.rowshard_n > 0:  # every rank takes part
+        rowshard = rowshard_bench(pqp_amd, dist, rank, world, dev, args.rowshard_n, args.rowshard_updates)
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -293,6 +340,8 @@ def main():
         "results_finite_nonneg": finite,
         "gather_ms": gather_ms,
     }
+    if rowshard is not None:
+        result["rowshard"] = rowshard
     if world == 1 and not args.no_bundled:
         result["bundled"] = bundled_bench(pqp_amd)
         result["mpc_batch"] = mpc_batch_bench(pqp_amd)

@@ -234,7 +234,7 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
  * (PQP_CPU.c:603-618 restricted to those rows); between steps the caller
  * assembles Y_next from every block (e.g. an RCCL all-gather).  Every row's
  * sums still run over k = 0..N-1 in order, so the assembled Y_next is
- * bit-identical to updateY2's whatever the partition.  N <= 38332 (the full
+ * bit-identical to updateY2's whatever the partition.  N <= 38016 (the full
  * y is staged in LDS).
  * -------------------------------------------------------------------- */
 typedef struct pqp_rowblock pqp_rowblock;

@@ -483,9 +483,11 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
     };
     if (w < G) load_seg(w);  // independent of y: in flight while y is staged
     const float fd = live ? fdpn[p] : 0.0f;
-    // y staged by all W waves (loads issued before the LDS stores)
+    // y staged by all W waves (loads issued before the LDS stores), zeroed up
+    // to the end of the last segment: the products of the tail packets read
+    // it, and LDS is not cleared between launches (0 * stale NaN = NaN)
     {
-        const int t = threadIdx.x, n_lds = 4 * KB;
+        const int t = threadIdx.x, n_lds = 4 * G * S;
         for (int b = 0; b < n_lds; b += 64 * W * 8) {
             float v[8];
 #pragma unroll
@@ -550,7 +552,9 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
 
 int g_split_u = 0;  // tuning: k_split_update stage depth (0: 16, 1: 8, 2: 24)
 size_t split_floats(int N, int rows, int lw) { return (size_t)split_wgs(rows, lw) * split_kblocks(N) * lw * 4; }
-size_t split_lds_bytes(int N) { return sizeof(float) * ((size_t)4 * split_kblocks(N) + 128); }
+// LDS of the split updates (the full y, padded to a whole relay segment of up
+// to 64 packets, plus the relay's hand-off words)
+size_t split_lds_bytes(int N) { return sizeof(float) * ((size_t)4 * (split_kblocks(N) + 64) + 128); }
 
 int g_split_lw = 0;  // tuning: lanes per workgroup (0 auto, else 8/16/32/64)
 int split_pick_lw(int rows) {
@@ -580,8 +584,10 @@ int g_split_kind = 0;  // tuning: 0 auto (relay W8 S16), 1 k_split_update, 2 rel
 template <int W, int S>
 static void launch_relay(const float* SP, const float* fdpn, int N, int rows, int row0, int lw, const float* Yin,
                          float* Yout, hipStream_t s) {
-    hipLaunchKernelGGL((k_split_relay<W, S>), dim3(split_wgs(rows, lw)), dim3(64 * W), split_lds_bytes(N), s, SP,
-                       fdpn, N, rows, row0, lw, Yin, Yout);
+    const int G = (split_kblocks(N) + S - 1) / S;
+    const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);  // y to the end of the last segment
+    hipLaunchKernelGGL((k_split_relay<W, S>), dim3(split_wgs(rows, lw)), dim3(64 * W), lds, s, SP, fdpn, N, rows,
+                       row0, lw, Yin, Yout);
 }
 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
