@@ -26,6 +26,18 @@ extern "C" {
  * 4: 64).  Returns the previous value. */
 int pqp_tune_set_variant(int variant);
 
+/* Converge-mode solves of problems with n_dual >= n run over many workgroups
+ * (terminate() as multi-workgroup mat-vecs + the relay update, replayed from a
+ * hipGraph) instead of one persistent workgroup; n <= 0 sends every size
+ * there, LDS-sized problems included.  Default 384.  Returns the previous
+ * value. */
+int pqp_tune_wide_min_n(int n);
+
+/* Variants of that path: bit 0 launches the update on a forked graph branch
+ * beside terminate() instead of after it; bit 1 uses 64-value k-segments in
+ * the mat-vecs (default 32).  Returns the previous value. */
+int pqp_tune_wide_flags(int flags);
+
 /* Stream B problems' QdT with the hot kernel's exact access pattern and no
  * solver arithmetic (one float written per thread to d_out[B*256]). */
 int pqp_tune_stream_read(int B, int N, const float *d_QdT, int ldq, long long qstride, float *d_out, int nontemporal,

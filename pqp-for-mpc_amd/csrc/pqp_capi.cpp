@@ -238,11 +238,22 @@ struct pqp_problem {
     int split_lw = 0;                                // lanes per workgroup SP was built with
     hipGraphExec_t graph = nullptr;                  // captured fixed-mode launch sequence
     long long graph_updates = -1;
+    // converge mode over many workgroups (pqp_wide.hip), built on first use
+    pqp::DevBuf QinvT, GpT, tM, tq, tu, gu, wflag, wcap;
+    hipGraphExec_t wgraph = nullptr;                 // captured chunk of converge iterations
+    hipStream_t side = nullptr;                      // capture-time fork for the speculative update
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    long long wgraph_key = -1;
+    long long hcap = 0;
     int graph_variant = -1;                          // g_split_u the graph was captured with
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     ~pqp_problem() {
         if (graph) (void)hipGraphExecDestroy(graph);
+        if (wgraph) (void)hipGraphExecDestroy(wgraph);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (side) (void)hipStreamDestroy(side);
         if (hst) (void)hipHostFree(hst);
     }
 };
@@ -259,6 +270,7 @@ namespace {
 constexpr size_t kLdsBudget = 150 * 1024;
 bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
 bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
+int g_wide_min_n = 384;       // converge mode: smallest N solved over many workgroups (problem_run_wide)
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -305,19 +317,30 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 // from P.Y instead of Y = 1000 (used by the terminate() drop-in, mode 2).
 // Fixed mode of a large problem: one multi-workgroup launch per update
 // (k_split_update), the stored split matrices built once per problem.
+// The stored split matrices of the whole problem (rows 0..N-1) with lw row
+// sides per workgroup, built on first use (and rebuilt if lw changes).
+int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
+    const int N = P.N;
+    if (P.SP.p && P.split_lw == lw) return PQP_OK;
+    if (split_lds_bytes(N) > kLdsBudget)
+        return set_error(PQP_ERR_ARG, "multi-workgroup solve: N=%d needs more than %zu B of LDS", N, kLdsBudget);
+    if (!P.theta.p) {  // small problems skip the large-path setup of problem_finish
+        PQP_TRY(P.theta.floats(N));
+        PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
+    }
+    PQP_TRY(P.SP.floats(split_floats(N, N, lw)));
+    PQP_TRY(P.fdpn.floats((size_t)2 * N));
+    PQP_TRY(P.Yb.floats(N));
+    PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N, lw), s));
+    PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
+    P.split_lw = lw;
+    return PQP_OK;
+}
+
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     const int lw = split_pick_lw(N);
-    if (!P.SP.p || P.split_lw != lw) {
-        if (split_lds_bytes(N) > kLdsBudget)
-            return set_error(PQP_ERR_ARG, "fixed-mode solve: N=%d needs more than %zu B of LDS", N, kLdsBudget);
-        PQP_TRY(P.SP.floats(split_floats(N, N, lw)));
-        PQP_TRY(P.fdpn.floats((size_t)2 * N));
-        PQP_TRY(P.Yb.floats(N));
-        PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N, lw), s));
-        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
-        P.split_lw = lw;
-    }
+    PQP_TRY(ensure_split(P, lw, s));
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
     // The whole launch sequence (fill, `updates` dependent updates, final copy)
     // is captured once into a hipGraph and replayed: per-update host launch
@@ -356,10 +379,130 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     return PQP_OK;
 }
 
+// Converge mode of a large problem over many workgroups (pqp_wide.hip): one
+// iteration = terminate() as three multi-workgroup mat-vec launches and a
+// one-workgroup decision, then the relay update.  A chunk of kWideChunk
+// iterations is captured into a hipGraph and replayed until the device-side
+// status leaves Continue; launches after that point return at once.
+constexpr int kWideChunk = 16;  // even: each replay starts and ends with the iterate in P.Y
+int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
+    const int N = P.N, M = P.M;
+    const int lw = split_pick_lw(N);
+    PQP_TRY(ensure_split(P, lw, s));
+    if (!P.QinvT.p) {
+        PQP_TRY(P.QinvT.floats((size_t)M * M));
+        PQP_TRY(P.GpT.floats((size_t)M * N));
+        PQP_TRY(P.tM.floats(M));
+        PQP_TRY(P.tq.floats(N));
+        PQP_TRY(P.tu.floats(M));
+        PQP_TRY(P.gu.floats(N));
+        PQP_TRY(P.wflag.alloc(sizeof(int)));
+        PQP_TRY(P.wcap.alloc(sizeof(long long)));
+        PQP_HIP(launch_transpose(P.Qinv.f(), M, M, P.QinvT.f(), s));  // QinvT[k][i] = Qp_inv[i][k]
+        PQP_HIP(launch_transpose(P.Gp.f(), N, M, P.GpT.f(), s));      // GpT[k][i] = Gp[i][k]
+    }
+    SolveState* dst = static_cast<SolveState*>(P.state.p);
+    int* flag = static_cast<int*>(P.wflag.p);
+    long long* cap = static_cast<long long*>(P.wcap.p);
+    const long long key = ((long long)g_wide_flags << 16) ^ ((long long)g_split_kind << 8) ^ lw;  // cap: device word
+    if (!P.wgraph || P.wgraph_key != key) {
+        if (P.wgraph) {
+            (void)hipGraphExecDestroy(P.wgraph);
+            P.wgraph = nullptr;
+        }
+        if (!P.side) {
+            PQP_HIP(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
+            PQP_HIP(hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming));
+            PQP_HIP(hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming));
+        }
+        // One iteration.  The update depends only on the current iterate, so
+        // it may also run speculatively on a forked branch beside terminate()
+        // (tuning bit; measured slower as a graph branch): if the iteration
+        // stops or hits the cap, its result in `nxt` is not used, and the next
+        // iteration's launches, gated on the status, do nothing.
+        const bool fork = (g_wide_flags & 1) != 0;
+        auto iteration = [&](const float* cur, float* nxt) -> hipError_t {
+            hipError_t e = hipSuccess;
+            if (fork) {
+                e = hipEventRecord(P.ev_fork, s);
+                if (e == hipSuccess) e = hipStreamWaitEvent(P.side, P.ev_fork, 0);
+                if (e == hipSuccess) e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, cur, nxt, P.side,
+                                                             &dst->status);
+                if (e == hipSuccess) e = hipEventRecord(P.ev_join, P.side);
+                if (e != hipSuccess) return e;
+            }
+            GemvJobs j1{};  // tmp = Gp'Y + Fp (computeUfromY :354-356) and Y'Qd (computeCost :652, Jd)
+            j1.job[0] = GemvJob{P.Gp.f(), cur, P.tM.f(), P.Fp.f(), M, N, M, kEpiAdd};
+            j1.job[1] = GemvJob{P.Qd.f(), cur, P.tq.f(), nullptr, N, N, N, kEpiPlain};
+            j1.gate = &dst->status;
+            if ((e = launch_gemv_relay(j1, s)) != hipSuccess) return e;
+            GemvJobs j2{};  // U = -(Qp_inv tmp) (:357-358)
+            j2.job[0] = GemvJob{P.QinvT.f(), P.tM.f(), P.U.f(), nullptr, M, M, M, kEpiNeg};
+            j2.gate = &dst->status;
+            if ((e = launch_gemv_relay(j2, s)) != hipSuccess) return e;
+            GemvJobs j3{};  // checkFeas (:632-641) and U'Qp (computeCost, Jp)
+            j3.job[0] = GemvJob{P.GpT.f(), P.U.f(), P.gu.f(), P.Kp.f(), N, M, N, kEpiFeas};
+            j3.job[1] = GemvJob{P.Qp.f(), P.U.f(), P.tu.f(), nullptr, M, M, M, kEpiPlain};
+            j3.gate = &dst->status;
+            j3.flag = flag;
+            if ((e = launch_gemv_relay(j3, s)) != hipSuccess) return e;
+            const WideArgs w{dst, flag, P.tq.f(), P.tu.f(), cur, P.U.f(), P.Fd.f(), P.Fp.f(), P.Md.f(), P.Mp.f(),
+                             N, M, cap};
+            if ((e = launch_wide_decide(w, s)) != hipSuccess) return e;
+            if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join the update branch
+            return launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, cur, nxt, s, &dst->status);
+        };
+        hipGraph_t g = nullptr;
+        PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        hipError_t e = hipSuccess;
+        for (int it = 0; it < kWideChunk && e == hipSuccess; it += 2) {
+            e = iteration(P.Y.f(), P.Yb.f());
+            if (e == hipSuccess) e = iteration(P.Yb.f(), P.Y.f());
+        }
+        const hipError_t e2 = hipStreamEndCapture(s, &g);
+        if (e != hipSuccess || e2 != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            PQP_HIP(e != hipSuccess ? e : e2);
+        }
+        const hipError_t e3 = hipGraphInstantiate(&P.wgraph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        PQP_HIP(e3);
+        P.wgraph_key = key;
+    }
+    SolveState& st = *P.hst;
+    st = SolveState{};
+    st.h = 1;
+    PQP_HIP(hipMemcpyAsync(dst, &st, sizeof st, hipMemcpyHostToDevice, s));
+    const int one = 1;
+    PQP_HIP(hipMemcpyAsync(flag, &one, sizeof one, hipMemcpyHostToDevice, s));
+    P.hcap = max_updates;  // pinned host word (the copy is async)
+    PQP_HIP(hipMemcpyAsync(cap, &P.hcap, sizeof P.hcap, hipMemcpyHostToDevice, s));
+    PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
+    for (;;) {
+        PQP_HIP(hipGraphLaunch(P.wgraph, s));
+        PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (st.status != kStatusContinue) break;
+    }
+    if ((st.h - 1) & 1)  // odd number of updates: the iterate is in Yb
+        PQP_HIP(hipMemcpyAsync(P.Y.p, P.Yb.p, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+    out.h = st.h;
+    out.status = st.status;
+    out.have_costs = st.have_costs;
+    out.last_stop = st.last_stop;
+    if (st.have_costs) {
+        out.Jp = st.Jp;
+        out.Jd = st.Jd;
+    }
+    return PQP_OK;
+}
+
 int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_updates, bool resume, SolveOut& out,
                 hipStream_t s) {
     const int N = P.N, M = P.M;
     if (mode == kModeFixed && !P.small && !g_force_single && !resume) return problem_run_fixed_split(P, num_iter, out, s);
+    if (mode == kModeConverge && !g_force_single && !resume && N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0))
+        return problem_run_wide(P, max_updates, out, s);
     SolveState& st = *P.hst;
     st = SolveState{};
     st.h = 1;
@@ -1184,6 +1327,18 @@ extern "C" int pqp_tune_set_variant(int variant) {
     pqp::g_split_lw = (lwsel >= 1 && lwsel <= 4) ? (4 << lwsel) : 0;
     pqp::g_force_small = (variant & 0x100) != 0;
     pqp::g_force_single = (variant & 0x200) != 0;
+    return old;
+}
+
+extern "C" int pqp_tune_wide_flags(int flags) {
+    const int old = pqp::g_wide_flags;
+    pqp::g_wide_flags = flags;
+    return old;
+}
+
+extern "C" int pqp_tune_wide_min_n(int n) {
+    const int old = pqp::g_wide_min_n;
+    pqp::g_wide_min_n = n;
     return old;
 }
 

@@ -375,7 +375,8 @@ __device__ inline void stage_y_lds(const float* __restrict__ Y, int N, int n_lds
 template <int U>
 __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                      int N, int rows, int row0, int lw, const float* __restrict__ Yin,
-                                                     float* __restrict__ Yout) {
+                                                     float* __restrict__ Yout, const int* __restrict__ gate) {
+    if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
     extern __shared__ __attribute__((aligned(16))) float ys[];
     const int KB = split_kblocks(N);
     // lanes >= lw repeat lane % lw's loads (same cache lines) and are discarded
@@ -451,7 +452,9 @@ __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict_
 template <int W, int S>
 __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                         int N, int rows, int row0, int lw,
-                                                        const float* __restrict__ Yin, float* __restrict__ Yout) {
+                                                        const float* __restrict__ Yin, float* __restrict__ Yout,
+                                                        const int* __restrict__ gate) {
+    if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
     // LDS: [64] hand-off words, then y [4*KB]
     extern __shared__ __attribute__((aligned(16))) float lds[];
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds);  // per lane: (seq << 32) | bits(sum)
@@ -583,31 +586,31 @@ int g_split_kind = 0;  // tuning: 0 auto (relay W8 S16), 1 k_split_update, 2 rel
 
 template <int W, int S>
 static void launch_relay(const float* SP, const float* fdpn, int N, int rows, int row0, int lw, const float* Yin,
-                         float* Yout, hipStream_t s) {
+                         float* Yout, hipStream_t s, const int* gate) {
     const int G = (split_kblocks(N) + S - 1) / S;
     const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);  // y to the end of the last segment
     hipLaunchKernelGGL((k_split_relay<W, S>), dim3(split_wgs(rows, lw)), dim3(64 * W), lds, s, SP, fdpn, N, rows,
-                       row0, lw, Yin, Yout);
+                       row0, lw, Yin, Yout, gate);
 }
 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
-                               const float* Yin, float* Yout, hipStream_t s) {
+                               const float* Yin, float* Yout, hipStream_t s, const int* gate) {
     if (rows <= 0) return hipSuccess;
     switch (g_split_kind) {
         case 1: break;
-        case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
-        case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
-        case 4: launch_relay<16, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
-        default: launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s); return hipGetLastError();
+        case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
+        case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
+        case 4: launch_relay<16, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
+        default: launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
     }
     const size_t lds = split_lds_bytes(N);
     // one wave per CU with most of the register file as a 2-stage load buffer:
     // a lane's packet stream is latency-bound (Little's law) with few in flight
     const dim3 grid(split_wgs(rows, lw));
     switch (g_split_u) {
-        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout); break;
-        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout); break;
-        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout); break;
+        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
+        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
+        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
     }
     return hipGetLastError();
 }

@@ -62,8 +62,9 @@ hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_build_split(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows,
                               int row0, int lw, float* SP, float* fdpn, hipStream_t s);
 hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* theta, hipStream_t s);
+// gate: optional; the launch does nothing unless *gate == kStatusContinue
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
-                               const float* Yin, float* Yout, hipStream_t s);
+                               const float* Yin, float* Yout, hipStream_t s, const int* gate = nullptr);
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
 int split_pick_lw(int rows);                   // lanes per workgroup for a block of `rows`
@@ -85,6 +86,34 @@ hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, lo
 hipError_t launch_negate_b(int B, float* A, int n, long long sA, hipStream_t s);
 hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp, long long sMp6, hipStream_t s);
 hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
+// ---- converge mode of one large problem over many workgroups (pqp_wide.hip)
+enum GemvEpi : int { kEpiPlain = 0, kEpiAdd = 1, kEpiNeg = 2, kEpiFeas = 3 };
+// out[j] = epi( sum_k A[k * lda + j] * x[k] ), j < n_out, k = 0..n_in-1 in order
+struct GemvJob {
+    const float* A;
+    const float* x;
+    float* out;
+    const float* add;  // kEpiAdd: out += 1.0f * add[j]; kEpiFeas: Kp
+    int lda, n_in, n_out, epi;
+};
+struct WideArgs {
+    SolveState* st;
+    int* flag;
+    const float *tq, *tu, *Y, *U, *Fd, *Fp, *Md, *Mp;
+    int N, M;
+    const long long* max_updates;  // device word: <= 0 means no cap (read each iteration)
+};
+struct GemvJobs {
+    GemvJob job[2];          // job[1].A == nullptr: one job
+    int wgs0;                // set by the launcher
+    const int* gate;         // optional: skip unless *gate == kStatusContinue
+    int* flag;               // kEpiFeas: cleared to 0 by an infeasible row
+};
+hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s);
+hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s);
+extern int g_wide_flags;  // tuning (pqp_tune_wide_flags)
+hipError_t launch_wide_decide(const WideArgs& a, hipStream_t s);
+
 void set_variant(int v);
 int get_variant();
 hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,

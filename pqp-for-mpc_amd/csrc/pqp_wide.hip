@@ -1,0 +1,223 @@
+// pqp_wide.hip -- converge mode of ONE large problem spread over many
+// workgroups (solveQuadraticDual, PQP_CPU.c:694-750).
+//
+// The one-workgroup solver (k_solve_single) moves every byte of Qd, Gp and
+// Qp_inv through a single CU each iteration, so it runs at one CU's fetch
+// rate.  Here one iteration is a short chain of launches, replayed from a
+// hipGraph:
+//
+//   K1  tmp = Gp'Y + Fp          and   (Y'Qd)            [two jobs, one launch]
+//   K2  U = -(Qp_inv tmp)
+//   K3  Gp U vs Kp (feasibility) and   (U'Qp)            [two jobs]
+//   K4  costs Jp, Jd, the gap tests, the cap; h += 1 if the update follows
+//   K5  updateY2 (k_split_relay)
+//
+// Every launch first reads the solve's status word and returns at once when
+// the solve has finished, so a graph of C iterations can be replayed until
+// the status says Done/Capped.  Each product of K1-K3 is a column-access
+// mat-vec out[j] = sum_k A[k][j] x[k] with k in order from +0.0f on one lane
+// per output (the reference's matrixMultiply order), spread over W waves as
+// in k_split_relay: wave g % W owns the k-segment g, multiplies it by x ahead
+// of time, and adds it to the running sums handed over through LDS.
+#include "pqp_device.h"
+#include "pqp_launch.h"
+
+#pragma clang fp contract(off)
+
+namespace pqp {
+
+namespace {
+
+inline int cdivw(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// dst (cols x rows, row-major) = transpose of src (rows x cols, row-major)
+__global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ src, int rows, int cols,
+                                                   float* __restrict__ dst) {
+    __shared__ float tile[32][33];
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int r = ty; r < 32; r += 8) {
+        const int rr = r0 + r, cc = c0 + tx;
+        tile[r][tx] = (rr < rows && cc < cols) ? src[(size_t)rr * cols + cc] : 0.0f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int cc = c0 + r, rr = r0 + tx;
+        if (cc < cols && rr < rows) dst[(size_t)cc * rows + rr] = tile[tx][r];
+    }
+}
+
+// sum_k a[k] * b[k], k in order from +0.0f (one lane)
+__device__ inline float dot_seq(const float* __restrict__ a, const float* __restrict__ b, int n) {
+    float s = 0.0f;
+    for (int k = 0; k < n; ++k) s += a[k] * b[k];
+    return s;
+}
+
+// K4: the rest of terminate() (PQP_CPU.c:673-687) and the loop control.
+// (Folding this into K3's last workgroup to finish, behind an agent-scope
+// fence and a counter, measured 1-5 us slower per iteration than a launch.)
+__global__ void __launch_bounds__(128) k_wide_decide(WideArgs a) {
+    SolveState* st = a.st;
+    if (st->status != kStatusContinue) return;
+    __shared__ float sJ[2];
+    const int tid = threadIdx.x;
+    const int feasible = *a.flag;  // checkFeas :677
+    int stop = 0;
+    if (feasible) {
+        if (tid == 0 || tid == 64) {  // computeCost :648-666, dual on wave 0, primal on wave 1
+            const bool dual = (tid == 0);
+            const float* row = dual ? a.tq : a.tu;
+            const float* z = dual ? a.Y : a.U;
+            const float* F = dual ? a.Fd : a.Fp;
+            const int n = dual ? a.N : a.M;
+            const float quad = dot_seq(row, z, n);
+            const float lin = dot_seq(F, z, n);
+            float J = 0.0f;
+            J = (float)((double)J + 0.5 * (double)quad);
+            J += lin;
+            J += (dual ? a.Md[0] : a.Mp[0]) / 2;
+            sJ[dual ? 1 : 0] = J;
+        }
+        __syncthreads();
+        const float Jp = sJ[0], Jd = sJ[1];
+        stop = 1;  // the three gap tests :681-685
+        if (Jp > -Jd) stop = 0;
+        if ((double)(Jp + Jd) > kTol) stop = 0;
+        if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+        if (tid == 0) {
+            st->Jp = Jp;
+            st->Jd = Jd;
+            st->have_costs = 1;
+        }
+    }
+    if (tid == 0) {
+        if (stop)
+            st->status = kStatusDone;
+        else if (*a.max_updates > 0 && st->h - 1 >= *a.max_updates)
+            st->status = kStatusCapped;
+        else
+            st->h += 1;  // the updateY2 that follows (:718-720)
+        *a.flag = 1;     // re-armed for the next checkFeas
+    }
+}
+
+template <int W, int S>
+__global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
+    if (J.gate && *J.gate != kStatusContinue) return;  // the solve has finished
+    // LDS: [64] hand-off words, then x (zero-padded to whole segments)
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds);
+    float* xs = lds + 128;
+    const bool second = (int)blockIdx.x >= J.wgs0;
+    const GemvJob jb = second ? J.job[1] : J.job[0];
+    const int wg = second ? (int)blockIdx.x - J.wgs0 : (int)blockIdx.x;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = wg * 64 + lane;
+    const bool live = j < jb.n_out;
+    const int jc = live ? j : jb.n_out - 1;  // idle lanes re-read a valid column
+    const int n_in = jb.n_in;
+    const int G = (n_in + S - 1) / S;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    float q[S];
+    auto load_seg = [&](int g) {
+        const int nk = n_in - g * S;  // wave-uniform; k >= n_in is +0 and not loaded
+        const float* col = jb.A + (size_t)g * S * jb.lda + jc;
+#pragma unroll
+        for (int t = 0; t < S; ++t) q[t] = (t < nk) ? col[(size_t)t * jb.lda] : 0.0f;
+    };
+    if (w < G) load_seg(w);  // independent of x: in flight while x is staged
+    {
+        const int t = threadIdx.x, n_lds = G * S;
+        for (int b = 0; b < n_lds; b += 64 * W * 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = b + 64 * W * u + t;
+                v[u] = (k < n_in) ? jb.x[k] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = b + 64 * W * u + t;
+                if (k < n_lds) xs[k] = v[u];
+            }
+        }
+        if (w == 0) slot[lane] = 0ull;  // segment 0 starts from +0.0f
+    }
+    __syncthreads();
+    float acc = 0.0f;
+    for (int g = w; g < G; g += W) {
+#pragma unroll
+        for (int t = 0; t < S; t += 4) {
+            const f4v xv = *reinterpret_cast<const f4v*>(xs + g * S + t);
+            const f2v lo = f2v{q[t], q[t + 1]} * f2v{xv.x, xv.y};
+            const f2v hi = f2v{q[t + 2], q[t + 3]} * f2v{xv.z, xv.w};
+            q[t] = lo.x;
+            q[t + 1] = lo.y;
+            q[t + 2] = hi.x;
+            q[t + 3] = hi.y;
+            asm volatile("" : "+v"(q[t]), "+v"(q[t + 1]), "+v"(q[t + 2]), "+v"(q[t + 3]));
+        }
+        unsigned long long h;
+        for (int spin = 0;; ++spin) {
+            h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
+        }
+        __builtin_amdgcn_s_setprio(3);
+        acc = __uint_as_float((unsigned)h);
+#pragma unroll
+        for (int t = 0; t < S; ++t) acc += q[t];  // matrixMultiply :88-100, k in order
+        __hip_atomic_store(slot + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_s_setprio(0);
+        if (g + W < G) load_seg(g + W);
+    }
+    if (w == (G - 1) % W && live) {
+        switch (jb.epi) {
+            case kEpiAdd: jb.out[j] = acc + 1.0f * jb.add[j]; break;  // matrixAdd(tmp, Fp, 1) :356
+            case kEpiNeg: jb.out[j] = -acc; break;                    // U = -U :358
+            case kEpiFeas: {                                          // compare :334-343
+                const float kp = jb.add[j];
+                if (acc > kp + max_ref((float)(kTol * kp), (float)kTol)) atomicAnd(J.flag, 0);
+                jb.out[j] = acc;
+                break;
+            }
+            default: jb.out[j] = acc;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {
+    if (rows <= 0 || cols <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_transpose, dim3(cdivw(cols, 32), cdivw(rows, 32)), dim3(256), 0, s, src, rows, cols, dst);
+    return hipGetLastError();
+}
+
+int g_wide_flags = 0;  // tuning: bit 0 update on a forked graph branch, bit 1 gemv segments of 64 (default 32)
+
+template <int W, int S>
+static hipError_t gemv_launch(GemvJobs J, int n_in, hipStream_t s) {
+    const size_t lds = sizeof(float) * ((size_t)cdivw(n_in, S) * S + 128);
+    const int wgs1 = J.job[1].A ? cdivw(J.job[1].n_out, 64) : 0;
+    hipLaunchKernelGGL((k_gemv_relay<W, S>), dim3(J.wgs0 + wgs1), dim3(64 * W), lds, s, J);
+    return hipGetLastError();
+}
+
+hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s) {
+    GemvJobs J = jobs;
+    J.wgs0 = cdivw(J.job[0].n_out, 64);
+    int n_in = J.job[0].n_in;
+    if (J.job[1].A && J.job[1].n_in > n_in) n_in = J.job[1].n_in;
+    return (g_wide_flags & 2) ? gemv_launch<8, 64>(J, n_in, s) : gemv_launch<8, 32>(J, n_in, s);
+}
+
+
+hipError_t launch_wide_decide(const WideArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_wide_decide, dim3(1), dim3(128), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace pqp

@@ -1,0 +1,113 @@
+"""GPU parity of converge mode over many workgroups (pqp_wide.hip): one
+problem's terminate() as multi-workgroup mat-vecs plus the relay update,
+replayed from a hipGraph.  Bar: the reference's h, and Y*, U*, Jp, Jd bit
+for bit (golden fixtures from the compiled reference, and the oracle)."""
+from __future__ import annotations
+
+import gzip
+
+import numpy as np
+import pytest
+
+from conftest import CAP, GOLDEN, assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def wide_everywhere(gpu_lib):
+    """Route every converge-mode solve, LDS-sized ones included, to the wide path."""
+    L = gpu_lib.lib()
+    prev = L.pqp_tune_wide_min_n(0)
+    yield
+    L.pqp_tune_wide_min_n(prev)
+
+
+def test_wide_converge_fixtures(gpu_lib, golden_converge, orc, wide_everywhere):
+    """The converging synthetic cases (h from 3 to several thousand, odd and
+    even) against the reference's Y* and U*."""
+    cases, Ys, Us = golden_converge["cases"], golden_converge["Y"], golden_converge["U"]
+    yo = uo = 0
+    for (N, M, seed, h_ref) in cases:
+        N, M = int(N), int(M)
+        P = orc.synth_problem(int(seed), 0, N, M)
+        r = gpu_lib.solve_dual(P, max_updates=CAP)
+        assert r["converged"] and r["h"] == int(h_ref), (N, M, seed, r["h"])
+        assert_bitwise(r["Y"], Ys[yo:yo + N], f"Y {N}/{M}/{seed}")
+        assert_bitwise(r["U"], Us[uo:uo + M], f"U {N}/{M}/{seed}")
+        yo += N
+        uo += M
+
+
+def test_wide_bundled_converge(gpu_lib, golden_bundled, wide_everywhere):
+    g = golden_bundled
+    P = {k: np.ascontiguousarray(g[k], dtype=np.float32) for k in
+         ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    P.update(N=int(g["N"]), M=int(g["M"]))
+    r = gpu_lib.solve_dual(P, max_updates=CAP)
+    assert r["converged"] and r["h"] == 313
+    assert_bitwise(r["Y"], g["Ystar"], "Y*")
+    assert_bitwise(r["U"], g["Ustar"], "U*")
+    assert np.float32(r["Jp"]) == g["iter_Jp"][-1] and np.float32(r["Jd"]) == g["iter_Jd"][-1]
+
+
+def _testing_file(name, tmp_path):
+    """The reference's testing/sample test/<name> (committed, gzip'd for the
+    two large ones)."""
+    plain = GOLDEN / "testing" / name
+    if plain.exists():
+        return plain
+    out = tmp_path / name
+    out.write_bytes(gzip.decompress((GOLDEN / "testing" / (name + ".gz")).read_bytes()))
+    return out
+
+
+@pytest.mark.parametrize("name,cap", [("test1.txt", CAP), ("test2.txt", CAP), ("test3.txt", 60)])
+def test_wide_testing_files_vs_oracle(gpu_lib, orc, name, cap, tmp_path):
+    """The reference's testing/ sample problems (n_dual 1500, 400, 1200) on
+    the default routing (all >= the wide threshold): test1/test2 converge in a
+    few iterations, test3 is capped."""
+    P = gpu_lib.testfile_problem(_testing_file(name, tmp_path))
+    assert P["N"] >= 384
+    r = gpu_lib.solve_dual(P, max_updates=cap)
+    h, Y, U = orc.solve(P, max_updates=cap)
+    assert r["h"] == abs(h) and r["converged"] == (h > 0), (r["h"], h)
+    assert_bitwise(r["Y"], Y, f"{name} Y")
+    assert_bitwise(r["U"], U, f"{name} U")
+
+
+def test_wide_matches_one_workgroup_solver(gpu_lib, orc):
+    """A capped synthetic n_dual = 1024 solve: the wide path and the
+    one-workgroup k_solve_single give the same h, Y, U, Jp, Jd, and both
+    equal the oracle."""
+    N, M, cap = 1024, 512, 25
+    P = orc.synth_problem(3, 1, N, M)
+    L = gpu_lib.lib()
+    wide = gpu_lib.solve_dual(P, max_updates=cap)
+    prev = L.pqp_tune_set_variant(0x200)  # one workgroup
+    try:
+        single = gpu_lib.solve_dual(P, max_updates=cap)
+    finally:
+        L.pqp_tune_set_variant(prev)
+    assert wide["h"] == single["h"] == cap + 1 and not wide["converged"]
+    for k in ("Y", "U"):
+        assert_bitwise(wide[k], single[k], k)
+    assert (np.isnan(wide["Jp"]) and np.isnan(single["Jp"])) or np.float32(wide["Jp"]) == np.float32(single["Jp"])
+    h, Y, U = orc.solve(P, max_updates=cap)
+    assert abs(h) == wide["h"]
+    assert_bitwise(wide["Y"], Y, "Y vs oracle")
+    assert_bitwise(wide["U"], U, "U vs oracle")
+
+
+def test_wide_repeated_solves_and_odd_even(gpu_lib, golden_converge, orc, wide_everywhere):
+    """The captured graph is reused across solves and caps (odd and even
+    update counts leave the iterate in either ping-pong buffer)."""
+    N, M, seed, h_ref = (int(v) for v in golden_converge["cases"][0])
+    P = orc.synth_problem(seed, 0, N, M)
+    with gpu_lib.Problem(P) as prob:
+        for cap in (7, 8, 7, CAP):
+            r = prob.solve(max_updates=cap)
+            h, Y, U = orc.solve(P, max_updates=cap)
+            assert r["h"] == abs(h)
+            assert_bitwise(r["Y"], Y, f"cap {cap}")
+            assert_bitwise(r["U"], U, f"cap {cap}")
