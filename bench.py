@@ -24,6 +24,8 @@ Extra keys:
   mpc_batch     16384 MPC problems (bundled plant at perturbed states), one
                 workgroup each, converge mode with device-side terminate()
   single_n1024  configs[2]: one n_dual=1024 problem, 1000 fixed iterations
+  single_converge  the same problem size in the reference's converge mode
+                (terminate() before every update), capped at 200 updates
   rowshard      one large problem (n_dual = 16384) row-sharded over the job's
                 ranks: per update, every rank updates its
                 rows and an RCCL all-gather assembles y (all ranks take part)
@@ -189,6 +191,24 @@ def single_bench(pqp_amd, N: int = 1024, iters: int = 1000) -> dict:
             "note": "1 problem, fixed mode; per-iteration floor = one lane's N-long sequential sum"}
 
 
+def single_converge_bench(pqp_amd, N: int = 1024, updates: int = 200) -> dict:
+    """One synthetic problem (primal, Qp and duals built on the device) in
+    converge mode: terminate() + updateY2 per iteration over many
+    workgroups.  The synthetic problems do not meet the reference's exact
+    gap test at this size, so the solve is capped."""
+    pb = pqp_amd.ProblemBatch.synthetic(1, 0, 1, N)
+    P = pb.problem(0)
+    del pb
+    with pqp_amd.Problem(P) as prob:
+        prob.solve(max_updates=2)
+        t0 = time.perf_counter()
+        r = prob.solve(max_updates=updates)
+        dt = time.perf_counter() - t0
+    return {"n_dual": N, "m": N // 2, "iterations": r["h"], "converged": bool(r["converged"]),
+            "ms_per_solve": dt * 1e3, "us_per_iter": dt / r["h"] * 1e6, "iter_per_s": r["h"] / dt,
+            "note": "terminate() as multi-workgroup mat-vecs + relay update, hipGraph-replayed (pqp_wide.hip)"}
+
+
 def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: int) -> dict:
     """One synthetic problem of n_dual = N whose rows are spread over the
     ranks (pqp_amd.rowshard); fixed-mode updates, timed as the max over
@@ -346,6 +366,7 @@ def main():
         result["bundled"] = bundled_bench(pqp_amd)
         result["mpc_batch"] = mpc_batch_bench(pqp_amd)
         result["single_n1024"] = single_bench(pqp_amd)
+        result["single_converge"] = single_converge_bench(pqp_amd)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed)
     print(json.dumps(result), flush=True)

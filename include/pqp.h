@@ -174,6 +174,13 @@ int pqp_run_example(const char *dir, void *out);
 int pqp_batch_generate(uint32_t seed, long long inst0, int B, int N, int M, float *d_QdT, int ldq,
                        long long qstride, float *d_Fd, float *d_Md, float *d_theta, int ldv, void *stream);
 
+/* The primal problems behind pqp_batch_generate's duals, in the layout of
+ * 2c below: Qp_inv [B][M*M] (diagonal), Gp [B][N*M], Kp [B][N], Fp [B][M],
+ * Mp [B] (= 1).  With pqp_batch_gauss_jordan and pqp_batch_convert_to_dual
+ * this gives complete problems for converge-mode solves. */
+int pqp_batch_synth_primal(uint32_t seed, long long inst0, int B, int N, int M, float *d_Qp_inv, float *d_Gp,
+                           float *d_Kp, float *d_Fp, float *d_Mp, void *stream);
+
 /* Pack B row-major N x N Qd matrices (device, contiguous) into QdT layout. */
 int pqp_batch_pack(int B, int N, const float *d_Qd, float *d_QdT, int ldq, long long qstride, void *stream);
 

@@ -800,6 +800,16 @@ int pqp_batch_generate(uint32_t seed, long long inst0, int B, int N, int M, floa
     return PQP_OK;
 }
 
+int pqp_batch_synth_primal(uint32_t seed, long long inst0, int B, int N, int M, float* d_Qp_inv, float* d_Gp,
+                           float* d_Kp, float* d_Fp, float* d_Mp, void* stream) {
+    if (B <= 0 || N <= 0 || M <= 0 || !d_Qp_inv || !d_Gp || !d_Kp || !d_Fp || !d_Mp)
+        return set_error(PQP_ERR_ARG, "pqp_batch_synth_primal: bad arguments");
+    PQP_TRY(ensure_device());
+    PQP_HIP(launch_synth_primal(seed, inst0, B, N, M, d_Qp_inv, d_Gp, d_Kp, d_Fp, d_Mp,
+                                static_cast<hipStream_t>(stream)));
+    return PQP_OK;
+}
+
 int pqp_batch_pack(int B, int N, const float* d_Qd, float* d_QdT, int ldq, long long qstride, void* stream) {
     PQP_TRY(check_batch(B, N, d_QdT, ldq, qstride, N));
     if (!d_Qd) return set_error(PQP_ERR_ARG, "pqp_batch_pack: null input");

@@ -747,6 +747,48 @@ __global__ void __launch_bounds__(256) k_synth_fd(uint32_t seed, long long inst0
     }
 }
 
+// Synthetic primal problem (the generator behind pqp_batch_generate's duals):
+// Qp_inv = diag(0.1 + u), Gp in {-1, 0, +1}, Kp = 10u, Fp = 20u - 10, Mp = 1.
+__global__ void __launch_bounds__(256) k_synth_primal(uint32_t seed, long long inst0, int N, int M,
+                                                      float* __restrict__ Qinv, float* __restrict__ Gp,
+                                                      float* __restrict__ Kp, float* __restrict__ Fp,
+                                                      float* __restrict__ Mp) {
+    const int b = blockIdx.y;
+    const SynthKeys K = synth_keys(seed, (uint32_t)(inst0 + b));
+    const long long nG = (long long)N * M, nQ = (long long)M * M;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < nG + nQ + N + M + 1;
+         e += (long long)gridDim.x * 256) {
+        if (e < nG) {
+            Gp[(size_t)b * nG + e] = synth_gp(K, (int)(e / M), (int)(e % M), M);
+        } else if (e < nG + nQ) {
+            const long long q = e - nG;
+            const int r = (int)(q / M), c = (int)(q % M);
+            Qinv[(size_t)b * nQ + q] = (r == c) ? synth_qinv(K, r) : 0.0f;
+        } else if (e < nG + nQ + N) {
+            const int i = (int)(e - nG - nQ);
+            Kp[(size_t)b * N + i] = synth_kp(K, i);
+        } else if (e < nG + nQ + N + M) {
+            const int j = (int)(e - nG - nQ - N);
+            Fp[(size_t)b * M + j] = synth_fp(K, j);
+        } else {
+            Mp[b] = 1.0f;
+        }
+    }
+}
+
+hipError_t launch_synth_primal(uint32_t seed, long long inst0, int B, int N, int M, float* Qinv, float* Gp, float* Kp,
+                               float* Fp, float* Mp, hipStream_t s) {
+    for (int b0 = 0; b0 < B; b0 += 65535) {
+        const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        const long long n = (long long)N * M + (long long)M * M + N + M + 1;
+        const int gx = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+        hipLaunchKernelGGL(k_synth_primal, dim3(gx, nb), dim3(256), 0, s, seed, inst0 + b0, N, M,
+                           Qinv + (size_t)b0 * M * M, Gp + (size_t)b0 * N * M, Kp + (size_t)b0 * N,
+                           Fp + (size_t)b0 * M, Mp + b0);
+    }
+    return hipGetLastError();
+}
+
 // Zero the padding rows [N, ldq) of every column k < N (used when the
 // generator's tiles do not cover them).
 __global__ void k_zero_pad(float* __restrict__ QdT, int N, int ldq, long long qstride) {

@@ -44,6 +44,8 @@ hipError_t launch_theta(int B, const float* QdT, int ldq, long long qstride, int
                         hipStream_t s);
 hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, float* QdT, int ldq, long long qstride,
                         float* Fd, int ldv, float* Md, hipStream_t s);
+hipError_t launch_synth_primal(uint32_t seed, long long inst0, int B, int N, int M, float* Qinv, float* Gp, float* Kp,
+                               float* Fp, float* Mp, hipStream_t s);
 hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c,
                              hipStream_t s);
 hipError_t launch_axpy(float* A, const float* B, float sign, int n, hipStream_t s);

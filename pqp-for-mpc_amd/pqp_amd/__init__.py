@@ -68,6 +68,7 @@ SIGNATURES = {
     "pqp_read_testfile": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)] + [_fp] * 5),
     "pqp_batch_generate": (C.c_int, [C.c_uint32, C.c_longlong, C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_longlong,
                                      _vp, _vp, _vp, C.c_int, _vp]),
+    "pqp_batch_synth_primal": (C.c_int, [C.c_uint32, C.c_longlong] + [C.c_int] * 3 + [_vp] * 5 + [_vp]),
     "pqp_batch_pack": (C.c_int, [C.c_int, C.c_int, _vp, _vp, C.c_int, C.c_longlong, _vp]),
     "pqp_batch_theta": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, C.c_int, _vp]),
     "pqp_batch_update": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, _vp, C.c_int, _vp, _vp, _vp]),
@@ -485,6 +486,22 @@ class ProblemBatch:
                 v = pb.torch.as_tensor(np.asarray(P[k], np.float32).reshape(-1), device=pb.device)
                 getattr(pb, k).copy_(v.expand(B, -1) if getattr(pb, k).dim() == 2 else v.expand(B))
         return pb
+
+    @classmethod
+    def synthetic(cls, seed: int, inst0: int, B: int, N: int, M: int | None = None, device=None) -> "ProblemBatch":
+        """Synthetic problems inst0..inst0+B-1 of `seed` (the primal behind
+        Batch.generate), with Qp and the duals built on the device."""
+        M = int(M) if M else max(1, int(N) // 2)
+        pb = cls(B, N, M, device)
+        _check(lib().pqp_batch_synth_primal(seed, inst0, pb.B, pb.N, pb.M, *[pb._p(getattr(pb, k)) for k in
+                                                                            cls.PRIMAL], pb._s()))
+        return pb.gauss_jordan().convert_to_dual()
+
+    def problem(self, b: int = 0) -> dict:
+        """Problem b as a host dict (the keys of solve_dual / Problem)."""
+        P = {k: getattr(self, k)[b].cpu().numpy().reshape(-1) for k in self.PRIMAL + self.DUAL + ("Qp",)}
+        P.update(N=self.N, M=self.M)
+        return P
 
     def set(self, name: str, values):
         """Per-problem values for one array ([B, ...] numpy/torch)."""

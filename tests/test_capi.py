@@ -49,33 +49,41 @@ def test_python_mirror_binds_every_symbol():
     assert L.pqp_version() >= 100
 
 
-def test_hot_kernels_compile_for_gfx950_without_fma():
-    """The update kernels must not contract a*b+c into FMA (bit-parity rule,
-    SURVEY.md 8a): compile the kernel TU for gfx950 exactly as the Makefile
-    does and inspect the ISA of the hot kernels."""
+def _gfx950_asm(name: str) -> str:
     import tempfile
 
     hipcc = Path("/opt/rocm/bin/hipcc")
     if not hipcc.exists():
         pytest.skip("hipcc not present")
-    src = ROOT / "pqp-for-mpc_amd" / "csrc" / "pqp_kernels.hip"
+    src = ROOT / "pqp-for-mpc_amd" / "csrc" / name
     with tempfile.TemporaryDirectory() as td:
         out = Path(td) / "k.s"
         subprocess.run([str(hipcc), "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                         "-fno-fast-math", "--cuda-device-only", "-S", str(src), "-o", str(out)], check=True)
-        asm = out.read_text()
+        return out.read_text()
+
+
+@pytest.mark.parametrize("src,pattern,min_kernels", [
+    ("pqp_kernels.hip", r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|14k_split_update)",
+     13),
+    ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 3),
+])
+def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
+    """The update and terminate() kernels must not contract a*b+c into FMA
+    (bit-parity rule): compile each kernel TU for gfx950
+    exactly as the Makefile does and inspect the ISA of the hot kernels."""
+    asm = _gfx950_asm(src)
     bodies = re.split(r"\n(?=_ZN3pqp[A-Za-z0-9_]*:)", asm)
-    hot = [b for b in bodies if re.match(r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single)", b)]
-    assert len(hot) >= 6, "hot kernels not found in the gfx950 assembly"
+    hot = [b for b in bodies if re.match(pattern, b)]
+    assert len(hot) >= min_kernels, f"hot kernels of {src} not found in the gfx950 assembly ({len(hot)})"
     for body in hot:
         name = body.split(":", 1)[0]
         body = body.split(".Lfunc_end", 1)[0]
-        # the only FMAs allowed are the 5 inside each IEEE-correct division
+        # the only f32 FMAs allowed are the 5 inside each IEEE-correct division
         # expansion (v_div_scale .. v_div_fmas .. v_div_fixup); none may come
         # from contracting the solver's own products and sums
         n_div = len(re.findall(r"\bv_div_fixup_f32", body))
         n_fma = len(re.findall(r"\bv_(fma|fmac|mad|mac|pk_fma)_f32", body))
-        assert n_div > 0, name + ": division is not the IEEE-correct sequence"
         assert n_fma == 5 * n_div, f"{name}: {n_fma} FMAs for {n_div} divisions"
 
 

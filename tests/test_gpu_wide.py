@@ -111,3 +111,15 @@ def test_wide_repeated_solves_and_odd_even(gpu_lib, golden_converge, orc, wide_e
             assert r["h"] == abs(h)
             assert_bitwise(r["Y"], Y, f"cap {cap}")
             assert_bitwise(r["U"], U, f"cap {cap}")
+
+
+def test_device_synthetic_primal_matches_oracle(gpu_lib, orc):
+    """pqp_batch_synth_primal + Gauss_Jordan + convertToDual on the device ==
+    the oracle's generator and setup, for every array."""
+    B, N, M = 3, 300, 150
+    pb = gpu_lib.ProblemBatch.synthetic(5, 11, B, N, M)
+    for b in range(B):
+        got = pb.problem(b)
+        want = orc.synth_problem(5, 11 + b, N, M)
+        for k in ("Qp_inv", "Gp", "Kp", "Fp", "Mp", "Qp", "Qd", "Fd", "Md"):
+            assert_bitwise(got[k], np.asarray(want[k], np.float32).reshape(-1), f"problem {b} {k}")
