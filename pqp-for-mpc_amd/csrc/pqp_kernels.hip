@@ -1727,7 +1727,17 @@ hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp
     return hipGetLastError();
 }
 hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s) {
-    if (B > 0) hipLaunchKernelGGL(k_gauss_jordan, dim3(B), dim3(256), 0, s, A, aug, fac, res, n);
+    if (B <= 0) return hipSuccess;
+    if (n >= kGaussJordanWideMin && B <= 8) {  // few large matrices: each over many workgroups
+        for (int b = 0; b < B; ++b) {
+            const hipError_t e = launch_gauss_jordan_wide(A + (size_t)b * n * n, aug + (size_t)b * 2 * n * n,
+                                                          reinterpret_cast<int*>(fac + (size_t)b * n),
+                                                          res + (size_t)b * n * n, n, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    hipLaunchKernelGGL(k_gauss_jordan, dim3(B), dim3(256), 0, s, A, aug, fac, res, n);
     return hipGetLastError();
 }
 hipError_t launch_axpy(float* A, const float* B, float sign, int n, hipStream_t s) {
@@ -1755,8 +1765,7 @@ hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStre
     return hipGetLastError();
 }
 hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s) {
-    hipLaunchKernelGGL(k_gauss_jordan, dim3(1), dim3(256), 0, s, A, aug, fac, res, n);
-    return hipGetLastError();
+    return launch_gauss_jordan_b(1, A, aug, fac, res, n, s);
 }
 
 size_t solve_single_lds_bytes(int ldq, int ldm) { return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm); }

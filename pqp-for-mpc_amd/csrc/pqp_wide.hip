@@ -188,6 +188,49 @@ __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Gauss_Jordan (PQP_CPU.c:251-326) of one large matrix over many workgroups:
+// one launch per pivot, one workgroup per row.  Each element still sees the
+// reference's operations in the reference's order (the pivots in sequence,
+// row j's factor read before row j changes), so the inverse is bit-identical.
+// ---------------------------------------------------------------------------
+// the one bubble pass on column 0 (:280-289) decides swaps from column-0
+// values only: replay it on them to get the final row order
+__global__ void k_gj_order(const float* __restrict__ A, int n, int* __restrict__ perm) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int r = 0; r < n; ++r) perm[r] = r;
+    for (int r = n - 1; r > 0; --r) {
+        if (A[(size_t)perm[r - 1] * n] < A[(size_t)perm[r] * n]) {
+            const int t = perm[r];
+            perm[r] = perm[r - 1];
+            perm[r - 1] = t;
+        }
+    }
+}
+// [A | I] (:262-276) with the rows in that order
+__global__ void __launch_bounds__(256) k_gj_fill(const float* __restrict__ A, int n, const int* __restrict__ perm,
+                                                 float* __restrict__ aug) {
+    const int r = blockIdx.x, src = perm[r], w = 2 * n;
+    for (int c = threadIdx.x; c < w; c += 256)
+        aug[(size_t)r * w + c] = (c < n) ? A[(size_t)src * n + c] : ((c == n + src) ? 1.0f : 0.0f);
+}
+// pivot p (:291-305): row r -= row p * (aug[r][p] / aug[p][p]) for r != p
+__global__ void __launch_bounds__(256) k_gj_pivot(float* __restrict__ aug, int n, int p) {
+    const int r = blockIdx.x, w = 2 * n;
+    if (r == p) return;
+    float* row = aug + (size_t)r * w;
+    const float* prow = aug + (size_t)p * w;
+    const float f = row[p] / prow[p];  // every thread reads row[p] before any thread writes it
+    __syncthreads();
+    for (int c = threadIdx.x; c < w; c += 256) row[c] -= prow[c] * f;
+}
+// the row scaling (:307-314) and the extraction of the right half (:316-322)
+__global__ void __launch_bounds__(256) k_gj_finish(const float* __restrict__ aug, int n, float* __restrict__ res) {
+    const int r = blockIdx.x, w = 2 * n;
+    const float d = aug[(size_t)r * w + r];
+    for (int c = threadIdx.x; c < n; c += 256) res[(size_t)r * n + c] = aug[(size_t)r * w + n + c] / d;
+}
+
 }  // namespace
 
 hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {
@@ -214,6 +257,15 @@ hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s) {
     return (g_wide_flags & 2) ? gemv_launch<8, 64>(J, n_in, s) : gemv_launch<8, 32>(J, n_in, s);
 }
 
+
+hipError_t launch_gauss_jordan_wide(const float* A, float* aug, int* perm, float* res, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gj_order, dim3(1), dim3(64), 0, s, A, n, perm);
+    hipLaunchKernelGGL(k_gj_fill, dim3(n), dim3(256), 0, s, A, n, perm, aug);
+    for (int p = 0; p < n; ++p) hipLaunchKernelGGL(k_gj_pivot, dim3(n), dim3(256), 0, s, aug, n, p);
+    hipLaunchKernelGGL(k_gj_finish, dim3(n), dim3(256), 0, s, aug, n, res);
+    return hipGetLastError();
+}
 
 hipError_t launch_wide_decide(const WideArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_wide_decide, dim3(1), dim3(128), 0, s, a);

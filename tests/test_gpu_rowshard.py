@@ -187,13 +187,15 @@ def _rank_main(rank, world, port, N, ups, out):
     dist.destroy_process_group()
 
 
-def test_rowsharded_two_processes(gpu_lib, orc, tmp_path):
+@pytest.mark.parametrize("world,N", [(2, 1030), (3, 4)])
+def test_rowsharded_two_processes(gpu_lib, orc, tmp_path, world, N):
+    """2 ranks on a ragged N, and 3 ranks on N = 4 (the last rank owns no rows)."""
     import torch.multiprocessing as mp
 
-    N, ups, world = 1030, 6, 2
+    ups = 6
     out = str(tmp_path / "y")
     mp.spawn(_rank_main, args=(world, _free_port(), N, ups, out), nprocs=world, join=True)
-    P = orc.synth_problem(5, 9, N, N // 2, with_qp=False)
+    P = orc.synth_problem(5, 9, N, max(1, N // 2), with_qp=False)
     want = orc.iterate(P["Qd"], P["Fd"], N, ups)
     for r in range(world):
         assert_bitwise(np.load(f"{out}.{r}.npy"), want, f"rank {r}")
