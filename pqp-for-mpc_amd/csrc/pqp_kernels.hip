@@ -1368,7 +1368,7 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A0, SolveState* __
     SolveState* st = st0 + blockIdx.x;
     if (st->status == kStatusDone || st->status == kStatusCapped) return;
     __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
-    __shared__ float sc[2][8];  // [parity]: 0 s_dual, 1 lin_dual, 2 infeasible, 3 quad_p, 4 lin_p
+    __shared__ float sc[2][8];  // [parity]: 0 s_dual, 1 lin_dual, 2 infeasible, 3 quad_p, 4 lin_p, 5 stop
     const int N = A.N, M = A.M;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const bool conv = (A.mode != kModeFixed);
@@ -1510,26 +1510,34 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A0, SolveState* __
         }
         __syncthreads();
         if (conv) {
-            int stop = 0;
-            if (sc[par][2] == 0.0f) {
-                float Jp = 0.0f;
-                Jp = (float)((double)Jp + 0.5 * (double)sc[par][3]);
-                Jp += sc[par][4];
-                Jp += Mp / 2;
-                float Jd = 0.0f;
-                Jd = (float)((double)Jd + 0.5 * (double)sc[par][0]);
-                Jd += sc[par][1];
-                Jd += Md / 2;
-                stop = 1;
-                if (Jp > -Jd) stop = 0;
-                if ((double)(Jp + Jd) > kTol) stop = 0;
-                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
-                if (tid == 0) {
-                    st->Jp = Jp;
-                    st->Jd = Jd;
-                    st->have_costs = 1;
+            // the costs and gap tests (:648-687) on one wave only; the others
+            // wait for its verdict at a second barrier instead of repeating
+            // the double-precision tests four times
+            if (wave == 1) {
+                int stop1 = 0;
+                if (sc[par][2] == 0.0f) {
+                    float Jp = 0.0f;
+                    Jp = (float)((double)Jp + 0.5 * (double)sc[par][3]);
+                    Jp += sc[par][4];
+                    Jp += Mp / 2;
+                    float Jd = 0.0f;
+                    Jd = (float)((double)Jd + 0.5 * (double)sc[par][0]);
+                    Jd += sc[par][1];
+                    Jd += Md / 2;
+                    stop1 = 1;
+                    if (Jp > -Jd) stop1 = 0;
+                    if ((double)(Jp + Jd) > kTol) stop1 = 0;
+                    if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop1 = 0;
+                    if (lane == 0) {
+                        st->Jp = Jp;
+                        st->Jd = Jd;
+                        st->have_costs = 1;
+                    }
                 }
+                if (lane == 0) sc[par][5] = stop1 ? 1.0f : 0.0f;
             }
+            __syncthreads();
+            const int stop = sc[par][5] != 0.0f;
             if (A.mode == kModeTerminate) {
                 if (tid == 0) st->last_stop = stop;
                 status = kStatusDone;
