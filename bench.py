@@ -96,15 +96,30 @@ def cpu_baseline(n: int, seconds: float, seed: int) -> dict:
                 break
         kind = "reference"
         what = "oracle/_ref/libpqp_ref.so (PQP_CPU.c, gcc -O2 -ffp-contract=off) updateY2"
+        # configs[0]: the bundled example through the reference's own input(),
+        # setup and solveQuadraticDual (converge mode, C loop), median of 5
+        B = ref.bundled_problem(ROOT / "tests" / "golden")
+        times, h = [], 0
+        for _ in range(5):
+            tb = time.perf_counter()
+            h, _, _ = ref.solve(B)
+            times.append(time.perf_counter() - tb)
+        tb = sorted(times)[len(times) // 2]
+        bundled = {"converge_h": h, "converge_ms": tb * 1e3, "iter_per_s": h / tb,
+                   "what": "PQP_CPU.c solveQuadraticDual on the bundled example (configs[0]), 1 thread"}
     else:
         per, _ = orc.time_updates(P["Qd"], P["Fd"], n, 3)
         ups = max(3, int(seconds / max(per / 3, 1e-6)))
         el, _ = orc.time_updates(P["Qd"], P["Fd"], n, ups)
         kind = "port"
         what = "oracle/pqp_oracle.c (bit-exact restatement, -O2 -ffp-contract=off) updateY2"
-    return {"value": ups / el, "unit": "instance-iterations/s", "cores": 1, "kind": kind,
-            "sample": f"{what}: {ups} fixed-mode updates of 1 synthetic problem (n_dual={n}, M={n // 2}, seed "
-                      f"{seed}) in {el:.1f} s, 1 thread, setup excluded; host has {os.cpu_count()} logical CPUs"}
+        bundled = None
+    out = {"value": ups / el, "unit": "instance-iterations/s", "cores": 1, "kind": kind,
+           "sample": f"{what}: {ups} fixed-mode updates of 1 synthetic problem (n_dual={n}, M={n // 2}, seed "
+                     f"{seed}) in {el:.1f} s, 1 thread, setup excluded; host has {os.cpu_count()} logical CPUs"}
+    if bundled:
+        out["bundled"] = bundled
+    return out
 
 
 def bundled_bench(pqp_amd) -> dict:
