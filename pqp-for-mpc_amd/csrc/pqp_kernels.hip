@@ -475,14 +475,15 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * lw * 16, 0x00020000);
     const int vo = ll * 16, kstride = lw * 16;
     f4v q[S];
+    const bool lane_loads = lane < lw;  // lanes >= lw would only repeat lane % lw's requests
     auto load_seg = [&](int g) {
         // packets past KB (the last segment's tail) are +0, an exact no-op;
         // they are not loaded (the SGPR offset is not range-checked)
         const int nj = KB - g * S;  // wave-uniform
 #pragma unroll
         for (int j = 0; j < S; ++j)
-            q[j] = (j < nj) ? __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (g * S + j) * kstride, 0)
-                            : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+            q[j] = (j < nj && lane_loads) ? __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (g * S + j) * kstride, 0)
+                                          : f4v{0.0f, 0.0f, 0.0f, 0.0f};
     };
     if (w < G) load_seg(w);  // independent of y: in flight while y is staged
     const float fd = live ? fdpn[p] : 0.0f;
@@ -510,16 +511,25 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
     float acc = 0.0f;
     for (int g = w; g < G; g += W) {
         // products of this segment (packed multiplies, each product rounded
-        // exactly as q * y), overwriting the packets
+        // exactly as q * y), overwriting the packets; y is read from LDS four
+        // packets at a time so the reads overlap (one at a time, the first
+        // segment's products took twice as long on the critical path)
 #pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const f4v y = *reinterpret_cast<const f4v*>(ys + 4 * (g * S + j));
-            f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
-            f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
-            q[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+        for (int j0 = 0; j0 < S; j0 += 4) {
+            f4v y[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) y[u] = *reinterpret_cast<const f4v*>(ys + 4 * (g * S + j0 + u));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u;
+                const f2v lo = f2v{q[j].x, q[j].y} * f2v{y[u].x, y[u].y};
+                const f2v hi = f2v{q[j].z, q[j].w} * f2v{y[u].z, y[u].w};
+                q[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+            }
             // pin the products here, before the wait below: otherwise the
             // compiler sinks the multiplies into the add chain
-            asm volatile("" : "+v"(q[j]));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) asm volatile("" : "+v"(q[j0 + u]));
         }
         // wait until every lane's hand-off word carries sequence g (the sum
         // and its sequence number travel in one 64-bit LDS word).  Bounded:

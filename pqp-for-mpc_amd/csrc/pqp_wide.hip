@@ -149,15 +149,25 @@ __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
     float acc = 0.0f;
     for (int g = w; g < G; g += W) {
 #pragma unroll
-        for (int t = 0; t < S; t += 4) {
-            const f4v xv = *reinterpret_cast<const f4v*>(xs + g * S + t);
-            const f2v lo = f2v{q[t], q[t + 1]} * f2v{xv.x, xv.y};
-            const f2v hi = f2v{q[t + 2], q[t + 3]} * f2v{xv.z, xv.w};
-            q[t] = lo.x;
-            q[t + 1] = lo.y;
-            q[t + 2] = hi.x;
-            q[t + 3] = hi.y;
-            asm volatile("" : "+v"(q[t]), "+v"(q[t + 1]), "+v"(q[t + 2]), "+v"(q[t + 3]));
+        for (int t0 = 0; t0 < S; t0 += 16) {  // x read 16 values at a time so the LDS reads overlap
+            f4v xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) xv[u] = *reinterpret_cast<const f4v*>(xs + g * S + t0 + 4 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 4 * u;
+                const f2v lo = f2v{q[t], q[t + 1]} * f2v{xv[u].x, xv[u].y};
+                const f2v hi = f2v{q[t + 2], q[t + 3]} * f2v{xv[u].z, xv[u].w};
+                q[t] = lo.x;
+                q[t + 1] = lo.y;
+                q[t + 2] = hi.x;
+                q[t + 3] = hi.y;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + 4 * u;
+                asm volatile("" : "+v"(q[t]), "+v"(q[t + 1]), "+v"(q[t + 2]), "+v"(q[t + 3]));
+            }
         }
         unsigned long long h;
         for (int spin = 0;; ++spin) {
