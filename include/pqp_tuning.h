@@ -16,7 +16,8 @@ extern "C" {
  * launch_batch_iterate).  Bit 0x100: solve N, M <= 32 problems with the
  * LDS-staged k_solve_small instead of k_solve_tiny.  Bit 0x200: fixed-mode
  * solves of large single problems on one workgroup (k_solve_single) instead
- * of the multi-workgroup split-matrix update.  Bits 12-13: k_split_update
+ * of the multi-workgroup split-matrix update.  Bit 0x400: fixed mode of
+ * N <= 32 problems on k_solve_tiny instead of the one-wave k_fixed_tiny.  Bits 12-13: k_split_update
  * load stage depth (0: 16 packets, 1: 8, 2: 24).  Bits 14-16: the kernel
  * behind pqp_rowblock_update and large fixed-mode solves (0: default =
  * k_split_relay with 8 waves x 16-packet segments, 1: streaming

@@ -1328,6 +1328,7 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 
 extern "C" int pqp_tune_set_variant(int variant) {
     const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0) |
+                    (pqp::g_fixed_tiny_old ? 0x400 : 0) |
                     (pqp::g_split_u << 12) | (pqp::g_split_kind << 14) |
                     ((pqp::g_split_lw ? __builtin_ctz(pqp::g_split_lw) - 2 : 0) << 17);
     pqp::set_variant(variant & 0xff);
@@ -1336,6 +1337,7 @@ extern "C" int pqp_tune_set_variant(int variant) {
     const int lwsel = (variant >> 17) & 7;  // 0 auto, 1: 8, 2: 16, 3: 32, 4: 64 lanes per workgroup
     pqp::g_split_lw = (lwsel >= 1 && lwsel <= 4) ? (4 << lwsel) : 0;
     pqp::g_force_small = (variant & 0x100) != 0;
+    pqp::g_fixed_tiny_old = (variant & 0x400) != 0;
     pqp::g_force_single = (variant & 0x200) != 0;
     return old;
 }

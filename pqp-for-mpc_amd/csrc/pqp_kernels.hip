@@ -1582,6 +1582,97 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A0, SolveState* __
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_fixed_tiny<NMAX>: the fixed-iteration mode (while(h < NUM_ITER), no
+// terminate) of one N <= NMAX problem on ONE wave: lane 2i + side holds row
+// i's split row (Qdn_theta / Qdp_theta incl. Theta) in VGPRs, y lives in LDS.
+// Per update: the products (packed multiplies, off the add chain), the
+// sequential adds, the num/den exchange by a DPP lane swap (not an LDS
+// permute), the division.  The iterate's own y_i is read at the top of the
+// update so its latency hides under the chain.  One wave: a ds_write followed
+// by the next update's ds_reads needs no workgroup barrier.
+// ---------------------------------------------------------------------------
+template <int NMAX>
+__global__ void __launch_bounds__(64) k_fixed_tiny(SolveArgs A0, SolveState* __restrict__ st0) {
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;
+    __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
+    const int N = A.N;
+    const int lane = threadIdx.x, i = lane >> 1, side = lane & 1;
+    const bool row = i < N;
+    float mat[NMAX];
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) mat[k] = 0.0f;
+    float fd_own = 0.0f;
+    if (row) {
+        float th = 0.0f;  // computeTheta (:503-519)
+        for (int k = 0; k < N; ++k) th += max_ref(0.0f, -A.Qd[i * N + k]) * 1.0f;
+        th = max_ref(th, 5.0f);
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) {
+            if (k < N) {
+                const float q = A.Qd[i * N + k];
+                const float t = (i == k) ? th : 0.0f;
+                mat[k] = (side ? max_ref(0.0f, q) : max_ref(0.0f, -q)) + 1.0f * t;  // :524-537
+            }
+        }
+        const float f = A.Fd[i];
+        fd_own = side ? max_ref(0.0f, f) : max_ref(0.0f, -f);  // Fdp / Fdn (:703-704)
+    }
+    for (int k = lane; k < NMAX; k += 64) {
+        ybuf[0][k] = (k < N) ? (st->resume ? A.Y[k] : 1000.0f) : 0.0f;  // initMat(Y, 1000) :710
+        ybuf[1][k] = 0.0f;
+    }
+    __syncthreads();
+    const int ic = row ? i : 0;
+    long long h = st->h;
+    long long done_here = 0;
+    int cb = 0;
+    int status = kStatusContinue;
+    for (;;) {
+        if (h >= A.num_iter) {  // while(h < NUM_ITER)
+            status = kStatusDone;
+            break;
+        }
+        if (done_here >= A.chunk) break;
+        const float* cur = ybuf[cb];
+        float* nxt = ybuf[cb ^ 1];
+        const float yi = cur[ic];
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        float p[NMAX];
+#pragma unroll
+        for (int k = 0; k < NMAX; k += 4) {
+            const f4v y = *reinterpret_cast<const f4v*>(cur + k);
+            const f2v lo = f2v{mat[k], mat[k + 1]} * f2v{y.x, y.y};
+            const f2v hi = f2v{mat[k + 2], mat[k + 3]} * f2v{y.z, y.w};
+            p[k] = lo.x;
+            p[k + 1] = lo.y;
+            p[k + 2] = hi.x;
+            p[k + 3] = hi.y;
+        }
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) acc += p[k];  // :608-609, k in order
+        const float v = acc + 1.0f * fd_own;        // even lane: num (:611), odd lane: den (:612)
+        // lane ^ 1 by DPP quad_perm(1,0,3,2); the whole wave is active here
+        const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+        if (!side && row) nxt[i] = v / den * yi;    // :594
+        __syncthreads();
+        cb ^= 1;
+        ++h;
+        ++done_here;
+    }
+    for (int k = lane; k < N; k += 64) A.Y[k] = ybuf[cb][k];
+    if (lane == 0) {
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
+    }
+}
+
 template <int NMAX>
 static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads, hipStream_t s) {
     if (a.M <= 8)
@@ -1592,9 +1683,19 @@ static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads
         hipLaunchKernelGGL((k_solve_tiny<NMAX, 32>), dim3(B), dim3(threads), 0, s, a, st);
 }
 
+int g_fixed_tiny_old = 0;  // tuning: fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
+
 static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the
     // sequential chain is the critical path, so keep the padding small
+    if (a.mode == kModeFixed && !g_fixed_tiny_old) {
+        if (a.N <= 8) hipLaunchKernelGGL((k_fixed_tiny<8>), dim3(B), dim3(64), 0, s, a, st);
+        else if (a.N <= 16) hipLaunchKernelGGL((k_fixed_tiny<16>), dim3(B), dim3(64), 0, s, a, st);
+        else if (a.N <= 24) hipLaunchKernelGGL((k_fixed_tiny<24>), dim3(B), dim3(64), 0, s, a, st);
+        else if (a.N <= 28) hipLaunchKernelGGL((k_fixed_tiny<28>), dim3(B), dim3(64), 0, s, a, st);
+        else hipLaunchKernelGGL((k_fixed_tiny<32>), dim3(B), dim3(64), 0, s, a, st);
+        return hipGetLastError();
+    }
     const int threads = (a.mode == kModeFixed) ? 64 : 256;
     if (a.N <= 8) launch_tiny_m<8>(B, a, st, threads, s);
     else if (a.N <= 16) launch_tiny_m<16>(B, a, st, threads, s);
