@@ -126,7 +126,11 @@ int pqp_solve_dual(const float *Qd, const float *Fd, const float *Md, const floa
 
 /* A dual problem resident in HBM: upload and prepare once, then solve any
  * number of times (each solve restarts from Y = 1000).  Same semantics and
- * outputs as pqp_solve_dual, which is create + solve + destroy. */
+ * outputs as pqp_solve_dual, which is create + solve + destroy.  Problems
+ * that fit LDS run in one persistent workgroup; larger ones (N up to 38016)
+ * run over many workgroups, each solve replaying a captured hipGraph.  The
+ * terminate() drop-in also needs the one-workgroup solver, which limits it
+ * to 12N + 12M bytes <= 150 KiB. */
 typedef struct pqp_problem pqp_problem;
 int pqp_problem_create(const float *Qd, const float *Fd, const float *Md, const float *Qp, const float *Qp_inv,
                        const float *Fp, const float *Mp, const float *Gp, const float *Kp, int N, int M,

@@ -283,15 +283,24 @@ int problem_finish(pqp_problem& P, hipStream_t s) {
     PQP_TRY(P.state.alloc(sizeof(SolveState)));
     PQP_HIP(hipMemsetAsync(P.U.p, 0, sizeof(float) * M, s));
     if (!P.hst) PQP_HIP(hipHostMalloc((void**)&P.hst, sizeof(SolveState), hipHostMallocDefault));
-    if (!P.small) {
-        const int ldq = round4(N);
-        if (solve_single_lds_bytes(ldq, round4(M)) > kLdsBudget)
-            return set_error(PQP_ERR_ARG, "single-problem solve: N=%d, M=%d exceeds the LDS budget", N, M);
-        PQP_TRY(P.QdT.floats((size_t)N * ldq));
+    if (!P.small) {  // Theta for the large paths (computeTheta, PQP_CPU.c:503-519)
         PQP_TRY(P.theta.floats(N));
-        PQP_HIP(launch_pack_colmajor(1, P.Qd.f(), N, (long long)N * N, P.QdT.f(), ldq, (long long)N * ldq, s));
-        PQP_HIP(launch_theta(1, P.QdT.f(), ldq, (long long)N * ldq, N, P.theta.f(), N, s));
+        PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
     }
+    return PQP_OK;
+}
+
+// The one-workgroup solver's column-major copy of Qd, built on first use (the
+// multi-workgroup paths do not need it).
+int ensure_single(pqp_problem& P, hipStream_t s) {
+    if (P.QdT.p) return PQP_OK;
+    const int N = P.N, M = P.M, ldq = round4(N);
+    if (solve_single_lds_bytes(ldq, round4(M)) > kLdsBudget)
+        return set_error(PQP_ERR_ARG,
+                         "N=%d, M=%d exceeds the one-workgroup solver's LDS budget (terminate() drop-in / resumed "
+                         "solves); converge and fixed mode run over many workgroups", N, M);
+    PQP_TRY(P.QdT.floats((size_t)N * ldq));
+    PQP_HIP(launch_pack_colmajor(1, P.Qd.f(), N, (long long)N * N, P.QdT.f(), ldq, (long long)N * ldq, s));
     return PQP_OK;
 }
 
@@ -503,6 +512,7 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
     if (mode == kModeFixed && !P.small && !g_force_single && !resume) return problem_run_fixed_split(P, num_iter, out, s);
     if (mode == kModeConverge && !g_force_single && !resume && N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0))
         return problem_run_wide(P, max_updates, out, s);
+    if (!P.small) PQP_TRY(ensure_single(P, s));
     SolveState& st = *P.hst;
     st = SolveState{};
     st.h = 1;

@@ -144,3 +144,21 @@ def test_gauss_jordan_many_workgroups_vs_oracle(gpu_lib, orc, n, B):
     got = dR.cpu().numpy()
     for b in range(B):
         assert_bitwise(got[b], orc.gauss_jordan(A[b].reshape(-1), n), f"inverse {b}")
+
+
+def test_problem_beyond_one_workgroup_budget(gpu_lib, orc):
+    """n_dual = 9000 is past the one-workgroup solver's LDS budget: the problem
+    handle still solves it in converge mode (wide path) and fixed mode (relay
+    update), bit-identical to the oracle on the same dual data."""
+    N, M, cap = 9000, 4500, 2
+    pb = gpu_lib.ProblemBatch.synthetic(8, 0, 1, N, M)
+    P = pb.problem(0)
+    del pb
+    with gpu_lib.Problem(P) as prob:
+        r = prob.solve(max_updates=cap)
+        f = prob.solve(gpu_lib.MODE_FIXED, num_iter=3)
+    h, Y, U = orc.solve(P, max_updates=cap)
+    assert r["h"] == abs(h) == cap + 1
+    assert_bitwise(r["Y"], Y, "converge Y")
+    assert_bitwise(r["U"], U, "converge U")
+    assert_bitwise(f["Y"], orc.iterate(P["Qd"], P["Fd"], N, 2), "fixed-mode Y")
