@@ -236,8 +236,10 @@ struct pqp_problem {
     pqp::DevBuf QdT, theta;                          // large path only
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
     int split_lw = 0;                                // lanes per workgroup SP was built with
-    hipGraphExec_t graph = nullptr;                  // captured fixed-mode launch sequence
+    hipGraphExec_t graph = nullptr;                  // captured fixed-mode updates (the remainder)
     long long graph_updates = -1;
+    hipGraphExec_t chunk_graph = nullptr;            // captured fixed-mode chunk of kFixedChunk updates
+    bool chunk_ready = false;
     // converge mode over many workgroups (pqp_wide.hip), built on first use
     pqp::DevBuf QinvT, GpT, tM, tq, tu, gu, wflag, wcap;
     hipGraphExec_t wgraph = nullptr;                 // captured chunk of converge iterations
@@ -250,6 +252,7 @@ struct pqp_problem {
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     ~pqp_problem() {
         if (graph) (void)hipGraphExecDestroy(graph);
+        if (chunk_graph) (void)hipGraphExecDestroy(chunk_graph);
         if (wgraph) (void)hipGraphExecDestroy(wgraph);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
@@ -346,42 +349,63 @@ int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
     return PQP_OK;
 }
 
+// Capture `n` dependent updates P.Y -> P.Yb -> P.Y ... into *exec (plus a
+// copy back into P.Y when n is odd).
+static int capture_updates(pqp_problem& P, int lw, long long n, hipGraphExec_t* exec, hipStream_t s) {
+    const int N = P.N;
+    if (*exec) {
+        (void)hipGraphExecDestroy(*exec);
+        *exec = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    float* a = P.Y.f();
+    float* b = P.Yb.f();
+    hipError_t e = hipSuccess;
+    for (long long u = 0; u < n && e == hipSuccess; ++u) {
+        e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, a, b, s);
+        std::swap(a, b);
+    }
+    if (e == hipSuccess && a != P.Y.f()) e = hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s);
+    const hipError_t e2 = hipStreamEndCapture(s, &g);
+    if (e != hipSuccess || e2 != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        PQP_HIP(e != hipSuccess ? e : e2);
+    }
+    const hipError_t e3 = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    PQP_HIP(e3);
+    return PQP_OK;
+}
+
+// Fixed mode of a large problem: the relay update once per iteration, from
+// hipGraphs (per-update host launch overhead would otherwise exceed the
+// kernel itself): a chunk of kFixedChunk updates replayed as often as needed,
+// then a graph of the remainder.
+constexpr long long kFixedChunk = 256;  // even: a chunk starts and ends with the iterate in P.Y
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     const int lw = split_pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
-    // The whole launch sequence (fill, `updates` dependent updates, final copy)
-    // is captured once into a hipGraph and replayed: per-update host launch
-    // overhead would otherwise exceed the kernel itself.
-    if (!P.graph || P.graph_updates != updates || P.graph_variant != (g_split_u | (g_split_kind << 4) | (lw << 8))) {
-        if (P.graph) {
-            (void)hipGraphExecDestroy(P.graph);
-            P.graph = nullptr;
-        }
-        hipGraph_t g = nullptr;
-        PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        float* a = P.Y.f();
-        float* b = P.Yb.f();
-        hipError_t e = launch_fill(a, 1000.0f, N, s);  // initMat(Y, 1000) :710
-        for (long long u = 0; u < updates && e == hipSuccess; ++u) {
-            e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, a, b, s);
-            std::swap(a, b);
-        }
-        if (e == hipSuccess && a != P.Y.f())
-            e = hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s);
-        const hipError_t e2 = hipStreamEndCapture(s, &g);
-        if (e != hipSuccess || e2 != hipSuccess) {
-            if (g) (void)hipGraphDestroy(g);
-            PQP_HIP(e != hipSuccess ? e : e2);
-        }
-        const hipError_t e3 = hipGraphInstantiate(&P.graph, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        PQP_HIP(e3);
-        P.graph_updates = updates;
-        P.graph_variant = g_split_u | (g_split_kind << 4) | (lw << 8);
+    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8);
+    if (P.graph_variant != variant) {  // kernel selection changed: recapture both
+        P.graph_updates = -1;
+        P.chunk_ready = false;
+        P.graph_variant = variant;
     }
-    PQP_HIP(hipGraphLaunch(P.graph, s));
+    const long long full = updates / kFixedChunk, rem = updates % kFixedChunk;
+    if (full > 0 && !P.chunk_ready) {
+        PQP_TRY(capture_updates(P, lw, kFixedChunk, &P.chunk_graph, s));
+        P.chunk_ready = true;
+    }
+    if (rem > 0 && P.graph_updates != rem) {
+        PQP_TRY(capture_updates(P, lw, rem, &P.graph, s));
+        P.graph_updates = rem;
+    }
+    PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
+    for (long long c = 0; c < full; ++c) PQP_HIP(hipGraphLaunch(P.chunk_graph, s));
+    if (rem > 0) PQP_HIP(hipGraphLaunch(P.graph, s));
     PQP_HIP(hipStreamSynchronize(s));
     out.h = updates + 1;
     out.status = kStatusDone;

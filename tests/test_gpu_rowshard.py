@@ -199,3 +199,21 @@ def test_rowsharded_two_processes(gpu_lib, orc, tmp_path, world, N):
     want = orc.iterate(P["Qd"], P["Fd"], N, ups)
     for r in range(world):
         assert_bitwise(np.load(f"{out}.{r}.npy"), want, f"rank {r}")
+
+
+@pytest.mark.parametrize("num_iter", [2, 257, 300, 513])
+def test_fixed_mode_graph_chunks(gpu_lib, num_iter):
+    """Fixed mode of a large problem replays 256-update graph chunks plus a
+    remainder graph: every split of the update count gives the iterate of
+    the (oracle-pinned) batched kernel run for num_iter - 1 updates."""
+    N, M = 400, 200
+    pb = gpu_lib.ProblemBatch.synthetic(4, 2, 1, N, M)
+    P = pb.problem(0)
+    with gpu_lib.Problem(P) as prob:
+        r = prob.solve(gpu_lib.MODE_FIXED, num_iter=num_iter)
+        r2 = prob.solve(gpu_lib.MODE_FIXED, num_iter=num_iter)  # graphs replayed
+    b = gpu_lib.Batch(1, N).load(P["Qd"][None, :], P["Fd"][None, :])
+    want = b.iterate(num_iter - 1).result()[0]
+    assert r["h"] == num_iter
+    assert_bitwise(r["Y"], want, f"num_iter={num_iter}")
+    assert_bitwise(r2["Y"], want, f"num_iter={num_iter} (replay)")
