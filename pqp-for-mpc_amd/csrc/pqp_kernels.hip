@@ -163,8 +163,9 @@ template <int NT, int U = 8, bool NTL = false>
 __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ QdT, long long qstride, int ldq,
                                                       int N, const float* __restrict__ theta,
                                                       const float* __restrict__ Fd, int ldv,
-                                                      const float* __restrict__ Y0, float* __restrict__ Y,
-                                                      int updates) {
+                                                      const float* Y0, float* Y, int updates) {
+    // Y0 may alias Y (chained launches): each workgroup reads its problem's
+    // Y0 into LDS before the loop and writes Y only after it
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* ya = lds;
     float* yb = lds + ldq;
@@ -1734,8 +1735,28 @@ static void launch_iterate_t(int B, const float* QdT, long long qstride, int ldq
                            Fd, ldv, Y0, Y, updates);
 }
 
+static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qstride, int ldq, int N,
+                                          const float* theta, const float* Fd, int ldv, const float* Y0, float* Y,
+                                          int updates, hipStream_t s);
+
+// Long runs are split into launches of at most kIterPerLaunch updates (each
+// continuing from the previous one's Y), so no single launch runs unbounded.
+constexpr int kIterPerLaunch = 256;
 hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
                                 const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
+    int done = 0;
+    do {
+        const int c = (updates - done) < kIterPerLaunch ? (updates - done) : kIterPerLaunch;
+        const hipError_t e = launch_batch_iterate_one(B, QdT, qstride, ldq, N, theta, Fd, ldv, done ? Y : Y0, Y, c, s);
+        if (e != hipSuccess) return e;
+        done += c;
+    } while (done < updates);
+    return hipSuccess;
+}
+
+static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qstride, int ldq, int N,
+                                          const float* theta, const float* Fd, int ldv, const float* Y0, float* Y,
+                                          int updates, hipStream_t s) {
     // 0 (shipped): 16-deep unroll with non-temporal Qd loads -- 6.88 TB/s at
     // N=1024, B=4096 vs 7.02 TB/s for a bare read of the same pattern
     // (profiles/r01/ab_4096.txt).  Others kept for A/B.
