@@ -31,6 +31,9 @@ Extra keys:
                 rows and an RCCL all-gather assembles y (all ranks take part)
   gather_ms     RCCL gather of every rank's Y* to rank 0 (outside the timed
                 region)
+  iters_to_tol  converge mode on the problems the reference converges on (the
+                bundled example, testing/ test1 and test2): h and time per
+                solve, with the reference's own h (cpu_baseline) beside it
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -74,7 +77,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n: int, seconds: float, seed: int) -> dict:
+def cpu_baseline(n: int, seconds: float, seed: int, tol_cases: dict | None = None) -> dict:
     """Time the reference's updateY2 on one problem of the same workload."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
@@ -107,6 +110,13 @@ def cpu_baseline(n: int, seconds: float, seed: int) -> dict:
         tb = sorted(times)[len(times) // 2]
         bundled = {"converge_h": h, "converge_ms": tb * 1e3, "iter_per_s": h / tb,
                    "what": "PQP_CPU.c solveQuadraticDual on the bundled example (configs[0]), 1 thread"}
+        if tol_cases:  # iterations to tolerance of the reference on the converging problems
+            ref_tol = {}
+            for name, Pc in tol_cases.items():
+                tb = time.perf_counter()
+                h, _, _ = ref.solve(Pc)
+                ref_tol[name] = {"h": h, "ms": (time.perf_counter() - tb) * 1e3}
+            bundled["iters_to_tol"] = ref_tol
     else:
         per, _ = orc.time_updates(P["Qd"], P["Fd"], n, 3)
         ups = max(3, int(seconds / max(per / 3, 1e-6)))
@@ -204,6 +214,45 @@ def single_bench(pqp_amd, N: int = 1024, iters: int = 1000) -> dict:
     return {"n_dual": N, "iterations": iters, "ms_per_solve": dt * 1e3, "iter_per_s": (iters - 1) / dt,
             "alg_GBps_split_matrices": 8.0 * N * N * (iters - 1) / dt / 1e9,
             "note": "1 problem, fixed mode; per-iteration floor = one lane's N-long sequential sum"}
+
+
+def _testing_file(name: str, tmpdir: Path) -> Path:
+    """testing/sample test/<name>, committed under tests/golden/testing (the
+    two large ones gzip'd)."""
+    import gzip
+
+    plain = ROOT / "tests" / "golden" / "testing" / name
+    if plain.exists():
+        return plain
+    out = tmpdir / name
+    out.write_bytes(gzip.decompress((plain.parent / (name + ".gz")).read_bytes()))
+    return out
+
+
+TOL_CASES = ("bundled", "test1.txt", "test2.txt")
+
+
+def tol_problems(pqp_amd, tmpdir: Path) -> dict:
+    """The converging reference problems: the bundled example and the two
+    testing/ samples that converge (n_dual 1500 and 400)."""
+    P = {"bundled": pqp_amd.example_problem(ROOT / "tests" / "golden" / "example")}
+    for name in TOL_CASES[1:]:
+        P[name] = pqp_amd.testfile_problem(_testing_file(name, tmpdir))
+    return P
+
+
+def iters_to_tol_bench(pqp_amd, problems: dict) -> dict:
+    """Converge mode on the GPU: iterations to the reference's tolerance and
+    wall time per solve (problem resident, launch + readback)."""
+    out = {}
+    for name, P in problems.items():
+        with pqp_amd.Problem(P) as prob:
+            r = prob.solve(max_updates=200000)
+            t0 = time.perf_counter()
+            r = prob.solve(max_updates=200000)
+            dt = time.perf_counter() - t0
+        out[name] = {"n_dual": int(P["N"]), "h": r["h"], "converged": bool(r["converged"]), "ms": dt * 1e3}
+    return out
 
 
 def single_converge_bench(pqp_amd, N: int = 1024, updates: int = 200) -> dict:
@@ -382,8 +431,19 @@ def main():
         result["mpc_batch"] = mpc_batch_bench(pqp_amd)
         result["single_n1024"] = single_bench(pqp_amd)
         result["single_converge"] = single_converge_bench(pqp_amd)
+    tol_cases = None
+    if world == 1 and not args.no_bundled:
+        import tempfile
+
+        with tempfile.TemporaryDirectory() as td:
+            tol_cases = tol_problems(pqp_amd, Path(td))
+        result["iters_to_tol"] = iters_to_tol_bench(pqp_amd, tol_cases)
     if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed)
+        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed, tol_cases)
+        ref_tol = result["cpu_baseline"].get("bundled", {}).get("iters_to_tol")
+        if ref_tol and "iters_to_tol" in result:
+            result["iters_to_tol_identical_to_reference"] = all(
+                result["iters_to_tol"][k]["h"] == ref_tol[k]["h"] for k in ref_tol)
     print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
