@@ -243,10 +243,10 @@ struct pqp_problem {
     // converge mode over many workgroups (pqp_wide.hip), built on first use
     pqp::DevBuf QinvT, GpT, tM, tq, tu, gu, wflag, wcap;
     hipGraphExec_t wgraph = nullptr;                 // captured chunk of converge iterations
+    hipGraphExec_t wgraph_first = nullptr;           // the short first chunk
     hipStream_t side = nullptr;                      // capture-time fork for the speculative update
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     long long wgraph_key = -1;
-    long long hcap = 0;
     int graph_variant = -1;                          // g_split_u the graph was captured with
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
@@ -254,6 +254,7 @@ struct pqp_problem {
         if (graph) (void)hipGraphExecDestroy(graph);
         if (chunk_graph) (void)hipGraphExecDestroy(chunk_graph);
         if (wgraph) (void)hipGraphExecDestroy(wgraph);
+        if (wgraph_first) (void)hipGraphExecDestroy(wgraph_first);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (side) (void)hipStreamDestroy(side);
@@ -417,7 +418,8 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
 // one-workgroup decision, then the relay update.  A chunk of kWideChunk
 // iterations is captured into a hipGraph and replayed until the device-side
 // status leaves Continue; launches after that point return at once.
-constexpr int kWideChunk = 16;  // even: each replay starts and ends with the iterate in P.Y
+constexpr int kWideChunk = 16;      // even: each replay starts and ends with the iterate in P.Y
+constexpr int kWideFirstChunk = 2;  // the first replay of a solve
 int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
     const int N = P.N, M = P.M;
     const int lw = split_pick_lw(N);
@@ -485,34 +487,39 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
             if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join the update branch
             return launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, cur, nxt, s, &dst->status);
         };
-        hipGraph_t g = nullptr;
-        PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        hipError_t e = hipSuccess;
-        for (int it = 0; it < kWideChunk && e == hipSuccess; it += 2) {
-            e = iteration(P.Y.f(), P.Yb.f());
-            if (e == hipSuccess) e = iteration(P.Yb.f(), P.Y.f());
+        // two graphs: a short first chunk (problems that stop within a few
+        // iterations do not pay for a long chunk of no-op launches), then
+        // kWideChunk iterations per replay
+        auto capture = [&](int iters, hipGraphExec_t* exec) -> int {
+            hipGraph_t g = nullptr;
+            PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            hipError_t e = hipSuccess;
+            for (int it = 0; it < iters && e == hipSuccess; it += 2) {
+                e = iteration(P.Y.f(), P.Yb.f());
+                if (e == hipSuccess) e = iteration(P.Yb.f(), P.Y.f());
+            }
+            const hipError_t e2 = hipStreamEndCapture(s, &g);
+            if (e != hipSuccess || e2 != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                PQP_HIP(e != hipSuccess ? e : e2);
+            }
+            const hipError_t e3 = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            PQP_HIP(e3);
+            return PQP_OK;
+        };
+        if (P.wgraph_first) {
+            (void)hipGraphExecDestroy(P.wgraph_first);
+            P.wgraph_first = nullptr;
         }
-        const hipError_t e2 = hipStreamEndCapture(s, &g);
-        if (e != hipSuccess || e2 != hipSuccess) {
-            if (g) (void)hipGraphDestroy(g);
-            PQP_HIP(e != hipSuccess ? e : e2);
-        }
-        const hipError_t e3 = hipGraphInstantiate(&P.wgraph, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        PQP_HIP(e3);
+        PQP_TRY(capture(kWideFirstChunk, &P.wgraph_first));
+        PQP_TRY(capture(kWideChunk, &P.wgraph));
         P.wgraph_key = key;
     }
+    PQP_HIP(launch_wide_init(dst, flag, cap, max_updates, P.Y.f(), N, s));
     SolveState& st = *P.hst;
-    st = SolveState{};
-    st.h = 1;
-    PQP_HIP(hipMemcpyAsync(dst, &st, sizeof st, hipMemcpyHostToDevice, s));
-    const int one = 1;
-    PQP_HIP(hipMemcpyAsync(flag, &one, sizeof one, hipMemcpyHostToDevice, s));
-    P.hcap = max_updates;  // pinned host word (the copy is async)
-    PQP_HIP(hipMemcpyAsync(cap, &P.hcap, sizeof P.hcap, hipMemcpyHostToDevice, s));
-    PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
-    for (;;) {
-        PQP_HIP(hipGraphLaunch(P.wgraph, s));
+    for (int launch = 0;; ++launch) {
+        PQP_HIP(hipGraphLaunch(launch == 0 ? P.wgraph_first : P.wgraph, s));
         PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
         if (st.status != kStatusContinue) break;

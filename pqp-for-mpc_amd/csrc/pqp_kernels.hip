@@ -1031,15 +1031,29 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
                 for (int j = tid; j < N; j += NT) tq[j] = seq_dot(A.Qd + j, N, cur, N);
                 for (int j = tid; j < M; j += NT) tu[j] = seq_dot(A.Qp + j, M, Us, M);
                 __syncthreads();
+                // the dot products' terms formed in parallel into LDS (the
+                // row buffers in place; Fd.Y into nxt and Fp.U into tM, both
+                // free until the update), then summed in k order by one lane
+                // each -- one lane reading Fd from global memory term by term
+                // was the slowest part of an iteration
+                for (int j = tid; j < N; j += NT) {
+                    tq[j] = tq[j] * cur[j];
+                    nxt[j] = A.Fd[j] * cur[j];
+                }
+                for (int j = tid; j < M; j += NT) {
+                    tu[j] = tu[j] * Us[j];
+                    tM[j] = A.Fp[j] * Us[j];
+                }
+                __syncthreads();
                 const int jt = (NT >= 128) ? 64 : 1;  // second scalar chain on another wave
                 if (tid == 0 || tid == jt) {
                     const bool dual = (tid == 0);
-                    const float* row = dual ? tq : tu;
-                    const float* z = dual ? cur : Us;
-                    const float* F = dual ? A.Fd : A.Fp;
+                    const float* qv = dual ? tq : tu;
+                    const float* lv = dual ? nxt : tM;
                     const int n = dual ? N : M;
-                    const float quad = seq_dot(row, 1, z, n);
-                    const float lin = seq_dot(F, 1, z, n);
+                    float quad = 0.0f, lin = 0.0f;
+                    for (int k = 0; k < n; ++k) quad += qv[k];  // (Z'Q).Z :652-655
+                    for (int k = 0; k < n; ++k) lin += lv[k];   // F'Z :656-657
                     float J = 0.0f;
                     J = (float)((double)J + 0.5 * (double)quad);
                     J += lin;

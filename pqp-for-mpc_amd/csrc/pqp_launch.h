@@ -116,6 +116,8 @@ hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hi
 hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s);
 extern int g_wide_flags;  // tuning (pqp_tune_wide_flags)
 hipError_t launch_wide_decide(const WideArgs& a, hipStream_t s);
+hipError_t launch_wide_init(SolveState* st, int* flag, long long* cap, long long max_updates, float* Y, int N,
+                            hipStream_t s);
 // Gauss_Jordan of one n x n matrix, one launch per pivot (aug: 2n*n floats, perm: n ints)
 hipError_t launch_gauss_jordan_wide(const float* A, float* aug, int* perm, float* res, int n, hipStream_t s);
 constexpr int kGaussJordanWideMin = 64;  // n from which one matrix is inverted over many workgroups

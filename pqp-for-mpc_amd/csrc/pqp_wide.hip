@@ -47,40 +47,51 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ src
     }
 }
 
-// sum_k a[k] * b[k], k in order from +0.0f (one lane)
-__device__ inline float dot_seq(const float* __restrict__ a, const float* __restrict__ b, int n) {
-    float s = 0.0f;
-    for (int k = 0; k < n; ++k) s += a[k] * b[k];
-    return s;
-}
-
 // K4: the rest of terminate() (PQP_CPU.c:673-687) and the loop control.
-// (Folding this into K3's last workgroup to finish, behind an agent-scope
-// fence and a counter, measured 1-5 us slower per iteration than a launch.)
-__global__ void __launch_bounds__(128) k_wide_decide(WideArgs a) {
+// The four dot products of computeCost (:648-666) -- (Y'Qd).Y, Fd.Y,
+// (U'Qp).U, Fp.U -- are sums in k order on one lane each (waves 0-3); their
+// products are formed by all 256 threads into LDS a chunk at a time, so the
+// summing lanes read LDS instead of waiting on one global load per term
+// (one lane walking Fd from global memory took ~200 us at n_dual = 1500).
+// Folding this launch into the last workgroup of K3 behind an agent-scope
+// fence and a counter measured 1-5 us slower per iteration.
+constexpr int kDecideChunk = 1024;
+__global__ void __launch_bounds__(256) k_wide_decide(WideArgs a) {
     SolveState* st = a.st;
     if (st->status != kStatusContinue) return;
-    __shared__ float sJ[2];
-    const int tid = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) float prod[4][kDecideChunk];
+    __shared__ float sJ[4];
+    const int tid = threadIdx.x, wave = tid >> 6;
     const int feasible = *a.flag;  // checkFeas :677
     int stop = 0;
     if (feasible) {
-        if (tid == 0 || tid == 64) {  // computeCost :648-666, dual on wave 0, primal on wave 1
-            const bool dual = (tid == 0);
-            const float* row = dual ? a.tq : a.tu;
-            const float* z = dual ? a.Y : a.U;
-            const float* F = dual ? a.Fd : a.Fp;
-            const int n = dual ? a.N : a.M;
-            const float quad = dot_seq(row, z, n);
-            const float lin = dot_seq(F, z, n);
-            float J = 0.0f;
-            J = (float)((double)J + 0.5 * (double)quad);
-            J += lin;
-            J += (dual ? a.Md[0] : a.Mp[0]) / 2;
-            sJ[dual ? 1 : 0] = J;
+        // wave w sums dot w: 0 quad_dual, 1 lin_dual, 2 quad_primal, 3 lin_primal
+        const float* rowv[4] = {a.tq, a.Fd, a.tu, a.Fp};
+        const float* zv[4] = {a.Y, a.Y, a.U, a.U};
+        const int nv[4] = {a.N, a.N, a.M, a.M};
+        float acc = 0.0f;
+        const int nmax = a.N > a.M ? a.N : a.M;
+        for (int c0 = 0; c0 < nmax; c0 += kDecideChunk) {
+            for (int e = tid; e < 4 * kDecideChunk; e += 256) {
+                const int d = e / kDecideChunk, k = c0 + e % kDecideChunk;
+                prod[d][e % kDecideChunk] = (k < nv[d]) ? rowv[d][k] * zv[d][k] : 0.0f;
+            }
+            __syncthreads();
+            if ((tid & 63) == 0) {
+                const int n = (nv[wave] - c0) < kDecideChunk ? (nv[wave] - c0) : kDecideChunk;
+                for (int k = 0; k < n; ++k) acc += prod[wave][k];  // :652-657, k in order
+            }
+            __syncthreads();
         }
+        if ((tid & 63) == 0) sJ[wave] = acc;
         __syncthreads();
-        const float Jp = sJ[0], Jd = sJ[1];
+        float Jd = 0.0f, Jp = 0.0f;
+        Jd = (float)((double)Jd + 0.5 * (double)sJ[0]);
+        Jd += sJ[1];
+        Jd += a.Md[0] / 2;
+        Jp = (float)((double)Jp + 0.5 * (double)sJ[2]);
+        Jp += sJ[3];
+        Jp += a.Mp[0] / 2;
         stop = 1;  // the three gap tests :681-685
         if (Jp > -Jd) stop = 0;
         if ((double)(Jp + Jd) > kTol) stop = 0;
@@ -241,7 +252,29 @@ __global__ void __launch_bounds__(256) k_gj_finish(const float* __restrict__ aug
     for (int c = threadIdx.x; c < n; c += 256) res[(size_t)r * n + c] = aug[(size_t)r * w + n + c] / d;
 }
 
+// start of a converge-mode solve: SolveState (h = 1, Continue), the
+// feasibility flag, the update cap, and Y = 1000 (initMat, PQP_CPU.c:710)
+__global__ void k_wide_init(SolveState* st, int* flag, long long* cap, long long max_updates, float* Y, int N) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        SolveState z{};
+        z.h = 1;
+        z.status = kStatusContinue;
+        *st = z;
+        *flag = 1;
+        *cap = max_updates;
+    }
+    for (int i = t; i < N; i += gridDim.x * blockDim.x) Y[i] = 1000.0f;
+}
+
 }  // namespace
+
+hipError_t launch_wide_init(SolveState* st, int* flag, long long* cap, long long max_updates, float* Y, int N,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_wide_init, dim3(cdivw(N, 256) < 64 ? cdivw(N, 256) : 64), dim3(256), 0, s, st, flag, cap,
+                       max_updates, Y, N);
+    return hipGetLastError();
+}
 
 hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {
     if (rows <= 0 || cols <= 0) return hipSuccess;
@@ -278,7 +311,7 @@ hipError_t launch_gauss_jordan_wide(const float* A, float* aug, int* perm, float
 }
 
 hipError_t launch_wide_decide(const WideArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_wide_decide, dim3(1), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(k_wide_decide, dim3(1), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
