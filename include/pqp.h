@@ -262,14 +262,6 @@ int pqp_rowblock_create(const float *d_Qd_rows, int ld, const float *d_Fd, int N
 int pqp_rowblock_update(pqp_rowblock *b, const float *d_Y, float *d_Y_rows, void *stream);
 int pqp_rowblock_destroy(pqp_rowblock *b);
 
-/* The relay kernels hand running sums between waves through LDS with a
- * bounded wait, so a broken hand-off cannot hang the GPU.  This waits for the
- * device and returns PQP_ERR_HIP if any hand-off since the previous check hit
- * its bound (never expected; the results of that launch are invalid).  The
- * synchronous solves check this themselves; pqp_rowblock_update callers call
- * it after their run. */
-int pqp_check_relays(void);
-
 /* Rows [row0, row0+rows) of synthetic problem `inst` of `seed` (the
  * generator of pqp_batch_generate), row-major with leading dimension ld >= N
  * (columns N..ld-1 zeroed), so that a rank can build its row block without

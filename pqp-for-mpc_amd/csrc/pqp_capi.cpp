@@ -350,48 +350,6 @@ int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
     return PQP_OK;
 }
 
-// A relay hand-off that hit its spin bound produced wrong sums: report it
-// instead of returning them.  enqueue_relay_check() copies the device
-// counters into pinned host words on the solve's stream (before its final
-// synchronization); check_relay_timeouts() compares them after it.  The
-// counters only ever grow.
-struct RelayCounters {
-    unsigned* host = nullptr;  // [0] relay, [1] gemv (pinned)
-    const unsigned* dev[2] = {nullptr, nullptr};
-    unsigned seen = 0;
-};
-RelayCounters& relay_counters() {  // per device (the counters live in each device's code object)
-    static RelayCounters cs[64];
-    static std::mutex mu;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    RelayCounters& c = cs[(dev >= 0 && dev < 64) ? dev : 0];
-    std::lock_guard<std::mutex> lk(mu);
-    if (!c.host) {
-        if (hipHostMalloc((void**)&c.host, 2 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess) c.host = nullptr;
-        else c.host[0] = c.host[1] = 0;
-        c.dev[0] = relay_timeouts_addr();
-        c.dev[1] = gemv_timeouts_addr();
-    }
-    return c;
-}
-int enqueue_relay_check(hipStream_t s) {
-    RelayCounters& c = relay_counters();
-    for (int i = 0; i < 2; ++i)
-        if (c.host && c.dev[i]) PQP_HIP(hipMemcpyAsync(c.host + i, c.dev[i], sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    return PQP_OK;
-}
-int check_relay_timeouts() {  // after the stream of enqueue_relay_check() has synchronized
-    RelayCounters& c = relay_counters();
-    if (!c.host) return PQP_OK;
-    const unsigned now = c.host[0] + c.host[1];
-    if (now != c.seen) {
-        c.seen = now;
-        return set_error(PQP_ERR_HIP, "a relay kernel hand-off timed out (%u so far); results are invalid", now);
-    }
-    return PQP_OK;
-}
-
 // Capture `n` dependent updates P.Y -> P.Yb -> P.Y ... into *exec (plus a
 // copy back into P.Y when n is odd).
 static int capture_updates(pqp_problem& P, int lw, long long n, hipGraphExec_t* exec, hipStream_t s) {
@@ -449,9 +407,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
     for (long long c = 0; c < full; ++c) PQP_HIP(hipGraphLaunch(P.chunk_graph, s));
     if (rem > 0) PQP_HIP(hipGraphLaunch(P.graph, s));
-    PQP_TRY(enqueue_relay_check(s));
     PQP_HIP(hipStreamSynchronize(s));
-    PQP_TRY(check_relay_timeouts());
     out.h = updates + 1;
     out.status = kStatusDone;
     return PQP_OK;
@@ -565,11 +521,9 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     for (int launch = 0;; ++launch) {
         PQP_HIP(hipGraphLaunch(launch == 0 ? P.wgraph_first : P.wgraph, s));
         PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
-        PQP_TRY(enqueue_relay_check(s));
         PQP_HIP(hipStreamSynchronize(s));
         if (st.status != kStatusContinue) break;
     }
-    PQP_TRY(check_relay_timeouts());
     if ((st.h - 1) & 1)  // odd number of updates: the iterate is in Yb
         PQP_HIP(hipMemcpyAsync(P.Y.p, P.Yb.p, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
     out.h = st.h;
@@ -977,15 +931,6 @@ int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void
 int pqp_rowblock_destroy(pqp_rowblock* b) {
     delete b;
     return PQP_OK;
-}
-
-int pqp_check_relays(void) {
-    PQP_TRY(ensure_device());
-    PQP_HIP(hipDeviceSynchronize());
-    hipStream_t s = lib_stream();
-    PQP_TRY(enqueue_relay_check(s));
-    PQP_HIP(hipStreamSynchronize(s));
-    return check_relay_timeouts();
 }
 
 int pqp_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float* d_Qd_rows, int ld,

@@ -450,10 +450,6 @@ __global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict_
 // k_split_update, while a workgroup keeps W*S KiB of packets in flight
 // instead of one wave's pipeline, and the chain issues 4 cycles per k
 // (an add) instead of 8 (a multiply and an add).
-// relay hand-offs that hit their spin bound (a broken hand-off would
-// otherwise hang the GPU); read by relay_timeouts() after a solve
-__device__ unsigned g_relay_timeouts = 0;
-
 template <int W, int S>
 __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                         int N, int rows, int row0, int lw,
@@ -542,11 +538,7 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
         unsigned long long h;
         for (int spin = 0;; ++spin) {
             h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__all((int)(h >> 32) == g)) break;
-            if (spin > (1 << 20)) {  // never expected: count it, the host turns it into an error
-                if (lane == 0) atomicAdd(&g_relay_timeouts, 1u);
-                break;
-            }
+            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
         }
         __builtin_amdgcn_s_setprio(3);
         acc = __uint_as_float((unsigned)h);
@@ -599,11 +591,6 @@ hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* th
     if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_theta_rows, dim3(cdiv(rows, 256)), dim3(256), 0, s, Qd, ld, N, rows, theta);
     return hipGetLastError();
-}
-
-const unsigned* relay_timeouts_addr() {
-    void* p = nullptr;
-    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_relay_timeouts)) == hipSuccess ? static_cast<unsigned*>(p) : nullptr;
 }
 
 int g_split_kind = 0;  // tuning: 0 auto (relay W8 S16), 1 k_split_update, 2 relay W4 S64, 3 W8 S32, 4 W16 S16, 5 W8 S16

@@ -77,10 +77,6 @@ hipError_t launch_synth_rows(uint32_t seed, long long inst, int N, int M, int ro
                              float* Fd, float* Md, hipStream_t s);
 extern int g_split_u;        // tuning: k_split_update stage depth selector
 extern int g_split_kind;     // tuning: relay / stream kernel selector
-// device addresses of the counters of relay hand-offs that hit their spin
-// bound since the process started (nonzero only if something is broken)
-const unsigned* relay_timeouts_addr();
-const unsigned* gemv_timeouts_addr();
 extern int g_split_lw;       // tuning: lanes per workgroup override (0 = auto)
 extern int g_fixed_tiny_old; // tuning: fixed mode of tiny problems on k_solve_tiny
 // batched forms: grid = B problems (states st[0..B-1])

@@ -113,8 +113,6 @@ __global__ void __launch_bounds__(256) k_wide_decide(WideArgs a) {
     }
 }
 
-__device__ unsigned g_gemv_timeouts = 0;  // see g_relay_timeouts (pqp_kernels.hip)
-
 template <int W, int S>
 __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
     if (J.gate && *J.gate != kStatusContinue) return;  // the solve has finished
@@ -185,11 +183,7 @@ __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
         unsigned long long h;
         for (int spin = 0;; ++spin) {
             h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__all((int)(h >> 32) == g)) break;
-            if (spin > (1 << 20)) {  // never expected: count it, the host turns it into an error
-                if (lane == 0) atomicAdd(&g_gemv_timeouts, 1u);
-                break;
-            }
+            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
         }
         __builtin_amdgcn_s_setprio(3);
         acc = __uint_as_float((unsigned)h);
@@ -280,11 +274,6 @@ hipError_t launch_wide_init(SolveState* st, int* flag, long long* cap, long long
     hipLaunchKernelGGL(k_wide_init, dim3(cdivw(N, 256) < 64 ? cdivw(N, 256) : 64), dim3(256), 0, s, st, flag, cap,
                        max_updates, Y, N);
     return hipGetLastError();
-}
-
-const unsigned* gemv_timeouts_addr() {
-    void* p = nullptr;
-    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_gemv_timeouts)) == hipSuccess ? static_cast<unsigned*>(p) : nullptr;
 }
 
 hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {

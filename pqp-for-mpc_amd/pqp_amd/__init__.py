@@ -83,7 +83,6 @@ SIGNATURES = {
     "pqp_rowblock_create": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(C.c_void_p)]),
     "pqp_rowblock_update": (C.c_int, [_vp, _vp, _vp, _vp]),
     "pqp_rowblock_destroy": (C.c_int, [_vp]),
-    "pqp_check_relays": (C.c_int, []),
     "pqp_synth_rows": (C.c_int, [C.c_uint32, C.c_longlong] + [C.c_int] * 4 + [_vp, C.c_int, _vp, _vp, _vp]),
     # include/pqp_tuning.h
     "pqp_tune_set_variant": (C.c_int, [C.c_int]),
@@ -619,11 +618,6 @@ class RowBlock:
         """Y_rows[:rows] = updateY2(Y)[row0:row0+rows] (async)."""
         _check(lib().pqp_rowblock_update(self._h, C.c_void_p(Y.data_ptr()),
                                          C.c_void_p(Y_rows.data_ptr()) if self.rows > 0 else None, self._s()))
-
-    def check(self):
-        """Raise if a relay hand-off timed out since the last check
-        (pqp_check_relays; waits for the device)."""
-        _check(lib().pqp_check_relays())
 
     def close(self):
         if getattr(self, "_h", None) and _LIB is not None:

@@ -68,7 +68,4 @@ class RowShardedSolver:
         self.Y.fill_(y0)
         for _ in range(max(0, int(num_iter) - 1)):
             self.step()
-        check = getattr(self.block, "check", None)
-        if check is not None:
-            check()
         return self.Y[: self.N]
