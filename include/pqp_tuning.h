@@ -27,6 +27,11 @@ extern "C" {
  * 4: 64).  Returns the previous value. */
 int pqp_tune_set_variant(int variant);
 
+/* Fixed mode of one problem with n_dual <= 1024 runs as ONE persistent launch
+ * (pqp_persist.hip) unless off = 1, which sends it through the hipGraph-replayed
+ * relay update (one launch per update).  Returns the previous setting. */
+int pqp_tune_persist(int off);
+
 /* Converge-mode solves of problems with n_dual >= n run over many workgroups
  * (terminate() as multi-workgroup mat-vecs + the relay update, replayed from a
  * hipGraph) instead of one persistent workgroup; n <= 0 sends every size

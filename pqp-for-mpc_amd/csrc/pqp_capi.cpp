@@ -235,6 +235,7 @@ struct pqp_problem {
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
+    pqp::DevBuf SPp, fdpnp, gran, perr;              // persistent fixed mode: split matrices (lw = 32), y granules, error word
     int split_lw = 0;                                // lanes per workgroup SP was built with
     hipGraphExec_t graph = nullptr;                  // captured fixed-mode updates (the remainder)
     long long graph_updates = -1;
@@ -384,11 +385,53 @@ static int capture_updates(pqp_problem& P, int lw, long long n, hipGraphExec_t* 
 // kernel itself): a chunk of kFixedChunk updates replayed as often as needed,
 // then a graph of the remainder.
 constexpr long long kFixedChunk = 256;  // even: a chunk starts and ends with the iterate in P.Y
+// Fixed mode of a problem with N <= persist_max_n(): every update in ONE
+// persistent launch (pqp_persist.hip), launches of at most kPersistChunk
+// updates chained through P.Y.
+constexpr long long kPersistChunk = 1 << 16;
+int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, hipStream_t s) {
+    const int N = P.N;
+    if (!P.SPp.p) {  // the stored split matrices in the 32-lane layout, built once per problem
+        if (!P.theta.p) {
+            PQP_TRY(P.theta.floats(N));
+            PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
+        }
+        if (!P.Yb.p) PQP_TRY(P.Yb.floats(N));
+        PQP_TRY(P.SPp.floats(split_floats(N, N, 32)));
+        PQP_TRY(P.fdpnp.floats((size_t)2 * N));
+        PQP_HIP(hipMemsetAsync(P.SPp.p, 0, sizeof(float) * split_floats(N, N, 32), s));
+        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, 32, P.SPp.f(), P.fdpnp.f(), s));
+        PQP_TRY(P.gran.alloc(sizeof(unsigned long long) * 2 * N));
+        PQP_TRY(P.perr.alloc(sizeof(int)));
+    }
+    auto* gran = static_cast<unsigned long long*>(P.gran.p);
+    int* err = static_cast<int*>(P.perr.p);
+    PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
+    for (long long done = 0; done < updates;) {
+        const long long n = std::min(kPersistChunk, updates - done);
+        // the launch reads its initial iterate from Yb while it writes P.Y
+        PQP_HIP(hipMemcpyAsync(P.Yb.p, P.Y.p, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+        PQP_HIP(launch_split_persist(P.SPp.f(), P.fdpnp.f(), N, (int)n, P.Yb.f(), P.Y.f(), gran, err, s));
+        int herr = 0;
+        PQP_HIP(hipMemcpyAsync(&herr, err, sizeof herr, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (herr)
+            return set_error(PQP_ERR_HIP, "persistent fixed-mode update: workgroup hand-off timed out (code %d); "
+                             "its %d workgroups must be resident at once", herr, (2 * N + 31) / 32);
+        done += n;
+    }
+    PQP_HIP(hipStreamSynchronize(s));
+    out.h = updates + 1;
+    out.status = kStatusDone;
+    return PQP_OK;
+}
+
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
+    const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
+    if (!g_persist_off && N <= persist_max_n()) return problem_run_fixed_persist(P, updates, out, s);
     const int lw = split_pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
-    const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
     const int variant = g_split_u | (g_split_kind << 4) | (lw << 8);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
@@ -1380,6 +1423,12 @@ extern "C" int pqp_tune_set_variant(int variant) {
     pqp::g_force_small = (variant & 0x100) != 0;
     pqp::g_fixed_tiny_old = (variant & 0x400) != 0;
     pqp::g_force_single = (variant & 0x200) != 0;
+    return old;
+}
+
+extern "C" int pqp_tune_persist(int off) {
+    const int old = pqp::g_persist_off;
+    pqp::g_persist_off = off ? 1 : 0;
     return old;
 }
 

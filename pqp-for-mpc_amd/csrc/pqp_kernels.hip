@@ -286,7 +286,6 @@ __global__ void __launch_bounds__(256) k_update_split(const float* __restrict__ 
 // padding lanes of the last workgroup hold zeros.  The per-update floor is
 // one lane's N-long mul/add chain plus the bytes one CU can pull.
 // ---------------------------------------------------------------------------
-__host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
 // lw = lanes (row sides) per workgroup: 64, 32, 16 or 8.  Fewer rows per
 // workgroup spread a block over more CUs (each CU then pulls fewer bytes per
 // update; the per-CU fetch rate, not HBM, bounds a single small problem).

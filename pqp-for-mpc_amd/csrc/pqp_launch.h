@@ -68,6 +68,15 @@ hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* th
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
                                const float* Yin, float* Yout, hipStream_t s, const int* gate = nullptr);
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
+// packets of 4 k per row side in the split layout (k padded to a multiple of 4)
+__host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
+// fixed mode of one problem with N <= persist_max_n() as ONE persistent launch
+// (pqp_persist.hip): SP built with lw = 32; gran = 2N granules, err = 1 int
+int persist_max_n();
+size_t persist_lds_bytes(int N);
+hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,
+                                unsigned long long* gran, int* err, hipStream_t s);
+extern int g_persist_off;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
 int split_pick_lw(int rows);                   // lanes per workgroup for a block of `rows`
 size_t split_lds_bytes(int N);         // k_split_update's LDS (the full y)

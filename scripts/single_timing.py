@@ -35,8 +35,10 @@ def main(N: int = 1024, iters: int = 1000, reps: int = 5):
             for lwsel, lw in ((1, 8), (2, 16), (4, 64)):
                 variants.append((f"relay_{kn}_lw{lw}", (kind << 14) | (lwsel << 17)))
         variants.append(("single_wg", 0x200))
+        variants.insert(0, ("persistent", 0))
         for name, var in variants:
             L.pqp_tune_set_variant(var)
+            L.pqp_tune_persist(0 if name == "persistent" else 1)
             prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
             t0 = time.perf_counter()
             for _ in range(reps):
@@ -46,9 +48,11 @@ def main(N: int = 1024, iters: int = 1000, reps: int = 5):
             out[name] = {"ms_per_solve": dt * 1e3, "us_per_iter": dt / (iters - 1) * 1e6,
                          "iter_per_s": (iters - 1) / dt}
         L.pqp_tune_set_variant(0)
+        L.pqp_tune_persist(0)
     out["bit_identical"] = all(bool(np.array_equal(y.view(np.uint32), ys["single_wg"].view(np.uint32)))
                                for y in ys.values())
     out["split_alg_GBps"] = 8 * N * N / (out["split_multi_wg"]["us_per_iter"] * 1e-6) / 1e9
+    out["persistent_alg_GBps"] = 8 * N * N / (out["persistent"]["us_per_iter"] * 1e-6) / 1e9
     bb = pqp_amd.Batch(1, N).generate(seed=1, inst0=0, M=M)
     bb.iterate(3)
     import torch

@@ -1,0 +1,95 @@
+"""GPU parity of the persistent fixed-mode launch (pqp_persist.hip): one
+problem of n_dual <= 1024, every update inside ONE kernel, the iterate handed
+between workgroups as tagged granules.  Bar: bit-exact with the oracle
+(PQP_CPU.c's updateY2 restated) and with the graph-replayed relay update
+(pqp_tune_persist(1)), for ragged sizes around the wave-slice (192 k) and
+workgroup (16 rows) boundaries, update counts of both parities, repeated
+solves, special values, and the size limit (N = 1025 falls back)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def _dual(orc, N, seed=8, inst=1):
+    M = max(1, N // 2)
+    P = orc.synth_problem(seed, inst, N, M, with_qp=False)
+    P.update(Qp=np.zeros(M * M, np.float32))
+    return P
+
+
+def _solve(gpu_lib, P, num_iter, persist=True, reps=1):
+    L = gpu_lib.lib()
+    old = L.pqp_tune_persist(0 if persist else 1)
+    try:
+        with gpu_lib.Problem(P) as prob:
+            rs = [prob.solve(gpu_lib.MODE_FIXED, num_iter=num_iter) for _ in range(reps)]
+    finally:
+        L.pqp_tune_persist(old)
+    return rs
+
+
+@pytest.mark.parametrize("N", [99, 100, 191, 192, 193, 257, 384, 575, 576, 577, 1000, 1023, 1024])
+def test_persistent_fixed_mode_vs_oracle(gpu_lib, orc, N):
+    P = _dual(orc, N)
+    ups = 11
+    want = orc.iterate(P["Qd"], P["Fd"], N, ups)
+    (r,) = _solve(gpu_lib, P, ups + 1)
+    assert r["h"] == ups + 1
+    assert_bitwise(r["Y"], want, f"persistent N={N}")
+
+
+@pytest.mark.parametrize("num_iter", [1, 2, 3, 4, 257, 1000])
+def test_persistent_update_counts_and_replays(gpu_lib, orc, num_iter):
+    """Both parities of the update count, a single update, no update at all
+    (num_iter = 1: Y stays 1000), three solves on one handle (the granules'
+    tags are reset before every launch); equal to the relay path."""
+    N = 1024
+    P = _dual(orc, N, seed=3, inst=5)
+    rs = _solve(gpu_lib, P, num_iter, persist=True, reps=3)
+    (rr,) = _solve(gpu_lib, P, num_iter, persist=False)
+    if num_iter <= 12:
+        want = orc.iterate(P["Qd"], P["Fd"], N, num_iter - 1) if num_iter > 1 else np.full(N, 1000, np.float32)
+        assert_bitwise(rr["Y"], want, "relay vs oracle")
+    for i, r in enumerate(rs):
+        assert r["h"] == num_iter
+        assert_bitwise(r["Y"], rr["Y"], f"persistent solve {i} vs relay, num_iter={num_iter}")
+
+
+def test_persistent_special_values(gpu_lib, orc):
+    """inf/NaN/-0 entries of Qd and Fd propagate exactly as in the literal
+    reference formula through many updates."""
+    N = 300
+    rng = np.random.default_rng(17)
+    Qd = rng.standard_normal((N, N)).astype(np.float32)
+    Qd[rng.random((N, N)) < 0.1] = 0.0
+    Qd[rng.random((N, N)) < 0.05] = -0.0
+    Qd[rng.random((N, N)) < 0.0005] = np.inf
+    Qd[rng.random((N, N)) < 0.0005] = np.nan
+    Qd = Qd.reshape(-1)
+    Fd = rng.standard_normal(N).astype(np.float32)
+    Fd[::7] = -0.0
+    M = 4
+    P = dict(Qd=Qd, Fd=Fd, Md=np.zeros(1, np.float32), Qp=np.zeros(M * M, np.float32),
+             Qp_inv=np.zeros(M * M, np.float32), Fp=np.zeros(M, np.float32), Mp=np.zeros(1, np.float32),
+             Gp=np.zeros(N * M, np.float32), Kp=np.zeros(N, np.float32), N=N, M=M)
+    ups = 6
+    want = orc.iterate(Qd, Fd, N, ups)
+    (r,) = _solve(gpu_lib, P, ups + 1)
+    (rr,) = _solve(gpu_lib, P, ups + 1, persist=False)
+    a, b, c = (np.asarray(x, np.float32) for x in (r["Y"], want, rr["Y"]))
+    nan = np.isnan(a) & np.isnan(b)
+    assert np.all(nan | (a.view(np.uint32) == b.view(np.uint32))), "persistent vs oracle"
+    assert np.array_equal(np.isnan(a), np.isnan(c)) and np.all(np.isnan(a) | (a.view(np.uint32) == c.view(np.uint32)))
+
+
+def test_beyond_persistent_limit_falls_back(gpu_lib, orc):
+    N = 1025
+    P = _dual(orc, N, seed=2, inst=2)
+    want = orc.iterate(P["Qd"], P["Fd"], N, 5)
+    (r,) = _solve(gpu_lib, P, 6)
+    assert_bitwise(r["Y"], want, "N=1025 (relay)")
