@@ -32,6 +32,12 @@ int pqp_tune_set_variant(int variant);
  * relay update (one launch per update).  Returns the previous setting. */
 int pqp_tune_persist(int off);
 
+/* Timeline of the persistent launch's workgroup 0 (s_memtime shader clocks):
+ * for the first `updates` updates, per update u and wave w, the four words
+ * d_trace[(u * waves + w) * 4 + e] = {sweep start, y staged, running sums
+ * received, chain done}.  updates = 0 turns the trace off. */
+int pqp_tune_persist_trace(void *d_trace, int updates);
+
 /* Converge-mode solves of problems with n_dual >= n run over many workgroups
  * (terminate() as multi-workgroup mat-vecs + the relay update, replayed from a
  * hipGraph) instead of one persistent workgroup; n <= 0 sends every size

@@ -1432,6 +1432,13 @@ extern "C" int pqp_tune_persist(int off) {
     return old;
 }
 
+extern "C" int pqp_tune_persist_trace(void* d_trace, int updates) {
+    if (updates < 0 || (updates > 0 && !d_trace)) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_persist_trace: bad arguments");
+    pqp::g_persist_trace = updates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
+    pqp::g_persist_trace_n = updates;
+    return PQP_OK;
+}
+
 extern "C" int pqp_tune_wide_flags(int flags) {
     const int old = pqp::g_wide_flags;
     pqp::g_wide_flags = flags;

@@ -76,7 +76,9 @@ int persist_max_n();
 size_t persist_lds_bytes(int N);
 hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,
                                 unsigned long long* gran, int* err, hipStream_t s);
-extern int g_persist_off;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
+extern int g_persist_off;
+extern unsigned long long* g_persist_trace;  // tuning: device buffer of 4 * waves * g_persist_trace_n words
+extern int g_persist_trace_n;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
 int split_pick_lw(int rows);                   // lanes per workgroup for a block of `rows`
 size_t split_lds_bytes(int N);         // k_split_update's LDS (the full y)

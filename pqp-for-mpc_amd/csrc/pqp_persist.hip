@@ -22,7 +22,9 @@
 //      repeated until every tag matches -- the data is its own flag);
 //   2. forms its slice's products q * y in registers (q from LDS);
 //   3. waits for wave w-1's running sums (one 64-bit LDS word per lane:
-//      tag and sum), adds its products in k order, hands the sums on;
+//      tag and sum), adds its products in k order, hands the sums on (wave 0
+//      starts the chain as soon as its slice is staged and forms its products
+//      inside it);
 //   4. the last wave adds Fdn/Fdp, divides, multiplies by y_i and publishes
 //      y_next[i] as a granule (`global_store_dwordx2 sc1`); the last update
 //      also writes Yout.
@@ -46,7 +48,8 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int kPLanes = 32;  // row sides per workgroup
-constexpr int kPW = 48;      // packets (4 values of k) per wave: the products live in 4 * kPW VGPRs
+constexpr int kPW0 = 24;     // packets (4 values of k) of wave 0's slice: multiplied inside its add chain
+constexpr int kPW = 48;      // packets per later slice: their products are formed ahead, in 4 * kPW VGPRs
 constexpr int kPMaxWaves = 6;
 constexpr long long kPTimeoutTicks = 200000000LL;  // s_memrealtime runs at 100 MHz: 2 s
 
@@ -59,31 +62,40 @@ __device__ __forceinline__ void fail(int* err, int code) {
 }  // namespace
 
 int g_persist_off = 0;
+unsigned long long* g_persist_trace = nullptr;  // tuning: timeline of workgroup 0 (pqp_tune_persist_trace)
+int g_persist_trace_n = 0;
 
-int persist_waves(int N) { return (split_kblocks(N) + kPW - 1) / kPW; }
-int persist_max_n() { return 4 * kPW * kPMaxWaves > 1024 ? 1024 : 4 * kPW * kPMaxWaves; }
-// LDS: the workgroup's packets zero-padded to W * kPW (so every wave runs the
-// same unguarded loops: a +0 packet times y = +0 adds exactly nothing to a sum
-// that is never -0), two y slices per wave, two hand-off words per lane and wave
+// waves: one slice of kPW0 packets, then slices of kPW
+__host__ __device__ inline int persist_waves_of(int KB) { return KB <= kPW0 ? 1 : 1 + (KB - kPW0 + kPW - 1) / kPW; }
+__host__ __device__ inline int persist_packets(int W) { return kPW0 + (W - 1) * kPW; }
+int persist_waves(int N) { return persist_waves_of(split_kblocks(N)); }
+int persist_max_n() {
+    const int n = 4 * persist_packets(kPMaxWaves);
+    return n > 1024 ? 1024 : n;
+}
+// LDS: the workgroup's packets zero-padded to whole slices (so every wave runs
+// the same unguarded loops: a +0 packet times y = +0 adds exactly nothing to a
+// sum that is never -0), y by update parity, two hand-off words per lane and wave
 size_t persist_lds_bytes(int N) {
-    const int W = persist_waves(N);
-    return sizeof(float) * ((size_t)W * kPW * kPLanes * 4 + (size_t)2 * W * kPW * 4) + sizeof(u64) * 2 * W * 64;
+    const int W = persist_waves(N), KP = persist_packets(W);
+    return sizeof(float) * ((size_t)KP * kPLanes * 4 + (size_t)2 * KP * 4) + sizeof(u64) * 2 * W * 64;
 }
 
 // SP: the k_build_split layout with lw = 32 (workgroup-major packets).
 // gran: 2 * N granules, zeroed before the launch.  err: zeroed before the launch.
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     k_split_persist(const float* __restrict__ SP, const float* __restrict__ fdpn, int N, int updates,
-                    const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err) {
+                    const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err, u64* trace,
+                    int trace_n) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     gu64* gran = (gu64*)gran_;
     const int KB = split_kblocks(N);
-    const int W = (KB + kPW - 1) / kPW;
-    const int KP = W * kPW;                       // packets incl. the zero padding
+    const int W = persist_waves_of(KB);
+    const int KP = persist_packets(W);            // packets incl. the zero padding
     f4v* qs = reinterpret_cast<f4v*>(lds);        // [KP][32] packets of this workgroup
-    float* ysb = lds + (size_t)KP * kPLanes * 4;  // [2][W * 4 kPW] y slices by update parity
-    u64* slot = reinterpret_cast<u64*>(ysb + 2 * W * kPW * 4);  // [2][W][64] hand-off words
-    const int ny = W * kPW * 4;
+    float* ysb = lds + (size_t)KP * kPLanes * 4;  // [2][4 KP] y by update parity
+    u64* slot = reinterpret_cast<u64*>(ysb + 2 * KP * 4);  // [2][W][64] hand-off words
+    const int ny = KP * 4;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ll = lane & (kPLanes - 1);  // lanes 32..63 repeat lanes 0..31 (discarded)
@@ -101,20 +113,31 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     const float fd = live ? fdpn[p] : 0.0f;
     __syncthreads();
 
-    const int pk0 = w * kPW;                                   // first packet of this wave's slice
-    const int k0 = 4 * pk0, k1 = (4 * (pk0 + kPW)) < N ? 4 * (pk0 + kPW) : N;  // y[k0, k1) of the slice
+    const int pk0 = w == 0 ? 0 : kPW0 + (w - 1) * kPW;          // first packet of this wave's slice
+    const int pk1 = w == 0 ? kPW0 : pk0 + kPW;                   // one past its last
+    const int k0 = 4 * pk0, k1 = 4 * pk1 < N ? 4 * pk1 : N;      // y[k0, k1) of the slice
     const bool last = (w == W - 1);
+    float yrow = 0.0f;  // last wave: y_i of this lane's row (for y_next = num / den * y_i)
+    // optional timeline (s_memtime) of workgroup 0: per update and wave,
+    // {sweep start, y staged, turn (sums received), chain done}
+    u64* tr = (trace && blockIdx.x == 0 && lane == 0) ? trace : nullptr;
+    auto mark = [&](int u, int e) {
+        if (tr && u < trace_n) tr[((size_t)u * W + w) * 4 + e] = __builtin_amdgcn_s_memtime();
+    };
     for (int u = 0; u < updates; ++u) {
         const int par = u & 1;
         float* ys = ysb + par * ny;
+        mark(u, 0);
         // ---- 1. y of this slice (k in [k0, k1)), staged in LDS ----
         if (u == 0) {
             for (int k = k0 + lane; k < k1; k += 64) ys[k] = Y0 ? Y0[k] : 1000.0f;  // initMat(Y, 1000) :710
+            if (last) yrow = (Y0 && row < N) ? Y0[row] : 1000.0f;
         } else {
             const gu64* g = gran + (size_t)par * N;
             const unsigned tag = (unsigned)u;
             for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
-                float v[4];
+                const bool own = last && kb == k0 && row < N;  // + y_i of the rows this workgroup finishes (:594)
+                float v[5] = {};
                 const u64 t0 = rt_now();
                 for (unsigned spins = 0;; ++spins) {
                     bool ok = true;
@@ -127,11 +150,18 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                             ok &= (unsigned)(x >> 32) == tag;
                         }
                     }
+                    if (own) {
+                        const u64 x = __hip_atomic_load(g + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        v[4] = __uint_as_float((unsigned)x);
+                        ok &= (unsigned)(x >> 32) == tag;
+                    }
                     if (__all(ok)) break;
                     if ((spins & 63) == 63 && (long long)(rt_now() - t0) > kPTimeoutTicks) {
                         fail(err, 1);
                         return;
                     }
+                    // one sweep at a time, a short pause between them (two sweeps
+                    // in flight measured 8 % slower: the pollers' own traffic)
                     __builtin_amdgcn_s_sleep(1);
                 }
 #pragma unroll
@@ -139,38 +169,56 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                     const int k = kb + 64 * m + lane;
                     if (k < k1) ys[k] = v[m];
                 }
+                if (own) yrow = v[4];
             }
         }
         // zero y past N up to the slice end (read by the last packet's products)
-        for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * (pk0 + kPW); k += 64) ys[k] = 0.0f;
-        // ---- 2. products of the slice, off the add chain ----
-        f4v prod[kPW];
+        for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
         // one base address per operand, the packet index as an immediate offset
         const f4v* qw = qs + (size_t)pk0 * kPLanes + ll;
         const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
+        float acc = 0.0f;
+        u64* sl = slot + (size_t)par * W * 64;
+        const unsigned want = (unsigned)(u + 1);
+        if (w == 0) {
+            // ---- 2/3 (wave 0). the chain starts here: products formed inside it ----
+            mark(u, 2);
+            __builtin_amdgcn_s_setprio(3);
+            f4v qv[kPW0], yv[kPW0];
 #pragma unroll
-        for (int j0 = 0; j0 < kPW; j0 += 4) {
+            for (int j = 0; j < kPW0; ++j) {
+                qv[j] = qw[j * kPLanes];
+                yv[j] = yw[j];
+            }
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int j = j0 + jj;
+            for (int j = 0; j < kPW0; ++j) {
+                const f4v q = qv[j], y = yv[j];
+                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+                acc += lo.x;  // :608-609, k in order
+                acc += lo.y;
+                acc += hi.x;
+                acc += hi.y;
+            }
+        } else {
+            // ---- 2. products of the slice, ahead of the turn ----
+            f4v prod[kPW];
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) {
                 const f4v q = qw[j * kPLanes];
                 const f4v y = yw[j];
                 const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
                 const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
                 prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
             }
+            // pinned here: otherwise the compiler sinks the multiplies into the chain
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(prod[j0 + jj]));
-        }
-        // ---- 3. the running sums of the previous slice, then this slice's adds ----
-        float acc = 0.0f;
-        u64* sl = slot + (size_t)par * W * 64;
-        const unsigned want = (unsigned)(u + 1);
-        if (w > 0) {
+            for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
+            // ---- 3. the running sums of the previous slice, then this slice's adds ----
             const u64 t0 = rt_now();
             u64 h;
             for (unsigned spins = 0;; ++spins) {
-                h = __hip_atomic_load(sl + (w - 1) * 64 + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                h = __hip_atomic_load(sl + (w - 1) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (__all((unsigned)(h >> 32) == want)) break;
                 if ((spins & 255) == 255 && (long long)(rt_now() - t0) > kPTimeoutTicks) {
                     fail(err, 2);
@@ -178,17 +226,20 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                 }
             }
             acc = __uint_as_float((unsigned)h);
-        }
-        __builtin_amdgcn_s_setprio(3);
+            mark(u, 2);
+            __builtin_amdgcn_s_setprio(3);
 #pragma unroll
-        for (int j = 0; j < kPW; ++j) {
-            acc += prod[j].x;  // :608-609, k in order
-            acc += prod[j].y;
-            acc += prod[j].z;
-            acc += prod[j].w;
+            for (int j = 0; j < kPW; ++j) {
+                acc += prod[j].x;  // :608-609, k in order
+                acc += prod[j].y;
+                acc += prod[j].z;
+                acc += prod[j].w;
+            }
         }
+        asm volatile("" : "+v"(acc));  // the mark below follows the chain
+        mark(u, 3);
         if (!last) {
-            __hip_atomic_store(sl + w * 64 + lane, ((u64)want << 32) | __float_as_uint(acc), __ATOMIC_RELEASE,
+            __hip_atomic_store(sl + w * 64 + lane, ((u64)want << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_s_setprio(0);
             continue;
@@ -198,7 +249,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         const float v = acc + 1.0f * fd;     // even lane: num (:611), odd lane: den (:612)
         const float den = __shfl_xor(v, 1);  // whole wave active
         if (!(p & 1) && live) {
-            const float yn = v / den * ys[row];  // :594; ys[row] was staged by its slice's wave (hand-off order)
+            const float yn = v / den * yrow;  // :594
             __hip_atomic_store(gran + (size_t)(par ^ 1) * N + row, ((u64)want << 32) | __float_as_uint(yn),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (u == updates - 1) Yout[row] = yn;
@@ -215,7 +266,7 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
     if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_split_persist, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N, updates, Y0,
-                       Yout, gran, err);
+                       Yout, gran, err, g_persist_trace, g_persist_trace_n);
     return hipGetLastError();
 }
 
