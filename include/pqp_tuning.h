@@ -32,6 +32,11 @@ int pqp_tune_set_variant(int variant);
  * relay update (one launch per update).  Returns the previous setting. */
 int pqp_tune_persist(int off);
 
+/* Converge-mode solves of N, M <= 32 problems run one wave per problem
+ * (k_solve_wave) when a launch holds at least b problems, else four waves per
+ * problem (k_solve_tiny).  Returns the previous threshold. */
+int pqp_tune_wave_min_b(int b);
+
 /* Timeline of the persistent launch's workgroup 0 (s_memtime shader clocks):
  * for the first `updates` updates, per update u and wave w, the four words
  * d_trace[(u * waves + w) * 4 + e] = {sweep start, y staged, running sums

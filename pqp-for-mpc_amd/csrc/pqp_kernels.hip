@@ -1687,6 +1687,253 @@ __global__ void __launch_bounds__(64) k_fixed_tiny(SolveArgs A0, SolveState* __r
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_solve_wave<NMAX, MMAX>: converge mode (terminate() before every update,
+// PQP_CPU.c:694-750) of one N <= NMAX, M <= MMAX problem on ONE wave, for
+// throughput over many problems (one problem per 64-thread workgroup, several
+// problems per SIMD).  The same arithmetic as k_solve_tiny, packed two sums per
+// lane so the terminate() mat-vecs ride along with the update's:
+//   pass over k (one v_pk_mul + one v_pk_add per k):
+//     .x  lanes 2i+side < 2N : the split row i (Qdn_theta / Qdp_theta)   -> num / den
+//     .y  lanes j < N        : Qd column j                                -> (Y'Qd)_j   (:652)
+//         lanes N + j < N + M: Gp column j                                -> (Gp'Y)_j   (:354)
+//   U = -(Qp_inv t) on lanes < M, then one pass over j < M:
+//     .x  lanes i < N : Gp row i -> (Gp U)_i (checkFeas :632-641)
+//     .y  lanes k < M : Qp column k -> (U'Qp)_k (computeCost :652)
+//   and the four scalar dot products in two packed pairs:
+//     (U'Qp . U, Fp . U) and (Y'Qd . Y, Fd . Y)  (:655-657)
+// Every sum keeps the reference's order from +0.0f with rounded products (no
+// FMA; a packed op rounds each half exactly like its scalar form), and the
+// padding terms (beyond N / M) add exactly +0 to sums that are never -0.
+// Vectors cross lanes through LDS (one wave: program order suffices).
+// ---------------------------------------------------------------------------
+template <int NMAX, int MMAX>
+__global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __restrict__ st0) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    static_assert(NMAX % 4 == 0 && MMAX % 4 == 0 && NMAX <= 32 && MMAX <= 32, "one wave");
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;
+    __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
+    __shared__ __attribute__((aligned(16))) float rowb[NMAX];  // Y'Qd
+    __shared__ __attribute__((aligned(16))) float tb[MMAX];    // t = Gp'Y + Fp
+    __shared__ __attribute__((aligned(16))) float ub[MMAX];    // U
+    __shared__ __attribute__((aligned(16))) float rpb[MMAX];   // U'Qp
+    const int N = A.N, M = A.M;
+    const int lane = threadIdx.x, i = lane >> 1, side = lane & 1;
+
+    f2v mat[NMAX];
+    f2v gq[MMAX];
+    float qinv[MMAX];
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) mat[k] = f2v{0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < MMAX; ++j) {
+        gq[j] = f2v{0.0f, 0.0f};
+        qinv[j] = 0.0f;
+    }
+    // setup: branch-free (clamped addresses, selects) and a few loads in flight
+    // at a time, so its register peak stays below the loop's
+    const bool rowl = i < N;
+    const int ir = rowl ? i : 0;
+    float th = 0.0f;  // computeTheta (:503-519)
+    for (int k = 0; k < N; ++k) th += max_ref(0.0f, -A.Qd[ir * N + k]) * 1.0f;
+    th = max_ref(th, 5.0f);
+    const bool colq = lane < N, colg = lane >= N && lane < N + M;
+    const int jq = colq ? lane : 0, jg = colg ? lane - N : 0;
+    // Fd . Y rides in the pass too: on the free .x lane 2N, or (N = 32) the
+    // free .y lane N + M (N = M = 32 is left to k_solve_tiny)
+    const int lf = (2 * N < 64) ? 2 * N : N + M;
+    const bool fx = (2 * N < 64) && lane == lf, fy = (2 * N >= 64) && lane == lf;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) {
+        if (k % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+        const int kc = (k < N) ? k : 0;
+        const float q = A.Qd[ir * N + kc];
+        const float t = (ir == k) ? th : 0.0f;
+        const float sp = (side ? max_ref(0.0f, q) : max_ref(0.0f, -q)) + 1.0f * t;  // :524-537
+        const float fk = A.Fd[kc];               // Fd (Fd . Y)
+        mat[k].x = (k < N) ? (rowl ? sp : (fx ? fk : 0.0f)) : 0.0f;
+        const float qc = A.Qd[kc * N + jq];      // Qd column (Y'Qd)
+        const float gc = A.Gp[kc * M + jg];      // Gp column (Gp'Y)
+        mat[k].y = (k < N) ? (colq ? qc : (colg ? gc : (fy ? fk : 0.0f))) : 0.0f;
+    }
+    const int jm = lane < M ? lane : 0, ig = lane < N ? lane : 0;
+#pragma unroll
+    for (int j = 0; j < MMAX; ++j) {
+        if (j % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+        const int jc = (j < M) ? j : 0;
+        const float gr = A.Gp[ig * M + jc];      // Gp row (Gp U): row i = lane
+        const float qp = A.Qp[jc * M + jm];      // Qp column (U'Qp)
+        const float qi = A.Qinv[jm * M + jc];    // Qp_inv row (Qp_inv t)
+        const float fj = A.Fp[jc];               // Fp (Fp . U) on the free .x lane N
+        gq[j].x = (j < M) ? ((lane < N) ? gr : (lane == N ? fj : 0.0f)) : 0.0f;
+        gq[j].y = (j < M && lane < M) ? qp : 0.0f;
+        qinv[j] = (j < M && lane < M) ? qi : 0.0f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float fd_own = 0.0f, fp_own = 0.0f, kp = 0.0f;
+    {
+        const float f = A.Fd[ir];
+        fd_own = rowl ? (side ? max_ref(0.0f, f) : max_ref(0.0f, -f)) : 0.0f;  // Fdp / Fdn (:703-704)
+        const float fp = A.Fp[jg];
+        fp_own = colg ? fp : 0.0f;
+    }
+    if (lane < N) kp = A.Kp[lane];
+    const float Md = A.Md[0], Mp = A.Mp[0];
+    for (int k = lane; k < NMAX; k += 64) {
+        ybuf[0][k] = (k < N) ? (st->resume ? A.Y[k] : 1000.0f) : 0.0f;  // initMat(Y, 1000) :710
+        ybuf[1][k] = 0.0f;
+        rowb[k] = 0.0f;
+    }
+    for (int j = lane; j < MMAX; j += 64) tb[j] = ub[j] = rpb[j] = 0.0f;
+    __syncthreads();
+
+    const int ic = (i < N) ? i : 0;
+    long long h = st->h;
+    long long done_here = 0;
+    int status = kStatusContinue;
+    int cb = 0;
+    float u_last = 0.0f, Jp_last = 0.0f, Jd_last = 0.0f;
+    bool have = false;
+    for (;;) {
+        const float* cur = ybuf[cb];
+        float* nxt = ybuf[cb ^ 1];
+        const float yi = cur[ic];
+        // ---- the fused pass over k ----
+        f2v acc = f2v{0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < NMAX; k += 4) {
+            const f4v y = *reinterpret_cast<const f4v*>(cur + k);
+            acc += mat[k] * f2v{y.x, y.x};  // :608-609 / :354 / :652, k in order
+            acc += mat[k + 1] * f2v{y.y, y.y};
+            acc += mat[k + 2] * f2v{y.z, y.z};
+            acc += mat[k + 3] * f2v{y.w, y.w};
+        }
+        // ---- updateY2's epilogue (applied only if terminate() says go on) ----
+        {
+            const float v = acc.x + 1.0f * fd_own;  // even lane: num (:611), odd lane: den (:612)
+            const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+            if (!side && i < N) nxt[i] = v / den * yi;  // :594
+        }
+        // ---- terminate(): computeUfromY (:352-360) ----
+        if (lane < N) rowb[lane] = acc.y;
+        else if (lane < N + M) tb[lane - N] = acc.y + 1.0f * fp_own;  // tmp = Gp'Y ; tmp += Fp
+        const float lin_d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fx ? acc.x : acc.y), lf));  // Fd . Y
+        float ua = 0.0f;
+#pragma unroll
+        for (int j = 0; j < MMAX; j += 4) {
+            const f4v t = *reinterpret_cast<const f4v*>(tb + j);
+            ua += qinv[j] * t.x;
+            ua += qinv[j + 1] * t.y;
+            ua += qinv[j + 2] * t.z;
+            ua += qinv[j + 3] * t.w;
+        }
+        const float u = (lane < M) ? -ua : 0.0f;  // U = -U
+        if (lane < MMAX) ub[lane] = u;
+        // ---- checkFeas (Gp U vs Kp) and U'Qp in one pass over j ----
+        f2v g = f2v{0.0f, 0.0f};
+        float uv[MMAX];
+#pragma unroll
+        for (int j = 0; j < MMAX; j += 4) {
+            const f4v t = *reinterpret_cast<const f4v*>(ub + j);
+            uv[j] = t.x;
+            uv[j + 1] = t.y;
+            uv[j + 2] = t.z;
+            uv[j + 3] = t.w;
+        }
+#pragma unroll
+        for (int j = 0; j < MMAX; ++j) g += gq[j] * f2v{uv[j], uv[j]};
+        const int bad = (lane < N) && (g.x > kp + max_ref((float)(kTol * kp), (float)kTol));
+        const bool infeasible = __any(bad);
+        if (lane < MMAX) rpb[lane] = g.y;
+        const float lin_p = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g.x), N));  // Fp . U
+        // ---- computeCost (:648-666): U'Qp . U and Y'Qd . Y, sequential ----
+        float quad = 0.0f;
+#pragma unroll
+        for (int j = 0; j < MMAX; j += 4) {
+            const f4v r = *reinterpret_cast<const f4v*>(rpb + j);
+            quad += r.x * uv[j];
+            quad += r.y * uv[j + 1];
+            quad += r.z * uv[j + 2];
+            quad += r.w * uv[j + 3];
+        }
+        float s2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NMAX; k += 4) {
+            const f4v r = *reinterpret_cast<const f4v*>(rowb + k);
+            const f4v y = *reinterpret_cast<const f4v*>(cur + k);
+            const f2v lo = f2v{r.x, r.y} * f2v{y.x, y.y};
+            const f2v hi = f2v{r.z, r.w} * f2v{y.z, y.w};
+            s2 += lo.x;
+            s2 += lo.y;
+            s2 += hi.x;
+            s2 += hi.y;
+        }
+        u_last = u;
+        // ---- the gap tests (:673-687), wave-uniform ----
+        int stop = 0;
+        if (!infeasible) {
+            float Jp = 0.0f;
+            Jp = (float)((double)Jp + 0.5 * (double)quad);
+            Jp += lin_p;
+            Jp += Mp / 2;
+            float Jd = 0.0f;
+            Jd = (float)((double)Jd + 0.5 * (double)s2);
+            Jd += lin_d;
+            Jd += Md / 2;
+            stop = 1;
+            if (Jp > -Jd) stop = 0;
+            if ((double)(Jp + Jd) > kTol) stop = 0;
+            if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+            Jp_last = Jp;
+            Jd_last = Jd;
+            have = true;
+        }
+        if (stop) {
+            status = kStatusDone;
+            break;
+        }
+        if (A.max_updates > 0 && h - 1 >= A.max_updates) {
+            status = kStatusCapped;
+            break;
+        }
+        if (done_here >= A.chunk) {
+            status = kStatusContinue;
+            break;
+        }
+        cb ^= 1;  // accept the update
+        ++h;
+        ++done_here;
+    }
+    for (int k = lane; k < N; k += 64) A.Y[k] = ybuf[cb][k];
+    if (lane < M) A.U[lane] = u_last;  // computeUfromY wrote U on every terminate(): the last one stands
+    if (lane == 0) {
+        if (have) {
+            st->Jp = Jp_last;
+            st->Jd = Jd_last;
+            st->have_costs = 1;
+        }
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
+    }
+}
+
+// (a register cap of 4 waves per SIMD was measured 30 % slower: it spills
+// inside the loop; uncapped, the bundled-size build holds 3 problems per SIMD)
+template <int NMAX>
+static void launch_wave_m(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    if (a.M <= 8)
+        hipLaunchKernelGGL((k_solve_wave<NMAX, 8>), dim3(B), dim3(64), 0, s, a, st);
+    else if (a.M <= 16)
+        hipLaunchKernelGGL((k_solve_wave<NMAX, 16>), dim3(B), dim3(64), 0, s, a, st);
+    else
+        hipLaunchKernelGGL((k_solve_wave<NMAX, 32>), dim3(B), dim3(64), 0, s, a, st);
+}
+
 template <int NMAX>
 static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads, hipStream_t s) {
     if (a.M <= 8)
@@ -1698,6 +1945,7 @@ static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads
 }
 
 int g_fixed_tiny_old = 0;  // tuning: fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
+int g_wave_min_b = 512;  // tuning: converge mode of N, M <= 32 on k_solve_wave from this many problems on
 
 static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the
@@ -1708,6 +1956,14 @@ static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hi
         else if (a.N <= 24) hipLaunchKernelGGL((k_fixed_tiny<24>), dim3(B), dim3(64), 0, s, a, st);
         else if (a.N <= 28) hipLaunchKernelGGL((k_fixed_tiny<28>), dim3(B), dim3(64), 0, s, a, st);
         else hipLaunchKernelGGL((k_fixed_tiny<32>), dim3(B), dim3(64), 0, s, a, st);
+        return hipGetLastError();
+    }
+    if (a.mode == kModeConverge && B >= g_wave_min_b && a.N + a.M < 64) {  // many problems: one wave each
+        if (a.N <= 8) launch_wave_m<8>(B, a, st, s);
+        else if (a.N <= 16) launch_wave_m<16>(B, a, st, s);
+        else if (a.N <= 24) launch_wave_m<24>(B, a, st, s);
+        else if (a.N <= 28) launch_wave_m<28>(B, a, st, s);
+        else launch_wave_m<32>(B, a, st, s);
         return hipGetLastError();
     }
     const int threads = (a.mode == kModeFixed) ? 64 : 256;

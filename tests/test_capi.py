@@ -65,8 +65,9 @@ def _gfx950_asm(name: str) -> str:
 
 @pytest.mark.parametrize("src,pattern,min_kernels", [
     ("pqp_kernels.hip",
-     r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|14k_split_update|12k_fixed_tiny)",
-     18),
+     r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|14k_split_update|12k_fixed_tiny"
+     r"|12k_solve_wave)",
+     33),
     ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 3),
     ("pqp_persist.hip", r"_ZN3pqp15k_split_persist", 1),
 ])
