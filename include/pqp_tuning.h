@@ -37,6 +37,11 @@ int pqp_tune_persist(int off);
  * problem (k_solve_tiny).  Returns the previous threshold. */
 int pqp_tune_wave_min_b(int b);
 
+/* k_solve_wave launches of at most b problems use its software-pipelined form
+ * (the next iterate's pass beside this iterate's terminate()): shorter
+ * iterations, more registers.  Returns the previous threshold. */
+int pqp_tune_wave_pipe_max_b(int b);
+
 /* Timeline of the persistent launch's workgroup 0 (s_memtime shader clocks):
  * for the first `updates` updates, per update u and wave w, the four words
  * d_trace[(u * waves + w) * 4 + e] = {sweep start, y staged, running sums

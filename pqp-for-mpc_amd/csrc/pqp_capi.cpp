@@ -1432,6 +1432,12 @@ extern "C" int pqp_tune_wave_min_b(int b) {
     return old;
 }
 
+extern "C" int pqp_tune_wave_pipe_max_b(int b) {
+    const int old = pqp::g_wave_pipe_max_b;
+    pqp::g_wave_pipe_max_b = b;
+    return old;
+}
+
 extern "C" int pqp_tune_persist(int off) {
     const int old = pqp::g_persist_off;
     pqp::g_persist_off = off ? 1 : 0;

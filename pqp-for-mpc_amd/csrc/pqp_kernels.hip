@@ -1707,7 +1707,7 @@ __global__ void __launch_bounds__(64) k_fixed_tiny(SolveArgs A0, SolveState* __r
 // padding terms (beyond N / M) add exactly +0 to sums that are never -0.
 // Vectors cross lanes through LDS (one wave: program order suffices).
 // ---------------------------------------------------------------------------
-template <int NMAX, int MMAX>
+template <int NMAX, int MMAX, bool PIPE>
 __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __restrict__ st0) {
     typedef float f2v __attribute__((ext_vector_type(2)));
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -1716,6 +1716,7 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
     SolveState* st = st0 + blockIdx.x;
     if (st->status == kStatusDone || st->status == kStatusCapped) return;
     __shared__ __attribute__((aligned(16))) float ybuf[2][NMAX];
+    __shared__ float junk[64];  // per-lane sink: stores are unconditional (no branch splits the iteration)
     __shared__ __attribute__((aligned(16))) float rowb[NMAX];  // Y'Qd
     __shared__ __attribute__((aligned(16))) float tb[MMAX];    // t = Gp'Y + Fp
     __shared__ __attribute__((aligned(16))) float ub[MMAX];    // U
@@ -1797,30 +1798,66 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
     int cb = 0;
     float u_last = 0.0f, Jp_last = 0.0f, Jd_last = 0.0f;
     bool have = false;
+    // the fused pass over k: one v_pk_mul + v_pk_add per k
+    auto pass = [&](const float* yb) {
+        f2v a = f2v{0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < NMAX; k += 4) {
+            const f4v y = *reinterpret_cast<const f4v*>(yb + k);
+            a += mat[k] * f2v{y.x, y.x};  // :608-609 / :354 / :652, k in order
+            a += mat[k + 1] * f2v{y.y, y.y};
+            a += mat[k + 2] * f2v{y.z, y.z};
+            a += mat[k + 3] * f2v{y.w, y.w};
+        }
+        return a;
+    };
+    const bool wr_y = !side && i < N, wr_row = lane < N, wr_t = lane >= N && lane < N + M, wr_m = lane < MMAX;
+    // PIPE: every store unconditional (lanes that do not own the word write
+    // their own junk word), so no branch splits the iteration; plain: masked
+    // stores (fewer registers)
+    auto put = [&](bool own, float* dst, float v) {
+        if constexpr (PIPE) {
+            *(own ? dst : junk + lane) = v;
+        } else {
+            if (own) *dst = v;
+        }
+    };
+    f2v acc = f2v{0.0f, 0.0f};
+    if constexpr (PIPE) acc = pass(ybuf[cb]);
     for (;;) {
+        // PIPE (software-pipelined): the pass over the NEXT iterate (speculative:
+        // used only if this terminate() says go on) runs beside this iterate's
+        // terminate() chains; nothing branches between them.  Shorter
+        // iterations, more registers (fewer problems per SIMD).
         const float* cur = ybuf[cb];
         float* nxt = ybuf[cb ^ 1];
         const float yi = cur[ic];
-        // ---- the fused pass over k ----
-        f2v acc = f2v{0.0f, 0.0f};
-#pragma unroll
-        for (int k = 0; k < NMAX; k += 4) {
-            const f4v y = *reinterpret_cast<const f4v*>(cur + k);
-            acc += mat[k] * f2v{y.x, y.x};  // :608-609 / :354 / :652, k in order
-            acc += mat[k + 1] * f2v{y.y, y.y};
-            acc += mat[k + 2] * f2v{y.z, y.z};
-            acc += mat[k + 3] * f2v{y.w, y.w};
-        }
-        // ---- updateY2's epilogue (applied only if terminate() says go on) ----
+        if constexpr (!PIPE) acc = pass(cur);
+        // ---- updateY2's epilogue ----
         {
             const float v = acc.x + 1.0f * fd_own;  // even lane: num (:611), odd lane: den (:612)
             const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
-            if (!side && i < N) nxt[i] = v / den * yi;  // :594
+            put(wr_y, nxt + i, v / den * yi);  // :594
         }
+        f2v acc_next = f2v{0.0f, 0.0f};
+        if constexpr (PIPE) acc_next = pass(nxt);
         // ---- terminate(): computeUfromY (:352-360) ----
-        if (lane < N) rowb[lane] = acc.y;
-        else if (lane < N + M) tb[lane - N] = acc.y + 1.0f * fp_own;  // tmp = Gp'Y ; tmp += Fp
+        put(wr_row, rowb + lane, acc.y);
+        put(wr_t, tb + (lane - N), acc.y + 1.0f * fp_own);  // tmp = Gp'Y ; tmp += Fp
         const float lin_d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fx ? acc.x : acc.y), lf));  // Fd . Y
+        // Y'Qd . Y (computeCost, Jd) first: its chain is independent of U's
+        float s2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NMAX; k += 4) {
+            const f4v r = *reinterpret_cast<const f4v*>(rowb + k);
+            const f4v y = *reinterpret_cast<const f4v*>(cur + k);
+            const f2v lo = f2v{r.x, r.y} * f2v{y.x, y.y};
+            const f2v hi = f2v{r.z, r.w} * f2v{y.z, y.w};
+            s2 += lo.x;
+            s2 += lo.y;
+            s2 += hi.x;
+            s2 += hi.y;
+        }
         float ua = 0.0f;
 #pragma unroll
         for (int j = 0; j < MMAX; j += 4) {
@@ -1831,7 +1868,7 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
             ua += qinv[j + 3] * t.w;
         }
         const float u = (lane < M) ? -ua : 0.0f;  // U = -U
-        if (lane < MMAX) ub[lane] = u;
+        put(wr_m, ub + lane, u);
         // ---- checkFeas (Gp U vs Kp) and U'Qp in one pass over j ----
         f2v g = f2v{0.0f, 0.0f};
         float uv[MMAX];
@@ -1847,7 +1884,7 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
         for (int j = 0; j < MMAX; ++j) g += gq[j] * f2v{uv[j], uv[j]};
         const int bad = (lane < N) && (g.x > kp + max_ref((float)(kTol * kp), (float)kTol));
         const bool infeasible = __any(bad);
-        if (lane < MMAX) rpb[lane] = g.y;
+        put(wr_m, rpb + lane, g.y);
         const float lin_p = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g.x), N));  // Fp . U
         // ---- computeCost (:648-666): U'Qp . U and Y'Qd . Y, sequential ----
         float quad = 0.0f;
@@ -1858,18 +1895,6 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
             quad += r.y * uv[j + 1];
             quad += r.z * uv[j + 2];
             quad += r.w * uv[j + 3];
-        }
-        float s2 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < NMAX; k += 4) {
-            const f4v r = *reinterpret_cast<const f4v*>(rowb + k);
-            const f4v y = *reinterpret_cast<const f4v*>(cur + k);
-            const f2v lo = f2v{r.x, r.y} * f2v{y.x, y.y};
-            const f2v hi = f2v{r.z, r.w} * f2v{y.z, y.w};
-            s2 += lo.x;
-            s2 += lo.y;
-            s2 += hi.x;
-            s2 += hi.y;
         }
         u_last = u;
         // ---- the gap tests (:673-687), wave-uniform ----
@@ -1883,10 +1908,9 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
             Jd = (float)((double)Jd + 0.5 * (double)s2);
             Jd += lin_d;
             Jd += Md / 2;
-            stop = 1;
-            if (Jp > -Jd) stop = 0;
-            if ((double)(Jp + Jd) > kTol) stop = 0;
-            if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+            // the three tests of :683-685, evaluated lazily (no side effects;
+            // the double division only once the first two pass)
+            stop = !(Jp > -Jd) && !((double)(Jp + Jd) > kTol) && !((double)(Jp + Jd) / fabs((double)Jd) > kTol);
             Jp_last = Jp;
             Jd_last = Jd;
             have = true;
@@ -1904,6 +1928,7 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
             break;
         }
         cb ^= 1;  // accept the update
+        if constexpr (PIPE) acc = acc_next;
         ++h;
         ++done_here;
     }
@@ -1923,15 +1948,24 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
 }
 
 // (a register cap of 4 waves per SIMD was measured 30 % slower: it spills
-// inside the loop; uncapped, the bundled-size build holds 3 problems per SIMD)
+// inside the loop).  Up to a few thousand problems every one gets its own SIMD
+// slot at once, so the pipelined form's shorter iterations win; beyond that
+// the plain form's smaller register file (3 vs 2 problems per SIMD at the
+// bundled size) wins on throughput.
+int g_wave_pipe_max_b = 4096;
+template <int NMAX, bool PIPE>
+static void launch_wave_mp(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    if (a.M <= 8)
+        hipLaunchKernelGGL((k_solve_wave<NMAX, 8, PIPE>), dim3(B), dim3(64), 0, s, a, st);
+    else if (a.M <= 16)
+        hipLaunchKernelGGL((k_solve_wave<NMAX, 16, PIPE>), dim3(B), dim3(64), 0, s, a, st);
+    else
+        hipLaunchKernelGGL((k_solve_wave<NMAX, 32, PIPE>), dim3(B), dim3(64), 0, s, a, st);
+}
 template <int NMAX>
 static void launch_wave_m(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
-    if (a.M <= 8)
-        hipLaunchKernelGGL((k_solve_wave<NMAX, 8>), dim3(B), dim3(64), 0, s, a, st);
-    else if (a.M <= 16)
-        hipLaunchKernelGGL((k_solve_wave<NMAX, 16>), dim3(B), dim3(64), 0, s, a, st);
-    else
-        hipLaunchKernelGGL((k_solve_wave<NMAX, 32>), dim3(B), dim3(64), 0, s, a, st);
+    if (B <= g_wave_pipe_max_b) launch_wave_mp<NMAX, true>(B, a, st, s);
+    else launch_wave_mp<NMAX, false>(B, a, st, s);
 }
 
 template <int NMAX>
@@ -1945,7 +1979,7 @@ static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads
 }
 
 int g_fixed_tiny_old = 0;  // tuning: fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
-int g_wave_min_b = 512;  // tuning: converge mode of N, M <= 32 on k_solve_wave from this many problems on
+int g_wave_min_b = 1;  // tuning: converge mode of N, M <= 32 on k_solve_wave from this many problems on
 
 static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the

@@ -30,8 +30,9 @@ def main():
         pb = pqp_amd.mpc_batch(ex_dir, xs)
         row = {}
         hs = {}
-        for name, thr in (("wave", 1), ("tiny", 1 << 30)):
+        for name, thr, pipe in (("wave_pipelined", 1, 1 << 30), ("wave_plain", 1, 0), ("tiny", 1 << 30, 0)):
             L.pqp_tune_wave_min_b(thr)
+            L.pqp_tune_wave_pipe_max_b(pipe)
             pb.solve(max_updates=200000)
             torch.cuda.synchronize()
             reps = 3 if B >= 16384 else 10
@@ -43,13 +44,14 @@ def main():
             h = pb.h.cpu().numpy()
             hs[name] = h.copy()
             row[name] = {"ms": dt * 1e3, "qp_solves_per_s": B / dt, "iterations_per_s": float(h.sum()) / dt}
-        row["h_identical"] = bool(np.array_equal(hs["wave"], hs["tiny"]))
-        row["speedup_wave_vs_tiny"] = row["tiny"]["ms"] / row["wave"]["ms"]
+        row["h_identical"] = all(bool(np.array_equal(hs[k], hs["tiny"])) for k in hs)
+        row["speedup_best_wave_vs_tiny"] = row["tiny"]["ms"] / min(row["wave_pipelined"]["ms"], row["wave_plain"]["ms"])
         out[f"B{B}"] = row
         print(json.dumps({f"B{B}": row}), flush=True)
         del pb
         torch.cuda.empty_cache()
-    L.pqp_tune_wave_min_b(512)
+    L.pqp_tune_wave_min_b(1)
+    L.pqp_tune_wave_pipe_max_b(4096)
 
 
 if __name__ == "__main__":

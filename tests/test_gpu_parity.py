@@ -25,9 +25,19 @@ def bundled_problem(g):
 # ---------------------------------------------------------------------------
 # bundled example (configs 1/2)
 # ---------------------------------------------------------------------------
-def test_bundled_converge_bit_exact(gpu_lib, golden_bundled):
+@pytest.mark.parametrize("solver", ["wave_pipelined", "wave_plain", "tiny"])
+def test_bundled_converge_bit_exact(gpu_lib, golden_bundled, solver):
+    """One problem in converge mode: the one-wave solver (default; pipelined
+    and plain forms) and the four-wave k_solve_tiny."""
     g = golden_bundled
-    r = gpu_lib.solve_dual(bundled_problem(g), max_updates=CAP)
+    L = gpu_lib.lib()
+    old_b = L.pqp_tune_wave_min_b(1 << 30 if solver == "tiny" else 1)
+    old_p = L.pqp_tune_wave_pipe_max_b(0 if solver == "wave_plain" else 1 << 30)
+    try:
+        r = gpu_lib.solve_dual(bundled_problem(g), max_updates=CAP)
+    finally:
+        L.pqp_tune_wave_min_b(old_b)
+        L.pqp_tune_wave_pipe_max_b(old_p)
     assert r["converged"]
     assert r["h"] == int(g["h"]) == 313
     assert_bitwise(r["Y"], g["Ystar"], "Y*")

@@ -15,13 +15,16 @@ pytestmark = pytest.mark.gpu
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 
 
-@pytest.fixture
-def wave_on(gpu_lib):
-    """k_solve_wave for every batch size."""
+@pytest.fixture(params=[1 << 30, 0], ids=["pipelined", "plain"])
+def wave_on(gpu_lib, request):
+    """k_solve_wave for every batch size, in its software-pipelined form and
+    in its plain form."""
     L = gpu_lib.lib()
     old = L.pqp_tune_wave_min_b(1)
+    old_pipe = L.pqp_tune_wave_pipe_max_b(request.param)
     yield
     L.pqp_tune_wave_min_b(old)
+    L.pqp_tune_wave_pipe_max_b(old_pipe)
 
 
 def _batch_of(gpu_lib, probs, N, M):
