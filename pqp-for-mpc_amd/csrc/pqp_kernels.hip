@@ -1831,7 +1831,8 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
         // iterations, more registers (fewer problems per SIMD).
         const float* cur = ybuf[cb];
         float* nxt = ybuf[cb ^ 1];
-        const float yi = cur[ic];
+        float yi = cur[ic];
+        asm volatile("" : "+v"(yi));  // read early: its latency hides under the pass
         if constexpr (!PIPE) acc = pass(cur);
         // ---- updateY2's epilogue ----
         {
