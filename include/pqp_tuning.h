@@ -32,6 +32,26 @@ int pqp_tune_set_variant(int variant);
  * relay update (one launch per update).  Returns the previous setting. */
 int pqp_tune_persist(int off);
 
+/* Converge mode of one problem with n_dual, M <= 1024 that goes over many
+ * workgroups runs as ONE persistent pipelined launch (pqp_converge.hip:
+ * terminate(Y_u) beside the update to Y_{u+1}) unless off = 1, which sends it
+ * through the graph-replayed launch chain of pqp_wide.hip.  Returns the
+ * previous setting. */
+int pqp_tune_converge_persist(int off);
+
+/* Iterates one persistent converge launch decides at most before the host
+ * relaunches from the iterate it left (default 65536; <= 0 restores it).
+ * Returns the previous value. */
+int pqp_tune_converge_chunk(int iterates);
+
+/* Timeline of the persistent converge launch: for the first `iterates`
+ * iterates of each launch, workgroup 0 of every role writes s_memrealtime
+ * (100 MHz, chip-wide) marks into d_trace[iterate][29][4] (role * 6 + wave
+ * for UPD, T1, T2, T3; 24 + wave for DEC, wave 0 deciding, waves 1-4 summing
+ * the dots): iterate start, inputs staged, turn
+ * (running sums received; DEC: sum done), done.  iterates = 0 turns it off. */
+int pqp_tune_converge_trace(void* d_trace, int iterates);
+
 /* Converge-mode solves of N, M <= 32 problems run one wave per problem
  * (k_solve_wave) when a launch holds at least b problems, else four waves per
  * problem (k_solve_tiny).  Returns the previous threshold. */

@@ -243,6 +243,8 @@ struct pqp_problem {
     bool chunk_ready = false;
     // converge mode over many workgroups (pqp_wide.hip), built on first use
     pqp::DevBuf QinvT, GpT, tM, tq, tu, gu, wflag, wcap;
+    // converge mode as one persistent pipelined launch (pqp_converge.hip), built on first use
+    pqp::DevBuf CA1, CA2, CA3, crings, cwords;
     hipGraphExec_t wgraph = nullptr;                 // captured chunk of converge iterations
     hipGraphExec_t wgraph_first = nullptr;           // the short first chunk
     hipStream_t side = nullptr;                      // capture-time fork for the speculative update
@@ -389,21 +391,29 @@ constexpr long long kFixedChunk = 256;  // even: a chunk starts and ends with th
 // persistent launch (pqp_persist.hip), launches of at most kPersistChunk
 // updates chained through P.Y.
 constexpr long long kPersistChunk = 1 << 16;
+// The stored split matrices in the 32-lane layout (k_build_split), built once
+// per problem: the persistent fixed-mode launch and the persistent converge
+// launch's update role hold them in LDS.
+int ensure_persist_split(pqp_problem& P, hipStream_t s) {
+    const int N = P.N;
+    if (P.SPp.p) return PQP_OK;
+    if (!P.theta.p) {
+        PQP_TRY(P.theta.floats(N));
+        PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
+    }
+    if (!P.Yb.p) PQP_TRY(P.Yb.floats(N));
+    PQP_TRY(P.SPp.floats(split_floats(N, N, 32)));
+    PQP_TRY(P.fdpnp.floats((size_t)2 * N));
+    PQP_HIP(hipMemsetAsync(P.SPp.p, 0, sizeof(float) * split_floats(N, N, 32), s));
+    PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, 32, P.SPp.f(), P.fdpnp.f(), s));
+    PQP_TRY(P.gran.alloc(sizeof(unsigned long long) * 2 * N));
+    PQP_TRY(P.perr.alloc(sizeof(int)));
+    return PQP_OK;
+}
+
 int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, hipStream_t s) {
     const int N = P.N;
-    if (!P.SPp.p) {  // the stored split matrices in the 32-lane layout, built once per problem
-        if (!P.theta.p) {
-            PQP_TRY(P.theta.floats(N));
-            PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
-        }
-        if (!P.Yb.p) PQP_TRY(P.Yb.floats(N));
-        PQP_TRY(P.SPp.floats(split_floats(N, N, 32)));
-        PQP_TRY(P.fdpnp.floats((size_t)2 * N));
-        PQP_HIP(hipMemsetAsync(P.SPp.p, 0, sizeof(float) * split_floats(N, N, 32), s));
-        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, 32, P.SPp.f(), P.fdpnp.f(), s));
-        PQP_TRY(P.gran.alloc(sizeof(unsigned long long) * 2 * N));
-        PQP_TRY(P.perr.alloc(sizeof(int)));
-    }
+    PQP_TRY(ensure_persist_split(P, s));
     auto* gran = static_cast<unsigned long long*>(P.gran.p);
     int* err = static_cast<int*>(P.perr.p);
     PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
@@ -461,10 +471,98 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
 // one-workgroup decision, then the relay update.  A chunk of kWideChunk
 // iterations is captured into a hipGraph and replayed until the device-side
 // status leaves Continue; launches after that point return at once.
+// Converge mode of a problem with N, M <= 1024 as ONE persistent launch
+// (pqp_converge.hip): the update and the stages of terminate() run as
+// concurrent roles, terminate(Y_u) beside the update to Y_{u+1}.  Launches
+// decide at most g_converge_chunk iterates each and are chained through P.Y.
+long long g_converge_chunk = 1 << 16;  // tuning: iterates decided per launch
+bool converge_persist_fits(int N, int M) {
+    if (g_converge_persist_off) return false;
+    const int G = converge_persist_wgs(N, M, nullptr);
+    if (G == 0) return false;
+    int dev = 0, cus = 0, lds = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) return false;
+    return G <= cus && converge_persist_lds_bytes(N, M) <= (size_t)lds;
+}
+
+int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
+    const int N = P.N, M = P.M;
+    PQP_TRY(ensure_persist_split(P, s));
+    if (!P.CA1.p) {
+        const size_t n1 = converge_stage_floats(N, M, 1), n2 = converge_stage_floats(N, M, 2),
+                     n3 = converge_stage_floats(N, M, 3);
+        PQP_TRY(P.CA1.floats(n1));
+        PQP_TRY(P.CA2.floats(n2));
+        PQP_TRY(P.CA3.floats(n3));
+        PQP_HIP(hipMemsetAsync(P.CA1.p, 0, sizeof(float) * n1, s));
+        PQP_HIP(hipMemsetAsync(P.CA2.p, 0, sizeof(float) * n2, s));
+        PQP_HIP(hipMemsetAsync(P.CA3.p, 0, sizeof(float) * n3, s));
+        PQP_HIP(launch_converge_pack(P.Qd.f(), P.Gp.f(), P.Qinv.f(), P.Qp.f(), N, M, P.CA1.f(), P.CA2.f(), P.CA3.f(),
+                                     s));
+        PQP_TRY(P.crings.alloc(sizeof(unsigned long long) * converge_ring_words(N, M)));
+        PQP_TRY(P.cwords.alloc(32));  // ctl, err (int), decided (long long)
+    }
+    SolveState& st = *P.hst;
+    st = SolveState{};
+    st.h = 1;
+    st.status = kStatusContinue;
+    SolveState* dst = static_cast<SolveState*>(P.state.p);
+    PQP_HIP(hipMemcpyAsync(dst, &st, sizeof st, hipMemcpyHostToDevice, s));
+    PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
+    char* words = static_cast<char*>(P.cwords.p);
+    ConvergeLaunch L{};
+    L.N = N;
+    L.M = M;
+    L.chunk = g_converge_chunk;
+    L.cap = max_updates;
+    L.SP = P.SPp.f();
+    L.A1 = P.CA1.f();
+    L.A2 = P.CA2.f();
+    L.A3 = P.CA3.f();
+    L.fdpn = P.fdpnp.f();
+    L.Fp = P.Fp.f();
+    L.Kp = P.Kp.f();
+    L.Fd = P.Fd.f();
+    L.Md = P.Md.f();
+    L.Mp = P.Mp.f();
+    L.rings = P.crings.p;
+    L.st = dst;
+    L.ctl = reinterpret_cast<int*>(words);
+    L.err = reinterpret_cast<int*>(words + 4);
+    L.decided = reinterpret_cast<long long*>(words + 8);
+    L.Y = P.Y.f();
+    L.U = P.U.f();
+    for (long long u0 = 0;;) {
+        L.u0 = u0;
+        PQP_HIP(launch_converge_persist(L, s));
+        int herr = 0;
+        PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipMemcpyAsync(&herr, L.err, sizeof herr, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (herr)
+            return set_error(PQP_ERR_HIP, "persistent converge launch: a wait timed out (code %d); its %d workgroups "
+                             "must be resident at once", herr, converge_persist_wgs(N, M, nullptr));
+        if (st.status != kStatusContinue) break;
+        u0 = st.h - 1;  // the next launch starts from the iterate this one left in P.Y
+    }
+    out.h = st.h;
+    out.status = st.status;
+    out.have_costs = st.have_costs;
+    out.last_stop = 0;
+    if (st.have_costs) {
+        out.Jp = st.Jp;
+        out.Jd = st.Jd;
+    }
+    return PQP_OK;
+}
+
 constexpr int kWideChunk = 16;      // even: each replay starts and ends with the iterate in P.Y
 constexpr int kWideFirstChunk = 2;  // the first replay of a solve
 int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
     const int N = P.N, M = P.M;
+    if (converge_persist_fits(N, M)) return problem_run_converge_persist(P, max_updates, out, s);
     const int lw = split_pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
     if (!P.QinvT.p) {
@@ -1449,6 +1547,26 @@ extern "C" int pqp_tune_persist_trace(void* d_trace, int updates) {
     pqp::g_persist_trace = updates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
     pqp::g_persist_trace_n = updates;
     return PQP_OK;
+}
+
+extern "C" int pqp_tune_converge_persist(int off) {
+    const int old = pqp::g_converge_persist_off;
+    pqp::g_converge_persist_off = off ? 1 : 0;
+    return old;
+}
+
+extern "C" int pqp_tune_converge_trace(void* d_trace, int iterates) {
+    if (iterates < 0 || (iterates > 0 && !d_trace))
+        return pqp::set_error(PQP_ERR_ARG, "pqp_tune_converge_trace: bad arguments");
+    pqp::g_converge_trace = iterates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
+    pqp::g_converge_trace_n = iterates;
+    return PQP_OK;
+}
+
+extern "C" int pqp_tune_converge_chunk(int iterates) {
+    const int old = (int)pqp::g_converge_chunk;
+    pqp::g_converge_chunk = iterates > 0 ? iterates : (1 << 16);
+    return old;
 }
 
 extern "C" int pqp_tune_wide_flags(int flags) {

@@ -1,0 +1,692 @@
+// pqp_converge.hip -- converge mode of ONE problem with n_dual, M <= 1024 as
+// ONE persistent, pipelined launch (solveQuadraticDual, PQP_CPU.c:694-750).
+//
+// The reference alternates terminate(Y_u) (:673-687) and updateY2 (:603-618).
+// updateY2 does not depend on terminate's answer, only on Y_u, so the two can
+// overlap: the launch runs the update chain and the stages of terminate() as
+// concurrent ROLES on disjoint workgroups, each looping over iterates u and
+// passing vectors downstream through rings of tagged 8-byte granules
+// {tag = u + 1, bits(value)} in global memory (the data is its own flag):
+//
+//   UPD  y_{u+1} = updateY2(y_u)             2N/32 workgroups  ring ry   [N]
+//   T1   tmp_u = Gp'y_u + Fp, tq_u = y_u'Qd  (N+M)/32          rtmp [M], rtq [N]
+//   T2   U_u = -(Qp_inv tmp_u)               M/32              rU   [M]
+//   T3   Gp U_u vs Kp, tu_u = U_u'Qp         (N+M)/32          rfeas[wg], rtu [M]
+//   DEC  the four dots of computeCost, the gap tests, the decision  (1 workgroup)
+//
+// Every output is one lane's sum over k in order from +0.0f, the reference's
+// matrixMultiply order (:88-100), formed exactly as in k_split_persist: the
+// stage's matrix columns stay in LDS for the whole solve (32 columns per
+// workgroup), wave w of a workgroup owns a k-slice, forms its products ahead
+// of its turn, adds them when the running sums arrive from wave w-1 and hands
+// them on through an LDS word; the last wave applies the epilogue (Fp add,
+// negation, the Kp comparison) and publishes.
+//
+// DEC decides iterates in order.  When terminate(y_u) passes (or u reaches the
+// cap) it writes h = u + 1, Jp, Jd, copies y_u and U_u out of the rings and
+// raises the control word; every waiting wave sees it and leaves.  Otherwise
+// it publishes `decided = u`.  Rings are kR deep and UPD publishes y_{u+1}
+// only once decided >= u + 1 - kR: every role has then finished iterate
+// u + 1 - kR, so no slot is overwritten while it is still read.  Speculative
+// updates past the stopping iterate are simply discarded.  Every wait is
+// bounded in time (2 s): a workgroup that never gets a CU ends the launch with
+// an error word instead of a hang.
+//
+// A launch decides at most `chunk` iterates; the host relaunches from the
+// iterate it left in Yout until the status leaves Continue.
+//
+// Requirement: all workgroups resident at once (one per CU by their LDS); the
+// host checks the count against the device's CUs.
+#include "pqp_device.h"
+#include "pqp_launch.h"
+
+#pragma clang fp contract(off)
+
+namespace pqp {
+
+namespace {
+
+typedef unsigned long long u64;
+typedef __attribute__((address_space(1))) u64 gu64;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+constexpr int kL = 32;     // output columns (update: row sides) per workgroup
+constexpr int kP0 = 24;    // packets (4 values of k) of wave 0's slice, multiplied inside its chain
+constexpr int kPW = 48;    // packets per later slice, products formed ahead in 4 kPW VGPRs
+constexpr int kMaxW = 6;   // waves for K <= 1024
+constexpr int kR = 8;      // ring depth (iterates in flight)
+constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
+constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
+constexpr int kDecChunk = 256;  // dot terms per unrolled chunk
+constexpr long long kTimeoutTicks = 200000000LL;  // s_memrealtime at 100 MHz: 2 s
+enum Role : int { kUpd = 0, kT1 = 1, kT2 = 2, kT3 = 3, kDec = 4 };
+
+__device__ __forceinline__ u64 rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+__host__ __device__ inline int waves_of(int KB) { return KB <= kP0 ? 1 : 1 + (KB - kP0 + kPW - 1) / kPW; }
+__host__ __device__ inline int packets_of(int W) { return kP0 + (W - 1) * kPW; }
+__host__ __device__ inline int cdiv_i(int a, int b) { return (a + b - 1) / b; }
+__device__ __forceinline__ u64 granule(unsigned tag, float v) { return ((u64)tag << 32) | __float_as_uint(v); }
+
+}  // namespace
+
+struct CvArgs {
+    int N, M;
+    int g1, g2, g3, g4;                  // role boundaries: [0,g1) UPD, [g1,g2) T1, [g2,g3) T2, [g3,g4) T3, g4 DEC
+    long long u0;                        // iterate this launch starts from (y_{u0} in ring slot u0 % kR)
+    long long u_dec_end;                 // last iterate DEC decides in this launch
+    long long u_prod_end;                // last iterate UPD produces
+    long long cap;                       // max_updates (<= 0: none)
+    const f4v *SPu, *A1, *A2, *A3;       // LDS-resident packets per role: [wg][KB][32]
+    const float *fdpn, *Fp, *Kp, *Fd, *Md, *Mp;
+    u64 *ry, *rtmp, *rtq, *rU, *rtu, *rfeas;
+    SolveState* st;
+    int* ctl;             // 0 running, 1 finished, 2 failed
+    long long* decided;   // last iterate DEC let through
+    int* err;
+    float *Yout, *Uout;
+    u64* trace;           // tuning: [iterate][29][4] s_memrealtime marks of workgroup 0 of each role
+    int trace_n;
+};
+
+namespace {
+
+__device__ __forceinline__ bool stopped(const CvArgs& a) {
+    return __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ void fail(const CvArgs& a, int code) {
+    __hip_atomic_store(a.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.ctl, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until every listed granule with on[m] carries `tag`; v[m] gets its
+// value.  Every g[m] must be a valid address, on or not.  Returns false when
+// the launch has been stopped or the wait timed out.
+template <int NG>
+__device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* const (&g)[NG], const bool (&on)[NG],
+                                               unsigned tag, float (&v)[NG], int code) {
+    const u64 t0 = rt_now();
+    for (unsigned spins = 0;; ++spins) {
+        // every address is valid (callers clamp the unused ones), so the loads
+        // are unconditional: all NG in flight at once, no branch around each
+        u64 x[NG];
+#pragma unroll
+        for (int m = 0; m < NG; ++m) x[m] = __hip_atomic_load(g[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < NG; ++m) {
+            v[m] = __uint_as_float((unsigned)x[m]);
+            ok &= !on[m] || (unsigned)(x[m] >> 32) == tag;
+        }
+        if (__all(ok)) return true;
+        if ((spins & 63) == 63) {
+            if (stopped(a)) return false;
+            if ((long long)(rt_now() - t0) > kTimeoutTicks) {
+                fail(a, code);
+                return false;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+constexpr int kTraceIds = 4 * kMaxW + kDecW;
+__device__ __forceinline__ void mark(const CvArgs& a, bool on, long long u, int id, int e) {
+    if (on && u - a.u0 < a.trace_n)
+        a.trace[((size_t)(u - a.u0) * kTraceIds + id) * 4 + e] = __builtin_amdgcn_s_memrealtime();
+}
+
+// One wave of a chain role (UPD, T1, T2, T3): iterates [ub, ue].
+template <int ROLE>
+__device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K, const f4v* qs, float* ysb, int ny,
+                                           u64* hs) {
+    const int N = a.N, M = a.M;
+    const int lane = threadIdx.x & 63, ll = lane & (kL - 1);
+    const int c = g * kL + ll;  // output column (UPD: row side p = 2i + side)
+    const int KB = split_kblocks(K), W = waves_of(KB);
+    const int pk0 = w == 0 ? 0 : kP0 + (w - 1) * kPW;
+    const int pk1 = w == 0 ? kP0 : pk0 + kPW;
+    const int k0 = 4 * pk0 < K ? 4 * pk0 : K, k1 = 4 * pk1 < K ? 4 * pk1 : K;
+    const bool last = (w == W - 1);
+    const u64* rx = (ROLE == kUpd || ROLE == kT1) ? a.ry : (ROLE == kT2 ? a.rtmp : a.rU);
+    const int nx = (ROLE == kUpd || ROLE == kT1) ? N : M;  // ring row length of x (= K)
+    // epilogue constants
+    const int row = c >> 1;
+    const bool upd_live = lane < kL && c < 2 * N;
+    float cst = 0.0f;
+    if (ROLE == kUpd && upd_live) cst = a.fdpn[c];
+    if (ROLE == kT1 && lane < kL && c < M) cst = a.Fp[c];
+    if (ROLE == kT3 && lane < kL && c < N) cst = a.Kp[c];
+    const long long ub = a.u0;
+    const long long ue = ROLE == kUpd ? a.u_prod_end - 1 : a.u_dec_end;
+    float yrow = 0.0f;
+    const bool tr = a.trace && g == 0 && lane == 0;
+    const int tid_ = ROLE * kMaxW + w;
+    for (long long u = ub; u <= ue; ++u) {
+        const unsigned tag = (unsigned)(u + 1);
+        const int slot = (int)(u & (kR - 1));
+        float* ys = ysb + (int)(u & 1) * ny;
+        mark(a, tr, u, tid_, 0);
+        // UPD's last wave: the slot y_{u+1} goes to must be free (issued early, tested after the chain)
+        long long dec_seen = 0;
+        const bool need_bp = ROLE == kUpd && last && u + 1 - kR >= a.u0;
+        if (need_bp) dec_seen = __hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- 1. x of this slice, staged in LDS ----
+        {
+            const gu64* gx = (const gu64*)rx + (size_t)slot * nx;
+            for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
+                const bool own = ROLE == kUpd && last && kb == k0 && row < N;  // y_i for y_next = num/den*y_i (:594)
+                const gu64* gp[5];
+                bool on[5];
+                float v[5] = {};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int k = kb + 64 * m + lane;
+                    on[m] = k < k1;
+                    gp[m] = gx + (on[m] ? k : 0);
+                }
+                on[4] = own;
+                gp[4] = gx + (own ? row : 0);
+                if (!await_granules<5>(a, gp, on, tag, v, 1 + ROLE)) return;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int k = kb + 64 * m + lane;
+                    if (k < k1) ys[k] = v[m];
+                }
+                if (own) yrow = v[4];
+            }
+            // zero y past K up to the slice end (the +0 packets' partners)
+            for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
+        }
+        mark(a, tr, u, tid_, 1);
+        const f4v* qw = qs + (size_t)pk0 * kL + ll;
+        const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
+        float acc = 0.0f;
+        if (w == 0) {
+            // ---- 2/3 (wave 0): the chain starts here, products formed inside it ----
+            __builtin_amdgcn_s_setprio(3);
+            f4v qv[kP0], yv[kP0];
+#pragma unroll
+            for (int j = 0; j < kP0; ++j) {
+                qv[j] = qw[j * kL];
+                yv[j] = yw[j];
+            }
+#pragma unroll
+            for (int j = 0; j < kP0; ++j) {
+                const f4v q = qv[j], y = yv[j];
+                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+                acc += lo.x;  // matrixMultiply :88-100 / updateY2 :608-609, k in order
+                acc += lo.y;
+                acc += hi.x;
+                acc += hi.y;
+            }
+        } else {
+            // ---- 2. products of the slice, ahead of the turn ----
+            f4v prod[kPW];
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) {
+                const f4v q = qw[j * kL];
+                const f4v y = yw[j];
+                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+                prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+            }
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
+            // ---- 3. the running sums of the previous slice, then this slice's adds ----
+            const u64* src = hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll;
+            const u64 t0 = rt_now();
+            u64 h;
+            for (unsigned spins = 0;; ++spins) {
+                h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (__all((unsigned)(h >> 32) == tag)) break;
+                if ((spins & 255) == 255) {
+                    if (stopped(a)) return;
+                    if ((long long)(rt_now() - t0) > kTimeoutTicks) {
+                        fail(a, 10 + ROLE);
+                        return;
+                    }
+                }
+            }
+            acc = __uint_as_float((unsigned)h);
+            mark(a, tr, u, tid_, 2);
+            __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) {
+                acc += prod[j].x;
+                acc += prod[j].y;
+                acc += prod[j].z;
+                acc += prod[j].w;
+            }
+        }
+        asm volatile("" : "+v"(acc));
+        mark(a, tr, u, tid_, 3);
+        if (!last) {
+            if (lane < kL)
+                __hip_atomic_store(hs + ((size_t)slot * kMaxW + w) * kL + ll, granule(tag, acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_s_setprio(0);
+            continue;
+        }
+        __builtin_amdgcn_s_setprio(0);
+        // ---- 4. the last wave's epilogue ----
+        if (ROLE == kUpd) {
+            const float v = acc + 1.0f * cst;    // even lane: num (:611), odd lane: den (:612)
+            const float den = __shfl_xor(v, 1);  // whole wave active
+            if (need_bp && dec_seen < u + 1 - kR) {
+                const u64 t0 = rt_now();
+                for (unsigned spins = 0;; ++spins) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= u + 1 - kR)
+                        break;
+                    if (stopped(a)) return;
+                    if ((spins & 63) == 63 && (long long)(rt_now() - t0) > kTimeoutTicks) {
+                        fail(a, 20);
+                        return;
+                    }
+                }
+            }
+            if (!(c & 1) && upd_live) {
+                const float yn = v / den * yrow;  // updY :594
+                __hip_atomic_store((gu64*)a.ry + (size_t)((u + 1) & (kR - 1)) * N + row, granule(tag + 1, yn),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            mark(a, tr, u, tid_, 3);  // the last wave's "done" is the publication of y_{u+1}
+        } else if (ROLE == kT1) {
+            if (lane < kL && c < M)  // matrixAdd(tmp, Fp, 1) :356
+                __hip_atomic_store((gu64*)a.rtmp + (size_t)slot * M + c, granule(tag, acc + 1.0f * cst),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (lane < kL && c < M + N)  // Y'Qd (computeCost :652)
+                __hip_atomic_store((gu64*)a.rtq + (size_t)slot * N + (c - M), granule(tag, acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else if (ROLE == kT2) {
+            if (lane < kL && c < M)  // U = -U :358
+                __hip_atomic_store((gu64*)a.rU + (size_t)slot * M + c, granule(tag, -acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {  // kT3
+            // compare :334-343 (erc * Kp in double, rounded to float by max())
+            const bool bad = lane < kL && c < N && acc > cst + max_ref((float)(kTol * cst), (float)kTol);
+            if (lane < kL && c >= N && c < N + M)  // U'Qp (computeCost, Jp)
+                __hip_atomic_store((gu64*)a.rtu + (size_t)slot * M + (c - N), granule(tag, acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            const bool any_bad = __any(bad);
+            if (lane == 0)
+                __hip_atomic_store((gu64*)a.rfeas + (size_t)slot * (a.g4 - a.g3) + g,
+                                   granule(tag, any_bad ? 1.0f : 0.0f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Copy a ring row (every granule already carries `tag`) to a plain vector.
+__device__ bool ring_copy(const CvArgs& a, const u64* ring, int n, int slot, unsigned tag, float* out) {
+    const int lane = threadIdx.x & 63;
+    for (int k0 = 0; k0 < n; k0 += 64) {
+        const int k = k0 + lane;
+        const gu64* gp[1] = {(const gu64*)ring + (size_t)slot * n + (k < n ? k : 0)};
+        const bool on[1] = {k < n};
+        float v[1];
+        if (!await_granules<1>(a, gp, on, tag, v, 30)) return false;
+        if (k < n) out[k] = v[0];
+    }
+    return true;
+}
+
+// DEC: waves 1..4 each sum one dot of computeCost (:648-666) per iterate --
+// 1: Fd.Y, 2: (U'Qp).U, 3: Fp.U, 4: (Y'Qd).Y -- in k order on every lane
+// alike (broadcast LDS reads of the products) and hand it to wave 0 through
+// an LDS word; wave 0 gathers the feasibility words of T3 and decides
+// (terminate :673-687, loop control :716-724), so the decision of iterate u
+// overlaps the dots of u + 1.
+__device__ void decide_role(const CvArgs& a, float* lds) {
+    const int N = a.N, M = a.M;
+    const int lane = threadIdx.x & 63, d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nmax = kDecChunk * cdiv_i(N > M ? N : M, kDecChunk);
+    float* pr = lds + (size_t)(d >= 1 && d < kDecW ? d - 1 : 0) * (nmax + 32);  // + 32: prefetch past the end
+    u64* dres = reinterpret_cast<u64*>(lds + (size_t)(kDecW - 1) * (nmax + 32));  // [kR][kDecW] hand-off words
+    for (int e = threadIdx.x; e < kR * kDecW; e += blockDim.x) dres[e] = 0ull;
+    __syncthreads();
+    if (d >= kDecW) return;
+    const bool tr = a.trace && lane == 0;
+    if (d == 0) {
+        SolveState* st = a.st;
+        float Jp = st->Jp, Jd = st->Jd;
+        int have = st->have_costs;
+        const float Md = a.Md[0], Mp = a.Mp[0];
+        const int G3 = a.g4 - a.g3;
+        for (long long u = a.u0; u <= a.u_dec_end; ++u) {
+            const unsigned tag = (unsigned)(u + 1);
+            const int slot = (int)(u & (kR - 1));
+            mark(a, tr, u, 4 * kMaxW, 0);
+            bool bad = false;  // checkFeas (:677): any T3 workgroup with a row over its bound
+            for (int k0 = 0; k0 < G3; k0 += 64) {
+                const int k = k0 + lane;
+                const gu64* gp[1] = {(const gu64*)a.rfeas + (size_t)slot * G3 + (k < G3 ? k : 0)};
+                const bool on[1] = {k < G3};
+                float v[1] = {0.0f};
+                if (!await_granules<1>(a, gp, on, tag, v, 50)) return;
+                bad |= k < G3 && v[0] != 0.0f;
+            }
+            const bool feasible = !__any(bad);
+            mark(a, tr, u, 4 * kMaxW, 1);
+            float s1, s2, s3, s4;
+            {
+                const u64 t0 = rt_now();
+                u64 h = 0;
+                const bool mine = lane >= 1 && lane < kDecW;
+                for (unsigned spins = 0;; ++spins) {
+                    if (mine)
+                        h = __hip_atomic_load(dres + (size_t)slot * kDecW + lane, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (__all(!mine || (unsigned)(h >> 32) == tag)) break;
+                    if ((spins & 255) == 255) {
+                        if (stopped(a)) return;
+                        if ((long long)(rt_now() - t0) > kTimeoutTicks) {
+                            fail(a, 51);
+                            return;
+                        }
+                    }
+                }
+                const float hv = __uint_as_float((unsigned)h);
+                s1 = __shfl(hv, 1);
+                s2 = __shfl(hv, 2);
+                s3 = __shfl(hv, 3);
+                s4 = __shfl(hv, 4);
+            }
+            mark(a, tr, u, 4 * kMaxW, 2);
+            int stop = 0;
+            if (feasible) {
+                Jd = 0.0f;  // computeCost :648-666 (J += 0.5 * tmp[0] in double)
+                Jd = (float)((double)Jd + 0.5 * (double)s4);
+                Jd += s1;
+                Jd += Md / 2;
+                Jp = 0.0f;
+                Jp = (float)((double)Jp + 0.5 * (double)s2);
+                Jp += s3;
+                Jp += Mp / 2;
+                have = 1;
+                stop = 1;  // the three gap tests :681-685
+                if (Jp > -Jd) stop = 0;
+                if ((double)(Jp + Jd) > kTol) stop = 0;
+                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+            }
+            const bool capped = a.cap > 0 && u >= a.cap;
+            if (stop || capped || u == a.u_dec_end) {
+                // finished (y_u, U_u) or the end of this launch's chunk (y_{u+1}, U_u)
+                const bool fin = stop || capped;
+                if (!ring_copy(a, a.ry, N, (int)((fin ? u : u + 1) & (kR - 1)), fin ? tag : tag + 1, a.Yout))
+                    return;
+                if (!ring_copy(a, a.rU, M, slot, tag, a.Uout)) return;
+                if (lane == 0) {
+                    st->h = fin ? u + 1 : u + 2;
+                    st->status = stop ? kStatusDone : (capped ? kStatusCapped : kStatusContinue);
+                    st->Jp = Jp;
+                    st->Jd = Jd;
+                    st->have_costs = have;
+                    __hip_atomic_store(a.ctl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                return;
+            }
+            if (lane == 0) __hip_atomic_store(a.decided, u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            mark(a, tr, u, 4 * kMaxW, 3);
+        }
+        return;
+    }
+    // ---- waves 1..4: one dot each ----
+    const int n = (d == 1 || d == 4) ? N : M;
+    const int nc = kDecChunk * cdiv_i(n, kDecChunk);
+    const u64* ra = d == 4 ? a.rtq : (d == 2 ? a.rtu : nullptr);  // ring operand (or the constant below)
+    const float* fa = d == 1 ? a.Fd : (d == 3 ? a.Fp : nullptr);
+    const u64* rb = (d == 1 || d == 4) ? a.ry : a.rU;
+    for (int k = n + lane; k < nc + 32; k += 64) pr[k] = 0.0f;  // +0 tail: adds nothing to a sum that is never -0
+    float fav[kDecPer];  // the constant operand (Fd, Fp), loaded once
+#pragma unroll
+    for (int m = 0; m < kDecPer; ++m) {
+        const int k = 64 * m + lane;
+        fav[m] = (fa && k < n) ? fa[k] : 0.0f;
+    }
+    for (long long u = a.u0; u <= a.u_dec_end; ++u) {
+        const unsigned tag = (unsigned)(u + 1);
+        const int slot = (int)(u & (kR - 1));
+        mark(a, tr, u, 4 * kMaxW + d, 0);
+        // products into LDS: every granule of the lane in one sweep
+        {
+            const gu64* gp[2 * kDecPer];
+            bool on[2 * kDecPer];
+            float v[2 * kDecPer];
+#pragma unroll
+            for (int m = 0; m < kDecPer; ++m) {
+                const int k = 64 * m + lane;
+                const bool in = k < n;
+                gp[m] = (const gu64*)rb + (size_t)slot * n + (in ? k : 0);
+                on[m] = in;
+                gp[kDecPer + m] = (const gu64*)(ra ? ra : rb) + (size_t)slot * n + (in ? k : 0);
+                on[kDecPer + m] = in && ra != nullptr;
+                v[m] = v[kDecPer + m] = 0.0f;
+            }
+            if (!await_granules<2 * kDecPer>(a, gp, on, tag, v, 40 + d)) return;
+#pragma unroll
+            for (int m = 0; m < kDecPer; ++m) {
+                const int k = 64 * m + lane;
+                if (k < n) pr[k] = (ra ? v[kDecPer + m] : fav[m]) * v[m];
+            }
+        }
+        mark(a, tr, u, 4 * kMaxW + d, 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // :652-657, k in order.  Chunks of kDecChunk terms, each fully unrolled
+        // (a loop back-edge waits for every read in flight); the reads run two
+        // groups of 16 ahead of the adds.
+        float acc = 0.0f;
+        const f4v* p4 = reinterpret_cast<const f4v*>(pr);
+        for (int c4 = 0; c4 < nc / 4; c4 += kDecChunk / 4) {
+            f4v R[3][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                R[0][j] = p4[c4 + j];
+                R[1][j] = p4[c4 + 4 + j];
+            }
+#pragma unroll
+            for (int gi = 0; gi < kDecChunk / 16; ++gi) {
+                if (gi + 2 < kDecChunk / 16) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) R[(gi + 2) % 3][j] = p4[c4 + 4 * (gi + 2) + j];
+                }
+                asm volatile("" : "+v"(acc)::"memory");  // the reads issue before the adds
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc += R[gi % 3][j].x;
+                    acc += R[gi % 3][j].y;
+                    acc += R[gi % 3][j].z;
+                    acc += R[gi % 3][j].w;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        mark(a, tr, u, 4 * kMaxW + d, 2);
+        if (lane == 0)
+            __hip_atomic_store(dres + (size_t)slot * kDecW + d, granule(tag, acc), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+__global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (b >= a.g4) {
+        decide_role(a, lds);
+        return;
+    }
+    const int role = b < a.g1 ? kUpd : (b < a.g2 ? kT1 : (b < a.g3 ? kT2 : kT3));
+    const int g = b - (role == kUpd ? 0 : role == kT1 ? a.g1 : role == kT2 ? a.g2 : a.g3);
+    const int K = (role == kUpd || role == kT1) ? a.N : a.M;
+    const f4v* src = role == kUpd ? a.SPu : role == kT1 ? a.A1 : role == kT2 ? a.A2 : a.A3;
+    const int KB = split_kblocks(K), W = waves_of(KB), KP = packets_of(W);
+    const int Kmax = a.N > a.M ? a.N : a.M, KPmax = packets_of(waves_of(split_kblocks(Kmax)));
+    f4v* qs = reinterpret_cast<f4v*>(lds);                 // [KP][32] this workgroup's packets
+    float* ysb = lds + (size_t)KPmax * kL * 4;             // [2][4 KPmax] x by iterate parity
+    u64* hs = reinterpret_cast<u64*>(ysb + 2 * KPmax * 4);  // [kR][kMaxW][32] hand-off words
+    {
+        const f4v* s = src + (size_t)g * KB * kL;
+        for (int e = tid; e < KP * kL; e += blockDim.x) qs[e] = (e < KB * kL) ? s[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int e = tid; e < kR * kMaxW * kL; e += blockDim.x) hs[e] = 0ull;
+    }
+    __syncthreads();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (w >= W) return;
+    const int ny = KPmax * 4;
+    switch (role) {
+        case kUpd: chain_wave<kUpd>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kT1: chain_wave<kT1>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kT2: chain_wave<kT2>(a, g, w, K, qs, ysb, ny, hs); break;
+        default: chain_wave<kT3>(a, g, w, K, qs, ysb, ny, hs); break;
+    }
+}
+
+// packets of stage columns [col0, col0 + ncols): column j of the job is
+// A[k][j] = trans ? src[j * ld + k] : src[k * ld + j], k < K (+0 beyond)
+__global__ void __launch_bounds__(256) k_pack_cols(const float* __restrict__ src, int ld, int trans, int K,
+                                                   int ncols, int col0, int KB, f4v* __restrict__ dst) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (kb, j), j fastest
+    if (e >= (long long)KB * ncols) return;
+    const int kb = (int)(e / ncols), j = (int)(e % ncols);
+    float v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int k = 4 * kb + t;
+        v[t] = k < K ? (trans ? src[(size_t)j * ld + k] : src[(size_t)k * ld + j]) : 0.0f;
+    }
+    const int c = col0 + j;
+    dst[((size_t)(c / kL) * KB + kb) * kL + (c % kL)] = f4v{v[0], v[1], v[2], v[3]};
+}
+
+// ring slot of y_{u0} <- Y, control words for a launch
+__global__ void k_converge_init(const float* __restrict__ Y, int N, long long u0, u64* ry, int* ctl,
+                                long long* decided, int* err) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = t; k < N; k += gridDim.x * blockDim.x)
+        ry[(size_t)(u0 & (kR - 1)) * N + k] = granule((unsigned)(u0 + 1), Y[k]);
+    if (t == 0) {
+        *ctl = 0;
+        *err = 0;
+        *decided = u0 - 1;
+    }
+}
+
+}  // namespace
+
+int g_converge_persist_off = 0;
+unsigned long long* g_converge_trace = nullptr;
+int g_converge_trace_n = 0;
+
+// Geometry of the launch for (N, M); 0 when it does not apply.
+int converge_persist_wgs(int N, int M, int* g) {
+    if (N < 1 || M < 1 || N > 1024 || M > 1024) return 0;
+    const int g1 = cdiv_i(2 * N, kL);
+    const int g2 = g1 + cdiv_i(N + M, kL);
+    const int g3 = g2 + cdiv_i(M, kL);
+    const int g4 = g3 + cdiv_i(N + M, kL);
+    if (g) {
+        g[0] = g1;
+        g[1] = g2;
+        g[2] = g3;
+        g[3] = g4;
+    }
+    return g4 + 1;
+}
+
+size_t converge_persist_lds_bytes(int N, int M) {
+    const int Kmax = N > M ? N : M;
+    const int KPmax = packets_of(waves_of(split_kblocks(Kmax)));
+    const size_t chain = sizeof(float) * ((size_t)KPmax * kL * 4 + (size_t)2 * KPmax * 4) + sizeof(u64) * kR * kMaxW * kL;
+    const size_t dec = sizeof(float) * (size_t)(kDecW - 1) * (kDecChunk * cdiv_i(Kmax, kDecChunk) + 32) +
+                       sizeof(u64) * kR * kDecW;
+    return chain > dec ? chain : dec;
+}
+
+size_t converge_ring_words(int N, int M) {
+    int g[4];
+    converge_persist_wgs(N, M, g);
+    return (size_t)kR * (2 * (size_t)N + 3 * (size_t)M + (size_t)(g[3] - g[2]));
+}
+
+size_t converge_stage_floats(int N, int M, int stage) {
+    int g[4];
+    converge_persist_wgs(N, M, g);
+    const int KBn = split_kblocks(N), KBm = split_kblocks(M);
+    switch (stage) {
+        case 1: return (size_t)(g[1] - g[0]) * KBn * kL * 4;
+        case 2: return (size_t)(g[2] - g[1]) * KBm * kL * 4;
+        default: return (size_t)(g[3] - g[2]) * KBm * kL * 4;
+    }
+}
+
+// Build the three stage packet arrays (buffers zeroed by the caller).
+hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Qinv, const float* Qp, int N, int M,
+                                float* A1, float* A2, float* A3, hipStream_t s) {
+    const int KBn = split_kblocks(N), KBm = split_kblocks(M);
+    auto pack = [&](const float* src, int ld, int trans, int K, int KB, int ncols, int col0, float* dst) {
+        const long long n = (long long)KB * ncols;
+        hipLaunchKernelGGL(k_pack_cols, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, ld, trans, K, ncols,
+                           col0, KB, reinterpret_cast<f4v*>(dst));
+    };
+    pack(Gp, M, 0, N, KBn, M, 0, A1);       // tmp = Gp'Y   (:354): A[k][j] = Gp[k][j]
+    pack(Qd, N, 0, N, KBn, N, M, A1);       // Y'Qd         (:652): A[k][j] = Qd[k][j]
+    pack(Qinv, M, 1, M, KBm, M, 0, A2);     // Qp_inv tmp   (:357): A[k][i] = Qp_inv[i][k]
+    pack(Gp, M, 1, M, KBm, N, 0, A3);       // Gp U         (:636): A[k][i] = Gp[i][k]
+    pack(Qp, M, 0, M, KBm, M, N, A3);       // U'Qp         (:652): A[k][j] = Qp[k][j]
+    return hipGetLastError();
+}
+
+hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s) {
+    int g[4];
+    const int G = converge_persist_wgs(L.N, L.M, g);
+    if (G == 0) return hipErrorInvalidValue;
+    u64* ring = static_cast<u64*>(L.rings);
+    CvArgs a{};
+    a.N = L.N;
+    a.M = L.M;
+    a.g1 = g[0];
+    a.g2 = g[1];
+    a.g3 = g[2];
+    a.g4 = g[3];
+    a.u0 = L.u0;
+    a.cap = L.cap;
+    long long dec_end = L.u0 + L.chunk - 1;
+    if (L.cap > 0 && dec_end > L.cap) dec_end = L.cap;
+    a.u_dec_end = dec_end;
+    a.u_prod_end = (L.cap > 0 && dec_end == L.cap) ? dec_end : dec_end + 1;
+    a.SPu = reinterpret_cast<const f4v*>(L.SP);
+    a.A1 = reinterpret_cast<const f4v*>(L.A1);
+    a.A2 = reinterpret_cast<const f4v*>(L.A2);
+    a.A3 = reinterpret_cast<const f4v*>(L.A3);
+    a.fdpn = L.fdpn;
+    a.Fp = L.Fp;
+    a.Kp = L.Kp;
+    a.Fd = L.Fd;
+    a.Md = L.Md;
+    a.Mp = L.Mp;
+    a.ry = ring;
+    a.rtmp = a.ry + (size_t)kR * L.N;
+    a.rtq = a.rtmp + (size_t)kR * L.M;
+    a.rU = a.rtq + (size_t)kR * L.N;
+    a.rtu = a.rU + (size_t)kR * L.M;
+    a.rfeas = a.rtu + (size_t)kR * L.M;
+    a.st = L.st;
+    a.ctl = L.ctl;
+    a.decided = L.decided;
+    a.err = L.err;
+    a.Yout = L.Y;
+    a.Uout = L.U;
+    a.trace = g_converge_trace;
+    a.trace_n = g_converge_trace_n;
+    hipError_t e = hipMemsetAsync(ring, 0, sizeof(u64) * converge_ring_words(L.N, L.M), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_converge_init, dim3(4), dim3(256), 0, s, L.Y, L.N, L.u0, a.ry, L.ctl, L.decided, L.err);
+    const int W = waves_of(split_kblocks(L.N > L.M ? L.N : L.M));
+    const int threads = 64 * (W > kDecW ? W : kDecW);
+    hipLaunchKernelGGL(k_converge_persist, dim3(G), dim3(threads), converge_persist_lds_bytes(L.N, L.M), s, a);
+    return hipGetLastError();
+}
+
+}  // namespace pqp

@@ -135,6 +135,34 @@ hipError_t launch_wide_init(SolveState* st, int* flag, long long* cap, long long
 hipError_t launch_gauss_jordan_wide(const float* A, float* aug, int* perm, float* res, int n, hipStream_t s);
 constexpr int kGaussJordanWideMin = 64;  // n from which one matrix is inverted over many workgroups
 
+// ---- converge mode of one problem with N, M <= 1024 as ONE persistent,
+// pipelined launch (pqp_converge.hip): update and terminate() stages as
+// concurrent roles exchanging tagged granules
+struct ConvergeLaunch {
+    int N, M;
+    long long u0;     // iterate the launch starts from (its y in Y)
+    long long chunk;  // iterates decided per launch at most
+    long long cap;    // max_updates (<= 0: none)
+    const float *SP, *A1, *A2, *A3;  // update packets (k_build_split, lw = 32) and stage packets
+    const float *fdpn, *Fp, *Kp, *Fd, *Md, *Mp;
+    void* rings;      // converge_ring_words() 8-byte words
+    SolveState* st;
+    int* ctl;
+    long long* decided;
+    int* err;
+    float *Y, *U;     // in: y_{u0}; out: the final (or next launch's) iterate, U of the last terminate()
+};
+int converge_persist_wgs(int N, int M, int* g);  // workgroups of the launch (0: not applicable)
+size_t converge_persist_lds_bytes(int N, int M);
+size_t converge_ring_words(int N, int M);
+size_t converge_stage_floats(int N, int M, int stage);  // stage 1..3 packet arrays
+hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Qinv, const float* Qp, int N, int M,
+                                float* A1, float* A2, float* A3, hipStream_t s);
+hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s);
+extern int g_converge_persist_off;
+extern unsigned long long* g_converge_trace;  // tuning: [iterate][29][4] words (pqp_tune_converge_trace)
+extern int g_converge_trace_n;
+
 void set_variant(int v);
 int get_variant();
 hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,

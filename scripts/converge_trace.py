@@ -1,0 +1,95 @@
+"""Timeline of the persistent converge launch (pqp_converge.hip) on one
+synthetic problem: s_memrealtime marks (100 MHz, chip-wide) of workgroup 0 of
+every role, per iterate and wave: start, inputs staged, turn (running sums in;
+DEC: its dot summed), done.  Prints medians over steady-state iterates in us:
+each wave's period and phases, and the hand-over latencies between roles."""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+
+ROLES = ("UPD", "T1", "T2", "T3")
+
+
+def waves_of(K):
+    KB = (K + 3) // 4
+    return 1 if KB <= 24 else 1 + (KB - 24 + 47) // 48
+
+
+def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
+    import numpy as np
+    import torch
+
+    import pqp_amd
+
+    M = N // 2
+    pb = pqp_amd.ProblemBatch.synthetic(1, 0, 1, N, M)
+    P = pb.problem(0)
+    del pb
+    L = pqp_amd.lib()
+    tr = torch.zeros(n_trace * 29 * 4, dtype=torch.int64, device="cuda")
+    with pqp_amd.Problem(P) as prob:
+        prob.solve(max_updates=cap)
+        L.pqp_tune_converge_trace(pqp_amd.C.c_void_p(tr.data_ptr()), n_trace)
+        r = prob.solve(max_updates=cap)
+        L.pqp_tune_converge_trace(None, 0)
+    torch.cuda.synchronize()
+    t = tr.cpu().numpy().reshape(n_trace, 29, 4).astype(np.float64) / 100.0  # us
+    lo, hi = n_trace // 3, n_trace - 10
+    W = {"UPD": waves_of(N), "T1": waves_of(N), "T2": waves_of(M), "T3": waves_of(M)}
+    med = lambda x: float(np.median(x))
+    out = {"n_dual": N, "m": M, "h": r["h"], "iterates": [lo, hi], "roles": {}}
+    for ri, role in enumerate(ROLES):
+        for w in range(W[role]):
+            i = ri * 6 + w
+            x = t[lo:hi, i]
+            out["roles"][f"{role}.w{w}"] = {
+                "period": med(np.diff(t[lo:hi + 1, i, 0])), "stage": med(x[:, 1] - x[:, 0]),
+                "turn_wait": med(x[:, 2] - x[:, 1]) if w else 0.0, "adds": med(x[:, 3] - x[:, 2]) if w else
+                med(x[:, 3] - x[:, 1])}
+    x = t[lo:hi, 24]
+    out["roles"]["DEC.w0 (decision)"] = {"period": med(np.diff(t[lo:hi + 1, 24, 0])),
+                                         "feasibility": med(x[:, 1] - x[:, 0]), "dots_wait": med(x[:, 2] - x[:, 1]),
+                                         "decide": med(x[:, 3] - x[:, 2])}
+    for d in range(1, 5):
+        i = 24 + d
+        x = t[lo:hi, i]
+        out["roles"][f"DEC.w{d}"] = {"period": med(np.diff(t[lo:hi + 1, i, 0])), "gather": med(x[:, 1] - x[:, 0]),
+                                     "sum": med(x[:, 2] - x[:, 1])}
+    lastw = lambda role: ROLES.index(role) * 6 + W[role] - 1
+    u = np.arange(lo, hi)
+    out["handover"] = {
+        "UPD done u -> UPD.w0 staged u+1": med(t[u + 1, 0, 1] - t[u, lastw("UPD"), 3]),
+        "UPD done u -> T1.w0 staged u+1": med(t[u + 1, 6, 1] - t[u, lastw("UPD"), 3]),
+        "T1 done u -> T2.w0 staged u": med(t[u, 12, 1] - t[u, lastw("T1"), 3]),
+        "T2 done u -> T3.w0 staged u": med(t[u, 18, 1] - t[u, lastw("T2"), 3]),
+        "T3 done u -> DEC.w2 gathered u": med(t[u, 26, 1] - t[u, lastw("T3"), 3]),
+        "T1 done u -> DEC.w4 gathered u": med(t[u, 28, 1] - t[u, lastw("T1"), 3]),
+        "DEC decided u": med(t[u, 24, 3] - t[u, lastw("UPD"), 3]),
+        "y_u published -> DEC decided u (latency)": med(t[u, 24, 3] - t[u - 1, lastw("UPD"), 3]),
+        "DEC decided u-8 -> y_u published": med(t[u - 1, lastw("UPD"), 3] - t[u - 8, 24, 3]),
+        "UPD ahead of DEC (iterates)": med(np.searchsorted(t[:, lastw("UPD"), 3], t[u, 24, 3]) - u),
+    }
+    # absolute timeline of a few iterates, relative to DEC's decision of u - 8
+    # (the decision that lets y_u be published)
+    sample = {}
+    for uu in range(lo, lo + 4):
+        base = t[uu - 8, 24, 3]
+        ev = {"y_u published (UPD last wave)": t[uu - 1, lastw("UPD"), 3],
+              "T1.w0 staged": t[uu, 6, 1], "T1 last done": t[uu, lastw("T1"), 3],
+              "T2.w0 staged": t[uu, 12, 1], "T2 last done": t[uu, lastw("T2"), 3],
+              "T3.w0 staged": t[uu, 18, 1], "T3 last done": t[uu, lastw("T3"), 3],
+              "DEC.w4 gathered": t[uu, 28, 1], "DEC.w4 summed": t[uu, 28, 2], "DEC.w2 summed": t[uu, 26, 2],
+              "DEC.w0 feasibility": t[uu, 24, 1], "DEC.w0 dots in": t[uu, 24, 2],
+              "DEC decided": t[uu, 24, 3]}
+        sample[f"u={uu}"] = {k: round(float(v - base), 2) for k, v in ev.items()}
+    out["timeline_from_decision_u-8"] = sample
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*(int(a) for a in sys.argv[1:]))
