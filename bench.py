@@ -25,7 +25,7 @@ Extra keys:
                 workgroup each, converge mode with device-side terminate()
   single_n1024  configs[2]: one n_dual=1024 problem, 1000 fixed iterations
   single_converge  the same problem size in the reference's converge mode
-                (terminate() before every update), capped at 200 updates
+                (terminate() before every update), capped at 2000 updates
   rowshard      one large problem (n_dual = 16384) row-sharded over the job's
                 ranks: per update, every rank updates its
                 rows and an RCCL all-gather assembles y (all ranks take part)
@@ -255,10 +255,10 @@ def iters_to_tol_bench(pqp_amd, problems: dict) -> dict:
     return out
 
 
-def single_converge_bench(pqp_amd, N: int = 1024, updates: int = 200) -> dict:
+def single_converge_bench(pqp_amd, N: int = 1024, updates: int = 2000) -> dict:
     """One synthetic problem (primal, Qp and duals built on the device) in
-    converge mode: terminate() + updateY2 per iteration over many
-    workgroups.  The synthetic problems do not meet the reference's exact
+    converge mode: terminate() + updateY2 per iteration, as one persistent
+    pipelined launch.  The synthetic problems do not meet the reference's exact
     gap test at this size, so the solve is capped."""
     pb = pqp_amd.ProblemBatch.synthetic(1, 0, 1, N)
     P = pb.problem(0)
@@ -270,7 +270,8 @@ def single_converge_bench(pqp_amd, N: int = 1024, updates: int = 200) -> dict:
         dt = time.perf_counter() - t0
     return {"n_dual": N, "m": N // 2, "iterations": r["h"], "converged": bool(r["converged"]),
             "ms_per_solve": dt * 1e3, "us_per_iter": dt / r["h"] * 1e6, "iter_per_s": r["h"] / dt,
-            "note": "terminate() as multi-workgroup mat-vecs + relay update, hipGraph-replayed (pqp_wide.hip)"}
+            "note": "one persistent pipelined launch (pqp_converge.hip): the update and terminate()'s stages as "
+                    "concurrent workgroup roles, terminate(Y_u) beside the update to Y_{u+1}"}
 
 
 def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: int) -> dict:

@@ -32,11 +32,12 @@ int pqp_tune_set_variant(int variant);
  * relay update (one launch per update).  Returns the previous setting. */
 int pqp_tune_persist(int off);
 
-/* Converge mode of one problem with n_dual, M <= 1024 that goes over many
- * workgroups runs as ONE persistent pipelined launch (pqp_converge.hip:
- * terminate(Y_u) beside the update to Y_{u+1}) unless off = 1, which sends it
- * through the graph-replayed launch chain of pqp_wide.hip.  Returns the
- * previous setting. */
+/* Converge mode of one problem with n_dual, M <= 1024 (other than the N, M <= 32
+ * problems of the one-wave solver) runs as ONE persistent pipelined launch
+ * (pqp_converge.hip: terminate(Y_u) beside the update to Y_{u+1}) unless
+ * off = 1, which restores the launch-per-step routing (one-workgroup solvers
+ * below pqp_tune_wide_min_n, the graph-replayed chain of pqp_wide.hip above).
+ * Returns the previous setting. */
 int pqp_tune_converge_persist(int off);
 
 /* Iterates one persistent converge launch decides at most before the host
@@ -68,10 +69,12 @@ int pqp_tune_wave_pipe_max_b(int b);
  * received, chain done}.  updates = 0 turns the trace off. */
 int pqp_tune_persist_trace(void *d_trace, int updates);
 
-/* Converge-mode solves of problems with n_dual >= n run over many workgroups
- * (terminate() as multi-workgroup mat-vecs + the relay update, replayed from a
- * hipGraph) instead of one persistent workgroup; n <= 0 sends every size
- * there, LDS-sized problems included.  Default 384.  Returns the previous
+/* Converge-mode solves of problems with n_dual >= n that the persistent
+ * launch above does not take (n_dual or M > 1024, or pqp_tune_converge_persist(1))
+ * run over many workgroups (terminate() as multi-workgroup mat-vecs + the
+ * relay update, replayed from a hipGraph) instead of one persistent workgroup;
+ * n <= 0 sends every size there, LDS-sized problems included (where they fit,
+ * those go on to the persistent launch).  Default 384.  Returns the previous
  * value. */
 int pqp_tune_wide_min_n(int n);
 

@@ -682,8 +682,14 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
                 hipStream_t s) {
     const int N = P.N, M = P.M;
     if (mode == kModeFixed && !P.small && !g_force_single && !resume) return problem_run_fixed_split(P, num_iter, out, s);
-    if (mode == kModeConverge && !g_force_single && !resume && N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0))
-        return problem_run_wide(P, max_updates, out, s);
+    if (mode == kModeConverge && !g_force_single && !resume) {
+        // the one-wave solver stays fastest for N, M <= 32 (0.65 us per iteration
+        // at 32/16 against 2.3 on the persistent launch); from n_dual 48 up the
+        // persistent launch wins (scripts/converge_crossover.py)
+        const bool tiny = N <= 32 && M <= 32 && !g_force_small;
+        if (!tiny && converge_persist_fits(N, M)) return problem_run_converge_persist(P, max_updates, out, s);
+        if (N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0)) return problem_run_wide(P, max_updates, out, s);
+    }
     if (!P.small) PQP_TRY(ensure_single(P, s));
     SolveState& st = *P.hst;
     st = SolveState{};
