@@ -59,6 +59,7 @@ constexpr int kR = 8;      // ring depth (iterates in flight)
 constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
 constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
 constexpr int kDecChunk = 256;  // dot terms per unrolled chunk
+constexpr int kDecAhead = 4;    // groups of 16 terms read ahead of the adds
 constexpr long long kTimeoutTicks = 200000000LL;  // s_memrealtime at 100 MHz: 2 s
 enum Role : int { kUpd = 0, kT1 = 1, kT2 = 2, kT3 = 3, kDec = 4 };
 
@@ -475,30 +476,31 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // :652-657, k in order.  Chunks of kDecChunk terms, each fully unrolled
-        // (a loop back-edge waits for every read in flight); the reads run two
-        // groups of 16 ahead of the adds.
+        // (a loop back-edge waits for every read in flight); the reads run
+        // kDecAhead groups of 16 ahead of the adds.
         float acc = 0.0f;
         const f4v* p4 = reinterpret_cast<const f4v*>(pr);
         for (int c4 = 0; c4 < nc / 4; c4 += kDecChunk / 4) {
-            f4v R[3][4];
+            f4v R[kDecAhead + 1][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                R[0][j] = p4[c4 + j];
-                R[1][j] = p4[c4 + 4 + j];
+            for (int g0 = 0; g0 < kDecAhead; ++g0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) R[g0][j] = p4[c4 + 4 * g0 + j];
             }
 #pragma unroll
             for (int gi = 0; gi < kDecChunk / 16; ++gi) {
-                if (gi + 2 < kDecChunk / 16) {
+                if (gi + kDecAhead < kDecChunk / 16) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) R[(gi + 2) % 3][j] = p4[c4 + 4 * (gi + 2) + j];
+                    for (int j = 0; j < 4; ++j)
+                        R[(gi + kDecAhead) % (kDecAhead + 1)][j] = p4[c4 + 4 * (gi + kDecAhead) + j];
                 }
                 asm volatile("" : "+v"(acc)::"memory");  // the reads issue before the adds
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    acc += R[gi % 3][j].x;
-                    acc += R[gi % 3][j].y;
-                    acc += R[gi % 3][j].z;
-                    acc += R[gi % 3][j].w;
+                    acc += R[gi % (kDecAhead + 1)][j].x;
+                    acc += R[gi % (kDecAhead + 1)][j].y;
+                    acc += R[gi % (kDecAhead + 1)][j].z;
+                    acc += R[gi % (kDecAhead + 1)][j].w;
                 }
             }
         }
