@@ -237,6 +237,7 @@ struct pqp_problem {
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
     pqp::DevBuf SPp, fdpnp, gran, perr;              // persistent fixed mode: split matrices (lw = 32), y granules, error word
     int split_lw = 0;                                // lanes per workgroup SP was built with
+    bool split_lean = false;                         // SP holds Qd packets (k_lean_relay), not the split matrices
     hipGraphExec_t graph = nullptr;                  // captured fixed-mode updates (the remainder)
     long long graph_updates = -1;
     hipGraphExec_t chunk_graph = nullptr;            // captured fixed-mode chunk of kFixedChunk updates
@@ -268,6 +269,7 @@ struct pqp_problem {
 // One row block of a large problem's stored split matrices (pqp_rowblock_*).
 struct pqp_rowblock {
     int N = 0, row0 = 0, rows = 0, lw = 64;
+    bool lean = false;  // SP holds Qd packets (k_lean_relay), fdpn the {Fdn, Fdp, Theta, 0} words
     pqp::DevBuf SP, fdpn;
 };
 
@@ -333,24 +335,45 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 // from P.Y instead of Y = 1000 (used by the terminate() drop-in, mode 2).
 // Fixed mode of a large problem: one multi-workgroup launch per update
 // (k_split_update), the stored split matrices built once per problem.
-// The stored split matrices of the whole problem (rows 0..N-1) with lw row
-// sides per workgroup, built on first use (and rebuilt if lw changes).
+// Lanes per workgroup of the relay update of an n_dual = N problem: row sides
+// of the stored split matrices, or rows of Qd for the lean relay.
+int pick_lw(int N) { return use_lean(N) ? lean_pick_lw(N) : split_pick_lw(N); }
+
+// The relay update's operand of the whole problem (rows 0..N-1), built on
+// first use (and rebuilt if lw or the layout changes): the stored split
+// matrices with lw row sides per workgroup, or, from n_dual >= g_lean_min_n,
+// Qd itself with lw rows per workgroup (k_lean_relay, half the bytes).
 int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
     const int N = P.N;
-    if (P.SP.p && P.split_lw == lw) return PQP_OK;
+    const bool lean = use_lean(N);
+    if (P.SP.p && P.split_lw == lw && P.split_lean == lean) return PQP_OK;
     if (split_lds_bytes(N) > kLdsBudget)
         return set_error(PQP_ERR_ARG, "multi-workgroup solve: N=%d needs more than %zu B of LDS", N, kLdsBudget);
     if (!P.theta.p) {  // small problems skip the large-path setup of problem_finish
         PQP_TRY(P.theta.floats(N));
         PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
     }
-    PQP_TRY(P.SP.floats(split_floats(N, N, lw)));
-    PQP_TRY(P.fdpn.floats((size_t)2 * N));
     PQP_TRY(P.Yb.floats(N));
-    PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N, lw), s));
-    PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
+    if (lean) {
+        PQP_TRY(P.SP.floats(lean_floats(N, N, lw)));
+        PQP_TRY(P.fdpn.floats(lean_aux_floats(N, lw)));
+        PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * lean_floats(N, N, lw), s));
+        PQP_HIP(launch_build_lean(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
+    } else {
+        PQP_TRY(P.SP.floats(split_floats(N, N, lw)));
+        PQP_TRY(P.fdpn.floats((size_t)2 * N));
+        PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * split_floats(N, N, lw), s));
+        PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
+    }
     P.split_lw = lw;
+    P.split_lean = lean;
     return PQP_OK;
+}
+
+// One relay update of the whole problem, a -> b, over the operand ensure_split built.
+hipError_t problem_update(pqp_problem& P, int lw, const float* a, float* b, hipStream_t s, const int* gate = nullptr) {
+    return P.split_lean ? launch_lean_update(P.SP.f(), P.fdpn.f(), P.N, P.N, 0, lw, a, b, s, gate)
+                        : launch_split_update(P.SP.f(), P.fdpn.f(), P.N, P.N, 0, lw, a, b, s, gate);
 }
 
 // Capture `n` dependent updates P.Y -> P.Yb -> P.Y ... into *exec (plus a
@@ -367,7 +390,7 @@ static int capture_updates(pqp_problem& P, int lw, long long n, hipGraphExec_t* 
     float* b = P.Yb.f();
     hipError_t e = hipSuccess;
     for (long long u = 0; u < n && e == hipSuccess; ++u) {
-        e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, a, b, s);
+        e = problem_update(P, lw, a, b, s);
         std::swap(a, b);
     }
     if (e == hipSuccess && a != P.Y.f()) e = hipMemcpyAsync(P.Y.p, a, sizeof(float) * N, hipMemcpyDeviceToDevice, s);
@@ -440,9 +463,9 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     const int N = P.N;
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
     if (!g_persist_off && N <= persist_max_n()) return problem_run_fixed_persist(P, updates, out, s);
-    const int lw = split_pick_lw(N);
+    const int lw = pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
-    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8);
+    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8) | ((int)use_lean(N) << 16);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
         P.chunk_ready = false;
@@ -563,7 +586,7 @@ constexpr int kWideFirstChunk = 2;  // the first replay of a solve
 int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
     const int N = P.N, M = P.M;
     if (converge_persist_fits(N, M)) return problem_run_converge_persist(P, max_updates, out, s);
-    const int lw = split_pick_lw(N);
+    const int lw = pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
     if (!P.QinvT.p) {
         PQP_TRY(P.QinvT.floats((size_t)M * M));
@@ -580,7 +603,8 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     int* flag = static_cast<int*>(P.wflag.p);
     long long* cap = static_cast<long long*>(P.wcap.p);
-    const long long key = ((long long)g_wide_flags << 16) ^ ((long long)g_split_kind << 8) ^ lw;  // cap: device word
+    const long long key = ((long long)use_lean(N) << 24) ^ ((long long)g_wide_flags << 16) ^
+                          ((long long)g_split_kind << 8) ^ lw;  // cap: device word
     if (!P.wgraph || P.wgraph_key != key) {
         if (P.wgraph) {
             (void)hipGraphExecDestroy(P.wgraph);
@@ -602,8 +626,7 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
             if (fork) {
                 e = hipEventRecord(P.ev_fork, s);
                 if (e == hipSuccess) e = hipStreamWaitEvent(P.side, P.ev_fork, 0);
-                if (e == hipSuccess) e = launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, cur, nxt, P.side,
-                                                             &dst->status);
+                if (e == hipSuccess) e = problem_update(P, lw, cur, nxt, P.side, &dst->status);
                 if (e == hipSuccess) e = hipEventRecord(P.ev_join, P.side);
                 if (e != hipSuccess) return e;
             }
@@ -626,7 +649,7 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
                              N, M, cap};
             if ((e = launch_wide_decide(w, s)) != hipSuccess) return e;
             if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join the update branch
-            return launch_split_update(P.SP.f(), P.fdpn.f(), N, N, 0, lw, cur, nxt, s, &dst->status);
+            return problem_update(P, lw, cur, nxt, s, &dst->status);
         };
         // two graphs: a short first chunk (problems that stop within a few
         // iterations do not pay for a long chunk of no-op launches), then
@@ -1056,12 +1079,23 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
     if (rows > 0) {
         DevBuf theta;
         PQP_TRY(theta.floats(rows));
-        b->lw = split_pick_lw(rows);
-        PQP_TRY(b->SP.floats(split_floats(N, rows, b->lw)));
-        PQP_TRY(b->fdpn.floats((size_t)2 * rows));
-        PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * split_floats(N, rows, b->lw), s));
+        b->lean = use_lean(N);
         PQP_HIP(launch_theta_rows(d_Qd_rows, ld, N, rows, theta.f(), s));
-        PQP_HIP(launch_build_split(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->lw, b->SP.f(), b->fdpn.f(), s));
+        if (b->lean) {  // Qd rows themselves (k_lean_relay): half the bytes of the split matrices
+            b->lw = lean_pick_lw(rows);
+            PQP_TRY(b->SP.floats(lean_floats(N, rows, b->lw)));
+            PQP_TRY(b->fdpn.floats(lean_aux_floats(rows, b->lw)));
+            PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * lean_floats(N, rows, b->lw), s));
+            PQP_HIP(launch_build_lean(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->lw, b->SP.f(), b->fdpn.f(),
+                                      s));
+        } else {
+            b->lw = split_pick_lw(rows);
+            PQP_TRY(b->SP.floats(split_floats(N, rows, b->lw)));
+            PQP_TRY(b->fdpn.floats((size_t)2 * rows));
+            PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * split_floats(N, rows, b->lw), s));
+            PQP_HIP(launch_build_split(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->lw, b->SP.f(),
+                                       b->fdpn.f(), s));
+        }
         PQP_HIP(hipStreamSynchronize(s));  // theta is freed on return
     }
     *out = b.release();
@@ -1070,8 +1104,11 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
 
 int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void* stream) {
     if (!b || !d_Y || (b->rows > 0 && !d_Y_rows)) return set_error(PQP_ERR_ARG, "pqp_rowblock_update: null argument");
-    PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows,
-                                static_cast<hipStream_t>(stream)));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (b->lean)
+        PQP_HIP(launch_lean_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s));
+    else
+        PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s));
     return PQP_OK;
 }
 
@@ -1553,6 +1590,12 @@ extern "C" int pqp_tune_persist_trace(void* d_trace, int updates) {
     pqp::g_persist_trace = updates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
     pqp::g_persist_trace_n = updates;
     return PQP_OK;
+}
+
+extern "C" int pqp_tune_lean_min_n(int n) {
+    const int old = pqp::g_lean_min_n;
+    pqp::g_lean_min_n = n;
+    return old;
 }
 
 extern "C" int pqp_tune_converge_persist(int off) {

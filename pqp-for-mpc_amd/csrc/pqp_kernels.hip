@@ -563,6 +563,185 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_lean_relay<W,S>: the relay update over Qd itself (4 B per entry) instead of
+// the stored split matrices (8 B): half the bytes for problems whose update is
+// HBM-bound (n_dual >= 8192; below that forming the terms -- two compares and
+// two selects per k against one packed multiply per packet -- costs more than
+// the bytes saved).  One lane owns one ROW and keeps both sums, num
+// and den, as the two halves of one packed accumulator: the chain is one
+// v_pk_add_f32 per k (each half rounds exactly like the scalar add), so it
+// issues like the split form's single add.  The terms are formed ahead of the
+// turn: off the diagonal the lean form
+//   den += (q < 0) ? 0*y : q*y ;   num += (q > 0) ? 0*y : -(q*y)
+// (bit-identical to (max(0,+-q) + 0.0f) * y, DESIGN.md "Lean form"); in the
+// one or two segments that hold this workgroup's diagonal, the reference's
+// literal (max(0,+-q) + (k == i ? Theta_i : +0)) * y for every k.
+// Layout LP[wg][kb][lw] packets of 4 k of row wg*lw + lane; aux[row] =
+// {Fdn, Fdp, Theta, 0}.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_build_lean(const float* __restrict__ Qd, int ld,
+                                                    const float* __restrict__ theta, const float* __restrict__ Fd,
+                                                    int N, int rows, int row0, int lw, float* __restrict__ LP,
+                                                    float* __restrict__ aux) {
+    const int KB = split_kblocks(N);
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (i, k), k fastest
+    if (e < (long long)rows * 4 * KB) {
+        const int i = (int)(e / (4 * KB)), k = (int)(e % (4 * KB));
+        const size_t at = (((size_t)(i / lw) * KB + (k >> 2)) * lw + (i % lw)) * 4 + (k & 3);
+        LP[at] = k < N ? Qd[(size_t)i * ld + k] : 0.0f;
+    }
+    if (e < rows) {
+        const float fd = Fd[row0 + e];
+        aux[4 * e + 0] = max_ref(0.0f, -fd);  // Fdn :704
+        aux[4 * e + 1] = max_ref(0.0f, fd);   // Fdp :703
+        aux[4 * e + 2] = theta[e];            // computeTheta :503-519
+        aux[4 * e + 3] = 0.0f;
+    }
+}
+
+template <int W, int S>
+__global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__ LP, const float* __restrict__ aux,
+                                                       int N, int rows, int row0, int lw,
+                                                       const float* __restrict__ Yin, float* __restrict__ Yout,
+                                                       const int* __restrict__ gate) {
+    if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
+    // LDS: [2][64] hand-off words (num, den), then y [4*G*S]
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds);
+    float* ys = lds + 256;
+    const int KB = split_kblocks(N);
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ll = lane % lw;  // lanes >= lw repeat lane % lw's row and are discarded
+    const int r = blockIdx.x * lw + ll;
+    const bool live = lane < lw && r < rows;
+    const int G = (KB + S - 1) / S;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const float* region = LP + (size_t)blockIdx.x * KB * lw * 4;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * lw * 16, 0x00020000);
+    const int vo = ll * 16, kstride = lw * 16;
+    f4v q[S];
+    const bool lane_loads = lane < lw;
+    auto load_seg = [&](int g) {
+        const int nj = KB - g * S;  // wave-uniform; packets past KB are +0 and not loaded
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+            q[j] = (j < nj && lane_loads) ? __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (g * S + j) * kstride, 0)
+                                          : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    };
+    if (w < G) load_seg(w);
+    const f4v ax = live ? *reinterpret_cast<const f4v*>(aux + 4 * (size_t)r) : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    {
+        const int t = threadIdx.x, n_lds = 4 * G * S;
+        for (int b = 0; b < n_lds; b += 64 * W * 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = b + 64 * W * j + t;
+                v[j] = (k < N) ? Yin[k] : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = b + 64 * W * j + t;
+                if (k < n_lds) ys[k] = v[j];
+            }
+        }
+        if (w == 0) slot[lane] = slot[64 + lane] = 0ull;  // segment 0 starts from +0.0f
+    }
+    __syncthreads();
+    const int d0 = row0 + blockIdx.x * lw;  // the workgroup's first diagonal k (wave-uniform)
+    const int diag = row0 + r;              // this lane's diagonal k
+    const float th = ax.z;
+    f2v acc = f2v{0.0f, 0.0f};  // .x num, .y den
+    f2v T[4 * S];               // per k: {num term, den term}, an adjacent register pair for v_pk_add_f32
+    for (int g = w; g < G; g += W) {
+        const int kbase = 4 * g * S;
+        const bool lit = kbase < d0 + lw && kbase + 4 * S > d0;  // a diagonal of this workgroup is in here
+#pragma unroll
+        for (int j0 = 0; j0 < S; j0 += 4) {
+            f4v y[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) y[u] = *reinterpret_cast<const f4v*>(ys + 4 * (g * S + j0 + u));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u;
+                const float qv[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+                const float yv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float qq = qv[c], yy = yv[c];
+                    float dn, nm;
+                    if (!lit) {
+                        const float p = qq * yy;
+                        const float z = 0.0f * yy;  // (+0)*y: NaN for inf/NaN y
+                        dn = qq < 0.0f ? z : p;
+                        nm = qq > 0.0f ? z : -p;
+                    } else {  // computeQdp/Qdn_theta :524-537, then :608-609
+                        const float t = (kbase + 4 * j + c == diag) ? th : 0.0f;
+                        dn = (max_ref(0.0f, qq) + t) * yy;
+                        nm = (max_ref(0.0f, -qq) + t) * yy;
+                    }
+                    T[4 * j + c] = f2v{nm, dn};
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) asm volatile("" : "+v"(T[4 * j0 + u]));
+        }
+        // q is free once the terms are formed: the next segment's packets are
+        // in flight during the turn wait and the adds
+        if (g + W < G) load_seg(g + W);
+        unsigned long long hn, hd;
+        for (int spin = 0;; ++spin) {
+            hn = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            hd = __hip_atomic_load(slot + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__all((int)(hn >> 32) == g && (int)(hd >> 32) == g) || spin > (1 << 20)) break;
+        }
+        __builtin_amdgcn_s_setprio(3);
+        acc = f2v{__uint_as_float((unsigned)hn), __uint_as_float((unsigned)hd)};
+#pragma unroll
+        for (int k = 0; k < 4 * S; ++k) acc += T[k];  // :608-609, k in order; both sums in one packed add
+        __hip_atomic_store(slot + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc.x),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(slot + 64 + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc.y),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_s_setprio(0);
+    }
+    if (w == (G - 1) % W && live) {
+        const float num = acc.x + 1.0f * ax.x;  // matrixAdd(num, Fdn, 1) :611
+        const float den = acc.y + 1.0f * ax.y;  // matrixAdd(den, Fdp, 1) :612
+        Yout[r] = num / den * ys[row0 + r];     // updY :594
+    }
+}
+
+int g_lean_min_n = 8192;  // tuning: smallest n_dual whose relay update streams Qd (lean) instead of the split matrices
+bool use_lean(int N) { return g_lean_min_n > 0 && N >= g_lean_min_n; }
+size_t lean_floats(int N, int rows, int lw) { return (size_t)cdiv(rows, lw) * split_kblocks(N) * lw * 4; }
+size_t lean_aux_floats(int rows, int lw) { return (size_t)cdiv(rows, lw) * lw * 4; }
+int lean_pick_lw(int rows) {
+    int lw = 8;  // about one workgroup per CU: rows / lw ~ 256
+    while (lw < 64 && rows > 256LL * lw) lw *= 2;
+    return lw;
+}
+hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows, int row0,
+                             int lw, float* LP, float* aux, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_build_lean, dim3(cdiv((long long)rows * 4 * split_kblocks(N), 256)), dim3(256), 0, s, Qd,
+                       ld, theta, Fd, N, rows, row0, lw, LP, aux);
+    return hipGetLastError();
+}
+hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows, int row0, int lw, const float* Yin,
+                              float* Yout, hipStream_t s, const int* gate) {
+    if (rows <= 0) return hipSuccess;
+    constexpr int W = 8, S = 16;
+    const int G = (split_kblocks(N) + S - 1) / S;
+    const size_t lds = sizeof(float) * ((size_t)4 * G * S + 256);
+    hipLaunchKernelGGL((k_lean_relay<W, S>), dim3(cdiv(rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows, row0, lw,
+                       Yin, Yout, gate);
+    return hipGetLastError();
+}
+
 int g_split_u = 0;  // tuning: k_split_update stage depth (0: 16, 1: 8, 2: 24)
 size_t split_floats(int N, int rows, int lw) { return (size_t)split_wgs(rows, lw) * split_kblocks(N) * lw * 4; }
 // LDS of the split updates (the full y, padded to a whole relay segment of up

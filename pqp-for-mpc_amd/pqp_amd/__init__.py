@@ -90,6 +90,7 @@ SIGNATURES = {
     "pqp_tune_wide_min_n": (C.c_int, [C.c_int]),
     "pqp_tune_persist": (C.c_int, [C.c_int]),
     "pqp_tune_converge_persist": (C.c_int, [C.c_int]),
+    "pqp_tune_lean_min_n": (C.c_int, [C.c_int]),
     "pqp_tune_converge_chunk": (C.c_int, [C.c_int]),
     "pqp_tune_converge_trace": (C.c_int, [_vp, C.c_int]),
     "pqp_tune_wave_min_b": (C.c_int, [C.c_int]),

@@ -66,10 +66,11 @@ def _gfx950_asm(name: str) -> str:
 @pytest.mark.parametrize("src,pattern,min_kernels", [
     ("pqp_kernels.hip",
      r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|14k_split_update|12k_fixed_tiny"
-     r"|12k_solve_wave)",
-     33),
+     r"|12k_solve_wave|12k_lean_relay)",
+     34),
     ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 3),
     ("pqp_persist.hip", r"_ZN3pqp15k_split_persist", 1),
+    ("pqp_converge.hip", r"_ZN3pqp12_GLOBAL__N_118k_converge_persist", 1),
 ])
 def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
     """The update and terminate() kernels must not contract a*b+c into FMA
