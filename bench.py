@@ -303,8 +303,15 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t[0]) / updates
     y = solver.Y[:N]
+    L = pqp_amd.lib()
+    lean_min = L.pqp_tune_lean_min_n(0)  # read the setting (and restore it)
+    L.pqp_tune_lean_min_n(lean_min)
+    lean = 0 < lean_min <= N
+    bpe = 4 if lean else 8  # bytes per matrix entry the update streams
     out = {"n_dual": N, "ranks": world, "rows_per_rank": R, "updates": updates, "us_per_update": dt * 1e6,
-           "iter_per_s": 1.0 / dt, "alg_GBps_split_matrices": 8.0 * N * N / dt / 1e9,
+           "iter_per_s": 1.0 / dt,
+           "layout": "Qd packets, k_lean_relay (4 B/entry)" if lean else "stored split matrices (8 B/entry)",
+           "alg_GBps": bpe * N * N / dt / 1e9,
            "finite_nonneg": bool(torch.isfinite(y).all().item()) and bool((y >= 0).all().item()),
            "note": "eager launches (pqp_rowblock_update + RCCL all_gather_into_tensor per update at N>1 ranks)"}
     del solver, blk
