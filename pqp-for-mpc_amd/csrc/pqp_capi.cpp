@@ -1079,7 +1079,10 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
     if (rows > 0) {
         DevBuf theta;
         PQP_TRY(theta.floats(rows));
-        b->lean = use_lean(N);
+        // by the block's row count: the lean update's cost grows with N per
+        // row block whatever its rows (its terms are formed along the whole
+        // chain), the bytes it saves with rows x N
+        b->lean = use_lean(rows);
         PQP_HIP(launch_theta_rows(d_Qd_rows, ld, N, rows, theta.f(), s));
         if (b->lean) {  // Qd rows themselves (k_lean_relay): half the bytes of the split matrices
             b->lw = lean_pick_lw(rows);

@@ -20,6 +20,8 @@
 // k*ldq + i) so that at a fixed k a wave's 64 lanes x 4 rows read 1 KiB of
 // contiguous HBM with one global_load_dwordx4 each (fully coalesced), while
 // y[k] is a wave-uniform LDS broadcast.
+#include <type_traits>
+
 #include "pqp_device.h"
 #include "pqp_launch.h"
 
@@ -565,10 +567,10 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
 
 // ---------------------------------------------------------------------------
 // k_lean_relay<W,S>: the relay update over Qd itself (4 B per entry) instead of
-// the stored split matrices (8 B): half the bytes for problems whose update is
-// HBM-bound (n_dual >= 8192; below that forming the terms -- two compares and
-// two selects per k against one packed multiply per packet -- costs more than
-// the bytes saved).  One lane owns one ROW and keeps both sums, num
+// the stored split matrices (8 B): half the bytes for row blocks whose update
+// is HBM-bound (>= 8192 rows; below that forming the terms -- two compares and
+// two selects per k along the whole chain, against one packed multiply per
+// packet for the split form -- costs more than the bytes saved).  One lane owns one ROW and keeps both sums, num
 // and den, as the two halves of one packed accumulator: the chain is one
 // v_pk_add_f32 per k (each half rounds exactly like the scalar add), so it
 // issues like the split form's single add.  The terms are formed ahead of the
@@ -659,36 +661,53 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
     for (int g = w; g < G; g += W) {
         const int kbase = 4 * g * S;
         const bool lit = kbase < d0 + lw && kbase + 4 * S > d0;  // a diagonal of this workgroup is in here
+        // the branch is per segment, each side one straight-line unrolled loop
+        auto form = [&](auto literal) {
+            // distinct volatile markers keep the two sides from being merged
+            // back into a branch per k
+            if constexpr (decltype(literal)::value)
+                asm volatile("; literal terms");
+            else
+                asm volatile("; lean terms");
 #pragma unroll
-        for (int j0 = 0; j0 < S; j0 += 4) {
-            f4v y[4];
+            for (int j0 = 0; j0 < S; j0 += 4) {
+                f4v y[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) y[u] = *reinterpret_cast<const f4v*>(ys + 4 * (g * S + j0 + u));
+                for (int u = 0; u < 4; ++u) y[u] = *reinterpret_cast<const f4v*>(ys + 4 * (g * S + j0 + u));
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = j0 + u;
-                const float qv[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-                const float yv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+                for (int u = 0; u < 4; ++u) {
+                    const int j = j0 + u;
+                    const float qv[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+                    const float yv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float qq = qv[c], yy = yv[c];
-                    float dn, nm;
-                    if (!lit) {
-                        const float p = qq * yy;
-                        const float z = 0.0f * yy;  // (+0)*y: NaN for inf/NaN y
-                        dn = qq < 0.0f ? z : p;
-                        nm = qq > 0.0f ? z : -p;
-                    } else {  // computeQdp/Qdn_theta :524-537, then :608-609
-                        const float t = (kbase + 4 * j + c == diag) ? th : 0.0f;
-                        dn = (max_ref(0.0f, qq) + t) * yy;
-                        nm = (max_ref(0.0f, -qq) + t) * yy;
+                    for (int c = 0; c < 4; ++c) {
+                        const float qq = qv[c], yy = yv[c];
+                        float dn, nm;
+                        if constexpr (!decltype(literal)::value) {
+                            const float p = qq * yy;
+                            const float z = 0.0f * yy;  // (+0)*y: NaN for inf/NaN y
+                            dn = qq < 0.0f ? z : p;
+                            nm = qq > 0.0f ? z : -p;
+                        } else {  // computeQdp/Qdn_theta :524-537, then :608-609
+                            const float t = (kbase + 4 * j + c == diag) ? th : 0.0f;
+                            dn = (max_ref(0.0f, qq) + t) * yy;
+                            nm = (max_ref(0.0f, -qq) + t) * yy;
+                        }
+                        T[4 * j + c] = f2v{nm, dn};
                     }
-                    T[4 * j + c] = f2v{nm, dn};
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) asm volatile("" : "+v"(T[4 * j0 + u]));
-        }
+                for (int u = 0; u < 16; ++u) asm volatile("" : "+v"(T[4 * j0 + u]));
+            }
+            if constexpr (decltype(literal)::value)
+                asm volatile("; literal terms end");
+            else
+                asm volatile("; lean terms end");
+        };
+        if (lit)
+            form(std::true_type{});
+        else
+            form(std::false_type{});
         // q is free once the terms are formed: the next segment's packets are
         // in flight during the turn wait and the adds
         if (g + W < G) load_seg(g + W);
