@@ -32,6 +32,12 @@ int pqp_tune_set_variant(int variant);
  * relay update (one launch per update).  Returns the previous setting. */
 int pqp_tune_persist(int off);
 
+/* Fixed mode of N <= 32 problems (k_fixed_tiny): launches of at most b
+ * problems keep the iterate in registers (y_k on lane 2k, broadcast by
+ * v_readlane), larger ones exchange it through LDS (fewer VALU instructions
+ * when problems share SIMDs).  Default 1024.  Returns the previous value. */
+int pqp_tune_fixed_rl_max_b(int b);
+
 /* The relay update of one large problem (fixed mode above n_dual 1024, the
  * converge graph chain) streams Qd itself (k_lean_relay: 4 B per entry, the
  * split terms formed in registers) instead of the stored split matrices

@@ -1570,6 +1570,12 @@ extern "C" int pqp_tune_set_variant(int variant) {
     return old;
 }
 
+extern "C" int pqp_tune_fixed_rl_max_b(int b) {
+    const int old = pqp::g_fixed_rl_max_b;
+    pqp::g_fixed_rl_max_b = b;
+    return old;
+}
+
 extern "C" int pqp_tune_wave_min_b(int b) {
     const int old = pqp::g_wave_min_b;
     pqp::g_wave_min_b = b;

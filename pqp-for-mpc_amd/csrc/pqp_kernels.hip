@@ -1802,9 +1802,10 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A0, SolveState* __
 // sequential adds, the num/den exchange by a DPP lane swap (not an LDS
 // permute), the division.  The iterate's own y_i is read at the top of the
 // update so its latency hides under the chain.  One wave: a ds_write followed
-// by the next update's ds_reads needs no workgroup barrier.
+// by the next update's ds_reads needs no workgroup barrier.  RL: the iterate
+// never leaves the registers -- y_k on lane 2k, broadcast by v_readlane.
 // ---------------------------------------------------------------------------
-template <int NMAX>
+template <int NMAX, bool RL>
 __global__ void __launch_bounds__(64) k_fixed_tiny(SolveArgs A0, SolveState* __restrict__ st0) {
     const SolveArgs A = problem_at(A0, blockIdx.x);
     SolveState* st = st0 + blockIdx.x;
@@ -1842,7 +1843,44 @@ __global__ void __launch_bounds__(64) k_fixed_tiny(SolveArgs A0, SolveState* __r
     long long done_here = 0;
     int cb = 0;
     int status = kStatusContinue;
+    if constexpr (RL) {
+        // the iterate stays in registers: y_k on lane 2k, broadcast to every
+        // lane by v_readlane (wave-uniform, SGPRs) -- no LDS round trip and no
+        // barrier between updates
+        float yk = (!side && row) ? ybuf[0][i] : 0.0f;
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        for (;;) {
+            if (h >= A.num_iter) {  // while(h < NUM_ITER)
+                status = kStatusDone;
+                break;
+            }
+            if (done_here >= A.chunk) break;
+            const float yi = __shfl(yk, 2 * ic);  // this row's y_i on both of its lanes
+            float p[NMAX];
+#pragma unroll
+            for (int k = 0; k < NMAX; k += 2) {
+                const float y0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yk), 2 * k));
+                const float y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yk), 2 * k + 2));
+                const f2v pr = f2v{mat[k], mat[k + 1]} * f2v{y0, y1};
+                p[k] = pr.x;
+                p[k + 1] = pr.y;
+            }
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < NMAX; ++k) acc += p[k];  // :608-609, k in order
+            const float v = acc + 1.0f * fd_own;        // even lane: num (:611), odd lane: den (:612)
+            const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+            const float yn = v / den * yi;              // :594
+            yk = (!side && row) ? yn : 0.0f;            // lanes past 2N hold +0 (the padding y_k)
+            ++h;
+            ++done_here;
+        }
+        if (!side && row) ybuf[0][i] = yk;
+        cb = 0;
+        __syncthreads();
+    }
     for (;;) {
+        if constexpr (RL) break;
         if (h >= A.num_iter) {  // while(h < NUM_ITER)
             status = kStatusDone;
             break;
@@ -2178,17 +2216,23 @@ static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads
 }
 
 int g_fixed_tiny_old = 0;  // tuning: fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
+int g_fixed_rl_max_b = 1024;  // tuning: largest batch whose k_fixed_tiny keeps y in registers (RL; 16384 bundled problems: 2.47 ms vs 1.76 through LDS)
+template <bool RL>
+static void launch_fixed_tiny(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    if (a.N <= 8) hipLaunchKernelGGL((k_fixed_tiny<8, RL>), dim3(B), dim3(64), 0, s, a, st);
+    else if (a.N <= 16) hipLaunchKernelGGL((k_fixed_tiny<16, RL>), dim3(B), dim3(64), 0, s, a, st);
+    else if (a.N <= 24) hipLaunchKernelGGL((k_fixed_tiny<24, RL>), dim3(B), dim3(64), 0, s, a, st);
+    else if (a.N <= 28) hipLaunchKernelGGL((k_fixed_tiny<28, RL>), dim3(B), dim3(64), 0, s, a, st);
+    else hipLaunchKernelGGL((k_fixed_tiny<32, RL>), dim3(B), dim3(64), 0, s, a, st);
+}
 int g_wave_min_b = 1;  // tuning: converge mode of N, M <= 32 on k_solve_wave from this many problems on
 
 static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the
     // sequential chain is the critical path, so keep the padding small
     if (a.mode == kModeFixed && !g_fixed_tiny_old) {
-        if (a.N <= 8) hipLaunchKernelGGL((k_fixed_tiny<8>), dim3(B), dim3(64), 0, s, a, st);
-        else if (a.N <= 16) hipLaunchKernelGGL((k_fixed_tiny<16>), dim3(B), dim3(64), 0, s, a, st);
-        else if (a.N <= 24) hipLaunchKernelGGL((k_fixed_tiny<24>), dim3(B), dim3(64), 0, s, a, st);
-        else if (a.N <= 28) hipLaunchKernelGGL((k_fixed_tiny<28>), dim3(B), dim3(64), 0, s, a, st);
-        else hipLaunchKernelGGL((k_fixed_tiny<32>), dim3(B), dim3(64), 0, s, a, st);
+        if (B <= g_fixed_rl_max_b) launch_fixed_tiny<true>(B, a, st, s);
+        else launch_fixed_tiny<false>(B, a, st, s);
         return hipGetLastError();
     }
     if (a.mode == kModeConverge && B >= g_wave_min_b && a.N + a.M < 64) {  // many problems: one wave each

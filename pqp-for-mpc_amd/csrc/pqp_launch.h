@@ -101,6 +101,7 @@ extern int g_split_u;        // tuning: k_split_update stage depth selector
 extern int g_split_kind;     // tuning: relay / stream kernel selector
 extern int g_split_lw;       // tuning: lanes per workgroup override (0 = auto)
 extern int g_fixed_tiny_old; // tuning: fixed mode of tiny problems on k_solve_tiny
+extern int g_fixed_rl_max_b; // tuning: largest batch whose k_fixed_tiny keeps the iterate in registers
 extern int g_wave_pipe_max_b; // tuning: largest batch whose k_solve_wave launch is the software-pipelined form
 extern int g_wave_min_b;     // tuning: smallest batch whose converge-mode tiny solves run one wave per problem
 // batched forms: grid = B problems (states st[0..B-1])

@@ -94,6 +94,7 @@ SIGNATURES = {
     "pqp_tune_converge_chunk": (C.c_int, [C.c_int]),
     "pqp_tune_converge_trace": (C.c_int, [_vp, C.c_int]),
     "pqp_tune_wave_min_b": (C.c_int, [C.c_int]),
+    "pqp_tune_fixed_rl_max_b": (C.c_int, [C.c_int]),
     "pqp_tune_wave_pipe_max_b": (C.c_int, [C.c_int]),
     "pqp_tune_persist_trace": (C.c_int, [_vp, C.c_int]),
     "pqp_tune_wide_flags": (C.c_int, [C.c_int]),
