@@ -222,6 +222,7 @@ struct SolveOut {
     long long h = 0;
     float Jp = NAN, Jd = NAN;
     int have_costs = 0, last_stop = 0, status = 0;
+    bool staged = false;  // Y (and U) already copied to the problem's pinned staging buffer
 };
 
 }  // namespace
@@ -254,6 +255,7 @@ struct pqp_problem {
     int graph_variant = -1;                          // g_split_u the graph was captured with
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
+    float* hio = nullptr;                            // pinned staging of Y (N floats) then U (M floats)
     ~pqp_problem() {
         if (graph) (void)hipGraphExecDestroy(graph);
         if (chunk_graph) (void)hipGraphExecDestroy(chunk_graph);
@@ -263,6 +265,7 @@ struct pqp_problem {
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (side) (void)hipStreamDestroy(side);
         if (hst) (void)hipHostFree(hst);
+        if (hio) (void)hipHostFree(hio);
     }
 };
 
@@ -292,6 +295,7 @@ int problem_finish(pqp_problem& P, hipStream_t s) {
     PQP_TRY(P.state.alloc(sizeof(SolveState)));
     PQP_HIP(hipMemsetAsync(P.U.p, 0, sizeof(float) * M, s));
     if (!P.hst) PQP_HIP(hipHostMalloc((void**)&P.hst, sizeof(SolveState), hipHostMallocDefault));
+    if (!P.hio) PQP_HIP(hipHostMalloc((void**)&P.hio, sizeof(float) * ((size_t)N + M), hipHostMallocDefault));
     if (!P.small) {  // Theta for the large paths (computeTheta, PQP_CPU.c:503-519)
         PQP_TRY(P.theta.floats(N));
         PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
@@ -751,10 +755,15 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
             PQP_HIP(launch_solve_small(a, dst, s));
         else
             PQP_HIP(launch_solve_single(a, dst, s));
+        // Y and U ride with the state readback (pinned, one sync per launch);
+        // the copies of the launch that finishes are the ones that stand
+        PQP_HIP(hipMemcpyAsync(P.hio, P.Y.p, sizeof(float) * N, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipMemcpyAsync(P.hio + N, P.U.p, sizeof(float) * M, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
         if (st.status != kStatusContinue) break;
     }
+    out.staged = true;
     out.h = st.h;
     out.status = st.status;
     out.have_costs = st.have_costs;
@@ -822,9 +831,14 @@ int pqp_problem_solve(pqp_problem* P, int mode, long long num_iter, long long ma
     SolveOut o;
     PQP_TRY(problem_run(*P, mode == PQP_MODE_CONVERGE ? kModeConverge : kModeFixed, num_iter, max_updates, false, o,
                         s));
-    PQP_TRY(download(Y, P->Y.p, P->N, s));
-    if (U && mode == PQP_MODE_CONVERGE) PQP_TRY(download(U, P->U.p, P->M, s));
-    PQP_HIP(hipStreamSynchronize(s));
+    const bool want_u = U && mode == PQP_MODE_CONVERGE;
+    if (!o.staged) {  // through the pinned staging buffer: one sync, no pageable DMA
+        PQP_HIP(hipMemcpyAsync(P->hio, P->Y.p, sizeof(float) * P->N, hipMemcpyDeviceToHost, s));
+        if (want_u) PQP_HIP(hipMemcpyAsync(P->hio + P->N, P->U.p, sizeof(float) * P->M, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+    }
+    std::memcpy(Y, P->hio, sizeof(float) * P->N);
+    if (want_u) std::memcpy(U, P->hio + P->N, sizeof(float) * P->M);
     if (h_out) *h_out = o.h;
     if (Jp_out) *Jp_out = o.Jp;
     if (Jd_out) *Jd_out = o.Jd;
