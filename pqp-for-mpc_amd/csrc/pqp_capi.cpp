@@ -40,27 +40,38 @@ inline int round4(int n) { return (n + 3) & ~3; }
 // RAII device allocation.
 struct DevBuf {
     void* p = nullptr;
+    size_t bytes_ = 0;
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
+    // (re)allocate; a buffer of the same size is kept (same address: no
+    // hipMalloc/hipFree pair, and graphs captured over it stay valid)
     int alloc(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (p && bytes == bytes_) return PQP_OK;
         if (p) {
             (void)hipFree(p);
             p = nullptr;
+            bytes_ = 0;
         }
-        if (bytes == 0) bytes = 16;
         hipError_t e = hipMalloc(&p, bytes);
         if (e != hipSuccess) {
             p = nullptr;
             return set_error(PQP_ERR_ALLOC, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
         }
+        bytes_ = bytes;
         return PQP_OK;
     }
     int floats(size_t n) { return alloc(n * sizeof(float)); }
     float* f() const { return static_cast<float*>(p); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes_ = 0;
+    }
 };
 
 // Verify that the current device is a gfx950 (the only code object we ship).
@@ -256,6 +267,9 @@ struct pqp_problem {
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     float* hio = nullptr;                            // pinned staging of Y (N floats) then U (M floats)
+    size_t hio_floats = 0;
+    float* hin = nullptr;                            // pinned staging of small problems' inputs
+    size_t hin_floats = 0;
     ~pqp_problem() {
         if (graph) (void)hipGraphExecDestroy(graph);
         if (chunk_graph) (void)hipGraphExecDestroy(chunk_graph);
@@ -266,6 +280,7 @@ struct pqp_problem {
         if (side) (void)hipStreamDestroy(side);
         if (hst) (void)hipHostFree(hst);
         if (hio) (void)hipHostFree(hio);
+        if (hin) (void)hipHostFree(hin);
     }
 };
 
@@ -295,7 +310,13 @@ int problem_finish(pqp_problem& P, hipStream_t s) {
     PQP_TRY(P.state.alloc(sizeof(SolveState)));
     PQP_HIP(hipMemsetAsync(P.U.p, 0, sizeof(float) * M, s));
     if (!P.hst) PQP_HIP(hipHostMalloc((void**)&P.hst, sizeof(SolveState), hipHostMallocDefault));
-    if (!P.hio) PQP_HIP(hipHostMalloc((void**)&P.hio, sizeof(float) * ((size_t)N + M), hipHostMallocDefault));
+    if (P.hio_floats < (size_t)N + M) {
+        if (P.hio) (void)hipHostFree(P.hio);
+        P.hio = nullptr;
+        P.hio_floats = 0;
+        PQP_HIP(hipHostMalloc((void**)&P.hio, sizeof(float) * ((size_t)N + M), hipHostMallocDefault));
+        P.hio_floats = (size_t)N + M;
+    }
     if (!P.small) {  // Theta for the large paths (computeTheta, PQP_CPU.c:503-519)
         PQP_TRY(P.theta.floats(N));
         PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
@@ -317,11 +338,65 @@ int ensure_single(pqp_problem& P, hipStream_t s) {
     return PQP_OK;
 }
 
+// Drop everything derived from a problem's data (built on first use by the
+// solve paths): called before new data goes into an existing handle.
+void problem_reset_derived(pqp_problem& P) {
+    for (DevBuf* b : {&P.QdT, &P.theta, &P.SP, &P.fdpn, &P.Yb, &P.SPp, &P.fdpnp, &P.gran, &P.perr, &P.QinvT, &P.GpT,
+                      &P.tM, &P.tq, &P.tu, &P.gu, &P.wflag, &P.wcap, &P.CA1, &P.CA2, &P.CA3, &P.crings, &P.cwords})
+        b->reset();
+    for (hipGraphExec_t* g : {&P.graph, &P.chunk_graph, &P.wgraph, &P.wgraph_first})
+        if (*g) {
+            (void)hipGraphExecDestroy(*g);
+            *g = nullptr;
+        }
+    P.split_lw = 0;
+    P.split_lean = false;
+    P.graph_updates = -1;
+    P.chunk_ready = false;
+    P.graph_variant = -1;
+    P.wgraph_key = -1;
+}
+
 int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float* md, const float* qp,
                    const float* qinv, const float* fp, const float* mp, const float* gp, const float* kp, int N, int M,
                    hipStream_t s) {
+    if (P.Qd.p) {  // new data into an existing handle
+        PQP_HIP(hipStreamSynchronize(s));
+        problem_reset_derived(P);
+    }
     P.N = N;
     P.M = M;
+    const size_t nn = (size_t)N * N, mm = (size_t)M * M, nm = (size_t)N * M;
+    const size_t total = nn + N + 1 + 2 * mm + M + 1 + nm + N;
+    if (total <= (size_t)1 << 18) {
+        // small problems: every input through one pinned staging buffer, so
+        // the nine H2D copies are asynchronous DMA instead of pageable copies
+        if (P.hin_floats < total) {
+            if (P.hin) (void)hipHostFree(P.hin);
+            P.hin = nullptr;
+            P.hin_floats = 0;
+            PQP_HIP(hipHostMalloc((void**)&P.hin, sizeof(float) * total, hipHostMallocDefault));
+            P.hin_floats = total;
+        }
+        float* h = P.hin;
+        auto put = [&](DevBuf& d, const float* src, size_t n) -> int {
+            std::memcpy(h, src, sizeof(float) * n);
+            PQP_TRY(d.floats(n));
+            PQP_HIP(hipMemcpyAsync(d.p, h, sizeof(float) * n, hipMemcpyHostToDevice, s));
+            h += n;
+            return PQP_OK;
+        };
+        PQP_TRY(put(P.Qd, qd, nn));
+        PQP_TRY(put(P.Fd, fd, N));
+        PQP_TRY(put(P.Md, md, 1));
+        PQP_TRY(put(P.Qp, qp, mm));
+        PQP_TRY(put(P.Qinv, qinv, mm));
+        PQP_TRY(put(P.Fp, fp, M));
+        PQP_TRY(put(P.Mp, mp, 1));
+        PQP_TRY(put(P.Gp, gp, nm));
+        PQP_TRY(put(P.Kp, kp, N));
+        return problem_finish(P, s);
+    }
     PQP_TRY(upload(P.Qd, qd, (size_t)N * N, s));
     PQP_TRY(upload(P.Fd, fd, N, s));
     PQP_TRY(upload(P.Md, md, 1, s));
@@ -853,6 +928,9 @@ int pqp_problem_destroy(pqp_problem* P) {
     return PQP_OK;
 }
 
+static std::mutex g_oneshot_mu;        // guards g_oneshot (taken before g_mu)
+static pqp_problem* g_oneshot = nullptr;  // cached handle of pqp_solve_dual's tiny problems
+
 int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
                    const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
                    long long num_iter, long long max_updates, float* Y, float* U, long long* h_out,
@@ -860,6 +938,24 @@ int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const floa
     if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
         return set_error(PQP_ERR_ARG, "pqp_solve_dual: unknown mode %d", mode);
     if (!Y) return set_error(PQP_ERR_ARG, "pqp_solve_dual: null Y");
+    if (N >= 1 && M >= 1 && N <= 32 && M <= 32) {
+        // the one-shot form of tiny problems (the reference's own call
+        // pattern, solveQuadraticDual per solve) reuses one cached handle: its
+        // buffers are re-filled in place (no allocations), and these problems
+        // build no derived per-problem data a new Qd could leave stale
+        std::lock_guard<std::mutex> lk(g_oneshot_mu);
+        if (!g_oneshot) {
+            PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &g_oneshot));
+        } else {
+            if (!Qd || !Fd || !Md || !Qp || !Qp_inv || !Fp || !Mp || !Gp || !Kp)
+                return set_error(PQP_ERR_ARG, "pqp_solve_dual: null input");
+            std::lock_guard<std::mutex> lk2(g_mu);
+            PQP_TRY(ensure_device());
+            hipStream_t s = lib_stream();
+            PQP_TRY(problem_upload(*g_oneshot, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
+        }
+        return pqp_problem_solve(g_oneshot, mode, num_iter, max_updates, Y, U, h_out, Jp_out, Jd_out);
+    }
     pqp_problem* P = nullptr;
     PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &P));
     const int rc = pqp_problem_solve(P, mode, num_iter, max_updates, Y, U, h_out, Jp_out, Jd_out);

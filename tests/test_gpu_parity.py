@@ -546,3 +546,26 @@ def test_pqp_update_host_vs_golden(gpu_lib, golden_bundled):
     for h in range(1, 10):
         Y = gpu_lib.update(g["Qd"], g["theta"], g["Fd"], Y, N)
     assert_bitwise(Y, g["Y_h10"], "9 updates via pqp_update_host")
+
+
+def test_oneshot_tiny_problems_back_to_back(gpu_lib, orc, golden_bundled):
+    """pqp_solve_dual on tiny problems re-fills one cached handle: solves of
+    different problems and sizes in a row (growing and shrinking N and M)
+    each give the reference's h, Y and U."""
+    g = golden_bundled
+    bundled = {k: np.ascontiguousarray(g[k], dtype=np.float32) for k in
+               ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    bundled.update(N=int(g["N"]), M=int(g["M"]))
+    cases = [bundled, orc.synth_problem(3, 0, 8, 4), orc.synth_problem(4, 1, 32, 16), bundled,
+             orc.synth_problem(5, 2, 16, 8)]
+    for j, P in enumerate(cases):
+        for mode in (gpu_lib.MODE_CONVERGE, gpu_lib.MODE_FIXED):
+            r = gpu_lib.solve_dual(P, mode=mode, num_iter=50, max_updates=3000)
+            if mode == gpu_lib.MODE_CONVERGE:
+                h, Y, U = orc.solve(P, max_updates=3000)
+                assert r["h"] == abs(h), (j, r["h"], h)
+                assert_bitwise(r["U"], U, f"case {j} U")
+            else:
+                Y = orc.iterate(P["Qd"], P["Fd"], int(P["N"]), 49)
+                assert r["h"] == 50
+            assert_bitwise(r["Y"], Y, f"case {j} mode {mode} Y")
