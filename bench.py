@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=1024, help="n_dual")
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
-    ap.add_argument("--chunk", type=int, default=1, help="iterations per kernel launch")
+    ap.add_argument("--chunk", type=int, default=10,
+                    help="iterations (steps) per kernel launch; the iterate stays in LDS between them")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
