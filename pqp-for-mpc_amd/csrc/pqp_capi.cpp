@@ -640,6 +640,9 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
         L.u0 = u0;
         PQP_HIP(launch_converge_persist(L, s));
         int herr = 0;
+        // Y and U ride with the state readback (pinned staging, one sync)
+        PQP_HIP(hipMemcpyAsync(P.hio, P.Y.p, sizeof(float) * N, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipMemcpyAsync(P.hio + N, P.U.p, sizeof(float) * M, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipMemcpyAsync(&herr, L.err, sizeof herr, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
@@ -649,6 +652,7 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
         if (st.status != kStatusContinue) break;
         u0 = st.h - 1;  // the next launch starts from the iterate this one left in P.Y
     }
+    out.staged = true;
     out.h = st.h;
     out.status = st.status;
     out.have_costs = st.have_costs;
