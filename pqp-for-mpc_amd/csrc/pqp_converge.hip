@@ -64,6 +64,21 @@ constexpr long long kTimeoutTicks = 200000000LL;  // s_memrealtime at 100 MHz: 2
 enum Role : int { kUpd = 0, kT1 = 1, kT2 = 2, kT3 = 3, kDec = 4 };
 
 __device__ __forceinline__ u64 rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+// A wait's time limit.  The clock is read only once the wait has spun:
+// s_memrealtime is a scalar memory access counted by lgkmcnt, so reading it at
+// the start of every wait delays the first LDS poll (which waits on lgkmcnt
+// too) by the clock's round trip.
+struct Deadline {
+    u64 t0 = 0;
+    __device__ __forceinline__ bool expired() {
+        const u64 now = rt_now();
+        if (t0 == 0) {
+            t0 = now;
+            return false;
+        }
+        return (long long)(now - t0) > kTimeoutTicks;
+    }
+};
 __host__ __device__ inline int waves_of(int KB) { return KB <= kP0 ? 1 : 1 + (KB - kP0 + kPW - 1) / kPW; }
 __host__ __device__ inline int packets_of(int W) { return kP0 + (W - 1) * kPW; }
 __host__ __device__ inline int cdiv_i(int a, int b) { return (a + b - 1) / b; }
@@ -106,7 +121,7 @@ __device__ __forceinline__ void fail(const CvArgs& a, int code) {
 template <int NG>
 __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* const (&g)[NG], const bool (&on)[NG],
                                                unsigned tag, float (&v)[NG], int code) {
-    const u64 t0 = rt_now();
+    Deadline dl;
     for (unsigned spins = 0;; ++spins) {
         // every address is valid (callers clamp the unused ones), so the loads
         // are unconditional: all NG in flight at once, no branch around each
@@ -122,7 +137,7 @@ __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* cons
         if (__all(ok)) return true;
         if ((spins & 63) == 63) {
             if (stopped(a)) return false;
-            if ((long long)(rt_now() - t0) > kTimeoutTicks) {
+            if (dl.expired()) {
                 fail(a, code);
                 return false;
             }
@@ -237,14 +252,14 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
             // ---- 3. the running sums of the previous slice, then this slice's adds ----
             const u64* src = hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll;
-            const u64 t0 = rt_now();
+            Deadline dl;
             u64 h;
             for (unsigned spins = 0;; ++spins) {
                 h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (__all((unsigned)(h >> 32) == tag)) break;
                 if ((spins & 255) == 255) {
                     if (stopped(a)) return;
-                    if ((long long)(rt_now() - t0) > kTimeoutTicks) {
+                    if (dl.expired()) {
                         fail(a, 10 + ROLE);
                         return;
                     }
@@ -276,13 +291,13 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             const float v = acc + 1.0f * cst;    // even lane: num (:611), odd lane: den (:612)
             const float den = __shfl_xor(v, 1);  // whole wave active
             if (need_bp && dec_seen < u + 1 - kR) {
-                const u64 t0 = rt_now();
+                Deadline dl;
                 for (unsigned spins = 0;; ++spins) {
                     __builtin_amdgcn_s_sleep(2);
                     if (__hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= u + 1 - kR)
                         break;
                     if (stopped(a)) return;
-                    if ((spins & 63) == 63 && (long long)(rt_now() - t0) > kTimeoutTicks) {
+                    if ((spins & 63) == 63 && dl.expired()) {
                         fail(a, 20);
                         return;
                     }
@@ -372,7 +387,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
             mark(a, tr, u, 4 * kMaxW, 1);
             float s1, s2, s3, s4;
             {
-                const u64 t0 = rt_now();
+                Deadline dl;
                 u64 h = 0;
                 const bool mine = lane >= 1 && lane < kDecW;
                 for (unsigned spins = 0;; ++spins) {
@@ -382,7 +397,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                     if (__all(!mine || (unsigned)(h >> 32) == tag)) break;
                     if ((spins & 255) == 255) {
                         if (stopped(a)) return;
-                        if ((long long)(rt_now() - t0) > kTimeoutTicks) {
+                        if (dl.expired()) {
                             fail(a, 51);
                             return;
                         }

@@ -54,6 +54,21 @@ constexpr int kPMaxWaves = 6;
 constexpr long long kPTimeoutTicks = 200000000LL;  // s_memrealtime runs at 100 MHz: 2 s
 
 __device__ __forceinline__ u64 rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+// A wait's time limit.  The clock is read only once the wait has spun:
+// s_memrealtime is a scalar memory access counted by lgkmcnt, so reading it at
+// the start of every wait delays the first LDS poll (which waits on lgkmcnt
+// too) by the clock's round trip.
+struct Deadline {
+    u64 t0 = 0;
+    __device__ __forceinline__ bool expired() {
+        const u64 now = rt_now();
+        if (t0 == 0) {
+            t0 = now;
+            return false;
+        }
+        return (long long)(now - t0) > kPTimeoutTicks;
+    }
+};
 
 __device__ __forceinline__ void fail(int* err, int code) {
     __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -138,7 +153,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
                 const bool own = last && kb == k0 && row < N;  // + y_i of the rows this workgroup finishes (:594)
                 float v[5] = {};
-                const u64 t0 = rt_now();
+                Deadline dl;
                 for (unsigned spins = 0;; ++spins) {
                     bool ok = true;
 #pragma unroll
@@ -156,7 +171,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                         ok &= (unsigned)(x >> 32) == tag;
                     }
                     if (__all(ok)) break;
-                    if ((spins & 63) == 63 && (long long)(rt_now() - t0) > kPTimeoutTicks) {
+                    if ((spins & 63) == 63 && dl.expired()) {
                         fail(err, 1);
                         return;
                     }
@@ -215,12 +230,12 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
 #pragma unroll
             for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
             // ---- 3. the running sums of the previous slice, then this slice's adds ----
-            const u64 t0 = rt_now();
+            Deadline dl;
             u64 h;
             for (unsigned spins = 0;; ++spins) {
                 h = __hip_atomic_load(sl + (w - 1) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (__all((unsigned)(h >> 32) == want)) break;
-                if ((spins & 255) == 255 && (long long)(rt_now() - t0) > kPTimeoutTicks) {
+                if ((spins & 255) == 255 && dl.expired()) {
                     fail(err, 2);
                     return;
                 }
