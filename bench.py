@@ -307,7 +307,7 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     L = pqp_amd.lib()
     lean_min = L.pqp_tune_lean_min_n(0)  # read the setting (and restore it)
     L.pqp_tune_lean_min_n(lean_min)
-    lean = 0 < lean_min <= rows  # row blocks choose the lean relay by their row count
+    lean = lean_min > 0 and rows * N >= lean_min * lean_min  # row blocks choose the lean relay by rows x N
     bpe = 4 if lean else 8  # bytes per matrix entry the update streams
     out = {"n_dual": N, "ranks": world, "rows_per_rank": R, "updates": updates, "us_per_update": dt * 1e6,
            "iter_per_s": 1.0 / dt,

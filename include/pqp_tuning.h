@@ -39,11 +39,11 @@ int pqp_tune_persist(int off);
 int pqp_tune_fixed_rl_max_b(int b);
 
 /* The relay update of one large problem (fixed mode above n_dual 1024, the
- * converge graph chain) streams Qd itself (k_lean_relay: 4 B per entry, the
- * split terms formed in registers) instead of the stored split matrices
- * (8 B) for n_dual >= n, and a row block (pqp_rowblock_*) does so for
- * rows >= n; n <= 0 never.  Default 8192.  Affects problems and row blocks
- * built afterwards.  Returns the previous value. */
+ * converge graph chain) and of a row block (pqp_rowblock_*) streams Qd itself
+ * (k_lean_relay: 4 B per entry, the split terms formed in registers) instead
+ * of the stored split matrices (8 B) when the block's rows x n_dual >= n^2;
+ * n <= 0 never.  Default 4096.  Affects problems and row blocks built
+ * afterwards.  Returns the previous value. */
 int pqp_tune_lean_min_n(int n);
 
 /* Converge mode of one problem with n_dual, M <= 1024 (other than the N, M <= 32

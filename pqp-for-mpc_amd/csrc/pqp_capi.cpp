@@ -416,7 +416,7 @@ int problem_upload(pqp_problem& P, const float* qd, const float* fd, const float
 // (k_split_update), the stored split matrices built once per problem.
 // Lanes per workgroup of the relay update of an n_dual = N problem: row sides
 // of the stored split matrices, or rows of Qd for the lean relay.
-int pick_lw(int N) { return use_lean(N) ? lean_pick_lw(N) : split_pick_lw(N); }
+int pick_lw(int N) { return use_lean(N, N) ? lean_pick_lw(N) : split_pick_lw(N); }
 
 // The relay update's operand of the whole problem (rows 0..N-1), built on
 // first use (and rebuilt if lw or the layout changes): the stored split
@@ -424,7 +424,7 @@ int pick_lw(int N) { return use_lean(N) ? lean_pick_lw(N) : split_pick_lw(N); }
 // Qd itself with lw rows per workgroup (k_lean_relay, half the bytes).
 int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
     const int N = P.N;
-    const bool lean = use_lean(N);
+    const bool lean = use_lean(N, N);
     if (P.SP.p && P.split_lw == lw && P.split_lean == lean) return PQP_OK;
     if (split_lds_bytes(N) > kLdsBudget)
         return set_error(PQP_ERR_ARG, "multi-workgroup solve: N=%d needs more than %zu B of LDS", N, kLdsBudget);
@@ -435,7 +435,7 @@ int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
     PQP_TRY(P.Yb.floats(N));
     if (lean) {
         PQP_TRY(P.SP.floats(lean_floats(N, N, lw)));
-        PQP_TRY(P.fdpn.floats(lean_aux_floats(N, lw)));
+        PQP_TRY(P.fdpn.floats(lean_aux_floats(N, N, lw)));
         PQP_HIP(hipMemsetAsync(P.SP.p, 0, sizeof(float) * lean_floats(N, N, lw), s));
         PQP_HIP(launch_build_lean(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, lw, P.SP.f(), P.fdpn.f(), s));
     } else {
@@ -544,7 +544,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     if (!g_persist_off && N <= persist_max_n()) return problem_run_fixed_persist(P, updates, out, s);
     const int lw = pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
-    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8) | ((int)use_lean(N) << 16);
+    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8) | ((int)use_lean(N, N) << 16);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
         P.chunk_ready = false;
@@ -686,7 +686,7 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     int* flag = static_cast<int*>(P.wflag.p);
     long long* cap = static_cast<long long*>(P.wcap.p);
-    const long long key = ((long long)use_lean(N) << 24) ^ ((long long)g_wide_flags << 16) ^
+    const long long key = ((long long)use_lean(N, N) << 24) ^ ((long long)g_wide_flags << 16) ^
                           ((long long)g_split_kind << 8) ^ lw;  // cap: device word
     if (!P.wgraph || P.wgraph_key != key) {
         if (P.wgraph) {
@@ -1193,15 +1193,14 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
     if (rows > 0) {
         DevBuf theta;
         PQP_TRY(theta.floats(rows));
-        // by the block's row count: the lean update's cost grows with N per
-        // row block whatever its rows (its terms are formed along the whole
-        // chain), the bytes it saves with rows x N
-        b->lean = use_lean(rows);
+        // by the block's entries: the bytes the lean layout saves grow with
+        // rows x N, the chain both layouts run with N alone
+        b->lean = use_lean(N, rows);
         PQP_HIP(launch_theta_rows(d_Qd_rows, ld, N, rows, theta.f(), s));
         if (b->lean) {  // Qd rows themselves (k_lean_relay): half the bytes of the split matrices
             b->lw = lean_pick_lw(rows);
             PQP_TRY(b->SP.floats(lean_floats(N, rows, b->lw)));
-            PQP_TRY(b->fdpn.floats(lean_aux_floats(rows, b->lw)));
+            PQP_TRY(b->fdpn.floats(lean_aux_floats(N, rows, b->lw)));
             PQP_HIP(hipMemsetAsync(b->SP.p, 0, sizeof(float) * lean_floats(N, rows, b->lw), s));
             PQP_HIP(launch_build_lean(d_Qd_rows, ld, theta.f(), d_Fd, N, rows, row0, b->lw, b->SP.f(), b->fdpn.f(),
                                       s));

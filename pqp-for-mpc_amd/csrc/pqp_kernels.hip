@@ -567,10 +567,11 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
 
 // ---------------------------------------------------------------------------
 // k_lean_relay<W,S>: the relay update over Qd itself (4 B per entry) instead of
-// the stored split matrices (8 B): half the bytes for row blocks whose update
-// is HBM-bound (>= 8192 rows; below that forming the terms -- two compares and
-// two selects per k along the whole chain, against one packed multiply per
-// packet for the split form -- costs more than the bytes saved).  One lane owns one ROW and keeps both sums, num
+// the stored split matrices (8 B): half the bytes, for blocks whose update the
+// bytes bound (rows x N >= 4096^2; below that the three instructions per k of
+// forming the terms cost more than the bytes saved).  Lanes 2i + side hold one
+// side of row i, as for the split matrices: both read row i's Qd packet (one
+// cache line), num negates q, and each lane sums one side with one add per k.  One lane owns one ROW and keeps both sums, num
 // and den, as the two halves of one packed accumulator: the chain is one
 // v_pk_add_f32 per k (each half rounds exactly like the scalar add), so it
 // issues like the split form's single add.  The terms are formed ahead of the
@@ -582,16 +583,24 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
 // Layout LP[wg][kb][lw] packets of 4 k of row wg*lw + lane; aux[row] =
 // {Fdn, Fdp, Theta, 0}.
 // ---------------------------------------------------------------------------
+constexpr int kLeanS = 16;  // packets per k_lean_relay segment (the builder flags NaN per segment)
 __global__ void __launch_bounds__(256) k_build_lean(const float* __restrict__ Qd, int ld,
                                                     const float* __restrict__ theta, const float* __restrict__ Fd,
                                                     int N, int rows, int row0, int lw, float* __restrict__ LP,
                                                     float* __restrict__ aux) {
     const int KB = split_kblocks(N);
+    const int rp = lw >> 1;  // rows per workgroup
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (i, k), k fastest
     if (e < (long long)rows * 4 * KB) {
         const int i = (int)(e / (4 * KB)), k = (int)(e % (4 * KB));
-        const size_t at = (((size_t)(i / lw) * KB + (k >> 2)) * lw + (i % lw)) * 4 + (k & 3);
-        LP[at] = k < N ? Qd[(size_t)i * ld + k] : 0.0f;
+        const size_t at = (((size_t)(i / rp) * KB + (k >> 2)) * rp + (i % rp)) * 4 + (k & 3);
+        const float q = k < N ? Qd[(size_t)i * ld + k] : 0.0f;
+        LP[at] = q;
+        if (q != q) {  // this (workgroup, segment) needs the compare/select form
+            const int G = (KB + kLeanS - 1) / kLeanS, nwg = (rows + rp - 1) / rp;
+            int* segnan = reinterpret_cast<int*>(aux + 4 * (size_t)nwg * rp);
+            atomicOr(segnan + (size_t)(i / rp) * G + (k >> 2) / kLeanS, 1);
+        }
     }
     if (e < rows) {
         const float fd = Fd[row0 + e];
@@ -608,22 +617,23 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
                                                        const float* __restrict__ Yin, float* __restrict__ Yout,
                                                        const int* __restrict__ gate) {
     if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
-    // LDS: [2][64] hand-off words (num, den), then y [4*G*S]
+    // LDS: [64] hand-off words, then y [4*G*S]
     extern __shared__ __attribute__((aligned(16))) float lds[];
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds);
-    float* ys = lds + 256;
+    float* ys = lds + 128;
     const int KB = split_kblocks(N);
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ll = lane % lw;  // lanes >= lw repeat lane % lw's row and are discarded
-    const int r = blockIdx.x * lw + ll;
+    const int ll = lane % lw;  // lanes >= lw repeat lane % lw's requests and are discarded
+    const int rp = lw >> 1;    // rows per workgroup: lane 2i + side holds one side of row i
+    const int side = ll & 1;   // 0: num (Qdn_theta), 1: den (Qdp_theta)
+    const int r = blockIdx.x * rp + (ll >> 1);
     const bool live = lane < lw && r < rows;
     const int G = (KB + S - 1) / S;
     typedef float f4v __attribute__((ext_vector_type(4)));
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    const float* region = LP + (size_t)blockIdx.x * KB * lw * 4;
+    const float* region = LP + (size_t)blockIdx.x * KB * rp * 4;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * lw * 16, 0x00020000);
-    const int vo = ll * 16, kstride = lw * 16;
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * rp * 16, 0x00020000);
+    const int vo = (ll >> 1) * 16, kstride = rp * 16;  // both lanes of a row read its packet (one cache line)
     f4v q[S];
     const bool lane_loads = lane < lw;
     auto load_seg = [&](int g) {
@@ -635,6 +645,7 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
     };
     if (w < G) load_seg(w);
     const f4v ax = live ? *reinterpret_cast<const f4v*>(aux + 4 * (size_t)r) : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    const int* segnan = reinterpret_cast<const int*>(aux + 4 * (size_t)gridDim.x * rp);  // [wg][G] NaN flags
     {
         const int t = threadIdx.x, n_lds = 4 * G * S;
         for (int b = 0; b < n_lds; b += 64 * W * 8) {
@@ -650,25 +661,34 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
                 if (k < n_lds) ys[k] = v[j];
             }
         }
-        if (w == 0) slot[lane] = slot[64 + lane] = 0ull;  // segment 0 starts from +0.0f
+        if (w == 0) slot[lane] = 0ull;  // segment 0 starts from +0.0f
     }
     __syncthreads();
-    const int d0 = row0 + blockIdx.x * lw;  // the workgroup's first diagonal k (wave-uniform)
+    const int d0 = row0 + blockIdx.x * rp;  // the workgroup's first diagonal k (wave-uniform)
     const int diag = row0 + r;              // this lane's diagonal k
     const float th = ax.z;
-    f2v acc = f2v{0.0f, 0.0f};  // .x num, .y den
-    f2v T[4 * S];               // per k: {num term, den term}, an adjacent register pair for v_pk_add_f32
+    const float fd = side ? ax.y : ax.x;    // Fdp / Fdn (:703-704)
+    // this lane's side of the split entry: den uses q, num uses -q (negation is
+    // exact), so every form below is the den formula on qs
+    const unsigned sgn = side ? 0u : 0x80000000u;
+    float acc = 0.0f;
     for (int g = w; g < G; g += W) {
         const int kbase = 4 * g * S;
-        const bool lit = kbase < d0 + lw && kbase + 4 * S > d0;  // a diagonal of this workgroup is in here
-        // the branch is per segment, each side one straight-line unrolled loop
-        auto form = [&](auto literal) {
-            // distinct volatile markers keep the two sides from being merged
-            // back into a branch per k
-            if constexpr (decltype(literal)::value)
+        const bool lit = kbase < d0 + rp && kbase + 4 * S > d0;  // a diagonal of this workgroup is in here
+        const bool nan_seg = !lit && segnan[(size_t)blockIdx.x * G + g] != 0;  // a NaN of Qd is in here
+        // the terms replace the packets in place; the branch is per segment,
+        // each side one straight-line unrolled loop (2: literal, 1: lean with
+        // compares, 0: lean by max)
+        auto form = [&](auto kind) {
+            constexpr int KIND = decltype(kind)::value;
+            // distinct volatile markers keep the sides from being merged back
+            // into a branch per k
+            if constexpr (KIND == 2)
                 asm volatile("; literal terms");
+            else if constexpr (KIND == 1)
+                asm volatile("; lean terms, compare/select");
             else
-                asm volatile("; lean terms");
+                asm volatile("; lean terms, max");
 #pragma unroll
             for (int j0 = 0; j0 < S; j0 += 4) {
                 f4v y[4];
@@ -677,75 +697,92 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = j0 + u;
-                    const float qv[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+                    float qv[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
                     const float yv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        const float qq = qv[c], yy = yv[c];
-                        float dn, nm;
-                        if constexpr (!decltype(literal)::value) {
-                            const float p = qq * yy;
+                        const float qs = __uint_as_float(__float_as_uint(qv[c]) ^ sgn);
+                        const float yy = yv[c];
+                        if constexpr (KIND == 0) {
+                            // no NaN in this segment's q: max(qs, 0) * y is the
+                            // reference's (max(0, qs) + 0.0f) * y up to the sign of
+                            // a zero term, which adds nothing to a sum that is never
+                            // -0 (0 * inf / NaN y still gives NaN).  v_max_f32
+                            // directly: fmaxf would first quiet a NaN (one more
+                            // instruction), and there is none here
+                            float m;
+                            asm("v_max_f32_e64 %0, 0, %1" : "=v"(m) : "v"(qs));
+                            qv[c] = m * yy;
+                        } else if constexpr (KIND == 1) {
+                            const float p = qs * yy;
                             const float z = 0.0f * yy;  // (+0)*y: NaN for inf/NaN y
-                            dn = qq < 0.0f ? z : p;
-                            nm = qq > 0.0f ? z : -p;
+                            qv[c] = qs < 0.0f ? z : p;
                         } else {  // computeQdp/Qdn_theta :524-537, then :608-609
                             const float t = (kbase + 4 * j + c == diag) ? th : 0.0f;
-                            dn = (max_ref(0.0f, qq) + t) * yy;
-                            nm = (max_ref(0.0f, -qq) + t) * yy;
+                            qv[c] = (max_ref(0.0f, qs) + t) * yy;
                         }
-                        T[4 * j + c] = f2v{nm, dn};
                     }
+                    q[j] = f4v{qv[0], qv[1], qv[2], qv[3]};
                 }
 #pragma unroll
-                for (int u = 0; u < 16; ++u) asm volatile("" : "+v"(T[4 * j0 + u]));
+                for (int u = 0; u < 4; ++u) asm volatile("" : "+v"(q[j0 + u]));
             }
-            if constexpr (decltype(literal)::value)
+            if constexpr (KIND == 2)
                 asm volatile("; literal terms end");
+            else if constexpr (KIND == 1)
+                asm volatile("; lean terms, compare/select, end");
             else
-                asm volatile("; lean terms end");
+                asm volatile("; lean terms, max, end");
         };
         if (lit)
-            form(std::true_type{});
+            form(std::integral_constant<int, 2>{});
+        else if (nan_seg)
+            form(std::integral_constant<int, 1>{});
         else
-            form(std::false_type{});
-        // q is free once the terms are formed: the next segment's packets are
-        // in flight during the turn wait and the adds
-        if (g + W < G) load_seg(g + W);
-        unsigned long long hn, hd;
+            form(std::integral_constant<int, 0>{});
+        unsigned long long h;
         for (int spin = 0;; ++spin) {
-            hn = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            hd = __hip_atomic_load(slot + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__all((int)(hn >> 32) == g && (int)(hd >> 32) == g) || spin > (1 << 20)) break;
+            h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
         }
         __builtin_amdgcn_s_setprio(3);
-        acc = f2v{__uint_as_float((unsigned)hn), __uint_as_float((unsigned)hd)};
+        acc = __uint_as_float((unsigned)h);
 #pragma unroll
-        for (int k = 0; k < 4 * S; ++k) acc += T[k];  // :608-609, k in order; both sums in one packed add
-        __hip_atomic_store(slot + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc.x),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(slot + 64 + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc.y),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int j = 0; j < S; ++j) {
+            acc += q[j].x;  // :608-609, k in order
+            acc += q[j].y;
+            acc += q[j].z;
+            acc += q[j].w;
+        }
+        __hip_atomic_store(slot + lane, ((unsigned long long)(g + 1) << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
         __builtin_amdgcn_s_setprio(0);
+        if (g + W < G) load_seg(g + W);
     }
-    if (w == (G - 1) % W && live) {
-        const float num = acc.x + 1.0f * ax.x;  // matrixAdd(num, Fdn, 1) :611
-        const float den = acc.y + 1.0f * ax.y;  // matrixAdd(den, Fdp, 1) :612
-        Yout[r] = num / den * ys[row0 + r];     // updY :594
+    if (w == (G - 1) % W) {  // the wave that summed the last segment
+        const float v = acc + 1.0f * fd;     // even lane: num (:611), odd lane: den (:612)
+        const float den = __shfl_xor(v, 1);  // the whole wave is here
+        if (!side && live) Yout[r] = v / den * ys[row0 + r];  // updY :594
     }
 }
 
-int g_lean_min_n = 8192;  // tuning: smallest n_dual whose relay update streams Qd (lean) instead of the split matrices
-bool use_lean(int N) { return g_lean_min_n > 0 && N >= g_lean_min_n; }
-size_t lean_floats(int N, int rows, int lw) { return (size_t)cdiv(rows, lw) * split_kblocks(N) * lw * 4; }
-size_t lean_aux_floats(int rows, int lw) { return (size_t)cdiv(rows, lw) * lw * 4; }
-int lean_pick_lw(int rows) {
-    int lw = 8;  // about one workgroup per CU: rows / lw ~ 256
-    while (lw < 64 && rows > 256LL * lw) lw *= 2;
-    return lw;
+int g_lean_min_n = 4096;  // tuning: k_lean_relay for blocks of rows x N >= g_lean_min_n^2 entries
+bool use_lean(int N, int rows) {
+    return g_lean_min_n > 0 && (long long)rows * N >= (long long)g_lean_min_n * g_lean_min_n;
 }
+// lw = row SIDES per workgroup (as for the split matrices): lw / 2 rows
+size_t lean_floats(int N, int rows, int lw) { return (size_t)cdiv(2LL * rows, lw) * split_kblocks(N) * (lw / 2) * 4; }
+size_t lean_aux_floats(int N, int rows, int lw) {  // per-row words, then the [wg][segment] NaN flags
+    const size_t nwg = cdiv(2LL * rows, lw);
+    return nwg * (lw / 2) * 4 + nwg * cdiv(split_kblocks(N), kLeanS);
+}
+int lean_pick_lw(int rows) { return split_pick_lw(rows); }
 hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows, int row0,
                              int lw, float* LP, float* aux, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
+    const size_t nwg = cdiv(2LL * rows, lw), nflag = nwg * cdiv(split_kblocks(N), kLeanS);
+    hipError_t e = hipMemsetAsync(aux + 4 * nwg * (lw / 2), 0, sizeof(int) * nflag, s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_build_lean, dim3(cdiv((long long)rows * 4 * split_kblocks(N), 256)), dim3(256), 0, s, Qd,
                        ld, theta, Fd, N, rows, row0, lw, LP, aux);
     return hipGetLastError();
@@ -753,11 +790,11 @@ hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const 
 hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows, int row0, int lw, const float* Yin,
                               float* Yout, hipStream_t s, const int* gate) {
     if (rows <= 0) return hipSuccess;
-    constexpr int W = 8, S = 16;
+    constexpr int W = 8, S = kLeanS;
     const int G = (split_kblocks(N) + S - 1) / S;
-    const size_t lds = sizeof(float) * ((size_t)4 * G * S + 256);
-    hipLaunchKernelGGL((k_lean_relay<W, S>), dim3(cdiv(rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows, row0, lw,
-                       Yin, Yout, gate);
+    const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);
+    hipLaunchKernelGGL((k_lean_relay<W, S>), dim3(cdiv(2LL * rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows, row0,
+                       lw, Yin, Yout, gate);
     return hipGetLastError();
 }
 

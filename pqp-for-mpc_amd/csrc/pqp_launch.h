@@ -80,12 +80,13 @@ extern int g_persist_off;
 extern unsigned long long* g_persist_trace;  // tuning: device buffer of 4 * waves * g_persist_trace_n words
 extern int g_persist_trace_n;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
-// lean relay (k_lean_relay): Qd packets (4 B per entry, lw ROWS per workgroup)
-// and aux[row] = {Fdn, Fdp, Theta, 0}; used from n_dual >= g_lean_min_n
+// lean relay (k_lean_relay): Qd packets (4 B per entry, lw / 2 rows per
+// workgroup) and aux[row] = {Fdn, Fdp, Theta, 0} + NaN flags; used for blocks
+// of rows x N >= g_lean_min_n^2 entries
 extern int g_lean_min_n;
-bool use_lean(int N);
+bool use_lean(int N, int rows);
 size_t lean_floats(int N, int rows, int lw);
-size_t lean_aux_floats(int rows, int lw);
+size_t lean_aux_floats(int N, int rows, int lw);  // per-row words + per-(workgroup, segment) NaN flags
 int lean_pick_lw(int rows);
 hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows, int row0,
                              int lw, float* LP, float* aux, hipStream_t s);
