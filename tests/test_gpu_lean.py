@@ -1,9 +1,9 @@
 """GPU parity of the lean relay update (k_lean_relay): one large problem's
-updateY2 streaming Qd itself (4 B per entry, the split terms formed in
-registers, num and den as one packed accumulator) instead of the stored
-split matrices.  Default for blocks of rows x n_dual >= 4096^2; forced here at every size through
-pqp_tune_lean_min_n.  Bar: bit-exact against the oracle (inf / NaN / -0
-included), the golden fixed-999 iterate, and the split-matrix relay."""
+updateY2 streaming Qd itself (4 B per entry; lanes 2i and 2i + 1 read row i's
+packet and form its num / den terms in registers) instead of the stored split
+matrices.  Default for blocks of rows x n_dual >= 4096^2; forced here at every
+size through pqp_tune_lean_min_n.  Bar: bit-exact against the oracle (inf /
+NaN / -0 included), the golden fixed-999 iterate, and the split-matrix relay."""
 from __future__ import annotations
 
 import numpy as np
