@@ -260,6 +260,7 @@ struct pqp_problem {
     pqp::DevBuf CA1, CA2, CA3, crings, cwords;
     hipGraphExec_t wgraph = nullptr;                 // captured chunk of converge iterations
     hipGraphExec_t wgraph_first = nullptr;           // the short first chunk
+    hipGraphExec_t wgraph4 = nullptr, wgraph8 = nullptr;  // the chunks that escalate to kWideChunk
     hipStream_t side = nullptr;                      // capture-time fork for the speculative update
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     long long wgraph_key = -1;
@@ -275,6 +276,8 @@ struct pqp_problem {
         if (chunk_graph) (void)hipGraphExecDestroy(chunk_graph);
         if (wgraph) (void)hipGraphExecDestroy(wgraph);
         if (wgraph_first) (void)hipGraphExecDestroy(wgraph_first);
+        if (wgraph4) (void)hipGraphExecDestroy(wgraph4);
+        if (wgraph8) (void)hipGraphExecDestroy(wgraph8);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (side) (void)hipStreamDestroy(side);
@@ -344,7 +347,7 @@ void problem_reset_derived(pqp_problem& P) {
     for (DevBuf* b : {&P.QdT, &P.theta, &P.SP, &P.fdpn, &P.Yb, &P.SPp, &P.fdpnp, &P.gran, &P.perr, &P.QinvT, &P.GpT,
                       &P.tM, &P.tq, &P.tu, &P.gu, &P.wflag, &P.wcap, &P.CA1, &P.CA2, &P.CA3, &P.crings, &P.cwords})
         b->reset();
-    for (hipGraphExec_t* g : {&P.graph, &P.chunk_graph, &P.wgraph, &P.wgraph_first})
+    for (hipGraphExec_t* g : {&P.graph, &P.chunk_graph, &P.wgraph, &P.wgraph_first, &P.wgraph4, &P.wgraph8})
         if (*g) {
             (void)hipGraphExecDestroy(*g);
             *g = nullptr;
@@ -734,9 +737,8 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
             if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join the update branch
             return problem_update(P, lw, cur, nxt, s, &dst->status);
         };
-        // two graphs: a short first chunk (problems that stop within a few
-        // iterations do not pay for a long chunk of no-op launches), then
-        // kWideChunk iterations per replay
+        // replays of 2, 2, 4, 8, then kWideChunk iterations: a solve that stops
+        // early launches at most about as many no-op iterations as it ran
         auto capture = [&](int iters, hipGraphExec_t* exec) -> int {
             hipGraph_t g = nullptr;
             PQP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -755,18 +757,22 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
             PQP_HIP(e3);
             return PQP_OK;
         };
-        if (P.wgraph_first) {
-            (void)hipGraphExecDestroy(P.wgraph_first);
-            P.wgraph_first = nullptr;
-        }
+        for (hipGraphExec_t* g : {&P.wgraph_first, &P.wgraph4, &P.wgraph8})
+            if (*g) {
+                (void)hipGraphExecDestroy(*g);
+                *g = nullptr;
+            }
         PQP_TRY(capture(kWideFirstChunk, &P.wgraph_first));
+        PQP_TRY(capture(4, &P.wgraph4));
+        PQP_TRY(capture(8, &P.wgraph8));
         PQP_TRY(capture(kWideChunk, &P.wgraph));
         P.wgraph_key = key;
     }
     PQP_HIP(launch_wide_init(dst, flag, cap, max_updates, P.Y.f(), N, s));
     SolveState& st = *P.hst;
     for (int launch = 0;; ++launch) {
-        PQP_HIP(hipGraphLaunch(launch == 0 ? P.wgraph_first : P.wgraph, s));
+        hipGraphExec_t g = launch < 2 ? P.wgraph_first : (launch == 2 ? P.wgraph4 : (launch == 3 ? P.wgraph8 : P.wgraph));
+        PQP_HIP(hipGraphLaunch(g, s));
         PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
         if (st.status != kStatusContinue) break;
