@@ -329,13 +329,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PQP_BENCH_REHEARSE=1: rehearse the N > 1 control flow on a one-GPU box.
+    # RCCL refuses two ranks on one device, so every rank takes cuda:0 and the
+    # collectives go over gloo (which takes device tensors).  The numbers of
+    # such a run are not throughput; the JSON line says "rehearsal".
+    rehearse = os.environ.get("PQP_BENCH_REHEARSE") == "1" and world > 1
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo" if rehearse else "nccl", device_id=None if rehearse else dev)
 
     N, B, K, W, C = args.n, args.batch, args.steps, args.warmup, max(1, args.chunk)
     # "scatter inputs": rank 0 hands each rank its (seed, first problem, count)
@@ -382,13 +389,16 @@ def main():
 
     # gather Y* to rank 0 over RCCL (reported separately, not in `value`)
     gather_ms = None
+    gather_ok = None
     if dist is not None:
         y = batch.Y[:, :N].contiguous()
         torch.cuda.synchronize(dev)
         g0 = time.perf_counter()
-        gather_rows(dist, rank, world, y)
+        full = gather_rows(dist, rank, world, y)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
+        if rank == 0:  # rank order = problem order: rank 0's own block leads
+            gather_ok = tuple(full.shape) == (B * world, N) and bool(torch.equal(full[:B], y))
     Yh = batch.Y[:, :N]
     finite = bool(torch.isfinite(Yh).all().item()) and bool((Yh >= 0).all().item())
 
@@ -432,7 +442,10 @@ def main():
                      "alg_bytes_per_launch": alg_bytes(N) * B * C, "avg_launch_ms": per_launch_ms},
         "results_finite_nonneg": finite,
         "gather_ms": gather_ms,
+        "gather_ok": gather_ok,
     }
+    if rehearse:
+        result["rehearsal"] = "all ranks on cuda:0 over gloo (PQP_BENCH_REHEARSE=1): control-flow check, not a measurement"
     if rowshard is not None:
         result["rowshard"] = rowshard
     if world == 1 and not args.no_bundled:
