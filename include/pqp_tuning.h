@@ -12,7 +12,8 @@ extern "C" {
 
 /* Select kernel variants.  Low byte: the k_batch_iterate instantiation used
  * by pqp_batch_iterate (0 = shipped default: unroll 16, non-temporal Qd
- * loads; 1..5 = other (unroll, non-temporal) variants, see pqp_kernels.hip
+ * loads; 1..5 = other (unroll, non-temporal) variants, 6 = max-based terms
+ * (timing only: exact only for NaN-free Qd), see pqp_kernels.hip
  * launch_batch_iterate).  Bit 0x100: solve N, M <= 32 problems with the
  * LDS-staged k_solve_small instead of k_solve_tiny.  Bit 0x200: fixed-mode
  * solves of large single problems on one workgroup (k_solve_single) instead

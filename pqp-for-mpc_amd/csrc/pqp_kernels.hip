@@ -74,9 +74,22 @@ __device__ __forceinline__ void literal4(Acc4& a, float4 q, float y, int k, int 
     literal1(a.p[3], a.n[3], q.w, y, (k == row + 3) ? th[3] : 0.0f);
 }
 
+// max-based lean step (A/B variant 6, timing only): equal to lean4 when q has
+// no NaN and y is finite and >= 0, up to the sign of an all-zero sum
+__device__ __forceinline__ void lean4mx(Acc4& a, float4 q, float y) {
+    a.p[0] += fmaxf(q.x, 0.0f) * y; a.n[0] += fmaxf(-q.x, 0.0f) * y;
+    a.p[1] += fmaxf(q.y, 0.0f) * y; a.n[1] += fmaxf(-q.y, 0.0f) * y;
+    a.p[2] += fmaxf(q.z, 0.0f) * y; a.n[2] += fmaxf(-q.z, 0.0f) * y;
+    a.p[3] += fmaxf(q.w, 0.0f) * y; a.n[3] += fmaxf(-q.w, 0.0f) * y;
+}
+template <bool MX>
+__device__ __forceinline__ void lean4v(Acc4& a, float4 q, float y) {
+    if constexpr (MX) lean4mx(a, q, y); else lean4(a, q, y);
+}
+
 // Stream k in [ka, kb) with the lean form.  ka % 4 == 0.  `col` points at
 // QdT + row (this lane's 4 rows), y is the iterate (LDS).
-template <int U, bool NTL>
+template <int U, bool NTL, bool MX = false>
 __device__ __forceinline__ void lean_segment(Acc4& a, const float* __restrict__ col, int ldq, int ka, int kb,
                                              const float* __restrict__ y) {
     static_assert(U % 4 == 0, "unroll must be a multiple of 4 (one float4 of y per 4 k)");
@@ -90,14 +103,14 @@ __device__ __forceinline__ void lean_segment(Acc4& a, const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < U; j += 4) {
             const float4 yv = *reinterpret_cast<const float4*>(y + k + j);
-            lean4(a, q[j + 0], yv.x);
-            lean4(a, q[j + 1], yv.y);
-            lean4(a, q[j + 2], yv.z);
-            lean4(a, q[j + 3], yv.w);
+            lean4v<MX>(a, q[j + 0], yv.x);
+            lean4v<MX>(a, q[j + 1], yv.y);
+            lean4v<MX>(a, q[j + 2], yv.z);
+            lean4v<MX>(a, q[j + 3], yv.w);
         }
     }
     for (; k < kb; ++k) {
-        lean4(a, ldq4<NTL>(src), y[k]);
+        lean4v<MX>(a, ldq4<NTL>(src), y[k]);
         src += ldq;
     }
 }
@@ -128,7 +141,7 @@ __device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict
 // out[i] = num/den * y[i] for the rows < N.  w0 = first row of this lane's
 // wave (wave-uniform): the diagonal of the wave's 256 rows lies in
 // k in [w0, w0+256) and only that window needs the literal form.
-template <int U, bool NTL, typename OutPtr>
+template <int U, bool NTL, typename OutPtr, bool MX = false>
 __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ldq, int N, int row, int w0,
                                              const float* __restrict__ th_g, const float* __restrict__ fd_g,
                                              const float* __restrict__ y, OutPtr out) {
@@ -141,9 +154,9 @@ __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ld
     const float* col = Q + row;
     const int wa = w0 < N ? w0 : N;
     const int wb = (w0 + 256) < N ? (w0 + 256) : N;
-    lean_segment<U, NTL>(a, col, ldq, 0, wa, y);
+    lean_segment<U, NTL, MX>(a, col, ldq, 0, wa, y);
     literal_segment<NTL>(a, col, ldq, wa, wb, y, row, th);
-    lean_segment<U, NTL>(a, col, ldq, wb, N, y);
+    lean_segment<U, NTL, MX>(a, col, ldq, wb, N, y);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = row + r;
@@ -161,7 +174,7 @@ __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ld
 // launch.  One workgroup owns one problem; its iterate ping-pongs between two
 // LDS buffers, so the only HBM traffic per iteration is Qd (streamed once).
 // ---------------------------------------------------------------------------
-template <int NT, int U = 8, bool NTL = false>
+template <int NT, int U = 8, bool NTL = false, bool MX = false>
 __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ QdT, long long qstride, int ldq,
                                                       int N, const float* __restrict__ theta,
                                                       const float* __restrict__ Fd, int ldv,
@@ -188,7 +201,7 @@ __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ 
         for (int r0 = 0; r0 < N; r0 += 4 * NT) {
             const int row = r0 + 4 * tid;
             const int w0 = r0 + 256 * wave;
-            if (row < N) update_rows4<U, NTL>(Q, ldq, N, row, w0, th, fd, cur, nxt);
+            if (row < N) update_rows4<U, NTL, float*, MX>(Q, ldq, N, row, w0, th, fd, cur, nxt);
         }
         __syncthreads();
     }
@@ -2306,15 +2319,15 @@ static int g_variant = 0;  // tuning knob (include/pqp_tuning.h); 0 = shipped de
 void set_variant(int v) { g_variant = v; }
 int get_variant() { return g_variant; }
 
-template <int U, bool NTL>
+template <int U, bool NTL, bool MX = false>
 static void launch_iterate_t(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
                              const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
     const size_t lds = (size_t)2 * ldq * sizeof(float);
     if (N <= 256)
-        hipLaunchKernelGGL((k_batch_iterate<64, U, NTL>), dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd,
+        hipLaunchKernelGGL((k_batch_iterate<64, U, NTL, MX>), dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd,
                            ldv, Y0, Y, updates);
     else
-        hipLaunchKernelGGL((k_batch_iterate<256, U, NTL>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
+        hipLaunchKernelGGL((k_batch_iterate<256, U, NTL, MX>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
                            Fd, ldv, Y0, Y, updates);
 }
 
@@ -2349,6 +2362,7 @@ static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qs
         case 3: launch_iterate_t<4, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
         case 4: launch_iterate_t<32, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
         case 5: launch_iterate_t<16, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
+        case 6: launch_iterate_t<16, true, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
         default: launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
     }
     return hipGetLastError();

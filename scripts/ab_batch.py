@@ -16,7 +16,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-VARIANTS = {0: "U16+nt (default)", 1: "U8", 2: "U8+nt", 3: "U4+nt", 4: "U32+nt", 5: "U16"}
+VARIANTS = {0: "U16+nt (default)", 1: "U8", 2: "U8+nt", 3: "U4+nt", 4: "U32+nt", 5: "U16", 6: "U16+nt max-terms (timing only)"}
 
 
 def main():
