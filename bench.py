@@ -36,7 +36,12 @@ Extra keys:
                 solve, with the reference's own h (cpu_baseline) beside it
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+       N > 1 either way:
+         python bench.py --gpus N      (this process spawns N ranks itself, one
+                                        per GPU, before it touches HIP; it
+                                        relays rank 0's line and exits with the
+                                        worst rank's status)
+         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
 
@@ -300,6 +305,7 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     if dist is not None:
         dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    solver.check()  # no expired in-kernel wait in any update (else this raises)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t[0]) / updates
@@ -320,13 +326,72 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     return out
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd: list[str], grace_s: float = 60.0) -> int:
+    """Run `cmd` as n ranks of one job on this node (one process per GPU, the
+    torchrun environment contract: RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT), wait for all of them and return the worst exit
+    status.  Nothing here imports torch or touches HIP: the GPUs belong to the
+    children.  When a rank fails, the others get `grace_s` to finish before
+    they are terminated (a rank stuck in a collective with a dead peer would
+    otherwise wait forever)."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    rcs: list[int | None] = [None] * n
+    deadline = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if deadline is None and any(rc not in (None, 0) for rc in rcs):
+            deadline = time.monotonic() + grace_s
+        if deadline is not None and time.monotonic() > deadline:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    os.killpg(p.pid, signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        os.killpg(p.pid, signal.SIGKILL)
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    if not bad:
+        return 0
+    # a signal death (negative) reports as 128 + signal, as a shell would
+    return max(128 - rc if rc < 0 else rc for rc in bad)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: become the launcher.
+        sys.exit(launch_ranks(args.gpus, [sys.executable, "-u", str(Path(__file__).resolve())] + sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+
     import torch
 
     import pqp_amd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PQP_BENCH_REHEARSE=1: rehearse the N > 1 control flow on a one-GPU box.

@@ -260,6 +260,13 @@ int pqp_rowblock_create(const float *d_Qd_rows, int ld, const float *d_Fd, int N
 /* d_Y_rows[i] = updateY2(Y)[row0 + i] for i < rows.  d_Y must hold N floats
  * (more is allowed and ignored).  Async on `stream`. */
 int pqp_rowblock_update(pqp_rowblock *b, const float *d_Y, float *d_Y_rows, void *stream);
+/* Synchronizes `stream` and reports whether any pqp_rowblock_update of this
+ * block since the last check hit an expired wait inside the kernel (a
+ * workgroup's wave-to-wave hand-off that never arrived): PQP_ERR_HIP when one
+ * did -- the rows it wrote are then not valid -- else PQP_OK.  The check clears
+ * the block's error word.  No reference counterpart (the CPU loop cannot
+ * fail); call it at the end of a run of updates. */
+int pqp_rowblock_check(pqp_rowblock *b, void *stream);
 int pqp_rowblock_destroy(pqp_rowblock *b);
 
 /* Rows [row0, row0+rows) of synthetic problem `inst` of `seed` (the

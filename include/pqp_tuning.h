@@ -47,6 +47,29 @@ int pqp_tune_fixed_rl_max_b(int b);
  * afterwards.  Returns the previous value. */
 int pqp_tune_lean_min_n(int n);
 
+/* Budget, in polls, of every wave-to-wave hand-off wait in the relay kernels
+ * (k_split_relay, k_lean_relay, k_gemv_relay); 0 restores the default (2^20).
+ * A negative budget expires every wait, so that a test can see the error path:
+ * the solve / pqp_rowblock_check then returns PQP_ERR_HIP.  Applies to launches
+ * (and graphs) made afterwards.  Returns the previous value. */
+int pqp_tune_relay_spin_max(int polls);
+
+/* The persistent single-problem launches (fixed mode: k_split_persist; converge
+ * mode: k_converge_persist) need all their workgroups resident at once.  Before
+ * launching, the library checks occupancy x CUs against the grid and otherwise
+ * takes the graph-replayed relay path; a launch whose wait still expires
+ * (CUs held by other work) is re-run on that path.  `cus` > 0 makes the check
+ * assume that many CUs (1 forces the does-not-fit branch in tests); 0 restores
+ * the device's count.  Returns the previous value. */
+int pqp_tune_persist_fit_cus(int cus);
+
+/* Which solver the last pqp_problem_solve / drop-in solve of one problem ran:
+ * 1 fixed-mode persistent launch, 2 fixed-mode graph-replayed relay, 3 converge
+ * persistent launch, 4 converge graph chain (pqp_wide.hip), 5 one-workgroup /
+ * one-wave solvers; 0 none yet.  *fallbacks (if not NULL) receives how many
+ * persistent launches fell back to the relay / graph path so far. */
+int pqp_tune_last_path(long long *fallbacks);
+
 /* Converge mode of one problem with n_dual, M <= 1024 (other than the N, M <= 32
  * problems of the one-wave solver) runs as ONE persistent pipelined launch
  * (pqp_converge.hip: terminate(Y_u) beside the update to Y_{u+1}) unless

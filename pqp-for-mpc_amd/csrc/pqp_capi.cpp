@@ -247,6 +247,7 @@ struct pqp_problem {
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
+    pqp::DevBuf rerr;                                // sticky relay hand-off error word (relay / graph paths)
     pqp::DevBuf SPp, fdpnp, gran, perr;              // persistent fixed mode: split matrices (lw = 32), y granules, error word
     int split_lw = 0;                                // lanes per workgroup SP was built with
     bool split_lean = false;                         // SP holds Qd packets (k_lean_relay), not the split matrices
@@ -292,6 +293,7 @@ struct pqp_rowblock {
     int N = 0, row0 = 0, rows = 0, lw = 64;
     bool lean = false;  // SP holds Qd packets (k_lean_relay), fdpn the {Fdn, Fdp, Theta, 0} words
     pqp::DevBuf SP, fdpn;
+    pqp::DevBuf err;    // sticky relay hand-off error word (pqp_rowblock_check)
 };
 
 namespace pqp {
@@ -344,7 +346,7 @@ int ensure_single(pqp_problem& P, hipStream_t s) {
 // Drop everything derived from a problem's data (built on first use by the
 // solve paths): called before new data goes into an existing handle.
 void problem_reset_derived(pqp_problem& P) {
-    for (DevBuf* b : {&P.QdT, &P.theta, &P.SP, &P.fdpn, &P.Yb, &P.SPp, &P.fdpnp, &P.gran, &P.perr, &P.QinvT, &P.GpT,
+    for (DevBuf* b : {&P.QdT, &P.theta, &P.SP, &P.fdpn, &P.Yb, &P.rerr, &P.SPp, &P.fdpnp, &P.gran, &P.perr, &P.QinvT, &P.GpT,
                       &P.tM, &P.tq, &P.tu, &P.gu, &P.wflag, &P.wcap, &P.CA1, &P.CA2, &P.CA3, &P.crings, &P.cwords})
         b->reset();
     for (hipGraphExec_t* g : {&P.graph, &P.chunk_graph, &P.wgraph, &P.wgraph_first, &P.wgraph4, &P.wgraph8})
@@ -436,6 +438,10 @@ int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
         PQP_HIP(launch_theta_rows(P.Qd.f(), N, N, N, P.theta.f(), s));
     }
     PQP_TRY(P.Yb.floats(N));
+    if (!P.rerr.p) {
+        PQP_TRY(P.rerr.alloc(sizeof(int)));
+        PQP_HIP(hipMemsetAsync(P.rerr.p, 0, sizeof(int), s));
+    }
     if (lean) {
         PQP_TRY(P.SP.floats(lean_floats(N, N, lw)));
         PQP_TRY(P.fdpn.floats(lean_aux_floats(N, N, lw)));
@@ -454,8 +460,24 @@ int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
 
 // One relay update of the whole problem, a -> b, over the operand ensure_split built.
 hipError_t problem_update(pqp_problem& P, int lw, const float* a, float* b, hipStream_t s, const int* gate = nullptr) {
-    return P.split_lean ? launch_lean_update(P.SP.f(), P.fdpn.f(), P.N, P.N, 0, lw, a, b, s, gate)
-                        : launch_split_update(P.SP.f(), P.fdpn.f(), P.N, P.N, 0, lw, a, b, s, gate);
+    int* err = static_cast<int*>(P.rerr.p);
+    return P.split_lean ? launch_lean_update(P.SP.f(), P.fdpn.f(), P.N, P.N, 0, lw, a, b, s, gate, err)
+                        : launch_split_update(P.SP.f(), P.fdpn.f(), P.N, P.N, 0, lw, a, b, s, gate, err);
+}
+
+// The relay kernels' sticky error word: read (the caller synchronizes s
+// after this call) and, when set, cleared and turned into PQP_ERR_HIP.
+int relay_error_check(DevBuf& word, int* host, hipStream_t s, const char* what) {
+    PQP_HIP(hipStreamSynchronize(s));
+    if (*host) {
+        const int code = *host;
+        *host = 0;
+        PQP_HIP(hipMemsetAsync(word.p, 0, sizeof(int), s));
+        PQP_HIP(hipStreamSynchronize(s));
+        return set_error(PQP_ERR_HIP, "%s: a relay hand-off wait expired (code %d); the result is not valid", what,
+                         code);
+    }
+    return PQP_OK;
 }
 
 // Capture `n` dependent updates P.Y -> P.Yb -> P.Y ... into *exec (plus a
@@ -516,6 +538,17 @@ int ensure_persist_split(pqp_problem& P, hipStream_t s) {
     return PQP_OK;
 }
 
+// Which solver the last single-problem solve ran (pqp_tune_last_path), and
+// how many persistent launches fell back to the relay / graph path.
+enum SolvePath : int {
+    kPathFixedPersist = 1, kPathFixedRelay = 2, kPathConvergePersist = 3, kPathConvergeWide = 4, kPathOneWorkgroup = 5
+};
+int g_last_path = 0;
+long long g_persist_fallbacks = 0;
+// problem_run_*_persist: a wait of the persistent launch expired (its
+// workgroups were not all resident); the caller falls back
+constexpr int kPersistStalled = 1;
+
 int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     PQP_TRY(ensure_persist_split(P, s));
@@ -530,24 +563,35 @@ int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, 
         int herr = 0;
         PQP_HIP(hipMemcpyAsync(&herr, err, sizeof herr, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
-        if (herr)
-            return set_error(PQP_ERR_HIP, "persistent fixed-mode update: workgroup hand-off timed out (code %d); "
-                             "its %d workgroups must be resident at once", herr, (2 * N + 31) / 32);
+        if (herr) {  // not all workgroups resident (other work on the device): fall back
+            set_error(PQP_ERR_HIP, "persistent fixed-mode update: workgroup hand-off timed out (code %d); "
+                      "its %d workgroups must be resident at once", herr, (2 * N + 31) / 32);
+            return kPersistStalled;
+        }
         done += n;
     }
     PQP_HIP(hipStreamSynchronize(s));
     out.h = updates + 1;
     out.status = kStatusDone;
+    g_last_path = kPathFixedPersist;
     return PQP_OK;
 }
 
 int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     const long long updates = num_iter > 1 ? num_iter - 1 : 0;  // while(h < NUM_ITER)
-    if (!g_persist_off && N <= persist_max_n()) return problem_run_fixed_persist(P, updates, out, s);
+    // one persistent launch when its workgroups can all be resident; if one of
+    // its waits still expires (CUs held by other work), the solve restarts on
+    // the graph-replayed relay below (fixed mode restarts from Y = 1000)
+    if (!g_persist_off && N <= persist_max_n() && split_persist_fits(N)) {
+        const int rc = problem_run_fixed_persist(P, updates, out, s);
+        if (rc != kPersistStalled) return rc;
+        ++g_persist_fallbacks;
+    }
     const int lw = pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
-    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8) | ((int)use_lean(N, N) << 16);
+    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8) | ((int)use_lean(N, N) << 16) |
+                        ((int)(g_relay_spin_max != kRelaySpinMax) << 20);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
         P.chunk_ready = false;
@@ -565,9 +609,12 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
     for (long long c = 0; c < full; ++c) PQP_HIP(hipGraphLaunch(P.chunk_graph, s));
     if (rem > 0) PQP_HIP(hipGraphLaunch(P.graph, s));
-    PQP_HIP(hipStreamSynchronize(s));
+    int herr = 0;
+    PQP_HIP(hipMemcpyAsync(&herr, P.rerr.p, sizeof herr, hipMemcpyDeviceToHost, s));
+    PQP_TRY(relay_error_check(P.rerr, &herr, s, "fixed-mode relay update"));
     out.h = updates + 1;
     out.status = kStatusDone;
+    g_last_path = kPathFixedRelay;
     return PQP_OK;
 }
 
@@ -589,7 +636,10 @@ bool converge_persist_fits(int N, int M) {
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) return false;
-    return G <= cus && converge_persist_lds_bytes(N, M) <= (size_t)lds;
+    if (converge_persist_lds_bytes(N, M) > (size_t)lds) return false;
+    if (g_persist_fit_cus > 0) cus = g_persist_fit_cus;
+    // every workgroup of the launch resident at once (its roles wait on each other)
+    return (long long)converge_persist_per_cu(N, M) * cus >= G;
 }
 
 int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
@@ -649,9 +699,11 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
         PQP_HIP(hipMemcpyAsync(&st, dst, sizeof st, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipMemcpyAsync(&herr, L.err, sizeof herr, hipMemcpyDeviceToHost, s));
         PQP_HIP(hipStreamSynchronize(s));
-        if (herr)
-            return set_error(PQP_ERR_HIP, "persistent converge launch: a wait timed out (code %d); its %d workgroups "
-                             "must be resident at once", herr, converge_persist_wgs(N, M, nullptr));
+        if (herr) {  // not all workgroups resident: the caller re-runs the solve on the graph chain
+            set_error(PQP_ERR_HIP, "persistent converge launch: a wait timed out (code %d); its %d workgroups "
+                      "must be resident at once", herr, converge_persist_wgs(N, M, nullptr));
+            return kPersistStalled;
+        }
         if (st.status != kStatusContinue) break;
         u0 = st.h - 1;  // the next launch starts from the iterate this one left in P.Y
     }
@@ -660,6 +712,7 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
     out.status = st.status;
     out.have_costs = st.have_costs;
     out.last_stop = 0;
+    g_last_path = kPathConvergePersist;
     if (st.have_costs) {
         out.Jp = st.Jp;
         out.Jd = st.Jd;
@@ -669,9 +722,13 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
 
 constexpr int kWideChunk = 16;      // even: each replay starts and ends with the iterate in P.Y
 constexpr int kWideFirstChunk = 2;  // the first replay of a solve
-int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s) {
+int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipStream_t s, bool try_persist = true) {
     const int N = P.N, M = P.M;
-    if (converge_persist_fits(N, M)) return problem_run_converge_persist(P, max_updates, out, s);
+    if (try_persist && converge_persist_fits(N, M)) {
+        const int rc = problem_run_converge_persist(P, max_updates, out, s);
+        if (rc != kPersistStalled) return rc;
+        ++g_persist_fallbacks;  // converge mode restarts from Y = 1000 on the graph chain
+    }
     const int lw = pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
     if (!P.QinvT.p) {
@@ -689,8 +746,9 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     int* flag = static_cast<int*>(P.wflag.p);
     long long* cap = static_cast<long long*>(P.wcap.p);
-    const long long key = ((long long)use_lean(N, N) << 24) ^ ((long long)g_wide_flags << 16) ^
-                          ((long long)g_split_kind << 8) ^ lw;  // cap: device word
+    const long long key = ((long long)(g_relay_spin_max != kRelaySpinMax) << 32) ^ ((long long)use_lean(N, N) << 24) ^
+                          ((long long)g_wide_flags << 16) ^ ((long long)g_split_kind << 8) ^ lw;  // cap: device word
+    int* rerr = static_cast<int*>(P.rerr.p);
     if (!P.wgraph || P.wgraph_key != key) {
         if (P.wgraph) {
             (void)hipGraphExecDestroy(P.wgraph);
@@ -720,16 +778,19 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
             j1.job[0] = GemvJob{P.Gp.f(), cur, P.tM.f(), P.Fp.f(), M, N, M, kEpiAdd};
             j1.job[1] = GemvJob{P.Qd.f(), cur, P.tq.f(), nullptr, N, N, N, kEpiPlain};
             j1.gate = &dst->status;
+            j1.err = rerr;
             if ((e = launch_gemv_relay(j1, s)) != hipSuccess) return e;
             GemvJobs j2{};  // U = -(Qp_inv tmp) (:357-358)
             j2.job[0] = GemvJob{P.QinvT.f(), P.tM.f(), P.U.f(), nullptr, M, M, M, kEpiNeg};
             j2.gate = &dst->status;
+            j2.err = rerr;
             if ((e = launch_gemv_relay(j2, s)) != hipSuccess) return e;
             GemvJobs j3{};  // checkFeas (:632-641) and U'Qp (computeCost, Jp)
             j3.job[0] = GemvJob{P.GpT.f(), P.U.f(), P.gu.f(), P.Kp.f(), N, M, N, kEpiFeas};
             j3.job[1] = GemvJob{P.Qp.f(), P.U.f(), P.tu.f(), nullptr, M, M, M, kEpiPlain};
             j3.gate = &dst->status;
             j3.flag = flag;
+            j3.err = rerr;
             if ((e = launch_gemv_relay(j3, s)) != hipSuccess) return e;
             const WideArgs w{dst, flag, P.tq.f(), P.tu.f(), cur, P.U.f(), P.Fd.f(), P.Fp.f(), P.Md.f(), P.Mp.f(),
                              N, M, cap};
@@ -779,6 +840,10 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     }
     if ((st.h - 1) & 1)  // odd number of updates: the iterate is in Yb
         PQP_HIP(hipMemcpyAsync(P.Y.p, P.Yb.p, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+    int herr = 0;
+    PQP_HIP(hipMemcpyAsync(&herr, rerr, sizeof herr, hipMemcpyDeviceToHost, s));
+    PQP_TRY(relay_error_check(P.rerr, &herr, s, "converge-mode relay chain"));
+    g_last_path = kPathConvergeWide;
     out.h = st.h;
     out.status = st.status;
     out.have_costs = st.have_costs;
@@ -799,8 +864,15 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
         // at 32/16 against 2.3 on the persistent launch); from n_dual 48 up the
         // persistent launch wins (scripts/converge_crossover.py)
         const bool tiny = N <= 32 && M <= 32 && !g_force_small;
-        if (!tiny && converge_persist_fits(N, M)) return problem_run_converge_persist(P, max_updates, out, s);
-        if (N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0)) return problem_run_wide(P, max_updates, out, s);
+        const bool wide_ok = N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0);
+        if (!tiny && converge_persist_fits(N, M)) {
+            const int rc = problem_run_converge_persist(P, max_updates, out, s);
+            if (rc != kPersistStalled) return rc;
+            ++g_persist_fallbacks;  // the solve restarts from Y = 1000 below
+            if (wide_ok) return problem_run_wide(P, max_updates, out, s, false);
+        } else if (wide_ok) {
+            return problem_run_wide(P, max_updates, out, s);
+        }
     }
     if (!P.small) PQP_TRY(ensure_single(P, s));
     SolveState& st = *P.hst;
@@ -853,6 +925,7 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
     out.status = st.status;
     out.have_costs = st.have_costs;
     out.last_stop = st.last_stop;
+    g_last_path = kPathOneWorkgroup;
     if (st.have_costs) {
         out.Jp = st.Jp;
         out.Jd = st.Jd;
@@ -1196,6 +1269,8 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
     b->N = N;
     b->row0 = row0;
     b->rows = rows;
+    PQP_TRY(b->err.alloc(sizeof(int)));
+    PQP_HIP(hipMemsetAsync(b->err.p, 0, sizeof(int), s));
     if (rows > 0) {
         DevBuf theta;
         PQP_TRY(theta.floats(rows));
@@ -1227,11 +1302,21 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
 int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void* stream) {
     if (!b || !d_Y || (b->rows > 0 && !d_Y_rows)) return set_error(PQP_ERR_ARG, "pqp_rowblock_update: null argument");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    int* err = static_cast<int*>(b->err.p);
     if (b->lean)
-        PQP_HIP(launch_lean_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s));
+        PQP_HIP(launch_lean_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s, nullptr, err));
     else
-        PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s));
+        PQP_HIP(launch_split_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s, nullptr,
+                                    err));
     return PQP_OK;
+}
+
+int pqp_rowblock_check(pqp_rowblock* b, void* stream) {
+    if (!b) return set_error(PQP_ERR_ARG, "pqp_rowblock_check: null block");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int herr = 0;
+    PQP_HIP(hipMemcpyAsync(&herr, b->err.p, sizeof herr, hipMemcpyDeviceToHost, s));
+    return relay_error_check(b->err, &herr, s, "pqp_rowblock_update");
 }
 
 int pqp_rowblock_destroy(pqp_rowblock* b) {
@@ -1718,6 +1803,23 @@ extern "C" int pqp_tune_persist_trace(void* d_trace, int updates) {
     pqp::g_persist_trace = updates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
     pqp::g_persist_trace_n = updates;
     return PQP_OK;
+}
+
+extern "C" int pqp_tune_persist_fit_cus(int cus) {
+    const int old = pqp::g_persist_fit_cus;
+    pqp::g_persist_fit_cus = cus > 0 ? cus : 0;
+    return old;
+}
+
+extern "C" int pqp_tune_last_path(long long* fallbacks) {
+    if (fallbacks) *fallbacks = pqp::g_persist_fallbacks;
+    return pqp::g_last_path;
+}
+
+extern "C" int pqp_tune_relay_spin_max(int polls) {
+    const int old = pqp::g_relay_spin_max;
+    pqp::g_relay_spin_max = polls == 0 ? pqp::kRelaySpinMax : polls;
+    return old;
 }
 
 extern "C" int pqp_tune_lean_min_n(int n) {

@@ -655,6 +655,18 @@ hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Q
     return hipGetLastError();
 }
 
+// Workgroups of k_converge_persist one CU can hold at once (LDS-bound: 1),
+// for the residency check of the host (converge_persist_fits).
+int converge_persist_per_cu(int N, int M) {
+    const int W = waves_of(split_kblocks(N > M ? N : M));
+    const int threads = 64 * (W > kDecW ? W : kDecW);
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_converge_persist), threads,
+                                                     converge_persist_lds_bytes(N, M)) != hipSuccess)
+        return 0;
+    return per;
+}
+
 hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s) {
     int g[4];
     const int G = converge_persist_wgs(L.N, L.M, g);

@@ -20,6 +20,34 @@ __host__ __device__ __forceinline__ float max_ref(float a, float b) { return (a 
 constexpr double kTol = 1e-6;
 
 // ---------------------------------------------------------------------------
+// Relay hand-off wait (k_split_relay, k_lean_relay, k_gemv_relay): spin until
+// every lane's 64-bit LDS word {sequence, bits(running sum)} carries sequence
+// g.  Bounded, so a broken hand-off cannot hang the GPU; an expired wait sets
+// `stale` (a register), and the kernel ORs it into the caller's sticky error
+// word once, at exit -- the host turns that into PQP_ERR_HIP instead of
+// returning wrong sums.  spin_max < 0 expires every wait (tests of the error
+// path only); the default budget is kRelaySpinMax (pqp_launch.h).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long relay_wait(unsigned long long* slot, int lane, int g, int spin_max,
+                                                         bool& stale) {
+    // the loop keeps the one-compare exit of a plain bounded spin (a second
+    // exit branch per poll measured 6-9 % slower on chain-bound blocks); the
+    // expiry is derived from the counter after the loop
+    unsigned long long h;
+    int spin = 0;
+    for (;; ++spin) {
+        h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__all((int)(h >> 32) == g) || spin > spin_max) break;
+    }
+    stale |= spin > spin_max;
+    return h;
+}
+// once per wave, at kernel exit (vector atomic; no store in the wait loop)
+__device__ __forceinline__ void relay_report(bool stale, int* err, int lane) {
+    if (stale && err && lane == 0) atomicOr(err, 1);
+}
+
+// ---------------------------------------------------------------------------
 // Counter-based synthetic generator.  MUST stay identical to
 // oracle/pqp_oracle.c (orc_hash32 / orc_synth_key / orc_synth_bits / orc_u01).
 // ---------------------------------------------------------------------------

@@ -468,7 +468,8 @@ template <int W, int S>
 __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                         int N, int rows, int row0, int lw,
                                                         const float* __restrict__ Yin, float* __restrict__ Yout,
-                                                        const int* __restrict__ gate) {
+                                                        const int* __restrict__ gate, int* __restrict__ err,
+                                                        int spin_max) {
     if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
     // LDS: [64] hand-off words, then y [4*KB]
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -524,6 +525,7 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
     }
     __syncthreads();
     float acc = 0.0f;
+    bool stale = false;
     for (int g = w; g < G; g += W) {
         // products of this segment (packed multiplies, each product rounded
         // exactly as q * y), overwriting the packets; y is read from LDS four
@@ -548,12 +550,8 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
         }
         // wait until every lane's hand-off word carries sequence g (the sum
         // and its sequence number travel in one 64-bit LDS word).  Bounded:
-        // a broken hand-off ends with wrong sums instead of a hang.
-        unsigned long long h;
-        for (int spin = 0;; ++spin) {
-            h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
-        }
+        // an expired wait is reported through *err at exit, not hung on.
+        const unsigned long long h = relay_wait(slot, lane, g, spin_max, stale);
         __builtin_amdgcn_s_setprio(3);
         acc = __uint_as_float((unsigned)h);
 #pragma unroll
@@ -576,6 +574,7 @@ __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict_
             Yout[i] = v / den * ys[row0 + i];  // :594
         }
     }
+    relay_report(stale, err, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -628,7 +627,8 @@ template <int W, int S>
 __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__ LP, const float* __restrict__ aux,
                                                        int N, int rows, int row0, int lw,
                                                        const float* __restrict__ Yin, float* __restrict__ Yout,
-                                                       const int* __restrict__ gate) {
+                                                       const int* __restrict__ gate, int* __restrict__ err,
+                                                       int spin_max) {
     if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
     // LDS: [64] hand-off words, then y [4*G*S]
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -685,6 +685,7 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
     // exact), so every form below is the den formula on qs
     const unsigned sgn = side ? 0u : 0x80000000u;
     float acc = 0.0f;
+    bool stale = false;
     for (int g = w; g < G; g += W) {
         const int kbase = 4 * g * S;
         const bool lit = kbase < d0 + rp && kbase + 4 * S > d0;  // a diagonal of this workgroup is in here
@@ -753,11 +754,7 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
             form(std::integral_constant<int, 1>{});
         else
             form(std::integral_constant<int, 0>{});
-        unsigned long long h;
-        for (int spin = 0;; ++spin) {
-            h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
-        }
+        const unsigned long long h = relay_wait(slot, lane, g, spin_max, stale);
         __builtin_amdgcn_s_setprio(3);
         acc = __uint_as_float((unsigned)h);
 #pragma unroll
@@ -777,8 +774,10 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
         const float den = __shfl_xor(v, 1);  // the whole wave is here
         if (!side && live) Yout[r] = v / den * ys[row0 + r];  // updY :594
     }
+    relay_report(stale, err, lane);
 }
 
+int g_relay_spin_max = kRelaySpinMax;  // tuning: hand-off wait budget (< 0 expires every wait: error-path tests)
 int g_lean_min_n = 4096;  // tuning: k_lean_relay for blocks of rows x N >= g_lean_min_n^2 entries
 bool use_lean(int N, int rows) {
     return g_lean_min_n > 0 && (long long)rows * N >= (long long)g_lean_min_n * g_lean_min_n;
@@ -801,13 +800,13 @@ hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const 
     return hipGetLastError();
 }
 hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows, int row0, int lw, const float* Yin,
-                              float* Yout, hipStream_t s, const int* gate) {
+                              float* Yout, hipStream_t s, const int* gate, int* err) {
     if (rows <= 0) return hipSuccess;
     constexpr int W = 8, S = kLeanS;
     const int G = (split_kblocks(N) + S - 1) / S;
     const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);
     hipLaunchKernelGGL((k_lean_relay<W, S>), dim3(cdiv(2LL * rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows, row0,
-                       lw, Yin, Yout, gate);
+                       lw, Yin, Yout, gate, err, g_relay_spin_max);
     return hipGetLastError();
 }
 
@@ -844,22 +843,22 @@ int g_split_kind = 0;  // tuning: 0 auto (relay W8 S16), 1 k_split_update, 2 rel
 
 template <int W, int S>
 static void launch_relay(const float* SP, const float* fdpn, int N, int rows, int row0, int lw, const float* Yin,
-                         float* Yout, hipStream_t s, const int* gate) {
+                         float* Yout, hipStream_t s, const int* gate, int* err) {
     const int G = (split_kblocks(N) + S - 1) / S;
     const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);  // y to the end of the last segment
     hipLaunchKernelGGL((k_split_relay<W, S>), dim3(split_wgs(rows, lw)), dim3(64 * W), lds, s, SP, fdpn, N, rows,
-                       row0, lw, Yin, Yout, gate);
+                       row0, lw, Yin, Yout, gate, err, g_relay_spin_max);
 }
 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
-                               const float* Yin, float* Yout, hipStream_t s, const int* gate) {
+                               const float* Yin, float* Yout, hipStream_t s, const int* gate, int* err) {
     if (rows <= 0) return hipSuccess;
     switch (g_split_kind) {
         case 1: break;
-        case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
-        case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
-        case 4: launch_relay<16, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
-        default: launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate); return hipGetLastError();
+        case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
+        case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
+        case 4: launch_relay<16, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
+        default: launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
     }
     const size_t lds = split_lds_bytes(N);
     // one wave per CU with most of the register file as a 2-stage load buffer:

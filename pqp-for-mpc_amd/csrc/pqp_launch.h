@@ -64,9 +64,14 @@ hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_build_split(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows,
                               int row0, int lw, float* SP, float* fdpn, hipStream_t s);
 hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* theta, hipStream_t s);
-// gate: optional; the launch does nothing unless *gate == kStatusContinue
+// gate: optional; the launch does nothing unless *gate == kStatusContinue.
+// err: optional sticky device word; a relay hand-off wait that expired ORs 1
+// into it (the relay kernels; the streaming k_split_update has no hand-off)
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
-                               const float* Yin, float* Yout, hipStream_t s, const int* gate = nullptr);
+                               const float* Yin, float* Yout, hipStream_t s, const int* gate = nullptr,
+                               int* err = nullptr);
+constexpr int kRelaySpinMax = 1 << 20;  // relay hand-off wait budget in polls (~0.1-1 s)
+extern int g_relay_spin_max;            // tuning: the budget in use
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
 // packets of 4 k per row side in the split layout (k padded to a multiple of 4)
 __host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
@@ -77,6 +82,8 @@ size_t persist_lds_bytes(int N);
 hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,
                                 unsigned long long* gran, int* err, hipStream_t s);
 extern int g_persist_off;
+bool split_persist_fits(int N);  // all of k_split_persist's workgroups co-resident on this device
+extern int g_persist_fit_cus;    // tuning: CU count the residency checks assume (0: the device's)
 extern unsigned long long* g_persist_trace;  // tuning: device buffer of 4 * waves * g_persist_trace_n words
 extern int g_persist_trace_n;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
@@ -91,7 +98,7 @@ int lean_pick_lw(int rows);
 hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const float* Fd, int N, int rows, int row0,
                              int lw, float* LP, float* aux, hipStream_t s);
 hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows, int row0, int lw, const float* Yin,
-                              float* Yout, hipStream_t s, const int* gate = nullptr);
+                              float* Yout, hipStream_t s, const int* gate = nullptr, int* err = nullptr);
 int split_pick_lw(int rows);                   // lanes per workgroup for a block of `rows`
 size_t split_lds_bytes(int N);         // k_split_update's LDS (the full y)
 // rows [row0, row0 + rows) of synthetic problem `inst` (row-major, ld >= N,
@@ -137,6 +144,8 @@ struct GemvJobs {
     int wgs0;                // set by the launcher
     const int* gate;         // optional: skip unless *gate == kStatusContinue
     int* flag;               // kEpiFeas: cleared to 0 by an infeasible row
+    int* err;                // optional sticky word: an expired hand-off wait ORs 1 into it
+    int spin_max;            // set by the launcher (g_relay_spin_max)
 };
 hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s);
 hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s);
@@ -167,6 +176,7 @@ struct ConvergeLaunch {
 };
 int converge_persist_wgs(int N, int M, int* g);  // workgroups of the launch (0: not applicable)
 size_t converge_persist_lds_bytes(int N, int M);
+int converge_persist_per_cu(int N, int M);  // k_converge_persist workgroups per CU (occupancy API)
 size_t converge_ring_words(int N, int M);
 size_t converge_stage_floats(int N, int M, int stage);  // stage 1..3 packet arrays
 hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Qinv, const float* Qp, int N, int M,

@@ -272,6 +272,25 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     }
 }
 
+int g_persist_fit_cus = 0;  // tuning: CU count the residency check assumes (0: the device's)
+
+// Can all G workgroups of k_split_persist be resident at once?  The launch's
+// waits need every producer running; a grid that cannot be co-resident would
+// only end by its deadline.  Occupancy of this kernel (LDS-bound: one per CU)
+// times the CUs, against G.
+bool split_persist_fits(int N) {
+    if (N < 1 || N > persist_max_n()) return false;
+    const int G = (2 * N + kPLanes - 1) / kPLanes, threads = 64 * persist_waves(N);
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (g_persist_fit_cus > 0) cus = g_persist_fit_cus;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_split_persist), threads,
+                                                     persist_lds_bytes(N)) != hipSuccess)
+        return false;
+    return (long long)per * cus >= G;
+}
+
 hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,
                                 unsigned long long* gran, int* err, hipStream_t s) {
     if (updates <= 0) return hipSuccess;

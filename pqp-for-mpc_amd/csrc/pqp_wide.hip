@@ -158,6 +158,7 @@ __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
     }
     __syncthreads();
     float acc = 0.0f;
+    bool stale = false;
     for (int g = w; g < G; g += W) {
 #pragma unroll
         for (int t0 = 0; t0 < S; t0 += 16) {  // x read 16 values at a time so the LDS reads overlap
@@ -180,11 +181,7 @@ __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
                 asm volatile("" : "+v"(q[t]), "+v"(q[t + 1]), "+v"(q[t + 2]), "+v"(q[t + 3]));
             }
         }
-        unsigned long long h;
-        for (int spin = 0;; ++spin) {
-            h = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__all((int)(h >> 32) == g) || spin > (1 << 20)) break;
-        }
+        const unsigned long long h = relay_wait(slot, lane, g, J.spin_max, stale);
         __builtin_amdgcn_s_setprio(3);
         acc = __uint_as_float((unsigned)h);
 #pragma unroll
@@ -207,6 +204,7 @@ __global__ void __launch_bounds__(64 * W) k_gemv_relay(GemvJobs J) {
             default: jb.out[j] = acc;
         }
     }
+    relay_report(stale, J.err, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -295,6 +293,7 @@ static hipError_t gemv_launch(GemvJobs J, int n_in, hipStream_t s) {
 hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s) {
     GemvJobs J = jobs;
     J.wgs0 = cdivw(J.job[0].n_out, 64);
+    J.spin_max = g_relay_spin_max;
     int n_in = J.job[0].n_in;
     if (J.job[1].A && J.job[1].n_in > n_in) n_in = J.job[1].n_in;
     return (g_wide_flags & 2) ? gemv_launch<8, 64>(J, n_in, s) : gemv_launch<8, 32>(J, n_in, s);

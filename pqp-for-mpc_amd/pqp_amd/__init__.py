@@ -27,7 +27,8 @@ from pathlib import Path
 import numpy as np
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libpqp.so"
+# PQP_LIB: another build of the library (A/B timing scripts only)
+LIB_PATH = Path(os.environ["PQP_LIB"]) if os.environ.get("PQP_LIB") else PKG / "libpqp.so"
 
 PQP_OK = 0
 PQP_ERR_ARG, PQP_ERR_HIP, PQP_ERR_ALLOC, PQP_ERR_IO, PQP_ERR_NOT_CONVERGED, PQP_ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
@@ -82,6 +83,7 @@ SIGNATURES = {
                         + [_vp]),
     "pqp_rowblock_create": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(C.c_void_p)]),
     "pqp_rowblock_update": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "pqp_rowblock_check": (C.c_int, [_vp, _vp]),
     "pqp_rowblock_destroy": (C.c_int, [_vp]),
     "pqp_synth_rows": (C.c_int, [C.c_uint32, C.c_longlong] + [C.c_int] * 4 + [_vp, C.c_int, _vp, _vp, _vp]),
     # include/pqp_tuning.h
@@ -91,6 +93,9 @@ SIGNATURES = {
     "pqp_tune_persist": (C.c_int, [C.c_int]),
     "pqp_tune_converge_persist": (C.c_int, [C.c_int]),
     "pqp_tune_lean_min_n": (C.c_int, [C.c_int]),
+    "pqp_tune_relay_spin_max": (C.c_int, [C.c_int]),
+    "pqp_tune_persist_fit_cus": (C.c_int, [C.c_int]),
+    "pqp_tune_last_path": (C.c_int, [C.POINTER(C.c_longlong)]),
     "pqp_tune_converge_chunk": (C.c_int, [C.c_int]),
     "pqp_tune_converge_trace": (C.c_int, [_vp, C.c_int]),
     "pqp_tune_wave_min_b": (C.c_int, [C.c_int]),
@@ -128,6 +133,8 @@ def lib() -> C.CDLL:
             pass
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("PQP_LIB") and not hasattr(L, name):
+                continue  # an older build under A/B: entry points it lacks stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -627,6 +634,12 @@ class RowBlock:
         """Y_rows[:rows] = updateY2(Y)[row0:row0+rows] (async)."""
         _check(lib().pqp_rowblock_update(self._h, C.c_void_p(Y.data_ptr()),
                                          C.c_void_p(Y_rows.data_ptr()) if self.rows > 0 else None, self._s()))
+
+    def check(self):
+        """Synchronize and raise PQPError if an update since the last check
+        hit an expired hand-off wait inside the kernel (its rows are then not
+        valid; pqp_rowblock_check)."""
+        _check(lib().pqp_rowblock_check(self._h, self._s()))
 
     def close(self):
         if getattr(self, "_h", None) and _LIB is not None:

@@ -62,10 +62,19 @@ class RowShardedSolver:
             self.dist.all_gather_into_tensor(self.Y2, self.local, group=self.group)
         self.Y, self.Y2 = self.Y2, self.Y
 
+    def check(self):
+        """Raise if any of this rank's block updates since the last check
+        reported an expired in-kernel wait (blocks without a ``check`` -- the
+        CPU stand-ins of the tests -- cannot fail that way)."""
+        chk = getattr(self.block, "check", None)
+        if chk is not None:
+            chk()
+
     def run(self, num_iter: int = 1000, y0: float = 1000.0):
         """The reference's fixed mode: Y = 1000, then num_iter-1 updates
         (``while (h < NUM_ITER)``).  Returns the final Y (N) on every rank."""
         self.Y.fill_(y0)
         for _ in range(max(0, int(num_iter) - 1)):
             self.step()
+        self.check()
         return self.Y[: self.N]
