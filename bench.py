@@ -59,6 +59,22 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 KERNEL = "k_batch_iterate<256,16,nt>"
 
 
+def hot_kernel_hash() -> str:
+    """SHA-256 (16 hex) of the hot kernel's source -- the text between the
+    <hot-kernel> markers of pqp_kernels.hip, plus the library's compile flags.
+    profiles/pmc_traffic.json records carry the hash they were measured with;
+    a record whose hash differs is stale and is not reported as `traffic`."""
+    import hashlib
+    import re
+
+    src = (ROOT / "pqp-for-mpc_amd" / "csrc" / "pqp_kernels.hip").read_text()
+    m = re.search(r"// <hot-kernel>.*?// </hot-kernel>", src, re.S)
+    flags = [ln for ln in (ROOT / "pqp-for-mpc_amd" / "Makefile").read_text().splitlines()
+             if ln.startswith("HIPFLAGS")]
+    text = (m.group(0) if m else src) + "\n".join(flags)
+    return hashlib.sha256(text.encode()).hexdigest()[:16]
+
+
 def alg_bytes(n: int) -> int:
     """Algorithmic HBM bytes per problem-iteration: Qd read once (the split
     matrices and Theta are derived in registers) + theta, Fd, y_in, y_out."""
@@ -76,6 +92,8 @@ def parse():
                     help="iterations (steps) per kernel launch; the iterate stays in LDS between them")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--cpu-instances", type=int, default=16,
+                    help="distinct problems the CPU baseline cycles through (>= 8, DRAM-resident)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bundled", action="store_true")
     ap.add_argument("--rowshard-n", type=int, default=16384, help="n_dual of the row-sharded leg (0: skip)")
@@ -83,26 +101,55 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n: int, seconds: float, seed: int, tol_cases: dict | None = None) -> dict:
-    """Time the reference's updateY2 on one problem of the same workload."""
+def host_cpu() -> dict:
+    """The host's CPU model and the CPUs this process may use."""
+    model = "unknown"
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"model": model, "logical_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
+def cpu_baseline(n: int, seconds: float, instances: list, tol_cases: dict | None = None,
+                 threads: int = 16) -> dict:
+    """The reference's updateY2 on `instances` (a list of (Qd, Fd) host
+    arrays: distinct problems of the bench's own workload, copied from the
+    GPU batch), DRAM-resident (8 MiB of split matrices each) and updated
+    round-robin for about `seconds`, one thread; the rate extrapolates
+    linearly to the batch (instances are independent).  Beside it, an
+    all-core row (OpenMP over the host CPUs this process may use, capped at
+    `threads`) of the bit-exact restatement, labelled "not reference"."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
 
     from oracle import REF_SO, Oracle, Reference
 
     orc = Oracle()
-    P = orc.synth_problem(seed, 0, n, n // 2, with_qp=False)
+    cpu = host_cpu()
+    K = len(instances)
+    mib = K * 8 * n * n / 2**20
     if REF_SO.exists():
         ref = Reference()
-        S = ref.split(P["Qd"], P["Fd"], n)
-        Y = np.full(n, 1000.0, np.float32)
+        S = [ref.split(Qd, Fd, n) for Qd, Fd in instances]
+        Fds = [np.ascontiguousarray(Fd, np.float32) for _, Fd in instances]
+        Ys = [np.full(n, 1000.0, np.float32) for _ in range(K)]
         ups, t0 = 0, time.perf_counter()
         while True:
-            Y = ref.update(Y, S, P["Fd"], n)
-            ups += 1
+            for j in range(K):
+                Ys[j] = ref.update(Ys[j], S[j], Fds[j], n)
+            ups += K
             el = time.perf_counter() - t0
             if el >= seconds:
                 break
+        del S
         kind = "reference"
         what = "oracle/_ref/libpqp_ref.so (PQP_CPU.c, gcc -O2 -ffp-contract=off) updateY2"
         # configs[0]: the bundled example through the reference's own input(),
@@ -124,17 +171,47 @@ def cpu_baseline(n: int, seconds: float, seed: int, tol_cases: dict | None = Non
                 ref_tol[name] = {"h": h, "ms": (time.perf_counter() - tb) * 1e3}
             bundled["iters_to_tol"] = ref_tol
     else:
-        per, _ = orc.time_updates(P["Qd"], P["Fd"], n, 3)
+        Qd, Fd = instances[0]
+        per, _ = orc.time_updates(Qd, Fd, n, 3)
         ups = max(3, int(seconds / max(per / 3, 1e-6)))
-        el, _ = orc.time_updates(P["Qd"], P["Fd"], n, ups)
+        el, _ = orc.time_updates(Qd, Fd, n, ups)
         kind = "port"
         what = "oracle/pqp_oracle.c (bit-exact restatement, -O2 -ffp-contract=off) updateY2"
+        K, mib = 1, 8 * n * n / 2**20
         bundled = None
     out = {"value": ups / el, "unit": "instance-iterations/s", "cores": 1, "kind": kind,
-           "sample": f"{what}: {ups} fixed-mode updates of 1 synthetic problem (n_dual={n}, M={n // 2}, seed "
-                     f"{seed}) in {el:.1f} s, 1 thread, setup excluded; host has {os.cpu_count()} logical CPUs"}
+           "sample": f"{what}: {ups} fixed-mode updates round-robin over {K} distinct synthetic problems of the "
+                     f"bench workload (n_dual={n}, M={n // 2}; {mib:.0f} MiB of split matrices, DRAM-resident) in "
+                     f"{el:.1f} s, 1 thread, setup excluded; the rate extrapolates linearly to the batch "
+                     f"(independent problems)",
+           "host_cpu": cpu}
     if bundled:
         out["bundled"] = bundled
+    # all-core row (not the reference: the bit-exact restatement over OpenMP)
+    thr = max(1, min(threads, cpu["usable_cpus"] or 1))
+    Kp = max(thr * 4, K)
+    reps = (Kp + K - 1) // K
+    qp = np.empty((Kp, n * n), np.float32)
+    qn = np.empty((Kp, n * n), np.float32)
+    fp = np.empty((Kp, n), np.float32)
+    fn = np.empty((Kp, n), np.float32)
+    for j in range(Kp):
+        Qd, Fd = instances[j % K]
+        th = orc.theta(Qd, n)
+        qp[j], qn[j] = orc.split_theta(Qd, th, n)
+        fp[j] = np.maximum(Fd, 0)  # matrixPos / matrixNeg (:703-704); Fd has no NaN / -0 here
+        fn[j] = np.maximum(-Fd, 0)
+    Y = np.full((Kp, n), 1000.0, np.float32)
+    rounds = 1
+    t1 = orc.time_updates_batch(Y, qp, qn, fp, fn, n, rounds, thr)
+    rounds = max(1, int(min(seconds, 15.0) / max(t1, 1e-6)))
+    t1 = orc.time_updates_batch(Y, qp, qn, fp, fn, n, rounds, thr)
+    out["all_cores"] = {"value": Kp * rounds / t1, "unit": "instance-iterations/s", "cores": thr,
+                        "kind": "port (OpenMP), not reference",
+                        "sample": f"oracle/pqp_oracle.c orc_update_split (bit-exact with PQP_CPU.c updateY2): "
+                                  f"{rounds} updates of each of {Kp} problems ({K} distinct, repeated {reps}x; "
+                                  f"{Kp * 8 * n * n / 2**30:.2f} GiB of split matrices) over {thr} threads in "
+                                  f"{t1:.1f} s"}
     return out
 
 
@@ -478,12 +555,17 @@ def main():
 
     per_launch_ms = kern_ms / launches
     achieved = alg_bytes(N) * B * C / (per_launch_ms * 1e-3) / 1e9 if launches else 0.0
-    traffic = None
+    traffic, traffic_src = None, "no PMC record for this shape"
+    khash = hot_kernel_hash()
     tf = ROOT / "profiles" / "pmc_traffic.json"
     if tf.exists():
         rec = json.loads(tf.read_text()).get(f"n{N}_b{B}_c{C}")
-        if rec:
+        if rec and rec.get("kernel_src_sha256") == khash:
             traffic = rec.get("hbm_bytes_per_launch")
+            traffic_src = f"profiles/pmc_traffic.json n{N}_b{B}_c{C} ({rec.get('source', '')})"
+        elif rec:
+            traffic_src = (f"stale: the PMC record was measured on kernel source {rec.get('kernel_src_sha256')}, "
+                           f"this tree's is {khash}; re-run scripts/gpu_profile.sh")
     result = {
         "metric": "PQP iterations/sec (and QP-instances/sec) at fixed n_dual",
         "value": B * world * K / elapsed,
@@ -503,7 +585,8 @@ def main():
                    "parallelism": f"problem-sharded x{world} (no data-path collective)"},
         "qp_instances_per_s_at_1000_iters": B * world * K / elapsed / 999.0,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel_src_sha256": khash, "kernel": KERNEL,
                      "alg_bytes_per_launch": alg_bytes(N) * B * C, "avg_launch_ms": per_launch_ms},
         "results_finite_nonneg": finite,
         "gather_ms": gather_ms,
@@ -526,7 +609,9 @@ def main():
             tol_cases = tol_problems(pqp_amd, Path(td))
         result["iters_to_tol"] = iters_to_tol_bench(pqp_amd, tol_cases)
     if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, seed, tol_cases)
+        # distinct problems of this very workload, from the GPU batch
+        inst = [(batch.qd_rowmajor(j), batch.Fd[j, :N].cpu().numpy()) for j in range(min(args.cpu_instances, B))]
+        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, inst, tol_cases)
         ref_tol = result["cpu_baseline"].get("bundled", {}).get("iters_to_tol")
         if ref_tol and "iters_to_tol" in result:
             result["iters_to_tol_identical_to_reference"] = all(

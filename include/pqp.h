@@ -157,8 +157,11 @@ int pqp_read_example(const char *dir, int m, int nd, int ns, float *Qp_inv, floa
  * `v % 3` (0 -> 0, 2 -> -1, otherwise +1, so a file -1 becomes +1).  With
  * glibc_kp != 0 the file's Kp is replaced, as the harness does, by
  * fabs(10.0*rand()/RAND_MAX) from glibc's unseeded rand() sequence.
- * Call with NULL arrays to get (*M_out, *N_out) first; Qp_inv is M x M dense.
- * (Host I/O; no GPU work.) */
+ * Call with NULL arrays to get (*M_out, *N_out) first; then call again with the
+ * arrays (Qp_inv is M x M dense) and *M_out / *N_out still holding those
+ * dimensions: a file whose header no longer matches them gives PQP_ERR_IO and
+ * nothing is written.  Headers beyond M, N <= 65536 (or N*M + M*M > 2^30) are
+ * rejected with PQP_ERR_IO.  (Host I/O; no GPU work.) */
 int pqp_read_testfile(const char *path, int glibc_kp, int *M_out, int *N_out, float *Qp_inv, float *Fp, float *Mp,
                       float *Gp, float *Kp);
 

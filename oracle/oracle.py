@@ -82,6 +82,8 @@ class Oracle:
         L.orc_synth_primal.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.c_int] + [_fp] * 5
         L.orc_time_updates.argtypes = [_fp, _fp, _fp, C.c_int, C.c_long]
         L.orc_time_updates.restype = C.c_double
+        L.orc_time_updates_batch.argtypes = [C.c_int] + [_fp] * 5 + [C.c_int, C.c_long, C.c_int]
+        L.orc_time_updates_batch.restype = C.c_double
 
     # -- primitives -------------------------------------------------------
     def matmul(self, A, tA, B, tB, a, b, c):
@@ -207,6 +209,12 @@ class Oracle:
         if with_qp:
             P["Qp"] = self.gauss_jordan(P["Qp_inv"], M)
         return P
+
+    def time_updates_batch(self, Y, Qp, Qn, Fp, Fn, N, rounds, threads):
+        """Seconds for `rounds` updates of each of the B problems of the
+        stacked split matrices (B x N x N), spread over OpenMP threads."""
+        B = Y.size // N
+        return float(self.lib.orc_time_updates_batch(B, _p(Y), _p(Qp), _p(Qn), _p(Fp), _p(Fn), N, rounds, threads))
 
     def time_updates(self, Qd, Fd, N, updates):
         """Seconds for `updates` reference-style updateY2 calls (split matrices stored)."""

@@ -435,3 +435,31 @@ double orc_time_updates(float *Y, const float *Qd, const float *Fd, int N, long 
     free(theta); free(Qp); free(Qn); free(Fp); free(Fn); free(nxt);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* All-core comparison row of bench.py's cpu_baseline (labelled "not
+ * reference"): `rounds` fixed-mode updates of each of B independent problems
+ * whose stored split matrices lie back to back (Qp/Qn: B x N x N, Fp/Fn/Y:
+ * B x N), the problems spread over `threads` OpenMP threads, each update the
+ * bit-exact orc_update_split (PQP_CPU.c:603-618).  Returns seconds. */
+double orc_time_updates_batch(int B, float *Y, const float *Qp, const float *Qn, const float *Fp, const float *Fn,
+                              int N, long rounds, int threads)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(threads)
+#endif
+    for (int b = 0; b < B; ++b) {
+        float *nxt = (float *)malloc(sizeof(float) * (size_t)N + 4);
+        float *y = Y + (size_t)b * N;
+        const size_t o = (size_t)b * N * N;
+        for (long r = 0; r < rounds; ++r) {
+            orc_update_split(nxt, y, Qp + o, Qn + o, Fp + (size_t)b * N, Fn + (size_t)b * N, N);
+            memcpy(y, nxt, sizeof(float) * N);
+        }
+        free(nxt);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    (void)threads;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -19,18 +19,6 @@
 
 namespace pqp {
 
-static thread_local std::string t_err;
-
-int set_error(int code, const char* fmt, ...) {
-    char buf[1024];
-    va_list ap;
-    va_start(ap, fmt);
-    std::vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    t_err = buf;
-    return code;
-}
-
 namespace {
 
 std::mutex g_mu;  // drop-in calls share the library stream and are serialized
@@ -934,7 +922,7 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
 }
 
 [[noreturn]] void die(const char* fn) {
-    std::fprintf(stderr, "libpqp: %s failed: %s\n", fn, t_err.c_str());
+    std::fprintf(stderr, "libpqp: %s failed: %s\n", fn, pqp_last_error());
     std::exit(EXIT_FAILURE);
 }
 
@@ -950,7 +938,6 @@ using namespace pqp;
 
 extern "C" {
 
-const char* pqp_last_error(void) { return t_err.c_str(); }
 int pqp_version(void) { return 100; }
 
 // ---------------------------------------------------------------------------
@@ -1042,9 +1029,9 @@ int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const floa
     pqp_problem* P = nullptr;
     PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &P));
     const int rc = pqp_problem_solve(P, mode, num_iter, max_updates, Y, U, h_out, Jp_out, Jd_out);
-    const std::string err = t_err;
+    const std::string err = pqp_last_error();
     pqp_problem_destroy(P);
-    t_err = err;
+    restore_error(err);
     return rc;
 }
 
@@ -1066,49 +1053,6 @@ int pqp_update_host(const float* Qd, const float* theta_diag, const float* Fd, c
     PQP_HIP(launch_batch_update(1, dQdT.f(), (long long)N * ldq, ldq, N, dth.f(), dFd.f(), N, dY.f(), dYn.f(), s));
     PQP_TRY(download(Y_next, dYn.p, N, s));
     PQP_HIP(hipStreamSynchronize(s));
-    return PQP_OK;
-}
-
-int pqp_read_example(const char* dir, int m, int nd, int ns, float* Qp_inv, float* Fp1, float* Fp2, float* Fp3,
-                     float* Mp1, float* Mp2, float* Mp3, float* Mp4, float* Mp5, float* Mp6, float* Gp, float* Kp,
-                     float* x, float* D) {
-    ExampleData e;
-    PQP_TRY(read_example(dir, m, nd, ns, e));
-    auto put = [](float* dst, const std::vector<float>& v) {
-        if (dst) std::memcpy(dst, v.data(), v.size() * sizeof(float));
-    };
-    put(Qp_inv, e.Qp_inv);
-    put(Fp1, e.Fp1);
-    put(Fp2, e.Fp2);
-    put(Fp3, e.Fp3);
-    put(Mp1, e.Mp1);
-    put(Mp2, e.Mp2);
-    put(Mp3, e.Mp3);
-    put(Mp4, e.Mp4);
-    put(Mp5, e.Mp5);
-    put(Mp6, e.Mp6);
-    put(Gp, e.Gp);
-    put(Kp, e.Kp);
-    put(x, e.x);
-    put(D, e.D);
-    return PQP_OK;
-}
-
-int pqp_read_testfile(const char* path, int glibc_kp, int* M_out, int* N_out, float* Qp_inv, float* Fp, float* Mp,
-                      float* Gp, float* Kp) {
-    if (!path) return set_error(PQP_ERR_ARG, "pqp_read_testfile: null path");
-    TestfileData t;
-    PQP_TRY(read_testfile(path, glibc_kp != 0, t));
-    if (M_out) *M_out = t.M;
-    if (N_out) *N_out = t.N;
-    auto put = [](float* dst, const std::vector<float>& v) {
-        if (dst) std::memcpy(dst, v.data(), v.size() * sizeof(float));
-    };
-    put(Qp_inv, t.Qp_inv);
-    put(Fp, t.Fp);
-    put(Mp, t.Mp);
-    put(Gp, t.Gp);
-    put(Kp, t.Kp);
     return PQP_OK;
 }
 

@@ -1,8 +1,9 @@
 // pqp_internal.h -- host-side internals shared by the libpqp translation units.
 #pragma once
-#include <hip/hip_runtime.h>
-
+// No HIP here: pqp_io.cpp and pqp_host.cpp build without it (tests/asan/).
+// PQP_HIP expands only where pqp_launch.h (hip_runtime.h) is included.
 #include <cstddef>
+#include <string>
 #include <vector>
 
 #include "../../include/pqp.h"
@@ -11,6 +12,7 @@ namespace pqp {
 
 // Record an error for pqp_last_error() and return `code`.
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void restore_error(const std::string& text);  // put back a saved pqp_last_error() text
 
 #define PQP_HIP(expr)                                                                                  \
     do {                                                                                               \

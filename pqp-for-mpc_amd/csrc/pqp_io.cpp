@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -38,6 +39,8 @@ static int read_transposed(const std::string& path, float* out, int outer, int i
 
 int read_example(const char* dir, int m, int nd, int ns, ExampleData& e) {
     if (!dir || m <= 0 || nd <= 0 || ns <= 0) return set_error(PQP_ERR_ARG, "read_example: bad arguments");
+    if (m > (1 << 14) || nd > (1 << 14) || ns > (1 << 14))
+        return set_error(PQP_ERR_ARG, "read_example: dimensions out of range (m=%d nd=%d ns=%d)", m, nd, ns);
     const int N = 4 * m;
     e.m = m;
     e.nd = nd;
@@ -121,6 +124,11 @@ class GlibcRand {
 // by testing/GPU unoptimized version/PQP_GPU_unoptimized.cu:751-794 and
 // testing/CPU version/PQP_CPU_test.c:936-978): "M N", M diagonal entries of
 // Qp_inv, M of Fp, Mp, N of Kp, then N x M integers for Gp.
+// Largest header the reader accepts: M, N <= 65536 and Gp (N x M) plus the
+// dense Qp_inv (M x M) within 2^30 floats (4 GiB of host memory).  The
+// reference's own sample files are (100, 400), (500, 1500), (800, 1200).
+constexpr long long kTestfileMaxDim = 1 << 16, kTestfileMaxFloats = 1LL << 30;
+
 int read_testfile(const char* path, bool glibc_kp, TestfileData& t) {
     FILE* f = std::fopen(path, "r");
     if (!f) return set_error(PQP_ERR_IO, "cannot open %s", path);
@@ -130,13 +138,24 @@ int read_testfile(const char* path, bool glibc_kp, TestfileData& t) {
     };
     int M = 0, N = 0;
     if (std::fscanf(f, "%d%d", &M, &N) != 2 || M <= 0 || N <= 0) return fail("header");
+    if (M > kTestfileMaxDim || N > kTestfileMaxDim ||
+        (long long)N * M + (long long)M * M > kTestfileMaxFloats) {
+        std::fclose(f);
+        return set_error(PQP_ERR_IO, "%s: header M=%d N=%d exceeds the reader's bounds (M, N <= %lld)", path, M, N,
+                         kTestfileMaxDim);
+    }
     t.M = M;
     t.N = N;
-    t.Qp_inv.assign((size_t)M * M, 0.0f);
-    t.Fp.assign(M, 0.0f);
-    t.Mp.assign(1, 0.0f);
-    t.Kp.assign(N, 0.0f);
-    t.Gp.assign((size_t)N * M, 0.0f);
+    try {
+        t.Qp_inv.assign((size_t)M * M, 0.0f);
+        t.Fp.assign(M, 0.0f);
+        t.Mp.assign(1, 0.0f);
+        t.Kp.assign(N, 0.0f);
+        t.Gp.assign((size_t)N * M, 0.0f);
+    } catch (const std::bad_alloc&) {
+        std::fclose(f);
+        return set_error(PQP_ERR_ALLOC, "%s: no host memory for M=%d N=%d", path, M, N);
+    }
     for (int i = 0; i < M; ++i)
         if (std::fscanf(f, "%f", &t.Qp_inv[(size_t)i * M + i]) != 1) return fail("Qp_inv");
     for (int i = 0; i < M; ++i)

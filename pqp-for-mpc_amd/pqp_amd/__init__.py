@@ -314,7 +314,8 @@ def read_testfile(path, glibc_kp: bool = True) -> dict:
     M, N = M.value, N.value
     arr = dict(Qp_inv=np.zeros(M * M, np.float32), Fp=np.zeros(M, np.float32), Mp=np.zeros(1, np.float32),
                Gp=np.zeros(N * M, np.float32), Kp=np.zeros(N, np.float32))
-    _check(lib().pqp_read_testfile(str(path).encode(), int(glibc_kp), None, None,
+    Mi, Ni = C.c_int(M), C.c_int(N)  # the dimensions the arrays were sized for
+    _check(lib().pqp_read_testfile(str(path).encode(), int(glibc_kp), C.byref(Mi), C.byref(Ni),
                                    *[_buf(arr[k]) for k in ("Qp_inv", "Fp", "Mp", "Gp", "Kp")]))
     arr.update(N=N, M=M)
     return arr

@@ -33,7 +33,11 @@ def main():
     fetch, nf = per_launch(fetch_csv, "FETCH_SIZE", skip)
     write, nw = per_launch(write_csv, "WRITE_SIZE", skip)
     alg = (4 * N * N + 16 * N) * B * C
-    rec = {"kernel": "k_batch_iterate<256,16,nt>", "launches_averaged": min(nf, nw),
+    sys.path.insert(0, str(ROOT))
+    from bench import hot_kernel_hash
+
+    rec = {"kernel": "k_batch_iterate<256,16,nt>", "kernel_src_sha256": hot_kernel_hash(),
+           "launches_averaged": min(nf, nw),
            "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write,
            "hbm_bytes_per_launch": (2 * fetch + write) * 1024, "alg_bytes_per_launch": alg,
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are KiB; gfx950 "
