@@ -163,6 +163,15 @@ def cpu_baseline(n: int, seconds: float, instances: list, tol_cases: dict | None
         tb = sorted(times)[len(times) // 2]
         bundled = {"converge_h": h, "converge_ms": tb * 1e3, "iter_per_s": h / tb,
                    "what": "PQP_CPU.c solveQuadraticDual on the bundled example (configs[0]), 1 thread"}
+        # the reference's convertToDual of ONE N = 1024, M = 512 problem with a
+        # dense Qp_inv (the setup_convert leg's problems), one thread
+        sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+        from pqp_amd import dense_qinv
+
+        Pp = orc.synth_primal(3, 0, n, n // 2)
+        tb = time.perf_counter()
+        ref.convert_to_dual(dense_qinv(3, n // 2), Pp["Gp"], Pp["Kp"], Pp["Fp"], Pp["Mp"], n, n // 2)
+        bundled_setup_s = time.perf_counter() - tb
         if tol_cases:  # iterations to tolerance of the reference on the converging problems
             ref_tol = {}
             for name, Pc in tol_cases.items():
@@ -187,6 +196,7 @@ def cpu_baseline(n: int, seconds: float, instances: list, tol_cases: dict | None
            "host_cpu": cpu}
     if bundled:
         out["bundled"] = bundled
+        out["setup_convert_s"] = bundled_setup_s
     # all-core row (not the reference: the bit-exact restatement over OpenMP)
     thr = max(1, min(threads, cpu["usable_cpus"] or 1))
     Kp = max(thr * 4, K)
@@ -297,6 +307,60 @@ def single_bench(pqp_amd, N: int = 1024, iters: int = 1000) -> dict:
     return {"n_dual": N, "iterations": iters, "ms_per_solve": dt * 1e3, "iter_per_s": (iters - 1) / dt,
             "alg_GBps_split_matrices": 8.0 * N * N * (iters - 1) / dt / 1e9,
             "note": "1 problem, fixed mode; per-iteration floor = one lane's N-long sequential sum"}
+
+
+def setup_bench(pqp_amd, N: int = 1024, M: int = 512, B: int = 64) -> dict:
+    """convertToDual (PQP_CPU.c:440-498) of B problems with a
+    DENSE Qp_inv on the GPU -- the setup GEMMs (Gp Qp_inv) and (Gp Qp_inv) Gp'
+    LDS-tiled, bit-identical to the reference (tests/test_gpu_setup.py)."""
+    import torch
+
+    L = pqp_amd.lib()
+    pb = pqp_amd.ProblemBatch(B, N, M)
+    pqp_amd._check(L.pqp_batch_synth_primal(3, 0, B, N, M, *[pb._p(getattr(pb, k)) for k in pb.PRIMAL], pb._s()))
+    pb.Qp_inv.copy_(torch.from_numpy(pqp_amd.dense_qinv(3, M)).cuda().expand(B, -1))
+    pb.convert_to_dual()  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pb.convert_to_dual()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    flops = B * (2.0 * N * M * M + 2.0 * N * N * M)
+    del pb
+    torch.cuda.empty_cache()
+    return {"problems": B, "n_dual": N, "m": M, "ms": dt * 1e3, "problems_per_s": B / dt,
+            "gemm_TFLOPs": flops / dt / 1e12,
+            "note": "pqp_batch_convert_to_dual, dense Qp_inv (k_matmul_tiled; no FMA, k in order per output); "
+                    "the reference's one-problem setup time is cpu_baseline.setup_convert_s"}
+
+
+def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> dict:
+    """converge mode of B synthetic problems at once
+    (pqp_batch_solve, terminate() before every update), capped at K updates
+    (the synthetic problems do not meet the exact gap test at this size).
+    One iteration = terminate() + updateY2 (PQP_CPU.c:716-725).  Qd is
+    bit-symmetric here, so terminate()'s Y'Qd rides in the update's pass."""
+    import torch
+
+    pb = pqp_amd.ProblemBatch.synthetic(1, 0, B, N)
+    M = pb.M
+    pb.solve(max_updates=1)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pb.solve(max_updates=K)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    h = pb.h
+    ok = bool((h == K + 1).all().item())
+    del pb
+    torch.cuda.empty_cache()
+    # algorithmic bytes per problem-iteration: Qd once (update + Y'Qd), Gp
+    # twice (Gp'Y, Gp U), Qp_inv and Qp once
+    alg = 4.0 * N * N + 8.0 * N * M + 8.0 * M * M
+    gbs = alg * B * K / dt / 1e9
+    return {"problems": B, "n_dual": N, "m": M, "updates": K, "ms": dt * 1e3, "instance_iter_per_s": B * K / dt,
+            "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS, "all_capped": ok,
+            "note": "k_solve_single, one workgroup per problem; timed call includes the state readback"}
 
 
 def _testing_file(name: str, tmpdir: Path) -> Path:
@@ -601,6 +665,8 @@ def main():
         result["mpc_batch"] = mpc_batch_bench(pqp_amd)
         result["single_n1024"] = single_bench(pqp_amd)
         result["single_converge"] = single_converge_bench(pqp_amd)
+        result["setup_convert"] = setup_bench(pqp_amd)
+        result["batch_converge"] = batch_converge_bench(pqp_amd)
     tol_cases = None
     if world == 1 and not args.no_bundled:
         import tempfile

@@ -54,6 +54,21 @@ int pqp_tune_lean_min_n(int n);
  * (and graphs) made afterwards.  Returns the previous value. */
 int pqp_tune_relay_spin_max(int polls);
 
+/* Setup products (convertToDual and the other matrixMultiply drop-ins) with
+ * both output dimensions >= 32 run LDS-tiled (k_matmul_tiled); off != 0 sends
+ * every product through the one-thread-per-output k_matmul_seq instead (A/B
+ * timing; both are bit-identical to PQP_CPU.c).  Returns the previous value. */
+int pqp_tune_matmul_tiled(int off);
+
+/* Batched converge mode (pqp_batch_solve: one workgroup per problem, operands
+ * from global memory).  opts bit 0: for problems whose Qd is bit-symmetric,
+ * fuse terminate()'s Y'Qd into the update's pass over Qd after a feasible
+ * terminate() (the update runs first, speculatively); bit 1: read Gp and
+ * Qp_inv row by row through transposed copies made per call.  Both measured
+ * slower at n_dual 1024 x 4096 problems and are off by default;
+ * every setting is bit-identical.  Returns the previous value. */
+int pqp_tune_batch_converge(int opts);
+
 /* The persistent single-problem launches (fixed mode: k_split_persist; converge
  * mode: k_converge_persist) need all their workgroups resident at once.  Before
  * launching, the library checks occupancy x CUs against the grid and otherwise

@@ -291,6 +291,7 @@ constexpr size_t kLdsBudget = 150 * 1024;
 bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
 bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
 int g_wide_min_n = 384;       // converge mode: smallest N solved over many workgroups (problem_run_wide)
+int g_batch_opts = 0;         // tuning (pqp_tune_batch_converge): bit 0 fuse Y'Qd, bit 1 transposed Gp / Qp_inv
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -1379,14 +1380,40 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
         path = 0;
     else if (solve_small_lds_bytes(N, M) <= kLdsBudget)
         path = 1;
-    else if (solve_single_lds_bytes(ldq, ldm) > kLdsBudget)
+    else if (solve_single_lds_bytes(ldq, ldm, true) > kLdsBudget)
         return set_error(PQP_ERR_ARG, "pqp_batch_solve: N=%d, M=%d exceeds the LDS budget", N, M);
-    DevBuf QdT, theta, state, pending, Udummy;
+    DevBuf QdT, theta, state, pending, Udummy, sym, GpT, QinvT;
+    const float* qdt = nullptr;
     if (path == 2) {
-        PQP_TRY(QdT.floats((size_t)B * N * ldq));
+        // Qd bit-symmetric in every problem (convertToDual's (Gp Qp_inv) Gp'
+        // is, for a diagonal Qp_inv) and N % 4 == 0: the row-major Qd is its
+        // own column-major copy, no packing pass.  Optionally (tuning bit 0)
+        // converge mode then fuses terminate()'s Y'Qd into the update's pass.
+        bool all_sym = false;
+        if (ldq == N) {
+            PQP_TRY(sym.alloc(sizeof(int) * (size_t)B));
+            PQP_HIP(launch_check_symmetric(B, d_Qd, N, static_cast<int*>(sym.p), s));
+            std::vector<int> hs((size_t)B);
+            PQP_HIP(hipMemcpyAsync(hs.data(), sym.p, sizeof(int) * (size_t)B, hipMemcpyDeviceToHost, s));
+            PQP_HIP(hipStreamSynchronize(s));
+            all_sym = true;
+            for (int v : hs) all_sym = all_sym && v != 0;
+        }
+        if (all_sym && ldq == N) {
+            qdt = d_Qd;
+        } else {
+            PQP_TRY(QdT.floats((size_t)B * N * ldq));
+            PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, QdT.f(), ldq, (long long)N * ldq, s));
+            qdt = QdT.f();
+        }
         PQP_TRY(theta.floats((size_t)B * N));
-        PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, QdT.f(), ldq, (long long)N * ldq, s));
-        PQP_HIP(launch_theta(B, QdT.f(), ldq, (long long)N * ldq, N, theta.f(), N, s));
+        PQP_HIP(launch_theta(B, qdt, ldq, (long long)N * ldq, N, theta.f(), N, s));
+        if (mode == PQP_MODE_CONVERGE && (g_batch_opts & 2)) {  // coalesced row access of Gp, Qp_inv
+            PQP_TRY(GpT.floats((size_t)B * N * M));
+            PQP_TRY(QinvT.floats((size_t)B * M * M));
+            PQP_HIP(launch_transpose_b(B, d_Gp, N, M, GpT.f(), s));
+            PQP_HIP(launch_transpose_b(B, d_Qp_inv, M, M, QinvT.f(), s));
+        }
     }
     if (!d_U) {
         PQP_TRY(Udummy.floats((size_t)B * M));
@@ -1401,13 +1428,16 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
     }
     PQP_HIP(hipMemcpyAsync(state.p, init.data(), sizeof(SolveState) * (size_t)B, hipMemcpyHostToDevice, s));
     SolveArgs a{};
-    a.QdT = QdT.f();
+    a.QdT = qdt;
     a.Qd = d_Qd;
     a.theta = theta.f();
     a.Fd = d_Fd;
     a.Md = d_Md;
     a.Qp = d_Qp;
     a.Qinv = d_Qp_inv;
+    a.sym = (g_batch_opts & 1) ? static_cast<const int*>(sym.p) : nullptr;
+    a.GpT = GpT.f();
+    a.QinvT = QinvT.f();
     a.Fp = d_Fp;
     a.Mp = d_Mp;
     a.Gp = d_Gp;
@@ -1758,6 +1788,18 @@ extern "C" int pqp_tune_persist_fit_cus(int cus) {
 extern "C" int pqp_tune_last_path(long long* fallbacks) {
     if (fallbacks) *fallbacks = pqp::g_persist_fallbacks;
     return pqp::g_last_path;
+}
+
+extern "C" int pqp_tune_batch_converge(int opts) {
+    const int old = pqp::g_batch_opts;
+    pqp::g_batch_opts = opts & 3;
+    return old;
+}
+
+extern "C" int pqp_tune_matmul_tiled(int off) {
+    const int old = pqp::g_matmul_tiled_off;
+    pqp::g_matmul_tiled_off = off ? 1 : 0;
+    return old;
 }
 
 extern "C" int pqp_tune_relay_spin_max(int polls) {

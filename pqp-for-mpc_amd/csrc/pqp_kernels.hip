@@ -1080,6 +1080,87 @@ __global__ void __launch_bounds__(256) k_matmul_seq(float* __restrict__ out, con
     out[e] = s;
 }
 
+// The same product, LDS-tiled (setup GEMMs of convertToDual at scale: Qd =
+// (Gp Qp_inv) Gp', PQP_CPU.c:440-498).  A 64 x 64 output tile per 256-thread
+// workgroup, 4 x 4 outputs per thread; op(A) and op(B) are staged 32 k at a
+// time into LDS with coalesced reads in whichever layout the transpose flags
+// give, and every output still sums k = 0..b-1 in order from +0.0f with the
+// product rounded before each add (no FMA: -ffp-contract=off), exactly as
+// matrixMultiply (:88-146) and k_matmul_seq.  grid = (ceil(c/64), ceil(a/64),
+// problems); strides sA/sB/sO per problem (0 = shared operand).
+constexpr int MMT = 64, MMK = 32;
+__global__ void __launch_bounds__(256) k_matmul_tiled(float* __restrict__ out, const float* __restrict__ A, int tA,
+                                                      const float* __restrict__ B, int tB, int a, int bdim, int c,
+                                                      long long sA, long long sB, long long sO) {
+    __shared__ __attribute__((aligned(16))) float As[MMK][MMT + 4];  // op(A)(i0 + ii, k0 + kk) at [kk][ii]
+    __shared__ __attribute__((aligned(16))) float Bs[MMK][MMT + 4];  // op(B)(k0 + kk, j0 + jj) at [kk][jj]
+    const int z = blockIdx.z;
+    A += z * sA;
+    B += z * sB;
+    out += z * sO;
+    const int j0 = blockIdx.x * MMT, i0 = blockIdx.y * MMT;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    float acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[r][q] = 0.0f;
+    for (int k0 = 0; k0 < bdim; k0 += MMK) {
+        // stage 64 x 32 of each operand (8 elements per thread), the fastest
+        // thread index along the operand's contiguous dimension
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int e = tid + 256 * s;
+            int ii, kk;
+            if (tA) {  // A stored b x a: A(i,k) = A[k*a + i], i contiguous
+                ii = e & 63;
+                kk = e >> 6;
+            } else {  // A stored a x b: A(i,k) = A[i*b + k], k contiguous
+                kk = e & 31;
+                ii = e >> 5;
+            }
+            const int i = i0 + ii, k = k0 + kk;
+            float v = 0.0f;
+            if (i < a && k < bdim) v = tA ? A[(size_t)k * a + i] : A[(size_t)i * bdim + k];
+            As[kk][ii] = v;
+            int jj, kb;
+            if (tB) {  // B stored c x b: B(k,j) = B[j*b + k], k contiguous
+                kb = e & 31;
+                jj = e >> 5;
+            } else {  // B stored b x c: B(k,j) = B[k*c + j], j contiguous
+                jj = e & 63;
+                kb = e >> 6;
+            }
+            const int j = j0 + jj, k2 = k0 + kb;
+            float w = 0.0f;
+            if (j < c && k2 < bdim) w = tB ? B[(size_t)j * bdim + k2] : B[(size_t)k2 * c + j];
+            Bs[kb][jj] = w;
+        }
+        __syncthreads();
+        const int kend = (bdim - k0) < MMK ? (bdim - k0) : MMK;
+        for (int kk = 0; kk < kend; ++kk) {
+            const float4 av = *reinterpret_cast<const float4*>(&As[kk][4 * tx]);
+            const float4 bv = *reinterpret_cast<const float4*>(&Bs[kk][4 * ty]);
+            const float ar[4] = {av.x, av.y, av.z, av.w}, br[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[r][q] += ar[r] * br[q];  // :88-100, k in order
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 4 * tx + r;
+        if (i >= a) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = j0 + 4 * ty + q;
+            if (j < c) out[(size_t)i * c + j] = acc[r][q];
+        }
+    }
+}
+
 // A[i] += sign * B[i]   (matrixAdd, PQP_CPU.c:157-163)
 __global__ void k_axpy(float* __restrict__ A, const float* __restrict__ B, float sign, int n, long long sA = 0,
                        long long sB = 0) {
@@ -1197,6 +1278,8 @@ __device__ __forceinline__ SolveArgs problem_at(SolveArgs A, int b) {
     A.Fp = A.Fp ? A.Fp + b * M : nullptr;
     A.Mp = A.Mp ? A.Mp + b : nullptr;
     A.Gp = A.Gp ? A.Gp + b * N * M : nullptr;
+    A.GpT = A.GpT ? A.GpT + b * N * M : nullptr;
+    A.QinvT = A.QinvT ? A.QinvT + b * M * M : nullptr;
     A.Kp = A.Kp ? A.Kp + b * N : nullptr;
     A.Y += b * N;
     A.U = A.U ? A.U + b * M : nullptr;
@@ -1231,6 +1314,58 @@ __device__ __forceinline__ float seq_dot(const float* a, int astride, const floa
     return s;
 }
 
+// updateY2 (PQP_CPU.c:603-618) of rows i = tid, tid + NT, ... from `cur`
+// into `nxt`, one lane per row over the column-major QdT.  Split entries in
+// "max form": (q<0 ? 0 : q)*y and (q>0 ? 0 : -q)*y off the diagonal
+// (bit-identical to (max(0,+-q)+0.0f)*y), the stored literal
+// (max(0,+-q_ii)+theta_i) on it.  FUSE (Qd bit-symmetric, so QdT's column i
+// is also Qd's column i): the same stream also gives tq[i] = sum_k Y_k Qd[k][i]
+// in k order -- terminate()'s Y'Qd row (computeCost :648-653, :110) -- with
+// a third sequential sum, instead of a second pass over Qd.
+constexpr int kSU = 16;  // k per batch of loads in flight (per lane) in k_solve_single's passes
+template <int NT, bool FUSE>
+__device__ __forceinline__ void single_update(const SolveArgs& A, const float* __restrict__ cur,
+                                              float* __restrict__ nxt, float* __restrict__ tq) {
+    const int N = A.N, ldq = A.ldq;
+    for (int i = threadIdx.x; i < N; i += NT) {
+        float ap = 0.0f, an = 0.0f, aq = 0.0f;
+        const float thi = A.theta[i];
+        const float qii = A.QdT[(size_t)i * ldq + i];
+        const float dp = max_ref(0.0f, qii) + 1.0f * thi, dn = max_ref(0.0f, -qii) + 1.0f * thi;
+        const float* col = A.QdT + i;
+        int k = 0;
+        for (; k + kSU <= N; k += kSU) {
+            float q[kSU], yv[kSU];
+#pragma unroll
+            for (int j = 0; j < kSU; ++j) {
+                q[j] = col[(size_t)(k + j) * ldq];
+                yv[j] = cur[k + j];
+            }
+#pragma unroll
+            for (int j = 0; j < kSU; ++j) {
+                const bool d = (k + j == i);
+                const float qp = d ? dp : ((q[j] < 0.0f) ? 0.0f : q[j]);
+                const float qn = d ? dn : ((q[j] > 0.0f) ? 0.0f : -q[j]);
+                ap += qp * yv[j];
+                an += qn * yv[j];
+                if constexpr (FUSE) aq += yv[j] * q[j];  // Y'Qd :110, k in order
+            }
+        }
+        for (; k < N; ++k) {
+            const float q = col[(size_t)k * ldq], yk = cur[k];
+            const bool d = (k == i);
+            ap += (d ? dp : ((q < 0.0f) ? 0.0f : q)) * yk;
+            an += (d ? dn : ((q > 0.0f) ? 0.0f : -q)) * yk;
+            if constexpr (FUSE) aq += yk * q;
+        }
+        const float f = A.Fd[i];
+        const float num = an + 1.0f * max_ref(0.0f, -f);
+        const float den = ap + 1.0f * max_ref(0.0f, f);
+        nxt[i] = num / den * cur[i];
+        if constexpr (FUSE) tq[i] = aq;
+    }
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1238,14 +1373,25 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
     SolveState* st = st0 + blockIdx.x;
     if (st->status == kStatusDone || st->status == kStatusCapped) return;  // finished in an earlier launch
     const int N = A.N, M = A.M, ldq = A.ldq;
+    // the fused form keeps Y_{h+1} in nxt through terminate(), so the Fd.Y
+    // terms get a buffer of their own; otherwise they use nxt (free until the
+    // update), and the workgroup needs less LDS (more of them per CU)
     float* ya = lds;              // ldq
     float* yb = ya + ldq;         // ldq
     float* tq = yb + ldq;         // N   (Y'Qd row, Jd)
-    float* tM = tq + ldq;         // M   (Gp'Y + Fp)
+    float* fyb = tq + ldq;        // N   (Fd.Y terms; fused form only)
+    float* tM = (A.sym ? fyb + ldq : fyb);  // M   (Gp'Y + Fp)
     float* Us = tM + A.ldm;       // M   (U)
     float* tu = Us + A.ldm;       // M   (U'Qp row, Jp)
     __shared__ float s_J[2];
     const int tid = threadIdx.x;
+    // converge mode of a problem whose Qd is bit-symmetric: the update to
+    // Y_{h+1} runs first, speculatively, fused with terminate(Y_h)'s Y'Qd; it
+    // is dropped when terminate(Y_h) stops (every value is the reference's)
+    // (taken only after a feasible terminate(): an infeasible one stops at
+    // checkFeas and never reads Qd, so fusing would only add work)
+    const bool fuse_ok = A.mode == kModeConverge && A.sym && A.sym[blockIdx.x];
+    bool was_feasible = false;
 
     long long h = st->h;  // printed h of the current iterate
     for (int i = tid; i < ldq; i += NT) {
@@ -1258,35 +1404,46 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
     int status = kStatusContinue;
     long long done_here = 0;
     for (;;) {
+        const bool fuse = fuse_ok && was_feasible;
+        float* fy = A.sym ? fyb : nxt;
+        if (fuse) {
+            single_update<NT, true>(A, cur, nxt, tq);
+            __syncthreads();
+        }
         if (A.mode != kModeFixed) {
             // ---- terminate(Y)  PQP_CPU.c:673-687 ----
             // computeUfromY :352-360
-            for (int j = tid; j < M; j += NT) tM[j] = seq_dot(A.Gp + j, M, cur, N) + 1.0f * A.Fp[j];
+            for (int j = tid; j < M; j += NT) tM[j] = seq_dot<kSU>(A.Gp + j, M, cur, N) + 1.0f * A.Fp[j];
             __syncthreads();
-            for (int i = tid; i < M; i += NT) Us[i] = -seq_dot(A.Qinv + (size_t)i * M, 1, tM, M);
+            // row access of Qp_inv / Gp through their transposes when given (lane
+            // i walks column i of QinvT / GpT: coalesced), else row by row
+            for (int i = tid; i < M; i += NT)
+                Us[i] = -(A.QinvT ? seq_dot<kSU>(A.QinvT + i, M, tM, M) : seq_dot<kSU>(A.Qinv + (size_t)i * M, 1, tM, M));
             __syncthreads();
             // checkFeas :632-641
             int bad = 0;
             for (int i = tid; i < N; i += NT) {
-                const float s = seq_dot(A.Gp + (size_t)i * M, 1, Us, M);
+                const float s = A.GpT ? seq_dot<kSU>(A.GpT + i, N, Us, M) : seq_dot<kSU>(A.Gp + (size_t)i * M, 1, Us, M);
                 const float kp = A.Kp[i];
                 if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
             }
             const int infeasible = __syncthreads_or(bad);
+            was_feasible = !infeasible;
             int stop = 0;
             if (!infeasible) {
                 // computeCost(Y, Qd, Fd, Md) and computeCost(U, Qp, Fp, Mp) :648-666
-                for (int j = tid; j < N; j += NT) tq[j] = seq_dot(A.Qd + j, N, cur, N);
-                for (int j = tid; j < M; j += NT) tu[j] = seq_dot(A.Qp + j, M, Us, M);
+                if (!fuse)
+                    for (int j = tid; j < N; j += NT) tq[j] = seq_dot<kSU>(A.Qd + j, N, cur, N);
+                for (int j = tid; j < M; j += NT) tu[j] = seq_dot<kSU>(A.Qp + j, M, Us, M);
                 __syncthreads();
                 // the dot products' terms formed in parallel into LDS (the
-                // row buffers in place; Fd.Y into nxt and Fp.U into tM, both
-                // free until the update), then summed in k order by one lane
-                // each -- one lane reading Fd from global memory term by term
-                // was the slowest part of an iteration
+                // row buffers in place; Fd.Y into fy and Fp.U into tM), then
+                // summed in k order by one lane each -- one lane reading Fd
+                // from global memory term by term was the slowest part of an
+                // iteration
                 for (int j = tid; j < N; j += NT) {
                     tq[j] = tq[j] * cur[j];
-                    nxt[j] = A.Fd[j] * cur[j];
+                    fy[j] = A.Fd[j] * cur[j];
                 }
                 for (int j = tid; j < M; j += NT) {
                     tu[j] = tu[j] * Us[j];
@@ -1297,7 +1454,7 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
                 if (tid == 0 || tid == jt) {
                     const bool dual = (tid == 0);
                     const float* qv = dual ? tq : tu;
-                    const float* lv = dual ? nxt : tM;
+                    const float* lv = dual ? fy : tM;
                     const int n = dual ? N : M;
                     float quad = 0.0f, lin = 0.0f;
                     for (int k = 0; k < n; ++k) quad += qv[k];  // (Z'Q).Z :652-655
@@ -1344,43 +1501,7 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
             break;
         }
         // ---- updateY2  PQP_CPU.c:603-618 (one lane per row) ----
-        // Split entries in "max form": (q<0 ? 0 : q)*y and (q>0 ? 0 : -q)*y off
-        // the diagonal (bit-identical to (max(0,+-q)+0.0f)*y),
-        // and the stored literal (max(0,+-q_ii)+theta_i) on it.
-        for (int i = tid; i < N; i += NT) {
-            float ap = 0.0f, an = 0.0f;
-            const float thi = A.theta[i];
-            const float qii = A.QdT[(size_t)i * ldq + i];
-            const float dp = max_ref(0.0f, qii) + 1.0f * thi, dn = max_ref(0.0f, -qii) + 1.0f * thi;
-            const float* col = A.QdT + i;
-            int k = 0;
-            for (; k + 8 <= N; k += 8) {
-                float q[8], yv[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    q[j] = col[(size_t)(k + j) * ldq];
-                    yv[j] = cur[k + j];
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const bool d = (k + j == i);
-                    const float qp = d ? dp : ((q[j] < 0.0f) ? 0.0f : q[j]);
-                    const float qn = d ? dn : ((q[j] > 0.0f) ? 0.0f : -q[j]);
-                    ap += qp * yv[j];
-                    an += qn * yv[j];
-                }
-            }
-            for (; k < N; ++k) {
-                const float q = col[(size_t)k * ldq], yk = cur[k];
-                const bool d = (k == i);
-                ap += (d ? dp : ((q < 0.0f) ? 0.0f : q)) * yk;
-                an += (d ? dn : ((q > 0.0f) ? 0.0f : -q)) * yk;
-            }
-            const float f = A.Fd[i];
-            const float num = an + 1.0f * max_ref(0.0f, -f);
-            const float den = ap + 1.0f * max_ref(0.0f, f);
-            nxt[i] = num / den * cur[i];
-        }
+        if (!fuse) single_update<NT, false>(A, cur, nxt, nullptr);
         __syncthreads();
         float* t = cur;
         cur = nxt;
@@ -2437,18 +2558,26 @@ hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, flo
     return hipGetLastError();
 }
 
+int g_matmul_tiled_off = 0;  // tuning: every product through k_matmul_seq (A/B of the tiled setup GEMM)
+static bool use_tiled(int a, int c) { return !g_matmul_tiled_off && a >= 32 && c >= 32; }
+
 hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c,
                              hipStream_t s) {
-    const long long n = (long long)a * c;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_matmul_seq, dim3(cdiv(n, 256)), dim3(256), 0, s, out, A, tA, B, tB, a, b, c);
-    return hipGetLastError();
+    return launch_matmul_seq_b(1, out, A, tA, B, tB, a, b, c, 0, 0, 0, s);
 }
 hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const float* Bm, int tB, int a, int b,
                                int c, long long sA, long long sB, long long sO, hipStream_t s) {
     const long long n = (long long)a * c;
     if (n == 0 || B == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_matmul_seq, dim3(cdiv(n, 256), B), dim3(256), 0, s, out, A, tA, Bm, tB, a, b, c, sA, sB, sO);
+    for (int b0 = 0; b0 < B; b0 += 65535) {  // grid y / z limit
+        const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        if (use_tiled(a, c))
+            hipLaunchKernelGGL(k_matmul_tiled, dim3(cdiv(c, MMT), cdiv(a, MMT), nb), dim3(256), 0, s, out + b0 * sO,
+                               A + b0 * sA, tA, Bm + b0 * sB, tB, a, b, c, sA, sB, sO);
+        else
+            hipLaunchKernelGGL(k_matmul_seq, dim3(cdiv(n, 256), nb), dim3(256), 0, s, out + b0 * sO, A + b0 * sA, tA,
+                               Bm + b0 * sB, tB, a, b, c, sA, sB, sO);
+    }
     return hipGetLastError();
 }
 hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, long long sA, long long sB,
@@ -2506,10 +2635,12 @@ hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* re
     return launch_gauss_jordan_b(1, A, aug, fac, res, n, s);
 }
 
-size_t solve_single_lds_bytes(int ldq, int ldm) { return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm); }
+size_t solve_single_lds_bytes(int ldq, int ldm, bool fused) {
+    return sizeof(float) * ((size_t)(fused ? 4 : 3) * ldq + (size_t)3 * ldm);
+}
 
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
-    const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm);
+    const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
     if (a.N <= 64)
         hipLaunchKernelGGL(k_solve_single<64>, dim3(B), dim3(64), lds, s, a, st);
     else
@@ -2525,6 +2656,70 @@ hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* s
     if (path == 0) return launch_tiny_grid(B, a, st, s);
     if (path == 1) return launch_small_grid(B, a, st, s);
     return launch_single_grid(B, a, st, s);
+}
+
+// dst[b] (cols x rows, row-major) = transpose of src[b] (rows x cols), per problem
+__global__ void __launch_bounds__(256) k_transpose_b(const float* __restrict__ src, int rows, int cols,
+                                                     float* __restrict__ dst) {
+    __shared__ float tile[32][33];
+    const size_t b = blockIdx.z, n = (size_t)rows * cols;
+    src += b * n;
+    dst += b * n;
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int r = ty; r < 32; r += 8) {
+        const int rr = r0 + r, cc = c0 + tx;
+        tile[r][tx] = (rr < rows && cc < cols) ? src[(size_t)rr * cols + cc] : 0.0f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int cc = c0 + r, rr = r0 + tx;
+        if (cc < cols && rr < rows) dst[(size_t)cc * rows + rr] = tile[tx][r];
+    }
+}
+hipError_t launch_transpose_b(int B, const float* src, int rows, int cols, float* dst, hipStream_t s) {
+    if (B <= 0 || rows <= 0 || cols <= 0) return hipSuccess;
+    for (int b0 = 0; b0 < B; b0 += 65535) {
+        const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        hipLaunchKernelGGL(k_transpose_b, dim3(cdiv(cols, 32), cdiv(rows, 32), nb), dim3(256), 0, s,
+                           src + (size_t)b0 * rows * cols, rows, cols, dst + (size_t)b0 * rows * cols);
+    }
+    return hipGetLastError();
+}
+
+// sym[b] = 1 iff problem b's row-major Qd (N x N, stride N*N) equals its
+// transpose bit for bit (preset to 1; 32 x 32 tiles through LDS).
+__global__ void __launch_bounds__(256) k_check_symmetric(const float* __restrict__ Qd, int N, int* __restrict__ sym) {
+    __shared__ unsigned tile[32][33];
+    const int b = blockIdx.z;
+    const int bi = blockIdx.y, bj = blockIdx.x;
+    if (bj < bi) return;  // each pair of tiles once
+    const unsigned* q = reinterpret_cast<const unsigned*>(Qd) + (size_t)b * N * N;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int r = ty; r < 32; r += 8) {  // tile (bj, bi) transposed into LDS
+        const int i = bj * 32 + r, j = bi * 32 + tx;
+        tile[tx][r] = (i < N && j < N) ? q[(size_t)i * N + j] : 0u;
+    }
+    __syncthreads();
+    int bad = 0;
+    for (int r = ty; r < 32; r += 8) {
+        const int i = bi * 32 + r, j = bj * 32 + tx;
+        if (i < N && j < N && q[(size_t)i * N + j] != tile[r][tx]) bad = 1;
+    }
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicAnd(sym + b, 0);
+}
+hipError_t launch_check_symmetric(int B, const float* Qd, int N, int* sym, hipStream_t s) {
+    if (B <= 0 || N <= 0) return hipSuccess;
+    hipError_t e = hipSuccess;
+    for (int b0 = 0; b0 < B && e == hipSuccess; b0 += 65535) {
+        const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        e = hipMemsetAsync(sym + b0, 0x01, sizeof(int) * nb, s);  // bytes 0x01: nonzero = symmetric
+        if (e != hipSuccess) break;
+        hipLaunchKernelGGL(k_check_symmetric, dim3(cdiv(N, 32), cdiv(N, 32), nb), dim3(256), 0, s,
+                           Qd + (size_t)b0 * N * N, N, sym + b0);
+        e = hipGetLastError();
+    }
+    return e;
 }
 
 __global__ void k_extract_state(int B, const SolveState* __restrict__ st, long long* __restrict__ h,

@@ -30,7 +30,12 @@ struct SolveArgs {
     int N, M, ldq, ldm, mode;
     long long num_iter, max_updates, chunk;
     int* pending;  // optional: +1 per problem still running when a launch ends
+    const int* sym;  // optional (k_solve_single): sym[b] != 0 when problem b's Qd is bit-symmetric
+    const float *GpT, *QinvT;  // optional (k_solve_single): transposes of Gp (M x N) and Qp_inv, per problem
 };
+hipError_t launch_transpose_b(int B, const float* src, int rows, int cols, float* dst, hipStream_t s);
+// sym[b] = nonzero iff problem b's row-major Qd equals its transpose bit for bit
+hipError_t launch_check_symmetric(int B, const float* Qd, int N, int* sym, hipStream_t s);
 
 hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
                                 const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s);
@@ -55,7 +60,7 @@ hipError_t launch_theta_rowmajor(const float* Qd, int N, float* theta_mat, hipSt
 hipError_t launch_cost_finish(const float* quad, const float* lin, const float* Mc, float* J, hipStream_t s);
 hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStream_t s);
 hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
-size_t solve_single_lds_bytes(int ldq, int ldm);
+size_t solve_single_lds_bytes(int ldq, int ldm, bool fused = false);
 size_t solve_small_lds_bytes(int N, int M);
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);  // N, M <= 32
@@ -115,6 +120,7 @@ extern int g_wave_min_b;     // tuning: smallest batch whose converge-mode tiny 
 // batched forms: grid = B problems (states st[0..B-1])
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);
+extern int g_matmul_tiled_off;  // tuning: force k_matmul_seq for every product
 hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const float* Bm, int tB, int a, int b,
                                int c, long long sA, long long sB, long long sO, hipStream_t s);
 hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, long long sA, long long sB,

@@ -94,6 +94,8 @@ SIGNATURES = {
     "pqp_tune_converge_persist": (C.c_int, [C.c_int]),
     "pqp_tune_lean_min_n": (C.c_int, [C.c_int]),
     "pqp_tune_relay_spin_max": (C.c_int, [C.c_int]),
+    "pqp_tune_matmul_tiled": (C.c_int, [C.c_int]),
+    "pqp_tune_batch_converge": (C.c_int, [C.c_int]),
     "pqp_tune_persist_fit_cus": (C.c_int, [C.c_int]),
     "pqp_tune_last_path": (C.c_int, [C.POINTER(C.c_longlong)]),
     "pqp_tune_converge_chunk": (C.c_int, [C.c_int]),
@@ -370,6 +372,18 @@ def run_example(directory) -> str:
 # ---------------------------------------------------------------------------
 # batched device API (torch provides the HBM buffers and the stream)
 # ---------------------------------------------------------------------------
+def dense_qinv(seed: int, M: int) -> np.ndarray:
+    """A dense symmetric Qp_inv (M x M row-major, fp32) from numpy's seeded
+    generator: diagonal in [1, 2), off-diagonal in [-0.05, 0.05).  The general
+    (non-diagonal) setup case: its convertToDual Qd is not bit-symmetric.  The
+    golden fixture tests/golden/dense_dual.npz was made by the reference from it."""
+    rng = np.random.default_rng(1000 + seed)
+    A = rng.uniform(-0.05, 0.05, (M, M)).astype(np.float32)
+    Q = np.triu(A) + np.triu(A, 1).T
+    Q[np.diag_indices(M)] = rng.uniform(1.0, 2.0, M).astype(np.float32)
+    return np.ascontiguousarray(Q, np.float32).reshape(-1)
+
+
 def round_up(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 

@@ -16,6 +16,12 @@ Outputs (all small):
   synth_converge.npz    converge-mode (N, M, seed) cases that the reference solves
   synth_large.npz       N=1024/M=512 and N=1000/M=500: dual-data digests and Y
                         after a few reference updates
+  dense_dual.npz        convertToDual with a DENSE Qp_inv (numpy-seeded,
+                        pqp_amd.dense_qinv) at N=1024/M=512 and N=300/M=77: digests of
+                        Qd, and Fd / Md (the general setup GEMM's parity case)
+
+Usage: python tests/golden/make_golden.py [part ...]   (parts: bundled converge
+       large testing dense; default all)
 """
 from __future__ import annotations
 
@@ -29,6 +35,9 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "oracle"))
 from oracle import Oracle, Reference, ReferenceTesting, REF_BIN, build  # noqa: E402
+
+sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+from pqp_amd import dense_qinv  # noqa: E402  (numpy only; the library is not loaded)
 
 OUT = Path(__file__).resolve().parent
 REFERENCE_DIR = Path("/root/reference")
@@ -136,6 +145,26 @@ def synth_large(ref: Reference, orc: Oracle):
     np.savez(OUT / "synth_large.npz", **out)
 
 
+DENSE_CASES = [(1024, 512, 3, 0), (300, 77, 4, 2)]  # N, M, seed, instance
+
+
+def dense_dual(ref: Reference, orc: Oracle):
+    out = {}
+    for (N, M, seed, inst) in DENSE_CASES:
+        P = orc.synth_primal(seed, inst, N, M)
+        Qinv = dense_qinv(seed, M)
+        Qd, Fd, Md = ref.convert_to_dual(Qinv, P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+        tag = f"n{N}_m{M}_s{seed}_i{inst}"
+        out[f"{tag}_meta"] = np.asarray([N, M, seed, inst], np.int64)
+        out[f"{tag}_Qd_sha256"] = np.frombuffer(bytes.fromhex(digest(Qd)), np.uint8)
+        out[f"{tag}_Qinv_sha256"] = np.frombuffer(bytes.fromhex(digest(Qinv)), np.uint8)
+        out[f"{tag}_Qd_row0"] = Qd[:N].copy()
+        out[f"{tag}_Fd"] = Fd
+        out[f"{tag}_Md"] = Md
+        print("dense", tag, "done")
+    np.savez(OUT / "dense_dual.npz", **out)
+
+
 def testing_files(ref: Reference):
     """testing/ sample file test2.txt (M=100, N=400) read by the reference's own
     reader (PQP_CPU_test.c input()), converted and iterated by PQP_CPU.c."""
@@ -154,14 +183,21 @@ def testing_files(ref: Reference):
     print("testing/test2.txt: M", M, "N", N)
 
 
-def main():
+def main(parts=None):
     build()
     ref, orc = Reference(), Oracle()
-    bundled(ref)
-    synth_converge(ref, orc)
-    synth_large(ref, orc)
-    testing_files(ref)
+    parts = set(parts or ("bundled", "converge", "large", "testing", "dense"))
+    if "bundled" in parts:
+        bundled(ref)
+    if "converge" in parts:
+        synth_converge(ref, orc)
+    if "large" in parts:
+        synth_large(ref, orc)
+    if "testing" in parts:
+        testing_files(ref)
+    if "dense" in parts:
+        dense_dual(ref, orc)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

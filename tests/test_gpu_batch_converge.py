@@ -1,0 +1,83 @@
+"""Batched converge mode at larger sizes: pqp_batch_solve,
+one workgroup per problem from global memory (k_solve_single).  Problems whose
+Qd is bit-symmetric (diagonal Qp_inv: the synthetic and testing/ problems)
+skip the column-major copy; optionally (tuning) terminate()'s Y'Qd
+(PQP_CPU.c:648-653) rides in the same pass over Qd as the speculative update
+to Y_{h+1} (:603-618), and Gp / Qp_inv are read through transposes.  Bar: the
+reference's h, Y and U bit for bit (oracle) in every setting, and a batch
+mixing both kinds of Qd."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import CAP, assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(pb, b, h, Y, U, what):
+    assert int(pb.h[b]) == abs(h), (what, int(pb.h[b]), h)
+    assert int(pb.status[b]) == (1 if h > 0 else 2), (what, int(pb.status[b]))
+    assert_bitwise(pb.Y[b].cpu().numpy(), Y, f"{what} Y")
+    assert_bitwise(pb.U[b].cpu().numpy(), U, f"{what} U")
+
+
+@pytest.mark.parametrize("opts", [0, 1, 2, 3])
+def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts):
+    from test_gpu_wide import _testing_file
+
+    L = gpu_lib.lib()
+    P = gpu_lib.testfile_problem(_testing_file("test2.txt", tmp_path))
+    h, Y, U = orc.solve(P, max_updates=CAP)
+    prev = L.pqp_tune_batch_converge(opts)
+    try:
+        pb = gpu_lib.ProblemBatch.replicate(P, 3).solve(max_updates=CAP)
+    finally:
+        L.pqp_tune_batch_converge(prev)
+    for b in range(3):
+        _check(pb, b, h, Y, U, f"test2 copy {b} opts={opts}")
+
+
+@pytest.mark.parametrize("opts", [0, 3])
+def test_batch_synthetic_capped_vs_oracle(gpu_lib, orc, opts):
+    L = gpu_lib.lib()
+    N, M, B, cap = 256, 128, 3, 6
+    prev = L.pqp_tune_batch_converge(opts)
+    try:
+        pb = gpu_lib.ProblemBatch.synthetic(9, 4, B, N, M).solve(max_updates=cap)
+    finally:
+        L.pqp_tune_batch_converge(prev)
+    for b in range(B):
+        P = orc.synth_problem(9, 4 + b, N, M)
+        h, Y, U = orc.solve(P, max_updates=cap)
+        _check(pb, b, h, Y, U, f"synthetic {b} opts={opts}")
+
+
+@pytest.mark.parametrize("opts", [0, 1])
+def test_batch_mixed_symmetric_and_not(gpu_lib, orc, opts):
+    """Problem 0's Qd is bit-symmetric (diagonal Qp_inv), problem 1's is not
+    (dense Qp_inv): one launch, the packed column-major copy, and (opts 1) a
+    per-problem choice of the fused pass."""
+    from pqp_amd import dense_qinv
+
+    N, M, cap = 200, 60, 5
+    P0 = orc.synth_problem(5, 0, N, M)
+    P1 = orc.synth_primal(5, 1, N, M)
+    P1["Qp_inv"] = dense_qinv(5, M)
+    P1["Qd"], P1["Fd"], P1["Md"] = orc.convert_to_dual(P1["Qp_inv"], P1["Gp"], P1["Kp"], P1["Fp"], P1["Mp"], N, M)
+    P1["Qp"] = orc.gauss_jordan(P1["Qp_inv"], M)
+    Q1 = P1["Qd"].reshape(N, N)
+    assert not np.array_equal(Q1.view(np.uint32), Q1.T.view(np.uint32)), "want a non-symmetric Qd here"
+    pb = gpu_lib.ProblemBatch(2, N, M)
+    for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
+        pb.set(k, np.stack([np.asarray(P0[k], np.float32).reshape(-1), np.asarray(P1[k], np.float32).reshape(-1)]))
+    L = gpu_lib.lib()
+    prev = L.pqp_tune_batch_converge(opts)
+    try:
+        pb.solve(max_updates=cap)
+    finally:
+        L.pqp_tune_batch_converge(prev)
+    for b, P in enumerate((P0, P1)):
+        h, Y, U = orc.solve(P, max_updates=cap)
+        _check(pb, b, h, Y, U, f"mixed {b}")

@@ -185,3 +185,21 @@ def test_random_dense_duals_vs_reference(orc):
         flag_r, U_r = ref.terminate(Y, P)
         assert flag_o == flag_r
         assert_bitwise(U_o, U_r, "U")
+
+
+@pytest.mark.parametrize("tag", ["n1024_m512_s3_i0", "n300_m77_s4_i2"])
+def test_dense_qinv_duals_match_reference(orc, tag):
+    """convertToDual with a dense Qp_inv (tests/golden/dense_dual.npz, from
+    PQP_CPU.c): pins the oracle for the general setup GEMM's parity case."""
+    from conftest import GOLDEN
+    from pqp_amd import dense_qinv
+
+    g = np.load(GOLDEN / "dense_dual.npz")
+    N, M, seed, inst = (int(v) for v in g[f"{tag}_meta"])
+    P = orc.synth_primal(seed, inst, N, M)
+    Qinv = dense_qinv(seed, M)
+    assert hashlib.sha256(Qinv.tobytes()).digest() == g[f"{tag}_Qinv_sha256"].tobytes()
+    Qd, Fd, Md = orc.convert_to_dual(Qinv, P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+    assert hashlib.sha256(Qd.tobytes()).digest() == g[f"{tag}_Qd_sha256"].tobytes()
+    assert_bitwise(Fd, g[f"{tag}_Fd"], "Fd")
+    assert_bitwise(Md, g[f"{tag}_Md"], "Md")
