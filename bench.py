@@ -339,7 +339,7 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
     (pqp_batch_solve, terminate() before every update), capped at K updates
     (the synthetic problems do not meet the exact gap test at this size).
     One iteration = terminate() + updateY2 (PQP_CPU.c:716-725).  Qd is
-    bit-symmetric here, so terminate()'s Y'Qd rides in the update's pass."""
+    bit-symmetric here, so the row-major Qd serves as its own column-major copy."""
     import torch
 
     pb = pqp_amd.ProblemBatch.synthetic(1, 0, B, N)
@@ -354,9 +354,10 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
     ok = bool((h == K + 1).all().item())
     del pb
     torch.cuda.empty_cache()
-    # algorithmic bytes per problem-iteration: Qd once (update + Y'Qd), Gp
-    # twice (Gp'Y, Gp U), Qp_inv and Qp once
-    alg = 4.0 * N * N + 8.0 * N * M + 8.0 * M * M
+    # algorithmic bytes per problem-iteration: Qd once (the update), Gp twice
+    # (Gp'Y, Gp U), Qp_inv once -- terminate() of these iterates stops at
+    # checkFeas (infeasible), so Y'Qd and U'Qp are never formed
+    alg = 4.0 * N * N + 8.0 * N * M + 4.0 * M * M
     gbs = alg * B * K / dt / 1e9
     return {"problems": B, "n_dual": N, "m": M, "updates": K, "ms": dt * 1e3, "instance_iter_per_s": B * K / dt,
             "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS, "all_capped": ok,

@@ -189,6 +189,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         }
         // zero y past N up to the slice end (read by the last packet's products)
         for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
+        mark(u, 1);
         // one base address per operand, the packet index as an immediate offset
         const f4v* qw = qs + (size_t)pk0 * kPLanes + ll;
         const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
