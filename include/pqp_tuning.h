@@ -54,6 +54,7 @@ int pqp_tune_lean_min_n(int n);
  * (and graphs) made afterwards.  Returns the previous value. */
 int pqp_tune_relay_spin_max(int polls);
 
+
 /* Setup products (convertToDual and the other matrixMultiply drop-ins) with
  * both output dimensions >= 32 run LDS-tiled (k_matmul_tiled); off != 0 sends
  * every product through the one-thread-per-output k_matmul_seq instead (A/B

@@ -74,6 +74,35 @@ __device__ __forceinline__ void fail(int* err, int code) {
     __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Products of one slice, prod[j] = q[j] * y[j] (each product rounded as the
+// reference's q * y), with the reads of packet j + D issued before packet j
+// is multiplied (q straight into prod[j + D], y into a ring of D + 1): the
+// LDS latency is paid about once per slice instead of once per packet (the
+// compiler's own schedule kept two packets in flight, ~48 clocks each).
+template <int NP>
+__device__ __forceinline__ void slice_products(f4v (&prod)[NP], const f4v* qw, const f4v* yw) {
+    constexpr int D = NP < 6 ? NP : 6;
+    f4v yr[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        prod[j] = qw[j * kPLanes];
+        yr[j] = yw[j];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if (j + D < NP) {
+            prod[j + D] = qw[(j + D) * kPLanes];
+            yr[(j + D) % (D + 1)] = yw[j + D];
+        }
+        const f4v q = prod[j], y = yr[j % (D + 1)];
+        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads D packets ahead of their use
+    }
+}
+
 }  // namespace
 
 int g_persist_off = 0;
@@ -176,7 +205,8 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                         return;
                     }
                     // one sweep at a time, a short pause between them (two sweeps
-                    // in flight measured 8 % slower: the pollers' own traffic)
+                    // in flight measured 8 % slower: the pollers' own traffic;
+                    // longer pauses for the waves whose turn comes late: no change)
                     __builtin_amdgcn_s_sleep(1);
                 }
 #pragma unroll
@@ -197,36 +227,22 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         u64* sl = slot + (size_t)par * W * 64;
         const unsigned want = (unsigned)(u + 1);
         if (w == 0) {
-            // ---- 2/3 (wave 0). the chain starts here: products formed inside it ----
+            // ---- 2/3 (wave 0). the chain starts here, right after its products ----
             mark(u, 2);
             __builtin_amdgcn_s_setprio(3);
-            f4v qv[kPW0], yv[kPW0];
+            f4v prod[kPW0];
+            slice_products(prod, qw, yw);
 #pragma unroll
             for (int j = 0; j < kPW0; ++j) {
-                qv[j] = qw[j * kPLanes];
-                yv[j] = yw[j];
-            }
-#pragma unroll
-            for (int j = 0; j < kPW0; ++j) {
-                const f4v q = qv[j], y = yv[j];
-                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-                acc += lo.x;  // :608-609, k in order
-                acc += lo.y;
-                acc += hi.x;
-                acc += hi.y;
+                acc += prod[j].x;  // :608-609, k in order
+                acc += prod[j].y;
+                acc += prod[j].z;
+                acc += prod[j].w;
             }
         } else {
             // ---- 2. products of the slice, ahead of the turn ----
             f4v prod[kPW];
-#pragma unroll
-            for (int j = 0; j < kPW; ++j) {
-                const f4v q = qw[j * kPLanes];
-                const f4v y = yw[j];
-                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-                prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
-            }
+            slice_products(prod, qw, yw);
             // pinned here: otherwise the compiler sinks the multiplies into the chain
 #pragma unroll
             for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
