@@ -434,23 +434,38 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     row0, rows = plan[rank]
     blk, _, _ = pqp_amd.RowBlock.synthetic(7, 0, N, row0, rows, device=dev)
     solver = RowShardedSolver(blk, N, dev, dist=dist)
+
+    def timed(n):
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        solver.advance(n)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        solver.check()  # no expired in-kernel wait in any update (else this raises)
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0]) / n
+
     solver.Y.fill_(1000.0)
-    for _ in range(5):
-        solver.step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(updates):
-        solver.step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    solver.check()  # no expired in-kernel wait in any update (else this raises)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t[0]) / updates
+    solver.advance(5)
+    dt_eager = timed(updates)
+    y_eager = solver.Y[:N].clone()
+    # the same updates as hipGraph replays (block update + RCCL all-gather per
+    # step, 16 steps per graph); not on gloo (rehearsal), see RowShardedSolver.capture
+    G = 16
+    graphed = solver.capture(G)
+    dt_graph, same = None, None
+    if graphed:
+        solver.Y.fill_(1000.0)
+        solver.advance(5)
+        solver.advance(updates)  # reach the eager run's iterate, then time more
+        same = bool(torch.equal(solver.Y[:N], y_eager))
+        dt_graph = timed(max(G, updates // G * G))
+    dt = min(dt_eager, dt_graph) if dt_graph else dt_eager
     y = solver.Y[:N]
     L = pqp_amd.lib()
     lean_min = L.pqp_tune_lean_min_n(0)  # read the setting (and restore it)
@@ -462,7 +477,14 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
            "layout": "Qd packets, k_lean_relay (4 B/entry)" if lean else "stored split matrices (8 B/entry)",
            "alg_GBps": bpe * N * N / dt / 1e9,
            "finite_nonneg": bool(torch.isfinite(y).all().item()) and bool((y >= 0).all().item()),
-           "note": "eager launches (pqp_rowblock_update + RCCL all_gather_into_tensor per update at N>1 ranks)"}
+           "us_per_update_eager": dt_eager * 1e6,
+           "us_per_update_graph": dt_graph * 1e6 if dt_graph else None,
+           "graph_same_bits_as_eager": same,
+           "graph_note": (f"{G} updates ({'block update + all-gather' if dist is not None else 'block update'}) "
+                          "per hipGraph replay" if graphed else
+                          f"not captured: {solver.capture_error or 'gloo group (rehearsal)'}"),
+           "note": "us_per_update = the faster of eager launches (pqp_rowblock_update + all_gather_into_tensor per "
+                   "update at N>1 ranks) and graph replays"}
     del solver, blk
     torch.cuda.empty_cache()
     return out

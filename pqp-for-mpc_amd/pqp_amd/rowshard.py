@@ -41,6 +41,7 @@ class RowShardedSolver:
         self.torch = torch
         self.block = block
         self.N = int(N)
+        self.device = torch.device(device)
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group) if dist is not None else 1
@@ -52,15 +53,61 @@ class RowShardedSolver:
         self.Y = torch.empty(self.world * self.R, **kw)
         self.Y2 = torch.empty(self.world * self.R, **kw)
         self.local = torch.zeros(self.R, **kw)
+        self.graph = None  # (torch.cuda.CUDAGraph, steps) once capture() succeeded
+        self.capture_error = None
 
     def step(self):
-        """One updateY2 of the whole problem: Y <- Y_next."""
-        if self.world == 1:
+        """One updateY2 of the whole problem: Y <- Y_next.  With a process
+        group the new rows always go through the all-gather, also at world
+        size 1 (a one-rank RCCL group then exercises the captured collective)."""
+        if self.dist is None:
             self.block.update(self.Y, self.Y2)
         else:
             self.block.update(self.Y, self.local)
             self.dist.all_gather_into_tensor(self.Y2, self.local, group=self.group)
         self.Y, self.Y2 = self.Y2, self.Y
+
+    def capture(self, steps: int = 16) -> bool:
+        """Record `steps` (even) updates -- each rank's block update and the
+        RCCL all-gather -- as ONE hipGraph, replayed by :meth:`run`.  This
+        removes the per-update host launches and the cross-stream event waits
+        the eager collective adds between the update kernel and the gather.
+
+        Every rank must call it (the ranks agree on the outcome over an eager
+        all-reduce, so either all of them replay or none does).  Returns False
+        (and stays eager) where capture is not possible: gloo groups (CPU
+        collectives) or a capture error on any rank.  Clobbers Y: call it
+        before :meth:`run`, which re-fills Y."""
+        torch = self.torch
+        steps = int(steps)
+        if steps <= 0 or steps % 2:
+            raise ValueError("capture(steps): steps must be a positive even number (Y / Y2 end where they began)")
+        gloo = self.dist is not None and self.dist.get_backend(self.group) == "gloo"
+        ok = self.device.type == "cuda" and not gloo
+        if ok:
+            try:
+                self.Y.fill_(0.0)
+                for _ in range(2):  # communicator and kernels set up outside the capture
+                    self.step()
+                torch.cuda.synchronize(self.device)
+                self._graph_in = self.Y  # the buffer every replay starts from (and ends in: steps is even)
+                g = torch.cuda.CUDAGraph()
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.graph(g, stream=side):
+                    for _ in range(steps):
+                        self.step()
+                torch.cuda.current_stream(self.device).wait_stream(side)
+            except Exception as e:  # noqa: BLE001 -- reported through the agreement below
+                self.capture_error = f"{type(e).__name__}: {e}"
+                ok = False
+                g = None
+        if self.dist is not None and not gloo:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MIN, group=self.group)
+            ok = bool(flag.item())
+        self.graph = (g, steps) if ok else None
+        return ok
 
     def check(self):
         """Raise if any of this rank's block updates since the last check
@@ -74,7 +121,21 @@ class RowShardedSolver:
         """The reference's fixed mode: Y = 1000, then num_iter-1 updates
         (``while (h < NUM_ITER)``).  Returns the final Y (N) on every rank."""
         self.Y.fill_(y0)
-        for _ in range(max(0, int(num_iter) - 1)):
-            self.step()
+        self.advance(max(0, int(num_iter) - 1))
         self.check()
         return self.Y[: self.N]
+
+    def advance(self, updates: int):
+        """`updates` steps: whole replays of the captured graph (if any), then
+        eager steps for the remainder."""
+        left = int(updates)
+        if self.graph is not None and left >= self.graph[1]:
+            g, steps = self.graph
+            if self.Y is not self._graph_in:  # odd eager steps since capture: the graph reads the other buffer
+                self._graph_in.copy_(self.Y)
+                self.Y, self.Y2 = self.Y2, self.Y
+            while left >= steps:
+                g.replay()
+                left -= steps
+        for _ in range(left):
+            self.step()

@@ -201,6 +201,62 @@ def test_rowsharded_two_processes(gpu_lib, orc, tmp_path, world, N):
         assert_bitwise(np.load(f"{out}.{r}.npy"), want, f"rank {r}")
 
 
+def _graph_rank_main(rank, world, port, N, ups, out):
+    import sys
+
+    for p in (ROOT / "pqp-for-mpc_amd", ROOT / "oracle"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    import pqp_amd
+    from pqp_amd.rowshard import RowShardedSolver
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    blk, _, _ = pqp_amd.RowBlock.synthetic(5, 9, N, 0, N)
+    solver = RowShardedSolver(blk, N, dev, dist=dist)
+    ok = solver.capture(4)
+    y = solver.run(ups + 1)  # 3 replays of 4 updates + 1 eager step at ups = 13
+    np.save(f"{out}.npy", y.cpu().numpy())
+    np.save(f"{out}.ok.npy", np.array([1 if ok else 0]))
+    dist.destroy_process_group()
+
+
+def test_rowsharded_graph_rccl_one_rank(gpu_lib, orc, tmp_path):
+    """RowShardedSolver.capture over a one-rank RCCL group: the block update
+    and the all-gather recorded as one hipGraph, replayed three times plus an
+    eager remainder, give the oracle's iterate bit for bit."""
+    import torch.multiprocessing as mp
+
+    N, ups = 1030, 13
+    out = str(tmp_path / "g")
+    mp.spawn(_graph_rank_main, args=(1, _free_port(), N, ups, out), nprocs=1, join=True)
+    assert int(np.load(f"{out}.ok.npy")[0]) == 1, "capture over RCCL failed"
+    P = orc.synth_problem(5, 9, N, max(1, N // 2), with_qp=False)
+    assert_bitwise(np.load(f"{out}.npy"), orc.iterate(P["Qd"], P["Fd"], N, ups), "graph-replayed row shard")
+
+
+def test_rowsharded_graph_no_group(gpu_lib, orc):
+    """capture() without a process group (one GPU): block updates only."""
+    import torch
+
+    from pqp_amd.rowshard import RowShardedSolver
+
+    N, ups = 300, 9
+    blk, _, _ = gpu_lib.RowBlock.synthetic(5, 9, N, 0, N)
+    solver = RowShardedSolver(blk, N, torch.device("cuda"))
+    assert solver.capture(2)
+    P = orc.synth_problem(5, 9, N, max(1, N // 2), with_qp=False)
+    want = orc.iterate(P["Qd"], P["Fd"], N, ups)
+    assert_bitwise(solver.run(ups + 1).cpu().numpy(), want, "graph replays, no group")
+    assert_bitwise(solver.run(ups + 1).cpu().numpy(), want, "graph replays, second run")
+    with pytest.raises(ValueError):
+        solver.capture(3)
+
+
 @pytest.mark.parametrize("num_iter", [2, 257, 300, 513])
 def test_fixed_mode_graph_chunks(gpu_lib, num_iter):
     """Fixed mode of a large problem replays 256-update graph chunks plus a

@@ -60,7 +60,10 @@ def _worker(rank, world, port, N, out_path):
     _, plan = row_plan(N, world)
     row0, rows = plan[rank]
     blk = _OracleBlock(orc, P["Qd"], theta, P["Fd"], N, row0, rows)
-    y = RowShardedSolver(blk, N, torch.device("cpu"), dist=dist).run(UPDATES + 1)
+    solver = RowShardedSolver(blk, N, torch.device("cpu"), dist=dist)
+    # a gloo group cannot be captured: every rank declines and stays eager
+    assert solver.capture(2) is False and solver.graph is None
+    y = solver.run(UPDATES + 1)
     np.save(f"{out_path}.{rank}.npy", y.numpy())
     dist.barrier()
     dist.destroy_process_group()
