@@ -14,13 +14,17 @@
 // products are rounded one by one exactly as in the reference (q * y, no FMA).
 //
 // Geometry: workgroup b owns row sides [32b, 32b + 32) = rows [16b, 16b + 16);
-// its W waves split the k range into slices of PW packets (4 PW values of k).
+// its W waves split the k range into slices of 24, 36, then 49 packets
+// (4 values of k each): wave 1's slice is short so that its products are
+// ready when wave 0 hands over (waves 0 and 1 see y at about the same time).
 // Per update:
 //   1. wave w fetches y[k] of its slice: the initial iterate from Y0, later
 //      the granules {tag = update, bits(y)} published by the producing
 //      workgroups (agent-scope relaxed 8-byte loads, `global_load_dwordx2 sc1`,
 //      repeated until every tag matches -- the data is its own flag);
-//   2. forms its slice's products q * y in registers (q from LDS);
+//   2. forms its slice's products q * y in registers (q from LDS; wave 0
+//      reads its q while it waits for y; waves 4 and 5, which share SIMDs
+//      with waves 0 and 1, start their products once wave 1 is done);
 //   3. waits for wave w-1's running sums (one 64-bit LDS word per lane:
 //      tag and sum), adds its products in k order, hands the sums on (wave 0
 //      starts the chain as soon as its slice is staged and forms its products
@@ -38,6 +42,8 @@
 #include "pqp_device.h"
 #include "pqp_launch.h"
 
+#include <type_traits>
+
 namespace pqp {
 
 namespace {
@@ -49,7 +55,9 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int kPLanes = 32;  // row sides per workgroup
 constexpr int kPW0 = 24;     // packets (4 values of k) of wave 0's slice: multiplied inside its add chain
-constexpr int kPW = 48;      // packets per later slice: their products are formed ahead, in 4 * kPW VGPRs
+constexpr int kPW1 = 36;     // packets of wave 1's slice: its products must be ready when wave 0 is done
+constexpr int kPW = 49;      // packets per later slice: their products are formed ahead, in 4 * kPW VGPRs
+constexpr int kLateGate = 1; // waves 4, 5 form their products once this wave has handed on its sums
 constexpr int kPMaxWaves = 6;
 constexpr long long kPTimeoutTicks = 200000000LL;  // s_memrealtime runs at 100 MHz: 2 s
 
@@ -72,6 +80,48 @@ struct Deadline {
 
 __device__ __forceinline__ void fail(int* err, int code) {
     __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until every lane's 64-bit LDS word carries the tag `want` in its high
+// half (a hand-off word of another wave).  `doze`: s_sleep between polls, for
+// waits off the critical path.  False when the wait's time limit expired.
+__device__ __forceinline__ bool lds_wait(u64* word, unsigned want, bool doze, u64* out = nullptr) {
+    Deadline dl;
+    for (unsigned spins = 0;; ++spins) {
+        const u64 h = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__all((unsigned)(h >> 32) == want)) {
+            if (out) *out = h;
+            return true;
+        }
+        if ((spins & 255) == 255 && dl.expired()) return false;
+        if (doze) __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Wave 0's slice: its split entries were read into registers ahead (during
+// its wait for y), so each packet needs one LDS read (y, D packets ahead);
+// the packet's products are added as soon as they are formed, so the chain
+// starts with the first packet instead of after the whole slice.
+template <int NP>
+__device__ __forceinline__ float chain_qreg(float acc, const f4v (&q)[NP], const f4v* yw) {
+    constexpr int D = NP < 12 ? NP : 12;
+    f4v yr[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) yr[j] = yw[j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
+        const f4v y = yr[j % (D + 1)];
+        const f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
+        const f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
+        acc += lo.x;  // :608-609, k in order
+        acc += lo.y;
+        acc += hi.x;
+        acc += hi.y;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
 }
 
 // Products of one slice, prod[j] = q[j] * y[j] (each product rounded as the
@@ -109,9 +159,14 @@ int g_persist_off = 0;
 unsigned long long* g_persist_trace = nullptr;  // tuning: timeline of workgroup 0 (pqp_tune_persist_trace)
 int g_persist_trace_n = 0;
 
-// waves: one slice of kPW0 packets, then slices of kPW
-__host__ __device__ inline int persist_waves_of(int KB) { return KB <= kPW0 ? 1 : 1 + (KB - kPW0 + kPW - 1) / kPW; }
-__host__ __device__ inline int persist_packets(int W) { return kPW0 + (W - 1) * kPW; }
+// waves: slices of kPW0, kPW1, then kPW packets
+__host__ __device__ inline int persist_slice0(int w) { return w == 0 ? 0 : (w == 1 ? kPW0 : kPW0 + kPW1 + (w - 2) * kPW); }
+__host__ __device__ inline int persist_packets(int W) { return persist_slice0(W); }
+__host__ __device__ inline int persist_waves_of(int KB) {
+    int W = 1;
+    while (persist_packets(W) < KB) ++W;
+    return W;
+}
 int persist_waves(int N) { return persist_waves_of(split_kblocks(N)); }
 int persist_max_n() {
     const int n = 4 * persist_packets(kPMaxWaves);
@@ -157,8 +212,8 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     const float fd = live ? fdpn[p] : 0.0f;
     __syncthreads();
 
-    const int pk0 = w == 0 ? 0 : kPW0 + (w - 1) * kPW;          // first packet of this wave's slice
-    const int pk1 = w == 0 ? kPW0 : pk0 + kPW;                   // one past its last
+    const int pk0 = persist_slice0(w);                           // first packet of this wave's slice
+    const int pk1 = persist_slice0(w + 1);                       // one past its last
     const int k0 = 4 * pk0, k1 = 4 * pk1 < N ? 4 * pk1 : N;      // y[k0, k1) of the slice
     const bool last = (w == W - 1);
     float yrow = 0.0f;  // last wave: y_i of this lane's row (for y_next = num / den * y_i)
@@ -173,6 +228,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         float* ys = ysb + par * ny;
         mark(u, 0);
         // ---- 1. y of this slice (k in [k0, k1)), staged in LDS ----
+        auto stage_y = [&]() -> bool {
         if (u == 0) {
             for (int k = k0 + lane; k < k1; k += 64) ys[k] = Y0 ? Y0[k] : 1000.0f;  // initMat(Y, 1000) :710
             if (last) yrow = (Y0 && row < N) ? Y0[row] : 1000.0f;
@@ -181,92 +237,108 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             const unsigned tag = (unsigned)u;
             for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
                 const bool own = last && kb == k0 && row < N;  // + y_i of the rows this workgroup finishes (:594)
-                float v[5] = {};
-                Deadline dl;
-                for (unsigned spins = 0;; ++spins) {
-                    bool ok = true;
+                u64 x[5] = {};
+                // the sweep: every load of the slice in flight, then one
+                // wave-wide test of the tags (the data is its own flag)
+                auto issue = [&](u64 (&xs)[5]) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m) {
                         const int k = kb + 64 * m + lane;
-                        if (k < k1) {
-                            const u64 x = __hip_atomic_load(g + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            v[m] = __uint_as_float((unsigned)x);
-                            ok &= (unsigned)(x >> 32) == tag;
-                        }
+                        if (k < k1) xs[m] = __hip_atomic_load(g + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    if (own) {
-                        const u64 x = __hip_atomic_load(g + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        v[4] = __uint_as_float((unsigned)x);
-                        ok &= (unsigned)(x >> 32) == tag;
-                    }
-                    if (__all(ok)) break;
-                    if ((spins & 63) == 63 && dl.expired()) {
-                        fail(err, 1);
-                        return;
-                    }
+                    if (own) xs[4] = __hip_atomic_load(g + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                auto arrived = [&](const u64 (&xs)[5]) {
+                    bool ok = true;
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        if (kb + 64 * m + lane < k1) ok &= (unsigned)(xs[m] >> 32) == tag;
+                    if (own) ok &= (unsigned)(xs[4] >> 32) == tag;
+                    return __all(ok);
+                };
+                Deadline dl;
+                for (unsigned spins = 0;; ++spins) {
+                    issue(x);
+                    if (arrived(x)) break;
+                    if ((spins & 63) == 63 && dl.expired()) return false;
                     // one sweep at a time, a short pause between them (two sweeps
-                    // in flight measured 8 % slower: the pollers' own traffic;
-                    // longer pauses for the waves whose turn comes late: no change)
+                    // in flight, issued 256 to 512 clocks apart, measured 5-15 %
+                    // slower: the pollers' own traffic)
                     __builtin_amdgcn_s_sleep(1);
                 }
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const int k = kb + 64 * m + lane;
-                    if (k < k1) ys[k] = v[m];
+                    if (k < k1) ys[k] = __uint_as_float((unsigned)x[m]);
                 }
-                if (own) yrow = v[4];
+                if (own) yrow = __uint_as_float((unsigned)x[4]);
             }
         }
         // zero y past N up to the slice end (read by the last packet's products)
         for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
         mark(u, 1);
+        return true;
+        };
         // one base address per operand, the packet index as an immediate offset
         const f4v* qw = qs + (size_t)pk0 * kPLanes + ll;
         const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
         float acc = 0.0f;
         u64* sl = slot + (size_t)par * W * 64;
         const unsigned want = (unsigned)(u + 1);
+        bool ok = true;
         if (w == 0) {
+            // wave 0 reads its slice's split entries while it waits for y:
+            // its products start the chain, and then need only the y reads
+            f4v q0[kPW0];
+#pragma unroll
+            for (int j = 0; j < kPW0; ++j) q0[j] = qs[(size_t)j * kPLanes + ll];
+            if (!stage_y()) {
+                fail(err, 1);
+                return;
+            }
             // ---- 2/3 (wave 0). the chain starts here, right after its products ----
             mark(u, 2);
             __builtin_amdgcn_s_setprio(3);
-            f4v prod[kPW0];
-            slice_products(prod, qw, yw);
-#pragma unroll
-            for (int j = 0; j < kPW0; ++j) {
-                acc += prod[j].x;  // :608-609, k in order
-                acc += prod[j].y;
-                acc += prod[j].z;
-                acc += prod[j].w;
-            }
+            acc = chain_qreg(acc, q0, yw);
         } else {
-            // ---- 2. products of the slice, ahead of the turn ----
-            f4v prod[kPW];
-            slice_products(prod, qw, yw);
-            // pinned here: otherwise the compiler sinks the multiplies into the chain
-#pragma unroll
-            for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
-            // ---- 3. the running sums of the previous slice, then this slice's adds ----
-            Deadline dl;
-            u64 h;
-            for (unsigned spins = 0;; ++spins) {
-                h = __hip_atomic_load(sl + (w - 1) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (__all((unsigned)(h >> 32) == want)) break;
-                if ((spins & 255) == 255 && dl.expired()) {
-                    fail(err, 2);
-                    return;
+            if (!stage_y()) {
+                fail(err, 1);
+                return;
+            }
+            // products ahead of the turn, the running sums of the previous
+            // slice, then this slice's adds; NP = the slice's packets
+            auto turn = [&](auto np) {
+                constexpr int NP = decltype(np)::value;
+                f4v prod[NP];
+                if (w >= 4) {
+                    // waves 4, 5 share SIMDs with waves 0, 1: they form their
+                    // products once wave kLateGate has handed on its sums, so
+                    // the first waves' products and chains run alone
+                    if (!lds_wait(sl + kLateGate * 64 + lane, want, true)) return false;
                 }
-            }
-            acc = __uint_as_float((unsigned)h);
-            mark(u, 2);
-            __builtin_amdgcn_s_setprio(3);
+                slice_products(prod, qw, yw);
+                // pinned here: otherwise the compiler sinks the multiplies into the chain
 #pragma unroll
-            for (int j = 0; j < kPW; ++j) {
-                acc += prod[j].x;  // :608-609, k in order
-                acc += prod[j].y;
-                acc += prod[j].z;
-                acc += prod[j].w;
-            }
+                for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
+                u64 h;
+                if (!lds_wait(sl + (w - 1) * 64 + lane, want, false, &h)) return false;
+                acc = __uint_as_float((unsigned)h);
+                mark(u, 2);
+                __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+                for (int j = 0; j < NP; ++j) {
+                    acc += prod[j].x;  // :608-609, k in order
+                    acc += prod[j].y;
+                    acc += prod[j].z;
+                    acc += prod[j].w;
+                }
+                return true;
+            };
+            ok = (w == 1) ? turn(std::integral_constant<int, kPW1>{}) : turn(std::integral_constant<int, kPW>{});
+        }
+        if (!ok) {
+            fail(err, 2);
+            return;
         }
         asm volatile("" : "+v"(acc));  // the mark below follows the chain
         mark(u, 3);

@@ -28,7 +28,11 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
              Mp=np.zeros(1, np.float32), Gp=np.zeros(N * M, np.float32), Kp=np.zeros(N, np.float32), N=N, M=M)
     L = pqp_amd.lib()
     KB = (N + 3) // 4
-    W = 1 if KB <= 24 else 1 + (KB - 24 + 47) // 48  # pqp_persist.hip: slices of 24, then 48 packets
+    # pqp_persist.hip: slices of 24, 36, then 49 packets (persist_slice0)
+    first = lambda w: 0 if w == 0 else (24 if w == 1 else 60 + (w - 2) * 49)  # noqa: E731
+    W = 1
+    while first(W) < KB:
+        W += 1
     tr = torch.zeros(n_trace * W * 4, dtype=torch.int64, device="cuda")
     with pqp_amd.Problem(P) as prob:
         prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
