@@ -40,6 +40,8 @@
 #include "pqp_device.h"
 #include "pqp_launch.h"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace pqp {
@@ -53,7 +55,9 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int kL = 32;     // output columns (update: row sides) per workgroup
 constexpr int kP0 = 24;    // packets (4 values of k) of wave 0's slice, multiplied inside its chain
-constexpr int kPW = 48;    // packets per later slice, products formed ahead in 4 kPW VGPRs
+constexpr int kP1 = 36;    // packets of wave 1's slice: its products must be ready when wave 0 is done
+constexpr int kPW = 49;    // packets per later slice, products formed ahead in 4 kPW VGPRs
+constexpr int kLateGate = 1;  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
 constexpr int kMaxW = 6;   // waves for K <= 1024
 constexpr int kR = 8;      // ring depth (iterates in flight)
 constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
@@ -79,10 +83,68 @@ struct Deadline {
         return (long long)(now - t0) > kTimeoutTicks;
     }
 };
-__host__ __device__ inline int waves_of(int KB) { return KB <= kP0 ? 1 : 1 + (KB - kP0 + kPW - 1) / kPW; }
-__host__ __device__ inline int packets_of(int W) { return kP0 + (W - 1) * kPW; }
+// slices of kP0, kP1, then kPW packets (as k_split_persist)
+__host__ __device__ inline int slice0_of(int w) { return w == 0 ? 0 : (w == 1 ? kP0 : kP0 + kP1 + (w - 2) * kPW); }
+__host__ __device__ inline int packets_of(int W) { return slice0_of(W); }
+__host__ __device__ inline int waves_of(int KB) {
+    int W = 1;
+    while (packets_of(W) < KB) ++W;
+    return W;
+}
 __host__ __device__ inline int cdiv_i(int a, int b) { return (a + b - 1) / b; }
 __device__ __forceinline__ u64 granule(unsigned tag, float v) { return ((u64)tag << 32) | __float_as_uint(v); }
+
+// Products of one slice, prod[j] = q[j] * y[j] (each rounded as the
+// reference's q * y), the reads of packet j + D issued before packet j is
+// multiplied (q into prod[j + D], y into a ring of D + 1): the LDS latency is
+// paid about once per slice (pqp_persist.hip's slice_products).
+template <int NP>
+__device__ __forceinline__ void slice_products(f4v (&prod)[NP], const f4v* qw, const f4v* yw) {
+    constexpr int D = NP < 6 ? NP : 6;
+    f4v yr[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        prod[j] = qw[j * kL];
+        yr[j] = yw[j];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if (j + D < NP) {
+            prod[j + D] = qw[(j + D) * kL];
+            yr[(j + D) % (D + 1)] = yw[j + D];
+        }
+        const f4v q = prod[j], y = yr[j % (D + 1)];
+        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Wave 0's slice with its q already in registers: one LDS read (y) per
+// packet, D packets ahead, each packet added as soon as it is formed.
+template <int NP>
+__device__ __forceinline__ float chain_qreg(float acc, const f4v (&q)[NP], const f4v* yw) {
+    constexpr int D = NP < 12 ? NP : 12;
+    f4v yr[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) yr[j] = yw[j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
+        const f4v y = yr[j % (D + 1)];
+        const f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
+        const f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
+        acc += lo.x;  // matrixMultiply :88-100 / updateY2 :608-609, k in order
+        acc += lo.y;
+        acc += hi.x;
+        acc += hi.y;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+}
 
 }  // namespace
 
@@ -160,8 +222,8 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
     const int lane = threadIdx.x & 63, ll = lane & (kL - 1);
     const int c = g * kL + ll;  // output column (UPD: row side p = 2i + side)
     const int KB = split_kblocks(K), W = waves_of(KB);
-    const int pk0 = w == 0 ? 0 : kP0 + (w - 1) * kPW;
-    const int pk1 = w == 0 ? kP0 : pk0 + kPW;
+    const int pk0 = slice0_of(w);
+    const int pk1 = slice0_of(w + 1);
     const int k0 = 4 * pk0 < K ? 4 * pk0 : K, k1 = 4 * pk1 < K ? 4 * pk1 : K;
     const bool last = (w == W - 1);
     const u64* rx = (ROLE == kUpd || ROLE == kT1) ? a.ry : (ROLE == kT2 ? a.rtmp : a.rU);
@@ -187,8 +249,10 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
         long long dec_seen = 0;
         const bool need_bp = ROLE == kUpd && last && u + 1 - kR >= a.u0;
         if (need_bp) dec_seen = __hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // ---- 1. x of this slice, staged in LDS ----
-        {
+        // ---- 1. x of this slice, staged in LDS (run inside each wave's own
+        // branch below, so that wave 0's registered q does not stay live
+        // across the other branch) ----
+        auto stage_x = [&]() -> bool {
             const gu64* gx = (const gu64*)rx + (size_t)slot * nx;
             for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
                 const bool own = ROLE == kUpd && last && kb == k0 && row < N;  // y_i for y_next = num/den*y_i (:594)
@@ -203,7 +267,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
                 }
                 on[4] = own;
                 gp[4] = gx + (own ? row : 0);
-                if (!await_granules<5>(a, gp, on, tag, v, 1 + ROLE)) return;
+                if (!await_granules<5>(a, gp, on, tag, v, 1 + ROLE)) return false;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const int k = kb + 64 * m + lane;
@@ -213,68 +277,72 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             }
             // zero y past K up to the slice end (the +0 packets' partners)
             for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
-        }
-        mark(a, tr, u, tid_, 1);
+            mark(a, tr, u, tid_, 1);
+            return true;
+        };
         const f4v* qw = qs + (size_t)pk0 * kL + ll;
         const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
         float acc = 0.0f;
         if (w == 0) {
+            // wave 0 reads its slice's q while it waits for x
+            f4v q0[kP0];
+#pragma unroll
+            for (int j = 0; j < kP0; ++j) q0[j] = qw[j * kL];
+            if (!stage_x()) return;
             // ---- 2/3 (wave 0): the chain starts here, products formed inside it ----
             __builtin_amdgcn_s_setprio(3);
-            f4v qv[kP0], yv[kP0];
-#pragma unroll
-            for (int j = 0; j < kP0; ++j) {
-                qv[j] = qw[j * kL];
-                yv[j] = yw[j];
-            }
-#pragma unroll
-            for (int j = 0; j < kP0; ++j) {
-                const f4v q = qv[j], y = yv[j];
-                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-                acc += lo.x;  // matrixMultiply :88-100 / updateY2 :608-609, k in order
-                acc += lo.y;
-                acc += hi.x;
-                acc += hi.y;
-            }
+            acc = chain_qreg(acc, q0, yw);
         } else {
-            // ---- 2. products of the slice, ahead of the turn ----
-            f4v prod[kPW];
-#pragma unroll
-            for (int j = 0; j < kPW; ++j) {
-                const f4v q = qw[j * kL];
-                const f4v y = yw[j];
-                const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-                const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-                prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
-            }
-#pragma unroll
-            for (int j = 0; j < kPW; ++j) asm volatile("" : "+v"(prod[j]));
-            // ---- 3. the running sums of the previous slice, then this slice's adds ----
-            const u64* src = hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll;
-            Deadline dl;
-            u64 h;
-            for (unsigned spins = 0;; ++spins) {
-                h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (__all((unsigned)(h >> 32) == tag)) break;
-                if ((spins & 255) == 255) {
-                    if (stopped(a)) return;
-                    if (dl.expired()) {
-                        fail(a, 10 + ROLE);
-                        return;
+            if (!stage_x()) return;
+            // ---- 2. products of the slice, ahead of the turn; 3. the running
+            // sums of the previous slice, then this slice's adds ----
+            auto turn = [&](auto np) -> int {
+                constexpr int NP = decltype(np)::value;
+                f4v prod[NP];
+                if (w >= 4) {
+                    // waves 4, 5 share SIMDs with waves 0, 1: their products
+                    // start once wave kLateGate has handed on its sums
+                    const u64* gsrc = hs + ((size_t)slot * kMaxW + kLateGate) * kL + ll;
+                    Deadline dl;
+                    for (unsigned spins = 0;; ++spins) {
+                        const u64 h = __hip_atomic_load(gsrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (__all((unsigned)(h >> 32) == tag)) break;
+                        if ((spins & 255) == 255) {
+                            if (stopped(a)) return 1;
+                            if (dl.expired()) return 2;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
                     }
                 }
-            }
-            acc = __uint_as_float((unsigned)h);
-            mark(a, tr, u, tid_, 2);
-            __builtin_amdgcn_s_setprio(3);
+                slice_products(prod, qw, yw);
 #pragma unroll
-            for (int j = 0; j < kPW; ++j) {
-                acc += prod[j].x;
-                acc += prod[j].y;
-                acc += prod[j].z;
-                acc += prod[j].w;
-            }
+                for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
+                const u64* src = hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll;
+                Deadline dl;
+                u64 h;
+                for (unsigned spins = 0;; ++spins) {
+                    h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (__all((unsigned)(h >> 32) == tag)) break;
+                    if ((spins & 255) == 255) {
+                        if (stopped(a)) return 1;
+                        if (dl.expired()) return 2;
+                    }
+                }
+                acc = __uint_as_float((unsigned)h);
+                mark(a, tr, u, tid_, 2);
+                __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+                for (int j = 0; j < NP; ++j) {
+                    acc += prod[j].x;
+                    acc += prod[j].y;
+                    acc += prod[j].z;
+                    acc += prod[j].w;
+                }
+                return 0;
+            };
+            const int rc = (w == 1) ? turn(std::integral_constant<int, kP1>{}) : turn(std::integral_constant<int, kPW>{});
+            if (rc == 2) fail(a, 10 + ROLE);
+            if (rc) return;
         }
         asm volatile("" : "+v"(acc));
         mark(a, tr, u, tid_, 3);

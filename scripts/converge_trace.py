@@ -16,8 +16,13 @@ ROLES = ("UPD", "T1", "T2", "T3")
 
 
 def waves_of(K):
+    # pqp_converge.hip: slices of 24, 36, then 49 packets (slice0_of)
     KB = (K + 3) // 4
-    return 1 if KB <= 24 else 1 + (KB - 24 + 47) // 48
+    first = lambda w: 0 if w == 0 else (24 if w == 1 else 60 + (w - 2) * 49)  # noqa: E731
+    W = 1
+    while first(W) < KB:
+        W += 1
+    return W
 
 
 def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
