@@ -345,13 +345,18 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
     pb = pqp_amd.ProblemBatch.synthetic(1, 0, B, N)
     M = pb.M
     pb.solve(max_updates=1)  # warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    pb.solve(max_updates=K)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    h = pb.h
-    ok = bool((h == K + 1).all().item())
+
+    def call(k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pb.solve(max_updates=k)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    dt = call(K)
+    ok = bool((pb.h == K + 1).all().item())
+    dt3 = call(3 * K)  # the same call with 3K updates: the difference is 2K iterations without the per-call setup
+    ok = ok and bool((pb.h == 3 * K + 1).all().item())
     del pb
     torch.cuda.empty_cache()
     # algorithmic bytes per problem-iteration: Qd once (the update), Gp twice
@@ -359,9 +364,18 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
     # checkFeas (infeasible), so Y'Qd and U'Qp are never formed
     alg = 4.0 * N * N + 8.0 * N * M + 4.0 * M * M
     gbs = alg * B * K / dt / 1e9
+    per_iter = (dt3 - dt) / (2 * K)
+    ss_gbs = alg * B / per_iter / 1e9
     return {"problems": B, "n_dual": N, "m": M, "updates": K, "ms": dt * 1e3, "instance_iter_per_s": B * K / dt,
             "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS, "all_capped": ok,
-            "note": "k_solve_single, one workgroup per problem; timed call includes the state readback"}
+            "steady_state": {"ms_per_iteration": per_iter * 1e3, "instance_iter_per_s": B / per_iter,
+                             "alg_GBps": ss_gbs, "frac_of_hbm_peak": ss_gbs / HBM_PEAK_GBS,
+                             "per_call_setup_ms": (dt - K * per_iter) * 1e3,
+                             "note": f"(time of a {3 * K}-update call - time of a {K}-update call) / {2 * K}: the "
+                                     "iterations alone; the per-call setup (symmetry check, Theta, state upload and "
+                                     "readback) is per_call_setup_ms"},
+            "note": "k_solve_single, one workgroup per problem; the timed call includes the per-call setup and the "
+                    "state readback"}
 
 
 def _testing_file(name: str, tmpdir: Path) -> Path:

@@ -67,7 +67,9 @@ int pqp_tune_matmul_tiled(int off);
  * terminate() (the update runs first, speculatively); bit 1: read Gp and
  * Qp_inv row by row through transposed copies made per call.  Both measured
  * slower at n_dual 1024 x 4096 problems and are off by default;
- * every setting is bit-identical.  Returns the previous value. */
+ * bit 2: 4-byte loads only (the 8/16-byte load forms, used by default when N
+ * and M are multiples of 4 and the arrays 16-byte aligned, are turned off).
+ * Every setting is bit-identical.  Returns the previous value. */
 int pqp_tune_batch_converge(int opts);
 
 /* The persistent single-problem launches (fixed mode: k_split_persist; converge

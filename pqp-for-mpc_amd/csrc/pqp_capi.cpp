@@ -292,6 +292,7 @@ bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead 
 bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
 int g_wide_min_n = 384;       // converge mode: smallest N solved over many workgroups (problem_run_wide)
 int g_batch_opts = 0;         // tuning (pqp_tune_batch_converge): bit 0 fuse Y'Qd, bit 1 transposed Gp / Qp_inv
+                              // (bit 2, 4-byte loads only, is g_single_scalar)
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -1791,8 +1792,9 @@ extern "C" int pqp_tune_last_path(long long* fallbacks) {
 }
 
 extern "C" int pqp_tune_batch_converge(int opts) {
-    const int old = pqp::g_batch_opts;
+    const int old = pqp::g_batch_opts | (pqp::g_single_scalar ? 4 : 0);
     pqp::g_batch_opts = opts & 3;
+    pqp::g_single_scalar = (opts & 4) ? 1 : 0;
     return old;
 }
 

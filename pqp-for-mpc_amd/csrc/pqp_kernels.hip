@@ -919,6 +919,36 @@ __global__ void __launch_bounds__(256) k_theta(const float* __restrict__ QdT, in
     theta[(size_t)b * ldv + i] = max_ref(s, 5.0f);
 }
 
+// The same, four adjacent rows per lane with 16-byte loads, 8 columns of
+// loads in flight (ldq, qstride multiples of 4, QdT 16-byte aligned).
+__global__ void __launch_bounds__(256) k_theta4(const float* __restrict__ QdT, int ldq, long long qstride, int N,
+                                                float* __restrict__ theta, int ldv) {
+    typedef float tf4 __attribute__((ext_vector_type(4)));
+    const int b = blockIdx.y;
+    const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 >= N) return;
+    const float* col = QdT + (size_t)b * (size_t)qstride + i0;
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int k = 0;
+    for (; k + 8 <= N; k += 8) {
+        tf4 q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = *reinterpret_cast<const tf4*>(col + (size_t)(k + j) * ldq);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[r] += max_ref(0.0f, -q[j][r]) * 1.0f;
+    }
+    for (; k < N; ++k) {
+        const tf4 q = *reinterpret_cast<const tf4*>(col + (size_t)k * ldq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] += max_ref(0.0f, -q[r]) * 1.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (i0 + r < N) theta[(size_t)b * ldv + i0 + r] = max_ref(s[r], 5.0f);
+}
+
 // Synthetic dual: Qd(i,j) = sum_k (Gp(i,k) q_k) Gp(j,k), k sequential.  The
 // convertToDual products Gp.Qp_inv are exact for a diagonal Qp_inv (all other
 // terms are +-0), so (Gp Qp_inv)(i,k) = Gp(i,k)*q_k bit for bit.  64x64 output
@@ -1366,7 +1396,133 @@ __device__ __forceinline__ void single_update(const SolveArgs& A, const float* _
     }
 }
 
-template <int NT>
+// ---- wide-load forms (VEC: N and M multiples of 4; the arrays 16-byte
+// aligned per problem).  Each lane's sums keep the reference's k order; the
+// loads are 8 or 16 bytes per lane, so a wave moves 2-4x the bytes per
+// instruction and a pass needs 2-4x fewer dependent load batches.
+typedef float sf2 __attribute__((ext_vector_type(2)));
+typedef float sf4 __attribute__((ext_vector_type(4)));
+template <int V> struct SVec;
+template <> struct SVec<2> { typedef sf2 t; };
+template <> struct SVec<4> { typedef sf4 t; };
+
+// s[c] = sum_k A[k * lda + c] * x[k], c < V (V adjacent columns of a
+// row-major matrix), k = 0..n-1 in order, U rows of loads in flight
+template <int V, int U>
+__device__ __forceinline__ void col_dotv(const float* __restrict__ A, int lda, const float* x, int n, float (&s)[V]) {
+    typedef typename SVec<V>::t vt;
+#pragma unroll
+    for (int c = 0; c < V; ++c) s[c] = 0.0f;
+    int k = 0;
+    for (; k + U <= n; k += U) {
+        vt a[U];
+        float xv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            a[j] = *reinterpret_cast<const vt*>(A + (size_t)(k + j) * lda);
+            xv[j] = x[k + j];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+#pragma unroll
+            for (int c = 0; c < V; ++c) s[c] += a[j][c] * xv[j];
+    }
+    for (; k < n; ++k) {
+        const vt a = *reinterpret_cast<const vt*>(A + (size_t)k * lda);
+#pragma unroll
+        for (int c = 0; c < V; ++c) s[c] += a[c] * x[k];
+    }
+}
+
+// s = sum_k a[k] * x[k] over a contiguous row (16-byte aligned, as is x),
+// k in order, 4 terms per load, U loads in flight
+template <int U>
+__device__ __forceinline__ float row_dot4(const float* __restrict__ a, const float* x, int n) {
+    float s = 0.0f;
+    int k = 0;
+    for (; k + 4 * U <= n; k += 4 * U) {
+        sf4 av[U], xv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            av[j] = *reinterpret_cast<const sf4*>(a + k + 4 * j);
+            xv[j] = *reinterpret_cast<const sf4*>(x + k + 4 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            s += av[j].x * xv[j].x;
+            s += av[j].y * xv[j].y;
+            s += av[j].z * xv[j].z;
+            s += av[j].w * xv[j].w;
+        }
+    }
+    for (; k < n; ++k) s += a[k] * x[k];
+    return s;
+}
+
+// single_update with four adjacent rows per lane (16-byte loads of QdT)
+constexpr int kSU4 = 8;
+template <int NT, bool FUSE>
+__device__ __forceinline__ void single_update4(const SolveArgs& A, const float* __restrict__ cur,
+                                               float* __restrict__ nxt, float* __restrict__ tq) {
+    const int N = A.N, ldq = A.ldq;
+    for (int i0 = 4 * threadIdx.x; i0 < N; i0 += 4 * NT) {
+        float ap[4] = {}, an[4] = {}, aq[4] = {}, dp[4], dn[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + r;
+            const float thi = i < N ? A.theta[i] : 0.0f;
+            const float qii = i < N ? A.QdT[(size_t)i * ldq + i] : 0.0f;
+            dp[r] = max_ref(0.0f, qii) + 1.0f * thi;
+            dn[r] = max_ref(0.0f, -qii) + 1.0f * thi;
+        }
+        const float* col = A.QdT + i0;
+        int k = 0;
+        for (; k + kSU4 <= N; k += kSU4) {
+            sf4 q[kSU4];
+            float yv[kSU4];
+#pragma unroll
+            for (int j = 0; j < kSU4; ++j) {
+                q[j] = *reinterpret_cast<const sf4*>(col + (size_t)(k + j) * ldq);
+                yv[j] = cur[k + j];
+            }
+#pragma unroll
+            for (int j = 0; j < kSU4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool d = (k + j == i0 + r);
+                    const float qp = d ? dp[r] : ((q[j][r] < 0.0f) ? 0.0f : q[j][r]);
+                    const float qn = d ? dn[r] : ((q[j][r] > 0.0f) ? 0.0f : -q[j][r]);
+                    ap[r] += qp * yv[j];
+                    an[r] += qn * yv[j];
+                    if constexpr (FUSE) aq[r] += yv[j] * q[j][r];  // Y'Qd :110, k in order
+                }
+        }
+        for (; k < N; ++k) {
+            const sf4 q = *reinterpret_cast<const sf4*>(col + (size_t)k * ldq);
+            const float yk = cur[k];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool d = (k == i0 + r);
+                ap[r] += (d ? dp[r] : ((q[r] < 0.0f) ? 0.0f : q[r])) * yk;
+                an[r] += (d ? dn[r] : ((q[r] > 0.0f) ? 0.0f : -q[r])) * yk;
+                if constexpr (FUSE) aq[r] += yk * q[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + r;
+            if (i < N) {
+                const float f = A.Fd[i];
+                const float num = an[r] + 1.0f * max_ref(0.0f, -f);
+                const float den = ap[r] + 1.0f * max_ref(0.0f, f);
+                nxt[i] = num / den * cur[i];
+                if constexpr (FUSE) tq[i] = aq[r];
+            }
+        }
+    }
+}
+
+template <int NT, bool VEC>
 __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
@@ -1407,23 +1563,37 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
         const bool fuse = fuse_ok && was_feasible;
         float* fy = A.sym ? fyb : nxt;
         if (fuse) {
-            single_update<NT, true>(A, cur, nxt, tq);
+            if constexpr (VEC) single_update4<NT, true>(A, cur, nxt, tq);
+            else single_update<NT, true>(A, cur, nxt, tq);
             __syncthreads();
         }
         if (A.mode != kModeFixed) {
             // ---- terminate(Y)  PQP_CPU.c:673-687 ----
             // computeUfromY :352-360
-            for (int j = tid; j < M; j += NT) tM[j] = seq_dot<kSU>(A.Gp + j, M, cur, N) + 1.0f * A.Fp[j];
+            if constexpr (VEC) {
+                for (int j = 2 * tid; j < M; j += 2 * NT) {
+                    float t[2];
+                    col_dotv<2, kSU>(A.Gp + j, M, cur, N, t);
+                    tM[j] = t[0] + 1.0f * A.Fp[j];
+                    tM[j + 1] = t[1] + 1.0f * A.Fp[j + 1];
+                }
+            } else {
+                for (int j = tid; j < M; j += NT) tM[j] = seq_dot<kSU>(A.Gp + j, M, cur, N) + 1.0f * A.Fp[j];
+            }
             __syncthreads();
             // row access of Qp_inv / Gp through their transposes when given (lane
             // i walks column i of QinvT / GpT: coalesced), else row by row
             for (int i = tid; i < M; i += NT)
-                Us[i] = -(A.QinvT ? seq_dot<kSU>(A.QinvT + i, M, tM, M) : seq_dot<kSU>(A.Qinv + (size_t)i * M, 1, tM, M));
+                Us[i] = -(A.QinvT ? seq_dot<kSU>(A.QinvT + i, M, tM, M)
+                          : VEC   ? row_dot4<4>(A.Qinv + (size_t)i * M, tM, M)
+                                  : seq_dot<kSU>(A.Qinv + (size_t)i * M, 1, tM, M));
             __syncthreads();
             // checkFeas :632-641
             int bad = 0;
             for (int i = tid; i < N; i += NT) {
-                const float s = A.GpT ? seq_dot<kSU>(A.GpT + i, N, Us, M) : seq_dot<kSU>(A.Gp + (size_t)i * M, 1, Us, M);
+                const float s = A.GpT ? seq_dot<kSU>(A.GpT + i, N, Us, M)
+                                : VEC   ? row_dot4<4>(A.Gp + (size_t)i * M, Us, M)
+                                        : seq_dot<kSU>(A.Gp + (size_t)i * M, 1, Us, M);
                 const float kp = A.Kp[i];
                 if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
             }
@@ -1432,9 +1602,25 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
             int stop = 0;
             if (!infeasible) {
                 // computeCost(Y, Qd, Fd, Md) and computeCost(U, Qp, Fp, Mp) :648-666
-                if (!fuse)
-                    for (int j = tid; j < N; j += NT) tq[j] = seq_dot<kSU>(A.Qd + j, N, cur, N);
-                for (int j = tid; j < M; j += NT) tu[j] = seq_dot<kSU>(A.Qp + j, M, Us, M);
+                if constexpr (VEC) {
+                    if (!fuse)
+                        for (int j = 4 * tid; j < N; j += 4 * NT) {
+                            float t[4];
+                            col_dotv<4, kSU4>(A.Qd + j, N, cur, N, t);
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) tq[j + c] = t[c];
+                        }
+                    for (int j = 2 * tid; j < M; j += 2 * NT) {
+                        float t[2];
+                        col_dotv<2, kSU>(A.Qp + j, M, Us, M, t);
+                        tu[j] = t[0];
+                        tu[j + 1] = t[1];
+                    }
+                } else {
+                    if (!fuse)
+                        for (int j = tid; j < N; j += NT) tq[j] = seq_dot<kSU>(A.Qd + j, N, cur, N);
+                    for (int j = tid; j < M; j += NT) tu[j] = seq_dot<kSU>(A.Qp + j, M, Us, M);
+                }
                 __syncthreads();
                 // the dot products' terms formed in parallel into LDS (the
                 // row buffers in place; Fd.Y into fy and Fp.U into tM), then
@@ -1501,7 +1687,10 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
             break;
         }
         // ---- updateY2  PQP_CPU.c:603-618 (one lane per row) ----
-        if (!fuse) single_update<NT, false>(A, cur, nxt, nullptr);
+        if (!fuse) {
+            if constexpr (VEC) single_update4<NT, false>(A, cur, nxt, nullptr);
+            else single_update<NT, false>(A, cur, nxt, nullptr);
+        }
         __syncthreads();
         float* t = cur;
         cur = nxt;
@@ -2540,7 +2729,16 @@ hipError_t launch_synth_rows(uint32_t seed, long long inst, int N, int M, int ro
 
 hipError_t launch_theta(int B, const float* QdT, int ldq, long long qstride, int N, float* theta, int ldv,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_theta, dim3(cdiv(N, 256), B), dim3(256), 0, s, QdT, ldq, qstride, N, theta, ldv);
+    const bool wide = (ldq & 3) == 0 && (qstride & 3) == 0 && ((uintptr_t)QdT & 15) == 0;
+    for (int b0 = 0; b0 < B; b0 += 65535) {  // grid y is at most 65535
+        const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        const float* q = QdT + (size_t)b0 * (size_t)qstride;
+        float* t = theta + (size_t)b0 * ldv;
+        if (wide)
+            hipLaunchKernelGGL(k_theta4, dim3(cdiv(N, 1024), nb), dim3(256), 0, s, q, ldq, qstride, N, t, ldv);
+        else
+            hipLaunchKernelGGL(k_theta, dim3(cdiv(N, 256), nb), dim3(256), 0, s, q, ldq, qstride, N, t, ldv);
+    }
     return hipGetLastError();
 }
 
@@ -2639,12 +2837,21 @@ size_t solve_single_lds_bytes(int ldq, int ldm, bool fused) {
     return sizeof(float) * ((size_t)(fused ? 4 : 3) * ldq + (size_t)3 * ldm);
 }
 
+int g_single_scalar = 0;  // tuning: k_solve_single with 4-byte loads only
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
-    if (a.N <= 64)
-        hipLaunchKernelGGL(k_solve_single<64>, dim3(B), dim3(64), lds, s, a, st);
-    else
-        hipLaunchKernelGGL(k_solve_single<256>, dim3(B), dim3(256), lds, s, a, st);
+    // wide loads need every row and column start 16-byte aligned: N, M
+    // multiples of 4 and 16-byte-aligned arrays (null ones are not read)
+    const bool vec = !g_single_scalar && a.N % 4 == 0 && a.M % 4 == 0 && aligned16(a.QdT) && aligned16(a.Qd) &&
+                     aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
+    if (a.N <= 64) {
+        if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
+        else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
+    } else {
+        if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);
+        else hipLaunchKernelGGL((k_solve_single<256, false>), dim3(B), dim3(256), lds, s, a, st);
+    }
     return hipGetLastError();
 }
 hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s) {
@@ -2708,15 +2915,56 @@ __global__ void __launch_bounds__(256) k_check_symmetric(const float* __restrict
     }
     if (__syncthreads_or(bad) && threadIdx.x == 0) atomicAnd(sym + b, 0);
 }
+// The same for N % 4 == 0 and a 16-byte-aligned Qd: one workgroup per (problem,
+// 64-row band bi) walks the tile pairs (bi, bj >= bi) with 16-byte loads, so
+// the grid is B x N/64 workgroups instead of B x (N/32)^2 (most of which had
+// nothing to do).
+__global__ void __launch_bounds__(256) k_check_symmetric4(const float* __restrict__ Qd, int N, int* __restrict__ sym) {
+    __shared__ unsigned tile[64][65];
+    const int b = blockIdx.y, bi = blockIdx.x;
+    const unsigned* q = reinterpret_cast<const unsigned*>(Qd) + (size_t)b * N * N;
+    const int nt = (N + 63) / 64;
+    const int tc = (threadIdx.x & 15) * 4, tr = threadIdx.x >> 4;  // 16 rows x 4 columns per pass
+    int bad = 0;
+    for (int bj = bi; bj < nt; ++bj) {
+#pragma unroll
+        for (int pss = 0; pss < 4; ++pss) {  // tile (bj, bi), transposed into LDS
+            const int r = tr + 16 * pss, i = bj * 64 + r, j = bi * 64 + tc;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (i < N && j < N) v = *reinterpret_cast<const uint4*>(q + (size_t)i * N + j);
+            tile[tc + 0][r] = v.x;
+            tile[tc + 1][r] = v.y;
+            tile[tc + 2][r] = v.z;
+            tile[tc + 3][r] = v.w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int pss = 0; pss < 4; ++pss) {  // against tile (bi, bj)
+            const int r = tr + 16 * pss, i = bi * 64 + r, j = bj * 64 + tc;
+            if (i < N && j < N) {
+                const uint4 v = *reinterpret_cast<const uint4*>(q + (size_t)i * N + j);
+                bad |= (v.x != tile[r][tc + 0]) | (v.y != tile[r][tc + 1]) | (v.z != tile[r][tc + 2]) |
+                       (v.w != tile[r][tc + 3]);
+            }
+        }
+        __syncthreads();
+    }
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicAnd(sym + b, 0);
+}
 hipError_t launch_check_symmetric(int B, const float* Qd, int N, int* sym, hipStream_t s) {
     if (B <= 0 || N <= 0) return hipSuccess;
+    const bool wide = N % 4 == 0 && ((uintptr_t)Qd & 15) == 0;
     hipError_t e = hipSuccess;
     for (int b0 = 0; b0 < B && e == hipSuccess; b0 += 65535) {
         const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
         e = hipMemsetAsync(sym + b0, 0x01, sizeof(int) * nb, s);  // bytes 0x01: nonzero = symmetric
         if (e != hipSuccess) break;
-        hipLaunchKernelGGL(k_check_symmetric, dim3(cdiv(N, 32), cdiv(N, 32), nb), dim3(256), 0, s,
-                           Qd + (size_t)b0 * N * N, N, sym + b0);
+        if (wide)
+            hipLaunchKernelGGL(k_check_symmetric4, dim3(cdiv(N, 64), nb), dim3(256), 0, s, Qd + (size_t)b0 * N * N, N,
+                               sym + b0);
+        else
+            hipLaunchKernelGGL(k_check_symmetric, dim3(cdiv(N, 32), cdiv(N, 32), nb), dim3(256), 0, s,
+                               Qd + (size_t)b0 * N * N, N, sym + b0);
         e = hipGetLastError();
     }
     return e;

@@ -1,0 +1,27 @@
+"""One batched converge-mode call at n_dual 1024 x 4096 problems (the bench's
+batch_converge leg), for kernel traces: python scripts/batch_converge_one.py [K]"""
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "pqp-for-mpc_amd"))
+
+
+def main():
+    import torch
+
+    import pqp_amd
+
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    pb = pqp_amd.ProblemBatch.synthetic(3, 0, 4096, 1024, 512)
+    pb.solve(max_updates=1)
+    torch.cuda.synchronize()
+    for k in (K, 3 * K):
+        t0 = time.perf_counter()
+        pb.solve(max_updates=k)
+        torch.cuda.synchronize()
+        print(f"updates {k}: {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
