@@ -10,11 +10,8 @@
 extern "C" {
 #endif
 
-/* Select kernel variants.  Low byte: the k_batch_iterate instantiation used
- * by pqp_batch_iterate (0 = shipped default: unroll 16, non-temporal Qd
- * loads; 1..5 = other (unroll, non-temporal) variants, 6 = max-based terms
- * (timing only: exact only for NaN-free Qd), see pqp_kernels.hip
- * launch_batch_iterate).  Bit 0x100: solve N, M <= 32 problems with the
+/* Select kernel variants (every variant is bit-identical; the tests run the
+ * parity cases through each).  Bit 0x100: solve N, M <= 32 problems with the
  * LDS-staged k_solve_small instead of k_solve_tiny.  Bit 0x200: fixed-mode
  * solves of large single problems on one workgroup (k_solve_single) instead
  * of the multi-workgroup split-matrix update.  Bit 0x400: fixed mode of
@@ -138,11 +135,6 @@ int pqp_tune_wide_min_n(int n);
  * beside terminate() instead of after it; bit 1 uses 64-value k-segments in
  * the mat-vecs (default 32).  Returns the previous value. */
 int pqp_tune_wide_flags(int flags);
-
-/* Stream B problems' QdT with the hot kernel's exact access pattern and no
- * solver arithmetic (one float written per thread to d_out[B*256]). */
-int pqp_tune_stream_read(int B, int N, const float *d_QdT, int ldq, long long qstride, float *d_out, int nontemporal,
-                         void *stream);
 
 /* The first n values of glibc's unseeded rand() as reproduced by the
  * testing/ reader (for checking the emulation against the C library). */

@@ -1734,11 +1734,10 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 #include "../../include/pqp_tuning.h"
 
 extern "C" int pqp_tune_set_variant(int variant) {
-    const int old = pqp::get_variant() | (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0) |
+    const int old = (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0) |
                     (pqp::g_fixed_tiny_old ? 0x400 : 0) |
                     (pqp::g_split_u << 12) | (pqp::g_split_kind << 14) |
                     ((pqp::g_split_lw ? __builtin_ctz(pqp::g_split_lw) - 2 : 0) << 17);
-    pqp::set_variant(variant & 0xff);
     pqp::g_split_u = (variant >> 12) & 3;
     pqp::g_split_kind = (variant >> 14) & 7;
     const int lwsel = (variant >> 17) & 7;  // 0 auto, 1: 8, 2: 16, 3: 32, 4: 64 lanes per workgroup
@@ -1853,10 +1852,3 @@ extern "C" int pqp_tune_glibc_rand(int n, int* out) {
     return pqp::glibc_rand_sequence(n, out);
 }
 
-extern "C" int pqp_tune_stream_read(int B, int N, const float* d_QdT, int ldq, long long qstride, float* d_out,
-                                    int nontemporal, void* stream) {
-    if (B <= 0 || N <= 0 || !d_QdT || !d_out || ldq < N || (ldq & 3) || qstride < (long long)N * ldq)
-        return pqp::set_error(PQP_ERR_ARG, "pqp_tune_stream_read: bad arguments");
-    PQP_HIP(pqp::launch_stream_read(B, d_QdT, qstride, ldq, N, d_out, nontemporal, static_cast<hipStream_t>(stream)));
-    return PQP_OK;
-}

@@ -75,22 +75,9 @@ __device__ __forceinline__ void literal4(Acc4& a, float4 q, float y, int k, int 
     literal1(a.p[3], a.n[3], q.w, y, (k == row + 3) ? th[3] : 0.0f);
 }
 
-// max-based lean step (A/B variant 6, timing only): equal to lean4 when q has
-// no NaN and y is finite and >= 0, up to the sign of an all-zero sum
-__device__ __forceinline__ void lean4mx(Acc4& a, float4 q, float y) {
-    a.p[0] += fmaxf(q.x, 0.0f) * y; a.n[0] += fmaxf(-q.x, 0.0f) * y;
-    a.p[1] += fmaxf(q.y, 0.0f) * y; a.n[1] += fmaxf(-q.y, 0.0f) * y;
-    a.p[2] += fmaxf(q.z, 0.0f) * y; a.n[2] += fmaxf(-q.z, 0.0f) * y;
-    a.p[3] += fmaxf(q.w, 0.0f) * y; a.n[3] += fmaxf(-q.w, 0.0f) * y;
-}
-template <bool MX>
-__device__ __forceinline__ void lean4v(Acc4& a, float4 q, float y) {
-    if constexpr (MX) lean4mx(a, q, y); else lean4(a, q, y);
-}
-
 // Stream k in [ka, kb) with the lean form.  ka % 4 == 0.  `col` points at
 // QdT + row (this lane's 4 rows), y is the iterate (LDS).
-template <int U, bool NTL, bool MX = false>
+template <int U, bool NTL>
 __device__ __forceinline__ void lean_segment(Acc4& a, const float* __restrict__ col, int ldq, int ka, int kb,
                                              const float* __restrict__ y) {
     static_assert(U % 4 == 0, "unroll must be a multiple of 4 (one float4 of y per 4 k)");
@@ -104,14 +91,14 @@ __device__ __forceinline__ void lean_segment(Acc4& a, const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < U; j += 4) {
             const float4 yv = *reinterpret_cast<const float4*>(y + k + j);
-            lean4v<MX>(a, q[j + 0], yv.x);
-            lean4v<MX>(a, q[j + 1], yv.y);
-            lean4v<MX>(a, q[j + 2], yv.z);
-            lean4v<MX>(a, q[j + 3], yv.w);
+            lean4(a, q[j + 0], yv.x);
+            lean4(a, q[j + 1], yv.y);
+            lean4(a, q[j + 2], yv.z);
+            lean4(a, q[j + 3], yv.w);
         }
     }
     for (; k < kb; ++k) {
-        lean4v<MX>(a, ldq4<NTL>(src), y[k]);
+        lean4(a, ldq4<NTL>(src), y[k]);
         src += ldq;
     }
 }
@@ -142,7 +129,7 @@ __device__ __forceinline__ void literal_segment(Acc4& a, const float* __restrict
 // out[i] = num/den * y[i] for the rows < N.  w0 = first row of this lane's
 // wave (wave-uniform): the diagonal of the wave's 256 rows lies in
 // k in [w0, w0+256) and only that window needs the literal form.
-template <int U, bool NTL, typename OutPtr, bool MX = false>
+template <int U, bool NTL, typename OutPtr>
 __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ldq, int N, int row, int w0,
                                              const float* __restrict__ th_g, const float* __restrict__ fd_g,
                                              const float* __restrict__ y, OutPtr out) {
@@ -155,9 +142,9 @@ __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ld
     const float* col = Q + row;
     const int wa = w0 < N ? w0 : N;
     const int wb = (w0 + 256) < N ? (w0 + 256) : N;
-    lean_segment<U, NTL, MX>(a, col, ldq, 0, wa, y);
+    lean_segment<U, NTL>(a, col, ldq, 0, wa, y);
     literal_segment<NTL>(a, col, ldq, wa, wb, y, row, th);
-    lean_segment<U, NTL, MX>(a, col, ldq, wb, N, y);
+    lean_segment<U, NTL>(a, col, ldq, wb, N, y);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = row + r;
@@ -175,7 +162,7 @@ __device__ __forceinline__ void update_rows4(const float* __restrict__ Q, int ld
 // launch.  One workgroup owns one problem; its iterate ping-pongs between two
 // LDS buffers, so the only HBM traffic per iteration is Qd (streamed once).
 // ---------------------------------------------------------------------------
-template <int NT, int U = 8, bool NTL = false, bool MX = false>
+template <int NT, int U = 8, bool NTL = false>
 __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ QdT, long long qstride, int ldq,
                                                       int N, const float* __restrict__ theta,
                                                       const float* __restrict__ Fd, int ldv,
@@ -202,7 +189,7 @@ __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ 
         for (int r0 = 0; r0 < N; r0 += 4 * NT) {
             const int row = r0 + 4 * tid;
             const int w0 = r0 + 256 * wave;
-            if (row < N) update_rows4<U, NTL, float*, MX>(Q, ldq, N, row, w0, th, fd, cur, nxt);
+            if (row < N) update_rows4<U, NTL, float*>(Q, ldq, N, row, w0, th, fd, cur, nxt);
         }
         __syncthreads();
     }
@@ -232,43 +219,6 @@ __global__ void __launch_bounds__(NT) k_batch_update(const float* __restrict__ Q
     if (row < N)
         update_rows4<U, NTL>(QdT + (size_t)b * (size_t)qstride, ldq, N, row, w0, theta + (size_t)b * ldv,
                      Fd + (size_t)b * ldv, lds, Yout + (size_t)b * ldv);
-}
-
-// ---------------------------------------------------------------------------
-// k_stream_read: tuning reference only (include/pqp_tuning.h).  Streams QdT
-// with exactly the hot kernel's access pattern and no solver arithmetic, to
-// measure the practical read ceiling of that pattern on this device.
-// ---------------------------------------------------------------------------
-template <int U, bool NTL>
-__global__ void __launch_bounds__(256) k_stream_read(const float* __restrict__ QdT, long long qstride, int ldq, int N,
-                                                     float* __restrict__ out) {
-    const int b = blockIdx.x, tid = threadIdx.x;
-    const float* Q = QdT + (size_t)b * (size_t)qstride;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r0 = 0; r0 < N; r0 += 1024) {
-        const int row = r0 + 4 * tid;
-        if (row >= N) continue;
-        const float* src = Q + row;
-        int k = 0;
-        for (; k + U <= N; k += U) {
-            float4 q[U];
-#pragma unroll
-            for (int j = 0; j < U; ++j) q[j] = ldq4<NTL>(src + (size_t)j * ldq);
-            src += (size_t)U * ldq;
-#pragma unroll
-            for (int j = 0; j < U; ++j) {
-                acc.x += q[j].x;
-                acc.y += q[j].y;
-                acc.z += q[j].z;
-                acc.w += q[j].w;
-            }
-        }
-        for (; k < N; ++k, src += ldq) {
-            const float4 q = ldq4<NTL>(src);
-            acc.x += q.x;
-        }
-    }
-    out[(size_t)b * 256 + tid] = acc.x + acc.y + acc.z + acc.w;
 }
 
 // ---------------------------------------------------------------------------
@@ -2626,19 +2576,15 @@ hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s)
 // Host-side launchers (declared in pqp_launch.h)
 // ---------------------------------------------------------------------------
 
-static int g_variant = 0;  // tuning knob (include/pqp_tuning.h); 0 = shipped default
-void set_variant(int v) { g_variant = v; }
-int get_variant() { return g_variant; }
-
-template <int U, bool NTL, bool MX = false>
+template <int U, bool NTL>
 static void launch_iterate_t(int B, const float* QdT, long long qstride, int ldq, int N, const float* theta,
                              const float* Fd, int ldv, const float* Y0, float* Y, int updates, hipStream_t s) {
     const size_t lds = (size_t)2 * ldq * sizeof(float);
     if (N <= 256)
-        hipLaunchKernelGGL((k_batch_iterate<64, U, NTL, MX>), dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd,
+        hipLaunchKernelGGL((k_batch_iterate<64, U, NTL>), dim3(B), dim3(64), lds, s, QdT, qstride, ldq, N, theta, Fd,
                            ldv, Y0, Y, updates);
     else
-        hipLaunchKernelGGL((k_batch_iterate<256, U, NTL, MX>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
+        hipLaunchKernelGGL((k_batch_iterate<256, U, NTL>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
                            Fd, ldv, Y0, Y, updates);
 }
 
@@ -2664,27 +2610,11 @@ hipError_t launch_batch_iterate(int B, const float* QdT, long long qstride, int 
 static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qstride, int ldq, int N,
                                           const float* theta, const float* Fd, int ldv, const float* Y0, float* Y,
                                           int updates, hipStream_t s) {
-    // 0 (shipped): 16-deep unroll with non-temporal Qd loads -- 6.88 TB/s at
-    // N=1024, B=4096 vs 7.02 TB/s for a bare read of the same pattern
-    // (profiles/r01/ab_4096.txt).  Others kept for A/B.
-    switch (g_variant) {
-        case 1: launch_iterate_t<8, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 2: launch_iterate_t<8, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 3: launch_iterate_t<4, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 4: launch_iterate_t<32, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 5: launch_iterate_t<16, false>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        case 6: launch_iterate_t<16, true, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-        default: launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,
-                              hipStream_t s) {
-    if (nt)
-        hipLaunchKernelGGL((k_stream_read<8, true>), dim3(B), dim3(256), 0, s, QdT, qstride, ldq, N, out);
-    else
-        hipLaunchKernelGGL((k_stream_read<8, false>), dim3(B), dim3(256), 0, s, QdT, qstride, ldq, N, out);
+    // 16-deep unroll with non-temporal Qd loads: 7.03 TB/s at N = 1024,
+    // B = 4096, chunk 10.  The other unroll depths (4, 8, 32), default-policy
+    // loads and max-based terms were measured and removed (DESIGN.md section 4,
+    // profiles/r01/ab_4096*.txt).
+    launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s);
     return hipGetLastError();
 }
 

@@ -192,10 +192,6 @@ extern int g_converge_persist_off;
 extern unsigned long long* g_converge_trace;  // tuning: [iterate][29][4] words (pqp_tune_converge_trace)
 extern int g_converge_trace_n;
 
-void set_variant(int v);
-int get_variant();
-hipError_t launch_stream_read(int B, const float* QdT, long long qstride, int ldq, int N, float* out, int nt,
-                              hipStream_t s);
 hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s);
 extern int g_single_scalar;  // tuning: k_solve_single with 4-byte loads only (no 8/16-byte forms)
 

@@ -105,7 +105,6 @@ SIGNATURES = {
     "pqp_tune_wave_pipe_max_b": (C.c_int, [C.c_int]),
     "pqp_tune_persist_trace": (C.c_int, [_vp, C.c_int]),
     "pqp_tune_wide_flags": (C.c_int, [C.c_int]),
-    "pqp_tune_stream_read": (C.c_int, [C.c_int, C.c_int, _vp, C.c_int, C.c_longlong, _vp, C.c_int, _vp]),
 }
 
 
