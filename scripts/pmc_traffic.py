@@ -12,7 +12,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNEL = "k_batch_iterate<256, 16, true, false>"
+KERNEL = "k_batch_iterate<256, 16, true>"
 
 
 def per_launch(path: str, counter: str, skip: int) -> tuple[float, int]:
