@@ -119,7 +119,10 @@ int pqp_tune_wave_pipe_max_b(int b);
 /* Timeline of the persistent launch's workgroup 0 (s_memtime shader clocks):
  * for the first `updates` updates, per update u and wave w, the four words
  * d_trace[(u * waves + w) * 4 + e] = {sweep start, y staged, running sums
- * received, chain done}.  updates = 0 turns the trace off. */
+ * received, chain done}; then, from d_trace[updates * waves * 4], per update
+ * and wave 1..waves-1, 8 words: s_memtime before each seventh of the wave's
+ * add chain and after it.  The buffer holds updates * waves * 12 words.
+ * updates = 0 turns the trace off. */
 int pqp_tune_persist_trace(void *d_trace, int updates);
 
 /* Converge-mode solves of problems with n_dual >= n that the persistent

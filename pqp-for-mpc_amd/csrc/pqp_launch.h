@@ -89,7 +89,7 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
 extern int g_persist_off;
 bool split_persist_fits(int N);  // all of k_split_persist's workgroups co-resident on this device
 extern int g_persist_fit_cus;    // tuning: CU count the residency checks assume (0: the device's)
-extern unsigned long long* g_persist_trace;  // tuning: device buffer of 4 * waves * g_persist_trace_n words
+extern unsigned long long* g_persist_trace;  // tuning: device buffer of 12 * waves * g_persist_trace_n words
 extern int g_persist_trace_n;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
 // lean relay (k_lean_relay): Qd packets (4 B per entry, lw / 2 rows per

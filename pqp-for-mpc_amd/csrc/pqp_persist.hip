@@ -325,6 +325,35 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                 acc = __uint_as_float((unsigned)h);
                 mark(u, 2);
                 __builtin_amdgcn_s_setprio(3);
+                if (trace && blockIdx.x == 0 && u < trace_n) {
+                    // traced launches only: s_memtime before each seventh of
+                    // the chain (stored after it), to see where a slice loses time
+                    constexpr int G = 7, PG = (NP + G - 1) / G;
+                    u64 t[G + 1];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        t[g] = __builtin_amdgcn_s_memtime();
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int j = g * PG; j < (g + 1) * PG && j < NP; ++j) {
+                            acc += prod[j].x;  // :608-609, k in order
+                            acc += prod[j].y;
+                            acc += prod[j].z;
+                            acc += prod[j].w;
+                        }
+                        asm volatile("" : "+v"(acc));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    t[G] = __builtin_amdgcn_s_memtime();
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (lane == 0) {
+                        u64* ext = trace + (size_t)trace_n * W * 4 + ((size_t)u * W + w) * 8;
+#pragma unroll
+                        for (int g = 0; g < G + 1 && g < 8; ++g) ext[g] = t[g];
+                    }
+                    return true;
+                }
 #pragma unroll
                 for (int j = 0; j < NP; ++j) {
                     acc += prod[j].x;  // :608-609, k in order

@@ -33,7 +33,7 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
     W = 1
     while first(W) < KB:
         W += 1
-    tr = torch.zeros(n_trace * W * 4, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(n_trace * W * 12, dtype=torch.int64, device="cuda")
     with pqp_amd.Problem(P) as prob:
         prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
         t0 = time.perf_counter()
@@ -44,7 +44,9 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
         prob.solve(pqp_amd.MODE_FIXED, num_iter=iters)
         traced = time.perf_counter() - t0
         L.pqp_tune_persist_trace(None, 0)
-    t = tr.cpu().numpy().reshape(n_trace, W, 4).astype(np.int64)
+    full = tr.cpu().numpy().astype(np.int64)
+    t = full[: n_trace * W * 4].reshape(n_trace, W, 4)
+    fine = full[n_trace * W * 4:].reshape(n_trace, W, 8)
     lo, hi = 10, 30
     period = float(np.median(np.diff(t[lo:hi, 0, 2])))  # wave 0's turn, update to update
     us_per_update = untraced / (iters - 1) * 1e6
@@ -65,6 +67,9 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
     out["handoff_clocks (wave w done -> wave w+1 turn)"] = float(np.median(
         [t[u, w + 1, 2] - t[u, w, 3] for u in range(lo, hi) for w in range(W - 1)]))
     out["raw_update_10"] = (t[10] - t[10, 0, 0]).tolist()
+    # each later wave's chain in sevenths: clocks per seventh (median over updates)
+    out["chain_sevenths_clocks"] = {
+        f"wave{w}": np.median(np.diff(fine[lo:hi, w, :], axis=1), axis=0).tolist() for w in range(1, W)}
     print(json.dumps(out, indent=1))
 
 
