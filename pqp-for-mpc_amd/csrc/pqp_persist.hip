@@ -54,9 +54,14 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int kPLanes = 32;  // row sides per workgroup
-constexpr int kPW0 = 24;     // packets (4 values of k) of wave 0's slice: multiplied inside its add chain
-constexpr int kPW1 = 36;     // packets of wave 1's slice: its products must be ready when wave 0 is done
-constexpr int kPW = 49;      // packets per later slice: their products are formed ahead, in 4 * kPW VGPRs
+#ifndef PQP_PERSIST_SLICES  // A/B builds: -DPQP_PERSIST_SLICES=P0,P1,PW
+#define PQP_PERSIST_SLICES 24, 36, 49
+#endif
+constexpr int kSlices[3] = {PQP_PERSIST_SLICES};
+constexpr int kPW0 = kSlices[0];  // packets (4 values of k) of wave 0's slice: multiplied inside its add chain
+constexpr int kPW1 = kSlices[1];  // packets of wave 1's slice: its products must be ready when wave 0 is done
+constexpr int kPW = kSlices[2];   // packets per later slice: their products are formed ahead, in 4 * kPW VGPRs
+static_assert(kPW0 + kPW1 + 4 * kPW >= 256, "six waves must cover n_dual 1024");
 constexpr int kLateGate = 1; // waves 4, 5 form their products once this wave has handed on its sums
 constexpr int kPMaxWaves = 6;
 constexpr long long kPTimeoutTicks = 200000000LL;  // s_memrealtime runs at 100 MHz: 2 s
@@ -122,6 +127,26 @@ __device__ __forceinline__ float chain_qreg(float acc, const f4v (&q)[NP], const
         __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
+}
+
+// prod[j] = prod[j] * y[j] with the slice's q already in prod (read ahead,
+// while the wave waited for y): only y is read, D packets ahead.
+template <int NP>
+__device__ __forceinline__ void slice_products_inplace(f4v (&prod)[NP], const f4v* yw) {
+    constexpr int D = NP < 6 ? NP : 6;
+    f4v yr[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) yr[j] = yw[j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
+        const f4v q = prod[j], y = yr[j % (D + 1)];
+        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // Products of one slice, prod[j] = q[j] * y[j] (each product rounded as the
@@ -285,7 +310,6 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         float acc = 0.0f;
         u64* sl = slot + (size_t)par * W * 64;
         const unsigned want = (unsigned)(u + 1);
-        bool ok = true;
         if (w == 0) {
             // wave 0 reads its slice's split entries while it waits for y:
             // its products start the chain, and then need only the y reads
@@ -301,27 +325,28 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             __builtin_amdgcn_s_setprio(3);
             acc = chain_qreg(acc, q0, yw);
         } else {
-            if (!stage_y()) {
-                fail(err, 1);
-                return;
-            }
             // products ahead of the turn, the running sums of the previous
             // slice, then this slice's adds; NP = the slice's packets
-            auto turn = [&](auto np) {
+            auto turn = [&](auto np) -> int {
                 constexpr int NP = decltype(np)::value;
                 f4v prod[NP];
+                // the slice's split entries, read while the wave waits for y
+                // (multiplied in place once y is staged)
+#pragma unroll
+                for (int j = 0; j < NP; ++j) prod[j] = qw[(size_t)j * kPLanes];
+                if (!stage_y()) return 1;
                 if (w >= 4) {
                     // waves 4, 5 share SIMDs with waves 0, 1: they form their
                     // products once wave kLateGate has handed on its sums, so
                     // the first waves' products and chains run alone
-                    if (!lds_wait(sl + kLateGate * 64 + lane, want, true)) return false;
+                    if (!lds_wait(sl + kLateGate * 64 + lane, want, true)) return 2;
                 }
-                slice_products(prod, qw, yw);
+                slice_products_inplace(prod, yw);
                 // pinned here: otherwise the compiler sinks the multiplies into the chain
 #pragma unroll
                 for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
                 u64 h;
-                if (!lds_wait(sl + (w - 1) * 64 + lane, want, false, &h)) return false;
+                if (!lds_wait(sl + (w - 1) * 64 + lane, want, false, &h)) return 2;
                 acc = __uint_as_float((unsigned)h);
                 mark(u, 2);
                 __builtin_amdgcn_s_setprio(3);
@@ -352,7 +377,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
 #pragma unroll
                         for (int g = 0; g < G + 1 && g < 8; ++g) ext[g] = t[g];
                     }
-                    return true;
+                    return 0;
                 }
 #pragma unroll
                 for (int j = 0; j < NP; ++j) {
@@ -361,13 +386,13 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                     acc += prod[j].z;
                     acc += prod[j].w;
                 }
-                return true;
+                return 0;
             };
-            ok = (w == 1) ? turn(std::integral_constant<int, kPW1>{}) : turn(std::integral_constant<int, kPW>{});
-        }
-        if (!ok) {
-            fail(err, 2);
-            return;
+            const int rc = (w == 1) ? turn(std::integral_constant<int, kPW1>{}) : turn(std::integral_constant<int, kPW>{});
+            if (rc) {
+                fail(err, rc);
+                return;
+            }
         }
         asm volatile("" : "+v"(acc));  // the mark below follows the chain
         mark(u, 3);
