@@ -2,9 +2,11 @@
 problem of n_dual <= 1024, every update inside ONE kernel, the iterate handed
 between workgroups as tagged granules.  Bar: bit-exact with the oracle
 (PQP_CPU.c's updateY2 restated) and with the graph-replayed relay update
-(pqp_tune_persist(1)), for ragged sizes around the wave-slice (192 k) and
+(pqp_tune_persist(1)), for ragged sizes around the wave slices (k of 96,
+144, then 196 per wave: boundaries 96, 240, 436, 632, 828) and the
 workgroup (16 rows) boundaries, update counts of both parities, repeated
-solves, special values, and the size limit (N = 1025 falls back)."""
+solves, special values, the traced launch, and the size limit (N = 1025
+falls back)."""
 from __future__ import annotations
 
 import numpy as np
@@ -33,7 +35,8 @@ def _solve(gpu_lib, P, num_iter, persist=True, reps=1):
     return rs
 
 
-@pytest.mark.parametrize("N", [99, 100, 191, 192, 193, 257, 384, 575, 576, 577, 1000, 1023, 1024])
+@pytest.mark.parametrize("N", [1, 4, 95, 96, 97, 99, 100, 191, 192, 193, 240, 241, 257, 384, 436, 437, 575, 576,
+                               577, 632, 633, 828, 829, 1000, 1023, 1024])
 def test_persistent_fixed_mode_vs_oracle(gpu_lib, orc, N):
     P = _dual(orc, N)
     ups = 11
@@ -93,3 +96,30 @@ def test_beyond_persistent_limit_falls_back(gpu_lib, orc):
     want = orc.iterate(P["Qd"], P["Fd"], N, 5)
     (r,) = _solve(gpu_lib, P, 6)
     assert_bitwise(r["Y"], want, "N=1025 (relay)")
+
+
+def test_persistent_traced_launch_same_bits(gpu_lib, orc):
+    """The traced launch (pqp_tune_persist_trace: clock marks per wave and per
+    seventh of each later wave's chain, a separate code path for the adds)
+    gives the untraced launch's bits, and its marks are ordered."""
+    import ctypes as C
+
+    import torch
+
+    N, ups, n_tr = 1024, 40, 20
+    P = _dual(orc, N, seed=4, inst=2)
+    (plain,) = _solve(gpu_lib, P, ups + 1)
+    L = gpu_lib.lib()
+    W = 6
+    tr = torch.zeros(n_tr * W * 12, dtype=torch.int64, device="cuda")
+    assert L.pqp_tune_persist_trace(C.c_void_p(tr.data_ptr()), n_tr) == 0
+    try:
+        (traced,) = _solve(gpu_lib, P, ups + 1)
+    finally:
+        L.pqp_tune_persist_trace(None, 0)
+    assert_bitwise(traced["Y"], plain["Y"], "traced vs untraced")
+    t = tr.cpu().numpy()
+    coarse = t[: n_tr * W * 4].reshape(n_tr, W, 4)
+    fine = t[n_tr * W * 4:].reshape(n_tr, W, 8)
+    assert np.all(coarse[1:] > 0) and np.all(np.diff(coarse[1:], axis=2) >= 0)
+    assert np.all(fine[1:, 1:] > 0) and np.all(np.diff(fine[1:, 1:], axis=2) >= 0)
