@@ -27,8 +27,8 @@ def main(N=1024, B=4096, K=8):
     M = pb.M
     out = {"n_dual": N, "m": M, "problems": B, "updates": K, "setup_s": setup}
     ys = {}
-    for name, opts in (("default", 0), ("scalar_loads", 4), ("fused", 1), ("transposes", 2), ("default_again", 0),
-                       ("scalar_again", 4)):
+    for name, opts in (("default", 0), ("fused", 1), ("scalar_loads", 4), ("default_again", 0), ("fused_again", 1),
+                       ("transposes", 2)):
         prev = L.pqp_tune_batch_converge(opts)
         pb.solve(max_updates=1)  # warm
         torch.cuda.synchronize()
