@@ -5,7 +5,8 @@ skip the column-major copy; optionally (tuning) terminate()'s Y'Qd
 (PQP_CPU.c:648-653) rides in the same pass over Qd as the speculative update
 to Y_{h+1} (:603-618), and Gp / Qp_inv are read through transposes.  Bar: the
 reference's h, Y and U bit for bit (oracle) in every setting, and a batch
-mixing both kinds of Qd."""
+mixing both kinds of Qd.  N and M multiples of 4 take the 8/16-byte load
+forms of k_solve_single; opts bit 2 (and ragged N, M) the 4-byte form."""
 from __future__ import annotations
 
 import numpy as np
@@ -23,7 +24,7 @@ def _check(pb, b, h, Y, U, what):
     assert_bitwise(pb.U[b].cpu().numpy(), U, f"{what} U")
 
 
-@pytest.mark.parametrize("opts", [0, 1, 2, 3])
+@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4])
 def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts):
     from test_gpu_wide import _testing_file
 
@@ -39,10 +40,10 @@ def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts):
         _check(pb, b, h, Y, U, f"test2 copy {b} opts={opts}")
 
 
-@pytest.mark.parametrize("opts", [0, 3])
-def test_batch_synthetic_capped_vs_oracle(gpu_lib, orc, opts):
+@pytest.mark.parametrize("opts,N,M", [(0, 256, 128), (3, 256, 128), (4, 256, 128), (0, 201, 61), (0, 204, 62)])
+def test_batch_synthetic_capped_vs_oracle(gpu_lib, orc, opts, N, M):
     L = gpu_lib.lib()
-    N, M, B, cap = 256, 128, 3, 6
+    B, cap = 3, 6
     prev = L.pqp_tune_batch_converge(opts)
     try:
         pb = gpu_lib.ProblemBatch.synthetic(9, 4, B, N, M).solve(max_updates=cap)
