@@ -1,8 +1,8 @@
 /*
  * include/pqp_tuning.h -- tuning/diagnostic entry points of libpqp.  Not part
- * of the drop-in surface; used by scripts/ab_batch.py to A/B kernel variants
- * interleaved in one process and to measure the practical HBM read ceiling of
- * the hot kernel's access pattern on the device at hand.
+ * of the drop-in surface; used by the tests (every variant must give the same
+ * bits) and by scripts/ to A/B kernel variants and trace the persistent
+ * launches on the device at hand.
  */
 #ifndef PQP_TUNING_H
 #define PQP_TUNING_H

@@ -15,12 +15,15 @@ def shard_plan(world: int, per_rank: int, seed: int) -> list[tuple[int, int, int
     return [(int(seed), r * int(per_rank), int(per_rank)) for r in range(int(world))]
 
 
-def scatter_plan(dist, rank: int, world: int, per_rank: int, seed: int, device) -> tuple[int, int, int]:
-    """Rank 0 hands every rank its shard description (one small scatter)."""
+def scatter_plan(dist, rank: int, world: int, per_rank: int, seed: int, device,
+                 collective_at_one: bool = False) -> tuple[int, int, int]:
+    """Rank 0 hands every rank its shard description (one small scatter).
+    `collective_at_one`: run the collective even for one rank (tests of the
+    RCCL path on a one-GPU box)."""
     import torch
 
     mine = torch.zeros(3, dtype=torch.int64, device=device)
-    if dist is None or world == 1:
+    if dist is None or (world == 1 and not collective_at_one):
         return shard_plan(1, per_rank, seed)[0]
     parts = None
     if rank == 0:
@@ -30,12 +33,12 @@ def scatter_plan(dist, rank: int, world: int, per_rank: int, seed: int, device) 
     return s, i0, n
 
 
-def gather_rows(dist, rank: int, world: int, y):
+def gather_rows(dist, rank: int, world: int, y, collective_at_one: bool = False):
     """Concatenate every rank's [count, N] block on rank 0 (rank order =
     problem order).  Returns the full tensor on rank 0, None elsewhere."""
     import torch
 
-    if dist is None or world == 1:
+    if dist is None or (world == 1 and not collective_at_one):
         return y
     y = y.contiguous()
     outs = [torch.empty_like(y) for _ in range(world)] if rank == 0 else None

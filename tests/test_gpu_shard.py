@@ -65,3 +65,49 @@ def test_sharded_batches_gathered_in_problem_order(gpu_lib, orc, tmp_path, world
     for b in range(world * PER_RANK):
         P = orc.synth_problem(SEED, b, N, N // 2, with_qp=False)
         assert_bitwise(got[b], orc.iterate(P["Qd"], P["Fd"], N, UPDATES), f"problem {b}")
+
+
+def _rccl_one_rank_main(rank, world, port, out):
+    import sys
+
+    for p in (ROOT / "pqp-for-mpc_amd", ROOT / "oracle"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    import pqp_amd
+    from pqp_amd.shard import gather_rows, scatter_plan
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)  # bench.py's init
+    seed, inst0, B = scatter_plan(dist, rank, world, 3, 11, dev, collective_at_one=True)
+    b = pqp_amd.Batch(B, 300, device=dev).generate(seed, inst0=inst0, M=150)
+    b.iterate(4)
+    torch.cuda.synchronize(dev)
+    y = b.Y[:, :300].contiguous()
+    full = gather_rows(dist, rank, world, y, collective_at_one=True)
+    t = torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing
+    dist.barrier()
+    np.save(out + ".npy", full.cpu().numpy())
+    np.save(out + ".plan.npy", np.array([seed, inst0, B, int(t[1].item() == 2.5)]))
+    dist.destroy_process_group()
+
+
+def test_rccl_scatter_gather_one_rank(gpu_lib, orc, tmp_path):
+    """bench.py's RCCL calls -- nccl init with device_id, the shard-plan
+    scatter, the Y* gather, the max all-reduce, the barrier -- over a one-rank
+    group (RCCL refuses two ranks on one GPU), with the gathered iterates
+    checked against the oracle."""
+    import torch.multiprocessing as mp
+
+    out = str(tmp_path / "r")
+    mp.spawn(_rccl_one_rank_main, args=(1, _free_port(), out), nprocs=1, join=True)
+    seed, inst0, B, ok = (int(v) for v in np.load(out + ".plan.npy"))
+    assert (seed, inst0, B, ok) == (11, 0, 3, 1)
+    full = np.load(out + ".npy")
+    for j in range(B):
+        P = orc.synth_problem(11, j, 300, 150, with_qp=False)
+        assert_bitwise(full[j], orc.iterate(P["Qd"], P["Fd"], 300, 4), f"problem {j}")
