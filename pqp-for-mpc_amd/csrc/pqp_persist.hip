@@ -62,6 +62,7 @@ constexpr int kPW0 = kSlices[0];  // packets (4 values of k) of wave 0's slice: 
 constexpr int kPW1 = kSlices[1];  // packets of wave 1's slice: its products must be ready when wave 0 is done
 constexpr int kPW = kSlices[2];   // packets per later slice: their products are formed ahead, in 4 * kPW VGPRs
 static_assert(kPW0 + kPW1 + 4 * kPW >= 256, "six waves must cover n_dual 1024");
+static_assert(kPW0 <= 64 && kPW1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");
 constexpr int kLateGate = 1; // waves 4, 5 form their products once this wave has handed on its sums
 constexpr int kPMaxWaves = 6;
 constexpr long long kPTimeoutTicks = 200000000LL;  // s_memrealtime runs at 100 MHz: 2 s
@@ -101,6 +102,20 @@ __device__ __forceinline__ bool lds_wait(u64* word, unsigned want, bool doze, u6
         if ((spins & 255) == 255 && dl.expired()) return false;
         if (doze) __builtin_amdgcn_s_sleep(1);
     }
+}
+
+// The running sums' hand-off wait on the critical path: a bare poll whose
+// exit falls through into the adds, bounded by a spin count (each poll is an
+// LDS round trip of >= 64 clocks, so 2^25 polls last >= 0.9 s) instead of the
+// clock.  False when the bound ran out.
+constexpr unsigned kHandoffSpins = 1u << 25;
+__device__ __forceinline__ bool lds_wait_sums(u64* word, unsigned want, u64& h) {
+    unsigned spins = 0;
+#pragma clang loop unroll(disable)
+    do {
+        h = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } while (!__all((unsigned)(h >> 32) == want) && ++spins < kHandoffSpins);
+    return spins < kHandoffSpins;
 }
 
 // Wave 0's slice: its split entries were read into registers ahead (during
@@ -207,6 +222,9 @@ size_t persist_lds_bytes(int N) {
 
 // SP: the k_build_split layout with lw = 32 (workgroup-major packets).
 // gran: 2 * N granules, zeroed before the launch.  err: zeroed before the launch.
+// TRACE: the timeline instantiation (pqp_tune_persist_trace); the default one
+// carries no trace branches on its critical path.
+template <bool TRACE>
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     k_split_persist(const float* __restrict__ SP, const float* __restrict__ fdpn, int N, int updates,
                     const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err, u64* trace,
@@ -233,6 +251,9 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         for (int e = tid; e < KP * kPLanes; e += blockDim.x)
             qs[e] = (e < KB * kPLanes) ? src[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
         for (int e = tid; e < 2 * W * 64; e += blockDim.x) slot[e] = 0ull;
+        // y past N (read by the last packet's products) stays +0 for the whole
+        // solve: zeroed once in both parity buffers
+        for (int e = tid; e < 2 * (KP * 4 - N); e += blockDim.x) ysb[(e & 1) * KP * 4 + N + (e >> 1)] = 0.0f;
     }
     const float fd = live ? fdpn[p] : 0.0f;
     __syncthreads();
@@ -244,10 +265,13 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     float yrow = 0.0f;  // last wave: y_i of this lane's row (for y_next = num / den * y_i)
     // optional timeline (s_memtime) of workgroup 0: per update and wave,
     // {sweep start, y staged, turn (sums received), chain done}
-    u64* tr = (trace && blockIdx.x == 0 && lane == 0) ? trace : nullptr;
+    u64* tr = (TRACE && trace && blockIdx.x == 0 && lane == 0) ? trace : nullptr;
     auto mark = [&](int u, int e) {
-        if (tr && u < trace_n) tr[((size_t)u * W + w) * 4 + e] = __builtin_amdgcn_s_memtime();
+        if constexpr (TRACE)
+            if (tr && u < trace_n) tr[((size_t)u * W + w) * 4 + e] = __builtin_amdgcn_s_memtime();
     };
+    int bad = 0;  // an expired hand-off wait (code 2), reported after the update
+    float yn = 0.0f;  // last wave: this lane's row of y_next
     for (int u = 0; u < updates; ++u) {
         const int par = u & 1;
         float* ys = ysb + par * ny;
@@ -258,49 +282,50 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             for (int k = k0 + lane; k < k1; k += 64) ys[k] = Y0 ? Y0[k] : 1000.0f;  // initMat(Y, 1000) :710
             if (last) yrow = (Y0 && row < N) ? Y0[row] : 1000.0f;
         } else {
+            // the sweep: the slice's granules (4 per lane, indices clamped into
+            // the slice: a duplicate re-reads the slice's last granule, in the
+            // same request as its neighbours) and, for the last wave, y_i of
+            // this lane's row (:594); every load in flight, then one
+            // wave-wide test of the tags (the data is its own flag).  No
+            // per-lane conditions: the exit falls straight into the stores.
             const gu64* g = gran + (size_t)par * N;
             const unsigned tag = (unsigned)u;
-            for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
-                const bool own = last && kb == k0 && row < N;  // + y_i of the rows this workgroup finishes (:594)
-                u64 x[5] = {};
-                // the sweep: every load of the slice in flight, then one
-                // wave-wide test of the tags (the data is its own flag)
-                auto issue = [&](u64 (&xs)[5]) {
+            // this lane's granules, clamped into the slice; computed per call
+            // (the laundered lane keeps them out of the registers held across
+            // updates, where the products' 4 * kPW live)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            int kk[4];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const int k = kb + 64 * m + lane;
-                        if (k < k1) xs[m] = __hip_atomic_load(g + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    if (own) xs[4] = __hip_atomic_load(g + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                };
-                auto arrived = [&](const u64 (&xs)[5]) {
-                    bool ok = true;
+            for (int m = 0; m < 4; ++m) kk[m] = (k0 + 64 * m + ln < k1) ? k0 + 64 * m + ln : k1 - 1;
+            const int rowc = row < N ? row : N - 1;
+            u64 x[4], xo = 0;
+            Deadline dl;
+            unsigned spins = 0;
+            bool ok;
+#pragma clang loop unroll(disable)
+            do {
 #pragma unroll
-                    for (int m = 0; m < 4; ++m)
-                        if (kb + 64 * m + lane < k1) ok &= (unsigned)(xs[m] >> 32) == tag;
-                    if (own) ok &= (unsigned)(xs[4] >> 32) == tag;
-                    return __all(ok);
-                };
-                Deadline dl;
-                for (unsigned spins = 0;; ++spins) {
-                    issue(x);
-                    if (arrived(x)) break;
-                    if ((spins & 63) == 63 && dl.expired()) return false;
+                for (int m = 0; m < 4; ++m) x[m] = __hip_atomic_load(g + kk[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (last) xo = __hip_atomic_load(g + rowc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = true;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) ok &= (unsigned)(x[m] >> 32) == tag;
+                if (last) ok &= (unsigned)(xo >> 32) == tag;
+                ok = __all(ok);
+                if (!ok) {
+                    if ((++spins & 63) == 0 && dl.expired()) return false;
                     // one sweep at a time, a short pause between them (two sweeps
                     // in flight, issued 256 to 512 clocks apart, measured 5-15 %
                     // slower: the pollers' own traffic)
                     __builtin_amdgcn_s_sleep(1);
                 }
+            } while (!ok);
+            // duplicates store the same value to the same word
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int k = kb + 64 * m + lane;
-                    if (k < k1) ys[k] = __uint_as_float((unsigned)x[m]);
-                }
-                if (own) yrow = __uint_as_float((unsigned)x[4]);
-            }
+            for (int m = 0; m < 4; ++m) ys[kk[m]] = __uint_as_float((unsigned)x[m]);
+            if (last) yrow = __uint_as_float((unsigned)xo);
         }
-        // zero y past N up to the slice end (read by the last packet's products)
-        for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
         mark(u, 1);
         return true;
         };
@@ -339,18 +364,20 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                     // waves 4, 5 share SIMDs with waves 0, 1: they form their
                     // products once wave kLateGate has handed on its sums, so
                     // the first waves' products and chains run alone
-                    if (!lds_wait(sl + kLateGate * 64 + lane, want, true)) return 2;
+                    if (!lds_wait(sl + kLateGate * 64 + lane, want, true)) bad = 2;
                 }
                 slice_products_inplace(prod, yw);
                 // pinned here: otherwise the compiler sinks the multiplies into the chain
 #pragma unroll
                 for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
                 u64 h;
-                if (!lds_wait(sl + (w - 1) * 64 + lane, want, false, &h)) return 2;
+                // an expired wait is reported once the update's sums are handed
+                // on (no branch between the sums' arrival and the first add)
+                if (!lds_wait_sums(sl + (w - 1) * 64 + lane, want, h)) bad = 2;
                 acc = __uint_as_float((unsigned)h);
                 mark(u, 2);
                 __builtin_amdgcn_s_setprio(3);
-                if (trace && blockIdx.x == 0 && u < trace_n) {
+                if (TRACE && trace && blockIdx.x == 0 && u < trace_n) {
                     // traced launches only: s_memtime before each seventh of
                     // the chain (stored after it), to see where a slice loses time
                     constexpr int G = 7, PG = (NP + G - 1) / G;
@@ -400,19 +427,28 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             __hip_atomic_store(sl + w * 64 + lane, ((u64)want << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_s_setprio(0);
+            if (bad) {
+                fail(err, bad);
+                return;
+            }
             continue;
         }
         __builtin_amdgcn_s_setprio(0);
         // ---- 4. the last slice's wave finishes the rows ----
-        const float v = acc + 1.0f * fd;     // even lane: num (:611), odd lane: den (:612)
-        const float den = __shfl_xor(v, 1);  // whole wave active
-        if (!(p & 1) && live) {
-            const float yn = v / den * yrow;  // :594
+        const float v = acc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
+        // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2),
+        // not an LDS permute; every lane divides (odd lanes' quotients unused)
+        const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+        yn = v / den * yrow;  // :594
+        if (!(p & 1) && live)
             __hip_atomic_store(gran + (size_t)(par ^ 1) * N + row, ((u64)want << 32) | __float_as_uint(yn),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (u == updates - 1) Yout[row] = yn;
+        if (bad) {
+            fail(err, bad);
+            return;
         }
     }
+    if (last && updates > 0 && !(p & 1) && live) Yout[row] = yn;
 }
 
 int g_persist_fit_cus = 0;  // tuning: CU count the residency check assumes (0: the device's)
@@ -428,8 +464,9 @@ bool split_persist_fits(int N) {
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
     if (g_persist_fit_cus > 0) cus = g_persist_fit_cus;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_split_persist), threads,
-                                                     persist_lds_bytes(N)) != hipSuccess)
+    const void* kern = g_persist_trace ? reinterpret_cast<const void*>(&k_split_persist<true>)
+                                       : reinterpret_cast<const void*>(&k_split_persist<false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, persist_lds_bytes(N)) != hipSuccess)
         return false;
     return (long long)per * cus >= G;
 }
@@ -442,8 +479,12 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
     hipError_t e = hipMemsetAsync(gran, 0, sizeof(u64) * 2 * N, s);
     if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_split_persist, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N, updates, Y0,
-                       Yout, gran, err, g_persist_trace, g_persist_trace_n);
+    if (g_persist_trace)
+        hipLaunchKernelGGL(k_split_persist<true>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
+                           updates, Y0, Yout, gran, err, g_persist_trace, g_persist_trace_n);
+    else
+        hipLaunchKernelGGL(k_split_persist<false>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
+                           updates, Y0, Yout, gran, err, nullptr, 0);
     return hipGetLastError();
 }
 
