@@ -57,7 +57,8 @@ constexpr int kL = 32;     // output columns (update: row sides) per workgroup
 constexpr int kP0 = 24;    // packets (4 values of k) of wave 0's slice, multiplied inside its chain
 constexpr int kP1 = 36;    // packets of wave 1's slice: its products must be ready when wave 0 is done
 constexpr int kPW = 49;    // packets per later slice, products formed ahead in 4 kPW VGPRs
-constexpr int kLateGate = 1;  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
+constexpr int kLateGate = 1;
+static_assert(kP0 <= 64 && kP1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
 constexpr int kMaxW = 6;   // waves for K <= 1024
 constexpr int kR = 8;      // ring depth (iterates in flight)
 constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
@@ -209,13 +210,30 @@ __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* cons
 }
 
 constexpr int kTraceIds = 4 * kMaxW + kDecW;
+template <bool TRACE>
 __device__ __forceinline__ void mark(const CvArgs& a, bool on, long long u, int id, int e) {
-    if (on && u - a.u0 < a.trace_n)
-        a.trace[((size_t)(u - a.u0) * kTraceIds + id) * 4 + e] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (TRACE)
+        if (on && u - a.u0 < a.trace_n)
+            a.trace[((size_t)(u - a.u0) * kTraceIds + id) * 4 + e] = __builtin_amdgcn_s_memrealtime();
+}
+
+// The running sums' hand-off wait of a chain wave: a bare poll whose exit
+// falls through into the adds; the launch's stop flag and the time limit are
+// read every 256 polls only.  0: arrived, 1: the launch stopped, 2: timed out.
+__device__ __forceinline__ int wait_sums(const CvArgs& a, const u64* src, unsigned tag, u64& h) {
+    Deadline dl;
+    unsigned spins = 0;
+    bool ok;
+#pragma clang loop unroll(disable)
+    do {
+        h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ok = __all((unsigned)(h >> 32) == tag);
+    } while (!ok && ((++spins & 255) != 0 || !(stopped(a) || dl.expired())));
+    return ok ? 0 : (stopped(a) ? 1 : 2);
 }
 
 // One wave of a chain role (UPD, T1, T2, T3): iterates [ub, ue].
-template <int ROLE>
+template <int ROLE, bool TRACE>
 __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K, const f4v* qs, float* ysb, int ny,
                                            u64* hs) {
     const int N = a.N, M = a.M;
@@ -238,13 +256,14 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
     const long long ub = a.u0;
     const long long ue = ROLE == kUpd ? a.u_prod_end - 1 : a.u_dec_end;
     float yrow = 0.0f;
-    const bool tr = a.trace && g == 0 && lane == 0;
+    const bool tr = TRACE && a.trace && g == 0 && lane == 0;
     const int tid_ = ROLE * kMaxW + w;
+    int bad = 0;  // a hand-off wait that ended without the sums (wait_sums' code), acted on after the chain
     for (long long u = ub; u <= ue; ++u) {
         const unsigned tag = (unsigned)(u + 1);
         const int slot = (int)(u & (kR - 1));
         float* ys = ysb + (int)(u & 1) * ny;
-        mark(a, tr, u, tid_, 0);
+        mark<TRACE>(a, tr, u, tid_, 0);
         // UPD's last wave: the slot y_{u+1} goes to must be free (issued early, tested after the chain)
         long long dec_seen = 0;
         const bool need_bp = ROLE == kUpd && last && u + 1 - kR >= a.u0;
@@ -253,31 +272,32 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
         // branch below, so that wave 0's registered q does not stay live
         // across the other branch) ----
         auto stage_x = [&]() -> bool {
+            // the slice's granules, 4 per lane with indices clamped into the
+            // slice (a duplicate re-reads its last granule), + y_i for UPD's last
+            // wave: every load unconditional, and the stores too (a duplicate
+            // stores the same value to the same word); x past K is +0 from the
+            // launch's start
             const gu64* gx = (const gu64*)rx + (size_t)slot * nx;
-            for (int kb = k0; kb < k1; kb += 256) {  // up to 4 granules per lane per sweep
-                const bool own = ROLE == kUpd && last && kb == k0 && row < N;  // y_i for y_next = num/den*y_i (:594)
-                const gu64* gp[5];
-                bool on[5];
-                float v[5] = {};
+            int ln = lane;
+            asm volatile("" : "+v"(ln));  // keeps the indices out of the registers held across iterates
+            const gu64* gp[5];
+            bool on[5];
+            float v[5] = {};
+            int kk[4];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int k = kb + 64 * m + lane;
-                    on[m] = k < k1;
-                    gp[m] = gx + (on[m] ? k : 0);
-                }
-                on[4] = own;
-                gp[4] = gx + (own ? row : 0);
-                if (!await_granules<5>(a, gp, on, tag, v, 1 + ROLE)) return false;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int k = kb + 64 * m + lane;
-                    if (k < k1) ys[k] = v[m];
-                }
-                if (own) yrow = v[4];
+            for (int m = 0; m < 4; ++m) {
+                kk[m] = (k0 + 64 * m + ln < k1) ? k0 + 64 * m + ln : k1 - 1;
+                gp[m] = gx + kk[m];
+                on[m] = true;
             }
-            // zero y past K up to the slice end (the +0 packets' partners)
-            for (int k = (k1 > k0 ? k1 : k0) + lane; k < 4 * pk1; k += 64) ys[k] = 0.0f;
-            mark(a, tr, u, tid_, 1);
+            const bool own = ROLE == kUpd && last;  // y_i for y_next = num/den*y_i (:594)
+            gp[4] = gx + (row < N ? row : N - 1);
+            on[4] = own;
+            if (!await_granules<5>(a, gp, on, tag, v, 1 + ROLE)) return false;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) ys[kk[m]] = v[m];
+            if (own) yrow = v[4];
+            mark<TRACE>(a, tr, u, tid_, 1);
             return true;
         };
         const f4v* qw = qs + (size_t)pk0 * kL + ll;
@@ -317,19 +337,10 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
                 slice_products(prod, qw, yw);
 #pragma unroll
                 for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
-                const u64* src = hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll;
-                Deadline dl;
                 u64 h;
-                for (unsigned spins = 0;; ++spins) {
-                    h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (__all((unsigned)(h >> 32) == tag)) break;
-                    if ((spins & 255) == 255) {
-                        if (stopped(a)) return 1;
-                        if (dl.expired()) return 2;
-                    }
-                }
+                bad = wait_sums(a, hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll, tag, h);
                 acc = __uint_as_float((unsigned)h);
-                mark(a, tr, u, tid_, 2);
+                mark<TRACE>(a, tr, u, tid_, 2);
                 __builtin_amdgcn_s_setprio(3);
 #pragma unroll
                 for (int j = 0; j < NP; ++j) {
@@ -345,19 +356,30 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             if (rc) return;
         }
         asm volatile("" : "+v"(acc));
-        mark(a, tr, u, tid_, 3);
+        mark<TRACE>(a, tr, u, tid_, 3);
         if (!last) {
+            // (after a failed wait the next wave gets a tagged word too: it
+            // stops at its next sweep)
             if (lane < kL)
                 __hip_atomic_store(hs + ((size_t)slot * kMaxW + w) * kL + ll, granule(tag, acc), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_s_setprio(0);
+            if (bad) {
+                if (bad == 2) fail(a, 10 + ROLE);
+                return;
+            }
             continue;
         }
         __builtin_amdgcn_s_setprio(0);
+        if (bad) {  // the last wave publishes nothing after a failed wait
+            if (bad == 2) fail(a, 10 + ROLE);
+            return;
+        }
         // ---- 4. the last wave's epilogue ----
         if (ROLE == kUpd) {
             const float v = acc + 1.0f * cst;    // even lane: num (:611), odd lane: den (:612)
-            const float den = __shfl_xor(v, 1);  // whole wave active
+            // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2)
+            const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
             if (need_bp && dec_seen < u + 1 - kR) {
                 Deadline dl;
                 for (unsigned spins = 0;; ++spins) {
@@ -376,7 +398,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
                 __hip_atomic_store((gu64*)a.ry + (size_t)((u + 1) & (kR - 1)) * N + row, granule(tag + 1, yn),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            mark(a, tr, u, tid_, 3);  // the last wave's "done" is the publication of y_{u+1}
+            mark<TRACE>(a, tr, u, tid_, 3);  // the last wave's "done" is the publication of y_{u+1}
         } else if (ROLE == kT1) {
             if (lane < kL && c < M)  // matrixAdd(tmp, Fp, 1) :356
                 __hip_atomic_store((gu64*)a.rtmp + (size_t)slot * M + c, granule(tag, acc + 1.0f * cst),
@@ -422,6 +444,7 @@ __device__ bool ring_copy(const CvArgs& a, const u64* ring, int n, int slot, uns
 // an LDS word; wave 0 gathers the feasibility words of T3 and decides
 // (terminate :673-687, loop control :716-724), so the decision of iterate u
 // overlaps the dots of u + 1.
+template <bool TRACE>
 __device__ void decide_role(const CvArgs& a, float* lds) {
     const int N = a.N, M = a.M;
     const int lane = threadIdx.x & 63, d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -431,7 +454,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
     for (int e = threadIdx.x; e < kR * kDecW; e += blockDim.x) dres[e] = 0ull;
     __syncthreads();
     if (d >= kDecW) return;
-    const bool tr = a.trace && lane == 0;
+    const bool tr = TRACE && a.trace && lane == 0;
     if (d == 0) {
         SolveState* st = a.st;
         float Jp = st->Jp, Jd = st->Jd;
@@ -441,7 +464,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
         for (long long u = a.u0; u <= a.u_dec_end; ++u) {
             const unsigned tag = (unsigned)(u + 1);
             const int slot = (int)(u & (kR - 1));
-            mark(a, tr, u, 4 * kMaxW, 0);
+            mark<TRACE>(a, tr, u, 4 * kMaxW, 0);
             bool bad = false;  // checkFeas (:677): any T3 workgroup with a row over its bound
             for (int k0 = 0; k0 < G3; k0 += 64) {
                 const int k = k0 + lane;
@@ -452,7 +475,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                 bad |= k < G3 && v[0] != 0.0f;
             }
             const bool feasible = !__any(bad);
-            mark(a, tr, u, 4 * kMaxW, 1);
+            mark<TRACE>(a, tr, u, 4 * kMaxW, 1);
             float s1, s2, s3, s4;
             {
                 Deadline dl;
@@ -477,7 +500,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                 s3 = __shfl(hv, 3);
                 s4 = __shfl(hv, 4);
             }
-            mark(a, tr, u, 4 * kMaxW, 2);
+            mark<TRACE>(a, tr, u, 4 * kMaxW, 2);
             int stop = 0;
             if (feasible) {
                 Jd = 0.0f;  // computeCost :648-666 (J += 0.5 * tmp[0] in double)
@@ -512,7 +535,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                 return;
             }
             if (lane == 0) __hip_atomic_store(a.decided, u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            mark(a, tr, u, 4 * kMaxW, 3);
+            mark<TRACE>(a, tr, u, 4 * kMaxW, 3);
         }
         return;
     }
@@ -529,33 +552,65 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
         const int k = 64 * m + lane;
         fav[m] = (fa && k < n) ? fa[k] : 0.0f;
     }
+    // the granules of iterate uu, every load in flight (unused lanes re-read
+    // element 0); the next iterate's are issued before this iterate's sum, so
+    // that the sweep's round trip overlaps the chain (in steady state DEC runs
+    // behind its producers and the prefetched granules already carry the tag)
+    u64 x[2 * kDecPer];
+    auto issue = [&](long long uu) {
+        const int sl = (int)(uu & (kR - 1));
+        const gu64* gb = (const gu64*)rb + (size_t)sl * n;
+        const gu64* ga = (const gu64*)(ra ? ra : rb) + (size_t)sl * n;
+#pragma unroll
+        for (int m = 0; m < kDecPer; ++m) {
+            const int k = 64 * m + lane;
+            x[m] = __hip_atomic_load(gb + (k < n ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ra) {
+#pragma unroll
+            for (int m = 0; m < kDecPer; ++m) {
+                const int k = 64 * m + lane;
+                x[kDecPer + m] = __hip_atomic_load(ga + (k < n ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+    issue(a.u0);
     for (long long u = a.u0; u <= a.u_dec_end; ++u) {
         const unsigned tag = (unsigned)(u + 1);
         const int slot = (int)(u & (kR - 1));
-        mark(a, tr, u, 4 * kMaxW + d, 0);
-        // products into LDS: every granule of the lane in one sweep
+        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 0);
+        // products into LDS once every granule of the lane carries the tag
         {
-            const gu64* gp[2 * kDecPer];
-            bool on[2 * kDecPer];
-            float v[2 * kDecPer];
+            Deadline dl;
+            for (unsigned spins = 0;; ++spins) {
+                bool ok = true;
 #pragma unroll
-            for (int m = 0; m < kDecPer; ++m) {
-                const int k = 64 * m + lane;
-                const bool in = k < n;
-                gp[m] = (const gu64*)rb + (size_t)slot * n + (in ? k : 0);
-                on[m] = in;
-                gp[kDecPer + m] = (const gu64*)(ra ? ra : rb) + (size_t)slot * n + (in ? k : 0);
-                on[kDecPer + m] = in && ra != nullptr;
-                v[m] = v[kDecPer + m] = 0.0f;
+                for (int m = 0; m < kDecPer; ++m) {
+                    const bool in = 64 * m + lane < n;
+                    ok &= !in || (unsigned)(x[m] >> 32) == tag;
+                    if (ra) ok &= !in || (unsigned)(x[kDecPer + m] >> 32) == tag;
+                }
+                if (__all(ok)) break;
+                if ((spins & 63) == 63) {
+                    if (stopped(a)) return;
+                    if (dl.expired()) {
+                        fail(a, 40 + d);
+                        return;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+                issue(u);
             }
-            if (!await_granules<2 * kDecPer>(a, gp, on, tag, v, 40 + d)) return;
 #pragma unroll
             for (int m = 0; m < kDecPer; ++m) {
                 const int k = 64 * m + lane;
-                if (k < n) pr[k] = (ra ? v[kDecPer + m] : fav[m]) * v[m];
+                const float vb = __uint_as_float((unsigned)x[m]);
+                const float va = ra ? __uint_as_float((unsigned)x[kDecPer + m]) : fav[m];
+                if (k < n) pr[k] = va * vb;
             }
         }
-        mark(a, tr, u, 4 * kMaxW + d, 1);
+        if (u < a.u_dec_end) issue(u + 1);
+        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // :652-657, k in order.  Chunks of kDecChunk terms, each fully unrolled
@@ -588,18 +643,21 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
             }
         }
         __builtin_amdgcn_wave_barrier();
-        mark(a, tr, u, 4 * kMaxW + d, 2);
+        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 2);
         if (lane == 0)
             __hip_atomic_store(dres + (size_t)slot * kDecW + d, granule(tag, acc), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
+// TRACE: the timeline instantiation (pqp_tune_converge_trace); the default one
+// carries no trace branches.
+template <bool TRACE>
 __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.x, tid = threadIdx.x;
     if (b >= a.g4) {
-        decide_role(a, lds);
+        decide_role<TRACE>(a, lds);
         return;
     }
     const int role = b < a.g1 ? kUpd : (b < a.g2 ? kT1 : (b < a.g3 ? kT2 : kT3));
@@ -615,16 +673,19 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
         const f4v* s = src + (size_t)g * KB * kL;
         for (int e = tid; e < KP * kL; e += blockDim.x) qs[e] = (e < KB * kL) ? s[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
         for (int e = tid; e < kR * kMaxW * kL; e += blockDim.x) hs[e] = 0ull;
+        // x past K (read by the last packet's products) stays +0: zeroed once in
+        // both parity buffers
+        for (int e = tid; e < 2 * (KPmax * 4 - K); e += blockDim.x) ysb[(e & 1) * KPmax * 4 + K + (e >> 1)] = 0.0f;
     }
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (w >= W) return;
     const int ny = KPmax * 4;
     switch (role) {
-        case kUpd: chain_wave<kUpd>(a, g, w, K, qs, ysb, ny, hs); break;
-        case kT1: chain_wave<kT1>(a, g, w, K, qs, ysb, ny, hs); break;
-        case kT2: chain_wave<kT2>(a, g, w, K, qs, ysb, ny, hs); break;
-        default: chain_wave<kT3>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kUpd: chain_wave<kUpd, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kT1: chain_wave<kT1, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kT2: chain_wave<kT2, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+        default: chain_wave<kT3, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
     }
 }
 
@@ -729,8 +790,10 @@ int converge_persist_per_cu(int N, int M) {
     const int W = waves_of(split_kblocks(N > M ? N : M));
     const int threads = 64 * (W > kDecW ? W : kDecW);
     int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_converge_persist), threads,
-                                                     converge_persist_lds_bytes(N, M)) != hipSuccess)
+    const void* kern = g_converge_trace ? reinterpret_cast<const void*>(&k_converge_persist<true>)
+                                        : reinterpret_cast<const void*>(&k_converge_persist<false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, converge_persist_lds_bytes(N, M)) !=
+        hipSuccess)
         return 0;
     return per;
 }
@@ -782,7 +845,12 @@ hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s) {
     hipLaunchKernelGGL(k_converge_init, dim3(4), dim3(256), 0, s, L.Y, L.N, L.u0, a.ry, L.ctl, L.decided, L.err);
     const int W = waves_of(split_kblocks(L.N > L.M ? L.N : L.M));
     const int threads = 64 * (W > kDecW ? W : kDecW);
-    hipLaunchKernelGGL(k_converge_persist, dim3(G), dim3(threads), converge_persist_lds_bytes(L.N, L.M), s, a);
+    if (a.trace)
+        hipLaunchKernelGGL(k_converge_persist<true>, dim3(G), dim3(threads), converge_persist_lds_bytes(L.N, L.M), s,
+                           a);
+    else
+        hipLaunchKernelGGL(k_converge_persist<false>, dim3(G), dim3(threads), converge_persist_lds_bytes(L.N, L.M),
+                           s, a);
     return hipGetLastError();
 }
 
