@@ -58,9 +58,17 @@ constexpr int kP0 = 24;    // packets (4 values of k) of wave 0's slice, multipl
 constexpr int kP1 = 36;    // packets of wave 1's slice: its products must be ready when wave 0 is done
 constexpr int kPW = 49;    // packets per later slice, products formed ahead in 4 kPW VGPRs
 constexpr int kLateGate = 1;
+#ifndef PQP_T_POLL_SLEEP
+#define PQP_T_POLL_SLEEP 4
+#endif
+constexpr int kTPollSleep = PQP_T_POLL_SLEEP;  // s_sleep units (64 clocks) between the T roles' and DEC's sweeps
 static_assert(kP0 <= 64 && kP1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
 constexpr int kMaxW = 6;   // waves for K <= 1024
-constexpr int kR = 8;      // ring depth (iterates in flight)
+#ifndef PQP_CONVERGE_RING
+#define PQP_CONVERGE_RING 8
+#endif
+constexpr int kR = PQP_CONVERGE_RING;  // ring depth (iterates in flight), a power of 2
+static_assert((kR & (kR - 1)) == 0, "ring slots are iterate & (kR - 1)");
 constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
 constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
 constexpr int kDecChunk = 256;  // dot terms per unrolled chunk
@@ -181,7 +189,7 @@ __device__ __forceinline__ void fail(const CvArgs& a, int code) {
 // Wait until every listed granule with on[m] carries `tag`; v[m] gets its
 // value.  Every g[m] must be a valid address, on or not.  Returns false when
 // the launch has been stopped or the wait timed out.
-template <int NG>
+template <int NG, int SLEEP = 1>
 __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* const (&g)[NG], const bool (&on)[NG],
                                                unsigned tag, float (&v)[NG], int code) {
     Deadline dl;
@@ -205,7 +213,7 @@ __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* cons
                 return false;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(SLEEP);
     }
 }
 
@@ -293,7 +301,9 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             const bool own = ROLE == kUpd && last;  // y_i for y_next = num/den*y_i (:594)
             gp[4] = gx + (row < N ? row : N - 1);
             on[4] = own;
-            if (!await_granules<5>(a, gp, on, tag, v, 1 + ROLE)) return false;
+            // the terminate() roles poll more slowly than the update (off its
+            // critical path; fewer polls of the lines the update waits on)
+            if (!await_granules<5, ROLE == kUpd ? 1 : kTPollSleep>(a, gp, on, tag, v, 1 + ROLE)) return false;
 #pragma unroll
             for (int m = 0; m < 4; ++m) ys[kk[m]] = v[m];
             if (own) yrow = v[4];
@@ -598,7 +608,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                         return;
                     }
                 }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(kTPollSleep);
                 issue(u);
             }
 #pragma unroll
