@@ -335,6 +335,38 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         float acc = 0.0f;
         u64* sl = slot + (size_t)par * W * 64;
         const unsigned want = (unsigned)(u + 1);
+        // the wave's sums done: hand them on, or (last wave) finish the rows.
+        // Called at the end of each chain form, so that each runs straight
+        // into its hand-off.  False: the launch failed (reported).
+        auto finish = [&](float acc) -> bool {
+            asm volatile("" : "+v"(acc));  // the mark below follows the chain
+            mark(u, 3);
+            if (!last) {
+                __hip_atomic_store(sl + w * 64 + lane, ((u64)want << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_s_setprio(0);
+                if (bad) {
+                    fail(err, bad);
+                    return false;
+                }
+                return true;
+            }
+            __builtin_amdgcn_s_setprio(0);
+            // ---- 4. the last slice's wave finishes the rows ----
+            const float v = acc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
+            // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2),
+            // not an LDS permute; every lane divides (odd lanes' quotients unused)
+            const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+            yn = v / den * yrow;  // :594
+            if (!(p & 1) && live)
+                __hip_atomic_store(gran + (size_t)(par ^ 1) * N + row, ((u64)want << 32) | __float_as_uint(yn),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (bad) {
+                fail(err, bad);
+                return false;
+            }
+            return true;
+        };
         if (w == 0) {
             // wave 0 reads its slice's split entries while it waits for y:
             // its products start the chain, and then need only the y reads
@@ -348,7 +380,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             // ---- 2/3 (wave 0). the chain starts here, right after its products ----
             mark(u, 2);
             __builtin_amdgcn_s_setprio(3);
-            acc = chain_qreg(acc, q0, yw);
+            if (!finish(chain_qreg(acc, q0, yw))) return;
         } else {
             // products ahead of the turn, the running sums of the previous
             // slice, then this slice's adds; NP = the slice's packets
@@ -404,7 +436,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
 #pragma unroll
                         for (int g = 0; g < G + 1 && g < 8; ++g) ext[g] = t[g];
                     }
-                    return 0;
+                    return finish(acc) ? 0 : 3;
                 }
 #pragma unroll
                 for (int j = 0; j < NP; ++j) {
@@ -413,39 +445,13 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                     acc += prod[j].z;
                     acc += prod[j].w;
                 }
-                return 0;
+                return finish(acc) ? 0 : 3;
             };
             const int rc = (w == 1) ? turn(std::integral_constant<int, kPW1>{}) : turn(std::integral_constant<int, kPW>{});
             if (rc) {
-                fail(err, rc);
+                if (rc == 1) fail(err, rc);  // 3: reported by finish
                 return;
             }
-        }
-        asm volatile("" : "+v"(acc));  // the mark below follows the chain
-        mark(u, 3);
-        if (!last) {
-            __hip_atomic_store(sl + w * 64 + lane, ((u64)want << 32) | __float_as_uint(acc), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-            __builtin_amdgcn_s_setprio(0);
-            if (bad) {
-                fail(err, bad);
-                return;
-            }
-            continue;
-        }
-        __builtin_amdgcn_s_setprio(0);
-        // ---- 4. the last slice's wave finishes the rows ----
-        const float v = acc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
-        // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2),
-        // not an LDS permute; every lane divides (odd lanes' quotients unused)
-        const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-        yn = v / den * yrow;  // :594
-        if (!(p & 1) && live)
-            __hip_atomic_store(gran + (size_t)(par ^ 1) * N + row, ((u64)want << 32) | __float_as_uint(yn),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (bad) {
-            fail(err, bad);
-            return;
         }
     }
     if (last && updates > 0 && !(p & 1) && live) Yout[row] = yn;
