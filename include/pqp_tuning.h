@@ -103,7 +103,9 @@ int pqp_tune_converge_chunk(int iterates);
  * (100 MHz, chip-wide) marks into d_trace[iterate][29][4] (role * 6 + wave
  * for UPD, T1, T2, T3; 24 + wave for DEC, wave 0 deciding, waves 1-4 summing
  * the dots): iterate start, inputs staged, turn
- * (running sums received; DEC: sum done), done.  iterates = 0 turns it off. */
+ * (running sums received; DEC: sum done), done; the same marks in shader
+ * clocks (s_memtime) follow at d_trace[iterates * 29 * 4] (buffer of
+ * 2 * iterates * 29 * 4 words).  iterates = 0 turns it off. */
 int pqp_tune_converge_trace(void* d_trace, int iterates);
 
 /* Converge-mode solves of N, M <= 32 problems run one wave per problem

@@ -64,10 +64,20 @@ constexpr int kLateGate = 1;
 constexpr int kTPollSleep = PQP_T_POLL_SLEEP;  // s_sleep units (64 clocks) between the T roles' and DEC's sweeps
 static_assert(kP0 <= 64 && kP1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
 constexpr int kMaxW = 6;   // waves for K <= 1024
+#ifndef PQP_CV_HS64  // A/B: hand-off words one per lane (64 per wave), stored by every lane
+#define PQP_CV_HS64 0
+#endif
+#ifndef PQP_CV_SPINBOUND  // A/B: hand-off waits bounded by a spin count only (no stop-flag load)
+#define PQP_CV_SPINBOUND 0
+#endif
+#ifndef PQP_CV_RTROLE  // A/B: one copy of the chain code for all roles
+#define PQP_CV_RTROLE 0
+#endif
 #ifndef PQP_CONVERGE_RING
 #define PQP_CONVERGE_RING 8
 #endif
 constexpr int kR = PQP_CONVERGE_RING;  // ring depth (iterates in flight), a power of 2
+constexpr int kHL = PQP_CV_HS64 ? 64 : kL;  // hand-off words per wave and ring slot
 static_assert((kR & (kR - 1)) == 0, "ring slots are iterate & (kR - 1)");
 constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
 constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
@@ -172,7 +182,7 @@ struct CvArgs {
     long long* decided;   // last iterate DEC let through
     int* err;
     float *Yout, *Uout;
-    u64* trace;           // tuning: [iterate][29][4] s_memrealtime marks of workgroup 0 of each role
+    u64* trace;           // tuning: [2][iterate][29][4] s_memrealtime, then s_memtime marks of workgroup 0 of each role
     int trace_n;
 };
 
@@ -191,7 +201,7 @@ __device__ __forceinline__ void fail(const CvArgs& a, int code) {
 // the launch has been stopped or the wait timed out.
 template <int NG, int SLEEP = 1>
 __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* const (&g)[NG], const bool (&on)[NG],
-                                               unsigned tag, float (&v)[NG], int code) {
+                                               unsigned tag, float (&v)[NG], int code, int sleep_rt = 0) {
     Deadline dl;
     for (unsigned spins = 0;; ++spins) {
         // every address is valid (callers clamp the unused ones), so the loads
@@ -213,7 +223,10 @@ __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* cons
                 return false;
             }
         }
-        __builtin_amdgcn_s_sleep(SLEEP);
+        if (sleep_rt == kTPollSleep)  // (uniform) the runtime-role form's pause
+            __builtin_amdgcn_s_sleep(kTPollSleep);
+        else
+            __builtin_amdgcn_s_sleep(SLEEP);
     }
 }
 
@@ -221,14 +234,27 @@ constexpr int kTraceIds = 4 * kMaxW + kDecW;
 template <bool TRACE>
 __device__ __forceinline__ void mark(const CvArgs& a, bool on, long long u, int id, int e) {
     if constexpr (TRACE)
-        if (on && u - a.u0 < a.trace_n)
-            a.trace[((size_t)(u - a.u0) * kTraceIds + id) * 4 + e] = __builtin_amdgcn_s_memrealtime();
+        if (on && u - a.u0 < a.trace_n) {
+            // chip time (100 MHz), then the shader clock in a second block: the
+            // ratio over a span is the clock the launch ran at
+            const size_t i = ((size_t)(u - a.u0) * kTraceIds + id) * 4 + e;
+            a.trace[i] = __builtin_amdgcn_s_memrealtime();
+            a.trace[(size_t)a.trace_n * kTraceIds * 4 + i] = __builtin_amdgcn_s_memtime();
+        }
 }
 
 // The running sums' hand-off wait of a chain wave: a bare poll whose exit
 // falls through into the adds; the launch's stop flag and the time limit are
 // read every 256 polls only.  0: arrived, 1: the launch stopped, 2: timed out.
 __device__ __forceinline__ int wait_sums(const CvArgs& a, const u64* src, unsigned tag, u64& h) {
+#if PQP_CV_SPINBOUND
+    unsigned sp = 0;
+#pragma clang loop unroll(disable)
+    do {
+        h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } while (!__all((unsigned)(h >> 32) == tag) && ++sp < (1u << 25));
+    return sp < (1u << 25) ? 0 : (stopped(a) ? 1 : 2);
+#endif
     Deadline dl;
     unsigned spins = 0;
     bool ok;
@@ -241,9 +267,12 @@ __device__ __forceinline__ int wait_sums(const CvArgs& a, const u64* src, unsign
 }
 
 // One wave of a chain role (UPD, T1, T2, T3): iterates [ub, ue].
-template <int ROLE, bool TRACE>
+template <int ROLE_T, bool TRACE>
 __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K, const f4v* qs, float* ysb, int ny,
-                                           u64* hs) {
+                                           u64* hs, int role_rt) {
+    // PQP_CV_RTROLE: one copy of the code for every role (the role a uniform
+    // runtime value), a quarter of the instruction footprint
+    const int ROLE = PQP_CV_RTROLE ? role_rt : ROLE_T;
     const int N = a.N, M = a.M;
     const int lane = threadIdx.x & 63, ll = lane & (kL - 1);
     const int c = g * kL + ll;  // output column (UPD: row side p = 2i + side)
@@ -303,7 +332,9 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             on[4] = own;
             // the terminate() roles poll more slowly than the update (off its
             // critical path; fewer polls of the lines the update waits on)
-            if (!await_granules<5, ROLE == kUpd ? 1 : kTPollSleep>(a, gp, on, tag, v, 1 + ROLE)) return false;
+            if (PQP_CV_RTROLE ? !await_granules<5, 1>(a, gp, on, tag, v, 1 + ROLE, ROLE == kUpd ? 1 : kTPollSleep)
+                              : !await_granules<5, ROLE_T == kUpd ? 1 : kTPollSleep>(a, gp, on, tag, v, 1 + ROLE))
+                return false;
 #pragma unroll
             for (int m = 0; m < 4; ++m) ys[kk[m]] = v[m];
             if (own) yrow = v[4];
@@ -332,7 +363,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
                 if (w >= 4) {
                     // waves 4, 5 share SIMDs with waves 0, 1: their products
                     // start once wave kLateGate has handed on its sums
-                    const u64* gsrc = hs + ((size_t)slot * kMaxW + kLateGate) * kL + ll;
+                    const u64* gsrc = hs + ((size_t)slot * kMaxW + kLateGate) * kHL + (kHL == 64 ? lane : ll);
                     Deadline dl;
                     for (unsigned spins = 0;; ++spins) {
                         const u64 h = __hip_atomic_load(gsrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -348,7 +379,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
 #pragma unroll
                 for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
                 u64 h;
-                bad = wait_sums(a, hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll, tag, h);
+                bad = wait_sums(a, hs + ((size_t)slot * kMaxW + (w - 1)) * kHL + (kHL == 64 ? lane : ll), tag, h);
                 acc = __uint_as_float((unsigned)h);
                 mark<TRACE>(a, tr, u, tid_, 2);
                 __builtin_amdgcn_s_setprio(3);
@@ -370,8 +401,8 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
         if (!last) {
             // (after a failed wait the next wave gets a tagged word too: it
             // stops at its next sweep)
-            if (lane < kL)
-                __hip_atomic_store(hs + ((size_t)slot * kMaxW + w) * kL + ll, granule(tag, acc), __ATOMIC_RELAXED,
+            if (kHL == 64 || lane < kL)
+                __hip_atomic_store(hs + ((size_t)slot * kMaxW + w) * kHL + (kHL == 64 ? lane : ll), granule(tag, acc), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_s_setprio(0);
             if (bad) {
@@ -682,7 +713,7 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     {
         const f4v* s = src + (size_t)g * KB * kL;
         for (int e = tid; e < KP * kL; e += blockDim.x) qs[e] = (e < KB * kL) ? s[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-        for (int e = tid; e < kR * kMaxW * kL; e += blockDim.x) hs[e] = 0ull;
+        for (int e = tid; e < kR * kMaxW * kHL; e += blockDim.x) hs[e] = 0ull;
         // x past K (read by the last packet's products) stays +0: zeroed once in
         // both parity buffers
         for (int e = tid; e < 2 * (KPmax * 4 - K); e += blockDim.x) ysb[(e & 1) * KPmax * 4 + K + (e >> 1)] = 0.0f;
@@ -691,12 +722,16 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (w >= W) return;
     const int ny = KPmax * 4;
+#if PQP_CV_RTROLE
+    chain_wave<kUpd, TRACE>(a, g, w, K, qs, ysb, ny, hs, __builtin_amdgcn_readfirstlane(role));
+#else
     switch (role) {
-        case kUpd: chain_wave<kUpd, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
-        case kT1: chain_wave<kT1, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
-        case kT2: chain_wave<kT2, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
-        default: chain_wave<kT3, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kUpd: chain_wave<kUpd, TRACE>(a, g, w, K, qs, ysb, ny, hs, kUpd); break;
+        case kT1: chain_wave<kT1, TRACE>(a, g, w, K, qs, ysb, ny, hs, kT1); break;
+        case kT2: chain_wave<kT2, TRACE>(a, g, w, K, qs, ysb, ny, hs, kT2); break;
+        default: chain_wave<kT3, TRACE>(a, g, w, K, qs, ysb, ny, hs, kT3); break;
     }
+#endif
 }
 
 // packets of stage columns [col0, col0 + ncols): column j of the job is
@@ -754,7 +789,7 @@ int converge_persist_wgs(int N, int M, int* g) {
 size_t converge_persist_lds_bytes(int N, int M) {
     const int Kmax = N > M ? N : M;
     const int KPmax = packets_of(waves_of(split_kblocks(Kmax)));
-    const size_t chain = sizeof(float) * ((size_t)KPmax * kL * 4 + (size_t)2 * KPmax * 4) + sizeof(u64) * kR * kMaxW * kL;
+    const size_t chain = sizeof(float) * ((size_t)KPmax * kL * 4 + (size_t)2 * KPmax * 4) + sizeof(u64) * kR * kMaxW * kHL;
     const size_t dec = sizeof(float) * (size_t)(kDecW - 1) * (kDecChunk * cdiv_i(Kmax, kDecChunk) + 32) +
                        sizeof(u64) * kR * kDecW;
     return chain > dec ? chain : dec;

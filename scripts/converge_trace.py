@@ -36,18 +36,23 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
     P = pb.problem(0)
     del pb
     L = pqp_amd.lib()
-    tr = torch.zeros(n_trace * 29 * 4, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(2 * n_trace * 29 * 4, dtype=torch.int64, device="cuda")
     with pqp_amd.Problem(P) as prob:
         prob.solve(max_updates=cap)
         L.pqp_tune_converge_trace(pqp_amd.C.c_void_p(tr.data_ptr()), n_trace)
         r = prob.solve(max_updates=cap)
         L.pqp_tune_converge_trace(None, 0)
     torch.cuda.synchronize()
-    t = tr.cpu().numpy().reshape(n_trace, 29, 4).astype(np.float64) / 100.0  # us
+    both = tr.cpu().numpy().reshape(2, n_trace, 29, 4).astype(np.float64)
+    t = both[0] / 100.0  # us
+    clk = both[1]  # shader clocks
     lo, hi = n_trace // 3, n_trace - 10
     W = {"UPD": waves_of(N), "T1": waves_of(N), "T2": waves_of(M), "T3": waves_of(M)}
     med = lambda x: float(np.median(x))
     out = {"n_dual": N, "m": M, "h": r["h"], "iterates": [lo, hi], "roles": {}}
+    # the shader clock the launch ran at: clocks over chip time, per role's wave 0
+    out["clock_GHz"] = {role: float((clk[hi, ri * 6, 0] - clk[lo, ri * 6, 0]) / ((t[hi, ri * 6, 0] - t[lo, ri * 6, 0]) * 1e3))
+                        for ri, role in enumerate(ROLES)}
     for ri, role in enumerate(ROLES):
         for w in range(W[role]):
             i = ri * 6 + w
