@@ -12,7 +12,9 @@
 //   T1   tmp_u = Gp'y_u + Fp, tq_u = y_u'Qd  (N+M)/32          rtmp [M], rtq [N]
 //   T2   U_u = -(Qp_inv tmp_u)               M/32              rU   [M]
 //   T3   Gp U_u vs Kp, tu_u = U_u'Qp         (N+M)/32          rfeas[wg], rtu [M]
-//   DEC  the four dots of computeCost, the gap tests, the decision  (1 workgroup)
+//   DEC  the four dots of computeCost, the gap tests, the decision  (1 workgroup;
+//        the N-long dots on two waves each, even and odd iterates; the M-long
+//        dots skipped on an infeasible iterate, as terminate() skips them)
 //
 // Every output is one lane's sum over k in order from +0.0f, the reference's
 // matrixMultiply order (:88-100), formed exactly as in k_split_persist: the
@@ -64,22 +66,20 @@ constexpr int kLateGate = 1;
 constexpr int kTPollSleep = PQP_T_POLL_SLEEP;  // s_sleep units (64 clocks) between the T roles' and DEC's sweeps
 static_assert(kP0 <= 64 && kP1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
 constexpr int kMaxW = 6;   // waves for K <= 1024
-#ifndef PQP_CV_HS64  // A/B: hand-off words one per lane (64 per wave), stored by every lane
-#define PQP_CV_HS64 0
+#ifndef PQP_CV_DIAG  // timing diagnostic only (wrong results): 1 UPD alone, 2 UPD + T1, 3 UPD + T1-T3; DEC decides blind
+#define PQP_CV_DIAG 0
 #endif
-#ifndef PQP_CV_SPINBOUND  // A/B: hand-off waits bounded by a spin count only (no stop-flag load)
-#define PQP_CV_SPINBOUND 0
-#endif
-#ifndef PQP_CV_RTROLE  // A/B: one copy of the chain code for all roles
-#define PQP_CV_RTROLE 0
+#ifndef PQP_CV_UPD_INPLACE  // upd_wave: later waves read their q while they wait for y
+#define PQP_CV_UPD_INPLACE 0
 #endif
 #ifndef PQP_CONVERGE_RING
 #define PQP_CONVERGE_RING 8
 #endif
 constexpr int kR = PQP_CONVERGE_RING;  // ring depth (iterates in flight), a power of 2
-constexpr int kHL = PQP_CV_HS64 ? 64 : kL;  // hand-off words per wave and ring slot
 static_assert((kR & (kR - 1)) == 0, "ring slots are iterate & (kR - 1)");
-constexpr int kDecW = 5;     // DEC's waves: the decision, then one per dot
+constexpr int kDecW = 6;     // DEC's waves: the decision, then the dot waves (dec_dots)
+constexpr int kDots = 4;     // computeCost's dots, hand-off word 1..4 of a ring slot
+constexpr int kDecBufs = 6;  // product buffers: waves 1-4 one each, wave 5 two
 constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
 constexpr int kDecChunk = 256;  // dot terms per unrolled chunk
 constexpr int kDecAhead = 4;    // groups of 16 terms read ahead of the adds
@@ -133,6 +133,26 @@ __device__ __forceinline__ void slice_products(f4v (&prod)[NP], const f4v* qw, c
             prod[j + D] = qw[(j + D) * kL];
             yr[(j + D) % (D + 1)] = yw[j + D];
         }
+        const f4v q = prod[j], y = yr[j % (D + 1)];
+        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
+        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
+        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// prod[j] = prod[j] * y[j] with the slice's q already in prod (read while the
+// wave waited for y): only y is read, D packets ahead (as pqp_persist.hip).
+template <int NP>
+__device__ __forceinline__ void slice_products_inplace(f4v (&prod)[NP], const f4v* yw) {
+    constexpr int D = NP < 6 ? NP : 6;
+    f4v yr[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) yr[j] = yw[j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
         const f4v q = prod[j], y = yr[j % (D + 1)];
         const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
         const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
@@ -201,7 +221,7 @@ __device__ __forceinline__ void fail(const CvArgs& a, int code) {
 // the launch has been stopped or the wait timed out.
 template <int NG, int SLEEP = 1>
 __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* const (&g)[NG], const bool (&on)[NG],
-                                               unsigned tag, float (&v)[NG], int code, int sleep_rt = 0) {
+                                               unsigned tag, float (&v)[NG], int code) {
     Deadline dl;
     for (unsigned spins = 0;; ++spins) {
         // every address is valid (callers clamp the unused ones), so the loads
@@ -223,10 +243,7 @@ __device__ __forceinline__ bool await_granules(const CvArgs& a, const gu64* cons
                 return false;
             }
         }
-        if (sleep_rt == kTPollSleep)  // (uniform) the runtime-role form's pause
-            __builtin_amdgcn_s_sleep(kTPollSleep);
-        else
-            __builtin_amdgcn_s_sleep(SLEEP);
+        __builtin_amdgcn_s_sleep(SLEEP);
     }
 }
 
@@ -247,14 +264,6 @@ __device__ __forceinline__ void mark(const CvArgs& a, bool on, long long u, int 
 // falls through into the adds; the launch's stop flag and the time limit are
 // read every 256 polls only.  0: arrived, 1: the launch stopped, 2: timed out.
 __device__ __forceinline__ int wait_sums(const CvArgs& a, const u64* src, unsigned tag, u64& h) {
-#if PQP_CV_SPINBOUND
-    unsigned sp = 0;
-#pragma clang loop unroll(disable)
-    do {
-        h = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } while (!__all((unsigned)(h >> 32) == tag) && ++sp < (1u << 25));
-    return sp < (1u << 25) ? 0 : (stopped(a) ? 1 : 2);
-#endif
     Deadline dl;
     unsigned spins = 0;
     bool ok;
@@ -266,13 +275,196 @@ __device__ __forceinline__ int wait_sums(const CvArgs& a, const u64* src, unsign
     return ok ? 0 : (stopped(a) ? 1 : 2);
 }
 
-// One wave of a chain role (UPD, T1, T2, T3): iterates [ub, ue].
+// UPD role, one wave: k_split_persist's update (pqp_persist.hip) on the ring.
+// Per iterate u: the wave's slice of y_u from ring slot u % kR (tag u + 1),
+// products ahead of its turn (waves > 0 read their q while they wait for y and
+// multiply in place), the running sums through one 64-bit LDS word per lane
+// and update parity ([2][W][64] words inside the hand-off area), each chain
+// form running straight into its hand-off or epilogue; the last wave divides
+// and publishes y_{u+1} (tag u + 2) once slot (u + 1) % kR is free.  Waits
+// also end when the launch has stopped (DEC finished or a role failed).
+template <bool TRACE>
+__device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4v* qs, float* ysb, int ny, u64* hs) {
+    const int N = a.N;
+    const int lane = threadIdx.x & 63, ll = lane & (kL - 1);
+    const int p = g * kL + ll;  // row side 2i + side
+    const bool live = lane < kL && p < 2 * N;
+    const int row = p >> 1;
+    const int KB = split_kblocks(N), W = waves_of(KB);
+    const int pk0 = slice0_of(w), pk1 = slice0_of(w + 1);
+    const int k0 = 4 * pk0, k1 = 4 * pk1 < N ? 4 * pk1 : N;
+    const bool last = (w == W - 1);
+    const float fd = live ? a.fdpn[p] : 0.0f;
+    const bool tr = TRACE && a.trace && g == 0 && lane == 0;
+    float yrow = 0.0f;
+    int bad = 0;  // a hand-off wait that ended without the sums: 1 stopped, 2 timed out
+    for (long long u = a.u0; u < a.u_prod_end; ++u) {
+        const int par = (int)(u & 1);
+        float* ys = ysb + par * ny;
+        const unsigned tag = (unsigned)(u + 1);
+        const int rslot = (int)(u & (kR - 1));
+        mark<TRACE>(a, tr, u, w, 0);
+        long long dec_seen = 0;
+        const bool need_bp = last && u + 1 - kR >= a.u0;
+        if (need_bp) dec_seen = __hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- 1. y of this slice from the ring: every load in flight, one
+        // wave-wide tag test, the exit straight into the LDS stores ----
+        auto stage_y = [&]() -> bool {
+            const gu64* gsrc = (const gu64*)a.ry + (size_t)rslot * N;
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            int kk[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) kk[m] = (k0 + 64 * m + ln < k1) ? k0 + 64 * m + ln : k1 - 1;
+            const int rowc = row < N ? row : N - 1;
+            u64 x[4], xo = 0;
+            Deadline dl;
+            unsigned spins = 0;
+            bool ok;
+#pragma clang loop unroll(disable)
+            do {
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    x[m] = __hip_atomic_load(gsrc + kk[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (last) xo = __hip_atomic_load(gsrc + rowc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = true;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) ok &= (unsigned)(x[m] >> 32) == tag;
+                if (last) ok &= (unsigned)(xo >> 32) == tag;
+                ok = __all(ok);
+                if (!ok) {
+                    if ((++spins & 63) == 0) {
+                        if (stopped(a)) return false;
+                        if (dl.expired()) {
+                            fail(a, 1);
+                            return false;
+                        }
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            } while (!ok);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) ys[kk[m]] = __uint_as_float((unsigned)x[m]);
+            if (last) yrow = __uint_as_float((unsigned)xo);
+            // the backpressure word (loaded before the sweep, so back by now) into scalars
+            if (need_bp) dec_seen = ((long long)__builtin_amdgcn_readfirstlane((int)(dec_seen >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((int)dec_seen);
+            mark<TRACE>(a, tr, u, w, 1);
+            return true;
+        };
+        const f4v* qw = qs + (size_t)pk0 * kL + ll;
+        const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
+        u64* sl = hs + (size_t)par * W * 64;
+        // the wave's sums done: hand them on, or (last wave) finish the rows
+        auto finish = [&](float acc) -> bool {
+            asm volatile("" : "+v"(acc));
+            mark<TRACE>(a, tr, u, w, 3);
+            if (!last) {
+                // (after a failed wait the next wave gets a tagged word too: it
+                // stops at its next sweep)
+                __hip_atomic_store(sl + w * 64 + lane, granule(tag, acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_s_setprio(0);
+                if (bad) {
+                    if (bad == 2) fail(a, 10);
+                    return false;
+                }
+                return true;
+            }
+            __builtin_amdgcn_s_setprio(0);
+            if (bad) {
+                if (bad == 2) fail(a, 10);
+                return false;
+            }
+            const float v = acc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
+            // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2)
+            const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+            if (need_bp && dec_seen < u + 1 - kR) {
+                Deadline dl;
+                for (unsigned spins = 0;; ++spins) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= u + 1 - kR) break;
+                    if (stopped(a)) return false;
+                    if ((spins & 63) == 63 && dl.expired()) {
+                        fail(a, 20);
+                        return false;
+                    }
+                }
+            }
+            const float yn = v / den * yrow;  // updY :594
+            if (!(p & 1) && live)
+                __hip_atomic_store((gu64*)a.ry + (size_t)((u + 1) & (kR - 1)) * N + row, granule(tag + 1, yn),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return true;
+        };
+        if (w == 0) {
+            // wave 0 reads its slice's split entries while it waits for y
+            f4v q0[kP0];
+#pragma unroll
+            for (int j = 0; j < kP0; ++j) q0[j] = qw[j * kL];
+            if (!stage_y()) return;
+            mark<TRACE>(a, tr, u, w, 2);
+            __builtin_amdgcn_s_setprio(3);
+            if (!finish(chain_qreg(0.0f, q0, yw))) return;
+        } else {
+            auto turn = [&](auto np) -> int {
+                constexpr int NP = decltype(np)::value;
+                f4v prod[NP];
+                // the slice's split entries, read while the wave waits for y
+#if PQP_CV_UPD_INPLACE
+#pragma unroll
+                for (int j = 0; j < NP; ++j) prod[j] = qw[j * kL];
+#endif
+                if (!stage_y()) return 1;
+                if (w >= 4) {
+                    // waves 4, 5 share SIMDs with waves 0, 1: their products
+                    // start once wave kLateGate has handed on its sums
+                    Deadline dl;
+                    for (unsigned spins = 0;; ++spins) {
+                        const u64 h = __hip_atomic_load(sl + kLateGate * 64 + lane, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (__all((unsigned)(h >> 32) == tag)) break;
+                        if ((spins & 255) == 255) {
+                            if (stopped(a)) return 1;
+                            if (dl.expired()) return 2;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+#if PQP_CV_UPD_INPLACE
+                slice_products_inplace(prod, yw);
+#else
+                slice_products(prod, qw, yw);
+#endif
+#pragma unroll
+                for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
+                u64 h;
+                bad = wait_sums(a, sl + (w - 1) * 64 + lane, tag, h);
+                float acc = __uint_as_float((unsigned)h);
+                mark<TRACE>(a, tr, u, w, 2);
+                __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+                for (int j = 0; j < NP; ++j) {
+                    acc += prod[j].x;  // :608-609, k in order
+                    acc += prod[j].y;
+                    acc += prod[j].z;
+                    acc += prod[j].w;
+                }
+                return finish(acc) ? 0 : 3;
+            };
+            const int rc = (w == 1) ? turn(std::integral_constant<int, kP1>{}) : turn(std::integral_constant<int, kPW>{});
+            if (rc == 2) fail(a, 10);
+            if (rc) return;
+        }
+    }
+}
+
+// One wave of a terminate() chain role (T1, T2, T3): iterates [ub, ue].  (Its
+// UPD branches are the update's earlier form; UPD now runs upd_wave.)
 template <int ROLE_T, bool TRACE>
 __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K, const f4v* qs, float* ysb, int ny,
-                                           u64* hs, int role_rt) {
-    // PQP_CV_RTROLE: one copy of the code for every role (the role a uniform
-    // runtime value), a quarter of the instruction footprint
-    const int ROLE = PQP_CV_RTROLE ? role_rt : ROLE_T;
+                                           u64* hs) {
+    constexpr int ROLE = ROLE_T;
     const int N = a.N, M = a.M;
     const int lane = threadIdx.x & 63, ll = lane & (kL - 1);
     const int c = g * kL + ll;  // output column (UPD: row side p = 2i + side)
@@ -332,9 +524,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
             on[4] = own;
             // the terminate() roles poll more slowly than the update (off its
             // critical path; fewer polls of the lines the update waits on)
-            if (PQP_CV_RTROLE ? !await_granules<5, 1>(a, gp, on, tag, v, 1 + ROLE, ROLE == kUpd ? 1 : kTPollSleep)
-                              : !await_granules<5, ROLE_T == kUpd ? 1 : kTPollSleep>(a, gp, on, tag, v, 1 + ROLE))
-                return false;
+            if (!await_granules<5, ROLE == kUpd ? 1 : kTPollSleep>(a, gp, on, tag, v, 1 + ROLE)) return false;
 #pragma unroll
             for (int m = 0; m < 4; ++m) ys[kk[m]] = v[m];
             if (own) yrow = v[4];
@@ -363,7 +553,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
                 if (w >= 4) {
                     // waves 4, 5 share SIMDs with waves 0, 1: their products
                     // start once wave kLateGate has handed on its sums
-                    const u64* gsrc = hs + ((size_t)slot * kMaxW + kLateGate) * kHL + (kHL == 64 ? lane : ll);
+                    const u64* gsrc = hs + ((size_t)slot * kMaxW + kLateGate) * kL + ll;
                     Deadline dl;
                     for (unsigned spins = 0;; ++spins) {
                         const u64 h = __hip_atomic_load(gsrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -379,7 +569,7 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
 #pragma unroll
                 for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
                 u64 h;
-                bad = wait_sums(a, hs + ((size_t)slot * kMaxW + (w - 1)) * kHL + (kHL == 64 ? lane : ll), tag, h);
+                bad = wait_sums(a, hs + ((size_t)slot * kMaxW + (w - 1)) * kL + ll, tag, h);
                 acc = __uint_as_float((unsigned)h);
                 mark<TRACE>(a, tr, u, tid_, 2);
                 __builtin_amdgcn_s_setprio(3);
@@ -401,8 +591,8 @@ __device__ __forceinline__ void chain_wave(const CvArgs& a, int g, int w, int K,
         if (!last) {
             // (after a failed wait the next wave gets a tagged word too: it
             // stops at its next sweep)
-            if (kHL == 64 || lane < kL)
-                __hip_atomic_store(hs + ((size_t)slot * kMaxW + w) * kHL + (kHL == 64 ? lane : ll), granule(tag, acc), __ATOMIC_RELAXED,
+            if (lane < kL)
+                __hip_atomic_store(hs + ((size_t)slot * kMaxW + w) * kL + ll, granule(tag, acc), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_s_setprio(0);
             if (bad) {
@@ -479,22 +669,177 @@ __device__ bool ring_copy(const CvArgs& a, const u64* ring, int n, int slot, uns
     return true;
 }
 
-// DEC: waves 1..4 each sum one dot of computeCost (:648-666) per iterate --
-// 1: Fd.Y, 2: (U'Qp).U, 3: Fp.U, 4: (Y'Qd).Y -- in k order on every lane
-// alike (broadcast LDS reads of the products) and hand it to wave 0 through
-// an LDS word; wave 0 gathers the feasibility words of T3 and decides
-// (terminate :673-687, loop control :716-724), so the decision of iterate u
-// overlaps the dots of u + 1.
+// DEC's dot waves (computeCost :648-666, k in order on every lane alike,
+// broadcast LDS reads of the products; each dot handed to wave 0 through an
+// LDS word).  ND = 1: dot `dot0` (1: Fd.Y, 4: (Y'Qd).Y; N terms) of every
+// ustep-th iterate from ustart -- two waves per dot take the even and the odd
+// iterates, so each has two periods for its gather and its N-long sum.  ND = 2:
+// dots 2 ((U'Qp).U) and 3 (Fp.U) of every iterate, one U stream, their two
+// M-long chains side by side.
+template <int ND, bool TRACE>
+__device__ __forceinline__ void dec_dots(const CvArgs& a, int d, int dot0, float* pr0, float* pr1, long long ustart,
+                                         int ustep, u64* dres) {
+    const int N = a.N, M = a.M;
+    const int lane = threadIdx.x & 63;
+    const bool tr = TRACE && a.trace && lane == 0;
+    const int n = (dot0 == 1 || dot0 == 4) ? N : M;
+    const int nc = kDecChunk * cdiv_i(n, kDecChunk);
+    const u64* ra = dot0 == 4 ? a.rtq : (dot0 == 2 ? a.rtu : nullptr);  // ring operand (or the constant below)
+    const float* fa = ND == 2 ? a.Fp : (dot0 == 1 ? a.Fd : nullptr);   // ND = 2: dot 3's Fp
+    const u64* rb = (dot0 == 1 || dot0 == 4) ? a.ry : a.rU;
+    for (int k = n + lane; k < nc + 32; k += 64) {  // +0 tail: adds nothing to a sum that is never -0
+        pr0[k] = 0.0f;
+        if (ND == 2) pr1[k] = 0.0f;
+    }
+    float fav[kDecPer];  // the constant operand (Fd, Fp), loaded once
+#pragma unroll
+    for (int m = 0; m < kDecPer; ++m) {
+        const int k = 64 * m + lane;
+        fav[m] = (fa && k < n) ? fa[k] : 0.0f;
+    }
+    // the granules of iterate uu, every load in flight (unused lanes re-read
+    // element 0); the next iterate's are issued before this iterate's sum
+    u64 x[2 * kDecPer];
+    // ND = 2 also reads T3's feasibility words of the iterate (one per lane,
+    // G3 <= 64): computeCost runs only on a feasible iterate (terminate :677),
+    // so the two sums are skipped on an infeasible one (wave 0 ignores them)
+    const int G3 = a.g4 - a.g3;
+    u64 xf = 0;
+    auto issue = [&](long long uu) {
+        const int sl = (int)(uu & (kR - 1));
+        if (ND == 2)
+            xf = __hip_atomic_load((const gu64*)a.rfeas + (size_t)sl * G3 + (lane < G3 ? lane : 0), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        const gu64* gb = (const gu64*)rb + (size_t)sl * n;
+        const gu64* ga = (const gu64*)(ra ? ra : rb) + (size_t)sl * n;
+#pragma unroll
+        for (int m = 0; m < kDecPer; ++m) {
+            const int k = 64 * m + lane;
+            x[m] = __hip_atomic_load(gb + (k < n ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ra) {
+#pragma unroll
+            for (int m = 0; m < kDecPer; ++m) {
+                const int k = 64 * m + lane;
+                x[kDecPer + m] = __hip_atomic_load(ga + (k < n ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+    if (ustart <= a.u_dec_end) issue(ustart);
+    for (long long u = ustart; u <= a.u_dec_end; u += ustep) {
+        const unsigned tag = (unsigned)(u + 1);
+        const int slot = (int)(u & (kR - 1));
+        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 0);
+        // products into LDS once every granule of the lane carries the tag
+        {
+            Deadline dl;
+            for (unsigned spins = 0;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int m = 0; m < kDecPer; ++m) {
+                    const bool in = 64 * m + lane < n;
+                    ok &= !in || (unsigned)(x[m] >> 32) == tag;
+                    if (ra) ok &= !in || (unsigned)(x[kDecPer + m] >> 32) == tag;
+                }
+                if (ND == 2) ok &= lane >= G3 || (unsigned)(xf >> 32) == tag;
+                if (__all(ok)) break;
+                if ((spins & 63) == 63) {
+                    if (stopped(a)) return;
+                    if (dl.expired()) {
+                        fail(a, 40 + d);
+                        return;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(kTPollSleep);
+                issue(u);
+            }
+#pragma unroll
+            for (int m = 0; m < kDecPer; ++m) {
+                const int k = 64 * m + lane;
+                const float vb = __uint_as_float((unsigned)x[m]);
+                if (k < n) {
+                    if (ND == 2) {
+                        pr0[k] = __uint_as_float((unsigned)x[kDecPer + m]) * vb;  // (U'Qp)[k] * U[k]
+                        pr1[k] = fav[m] * vb;                                     // Fp[k] * U[k]
+                    } else {
+                        pr0[k] = (ra ? __uint_as_float((unsigned)x[kDecPer + m]) : fav[m]) * vb;
+                    }
+                }
+            }
+        }
+        const bool skip = ND == 2 && __any(lane < G3 && __uint_as_float((unsigned)xf) != 0.0f);  // infeasible
+        if (u + ustep <= a.u_dec_end) issue(u + ustep);
+        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // :652-657, k in order.  Chunks of kDecChunk terms, each fully unrolled
+        // (a loop back-edge waits for every read in flight); the reads run
+        // kDecAhead groups of 16 ahead of the adds.
+        float acc0 = 0.0f, acc1 = 0.0f;
+        const f4v* p0 = reinterpret_cast<const f4v*>(pr0);
+        const f4v* p1 = reinterpret_cast<const f4v*>(pr1);
+        constexpr int AH = ND == 2 ? 2 : kDecAhead;  // two chains: fewer groups ahead (registers)
+        for (int c4 = 0; c4 < (skip ? 0 : nc / 4); c4 += kDecChunk / 4) {
+            f4v R[AH + 1][4];
+            f4v S[ND == 2 ? AH + 1 : 1][4];
+#pragma unroll
+            for (int g0 = 0; g0 < AH; ++g0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    R[g0][j] = p0[c4 + 4 * g0 + j];
+                    if constexpr (ND == 2) S[g0][j] = p1[c4 + 4 * g0 + j];
+                }
+            }
+#pragma unroll
+            for (int gi = 0; gi < kDecChunk / 16; ++gi) {
+                if (gi + AH < kDecChunk / 16) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        R[(gi + AH) % (AH + 1)][j] = p0[c4 + 4 * (gi + AH) + j];
+                        if constexpr (ND == 2) S[(gi + AH) % (AH + 1)][j] = p1[c4 + 4 * (gi + AH) + j];
+                    }
+                }
+                asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");  // the reads issue before the adds
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f4v r = R[gi % (AH + 1)][j];
+                    acc0 += r.x;
+                    if constexpr (ND == 2) acc1 += S[gi % (AH + 1)][j].x;
+                    acc0 += r.y;
+                    if constexpr (ND == 2) acc1 += S[gi % (AH + 1)][j].y;
+                    acc0 += r.z;
+                    if constexpr (ND == 2) acc1 += S[gi % (AH + 1)][j].z;
+                    acc0 += r.w;
+                    if constexpr (ND == 2) acc1 += S[gi % (AH + 1)][j].w;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 2);
+        if (lane == 0) {
+            __hip_atomic_store(dres + (size_t)slot * kDecW + dot0, granule(tag, acc0), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (ND == 2)
+                __hip_atomic_store(dres + (size_t)slot * kDecW + 3, granule(tag, acc1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// DEC: wave 0 gathers the feasibility words of T3, receives the four dots
+// from waves 1-5 (dec_dots) and decides (terminate :673-687, loop control
+// :716-724), so the decision of iterate u overlaps the dots of u + 1.
 template <bool TRACE>
 __device__ void decide_role(const CvArgs& a, float* lds) {
     const int N = a.N, M = a.M;
     const int lane = threadIdx.x & 63, d = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nmax = kDecChunk * cdiv_i(N > M ? N : M, kDecChunk);
-    float* pr = lds + (size_t)(d >= 1 && d < kDecW ? d - 1 : 0) * (nmax + 32);  // + 32: prefetch past the end
-    u64* dres = reinterpret_cast<u64*>(lds + (size_t)(kDecW - 1) * (nmax + 32));  // [kR][kDecW] hand-off words
+    float* prb = lds;  // [kDecBufs][nmax + 32] products (+ 32: prefetch past the end)
+    u64* dres = reinterpret_cast<u64*>(lds + (size_t)kDecBufs * (nmax + 32));  // [kR][kDecW] hand-off words
     for (int e = threadIdx.x; e < kR * kDecW; e += blockDim.x) dres[e] = 0ull;
     __syncthreads();
     if (d >= kDecW) return;
+    if (PQP_CV_DIAG && d != 0) return;
     const bool tr = TRACE && a.trace && lane == 0;
     if (d == 0) {
         SolveState* st = a.st;
@@ -506,8 +851,8 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
             const unsigned tag = (unsigned)(u + 1);
             const int slot = (int)(u & (kR - 1));
             mark<TRACE>(a, tr, u, 4 * kMaxW, 0);
-            bool bad = false;  // checkFeas (:677): any T3 workgroup with a row over its bound
-            for (int k0 = 0; k0 < G3; k0 += 64) {
+            bool bad = PQP_CV_DIAG != 0;  // checkFeas (:677): any T3 workgroup with a row over its bound
+            for (int k0 = 0; k0 < (PQP_CV_DIAG ? 0 : G3); k0 += 64) {
                 const int k = k0 + lane;
                 const gu64* gp[1] = {(const gu64*)a.rfeas + (size_t)slot * G3 + (k < G3 ? k : 0)};
                 const bool on[1] = {k < G3};
@@ -517,11 +862,11 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
             }
             const bool feasible = !__any(bad);
             mark<TRACE>(a, tr, u, 4 * kMaxW, 1);
-            float s1, s2, s3, s4;
-            {
+            float s1 = 0.0f, s2 = 0.0f, s3 = 0.0f, s4 = 0.0f;
+            if (!PQP_CV_DIAG) {
                 Deadline dl;
                 u64 h = 0;
-                const bool mine = lane >= 1 && lane < kDecW;
+                const bool mine = lane >= 1 && lane <= kDots;
                 for (unsigned spins = 0;; ++spins) {
                     if (mine)
                         h = __hip_atomic_load(dres + (size_t)slot * kDecW + lane, __ATOMIC_RELAXED,
@@ -564,7 +909,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                 const bool fin = stop || capped;
                 if (!ring_copy(a, a.ry, N, (int)((fin ? u : u + 1) & (kR - 1)), fin ? tag : tag + 1, a.Yout))
                     return;
-                if (!ring_copy(a, a.rU, M, slot, tag, a.Uout)) return;
+                if (!PQP_CV_DIAG && !ring_copy(a, a.rU, M, slot, tag, a.Uout)) return;
                 if (lane == 0) {
                     st->h = fin ? u + 1 : u + 2;
                     st->status = stop ? kStatusDone : (capped ? kStatusCapped : kStatusContinue);
@@ -580,114 +925,16 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
         }
         return;
     }
-    // ---- waves 1..4: one dot each ----
-    const int n = (d == 1 || d == 4) ? N : M;
-    const int nc = kDecChunk * cdiv_i(n, kDecChunk);
-    const u64* ra = d == 4 ? a.rtq : (d == 2 ? a.rtu : nullptr);  // ring operand (or the constant below)
-    const float* fa = d == 1 ? a.Fd : (d == 3 ? a.Fp : nullptr);
-    const u64* rb = (d == 1 || d == 4) ? a.ry : a.rU;
-    for (int k = n + lane; k < nc + 32; k += 64) pr[k] = 0.0f;  // +0 tail: adds nothing to a sum that is never -0
-    float fav[kDecPer];  // the constant operand (Fd, Fp), loaded once
-#pragma unroll
-    for (int m = 0; m < kDecPer; ++m) {
-        const int k = 64 * m + lane;
-        fav[m] = (fa && k < n) ? fa[k] : 0.0f;
-    }
-    // the granules of iterate uu, every load in flight (unused lanes re-read
-    // element 0); the next iterate's are issued before this iterate's sum, so
-    // that the sweep's round trip overlaps the chain (in steady state DEC runs
-    // behind its producers and the prefetched granules already carry the tag)
-    u64 x[2 * kDecPer];
-    auto issue = [&](long long uu) {
-        const int sl = (int)(uu & (kR - 1));
-        const gu64* gb = (const gu64*)rb + (size_t)sl * n;
-        const gu64* ga = (const gu64*)(ra ? ra : rb) + (size_t)sl * n;
-#pragma unroll
-        for (int m = 0; m < kDecPer; ++m) {
-            const int k = 64 * m + lane;
-            x[m] = __hip_atomic_load(gb + (k < n ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (ra) {
-#pragma unroll
-            for (int m = 0; m < kDecPer; ++m) {
-                const int k = 64 * m + lane;
-                x[kDecPer + m] = __hip_atomic_load(ga + (k < n ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    };
-    issue(a.u0);
-    for (long long u = a.u0; u <= a.u_dec_end; ++u) {
-        const unsigned tag = (unsigned)(u + 1);
-        const int slot = (int)(u & (kR - 1));
-        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 0);
-        // products into LDS once every granule of the lane carries the tag
-        {
-            Deadline dl;
-            for (unsigned spins = 0;; ++spins) {
-                bool ok = true;
-#pragma unroll
-                for (int m = 0; m < kDecPer; ++m) {
-                    const bool in = 64 * m + lane < n;
-                    ok &= !in || (unsigned)(x[m] >> 32) == tag;
-                    if (ra) ok &= !in || (unsigned)(x[kDecPer + m] >> 32) == tag;
-                }
-                if (__all(ok)) break;
-                if ((spins & 63) == 63) {
-                    if (stopped(a)) return;
-                    if (dl.expired()) {
-                        fail(a, 40 + d);
-                        return;
-                    }
-                }
-                __builtin_amdgcn_s_sleep(kTPollSleep);
-                issue(u);
-            }
-#pragma unroll
-            for (int m = 0; m < kDecPer; ++m) {
-                const int k = 64 * m + lane;
-                const float vb = __uint_as_float((unsigned)x[m]);
-                const float va = ra ? __uint_as_float((unsigned)x[kDecPer + m]) : fav[m];
-                if (k < n) pr[k] = va * vb;
-            }
-        }
-        if (u < a.u_dec_end) issue(u + 1);
-        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 1);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // :652-657, k in order.  Chunks of kDecChunk terms, each fully unrolled
-        // (a loop back-edge waits for every read in flight); the reads run
-        // kDecAhead groups of 16 ahead of the adds.
-        float acc = 0.0f;
-        const f4v* p4 = reinterpret_cast<const f4v*>(pr);
-        for (int c4 = 0; c4 < nc / 4; c4 += kDecChunk / 4) {
-            f4v R[kDecAhead + 1][4];
-#pragma unroll
-            for (int g0 = 0; g0 < kDecAhead; ++g0) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) R[g0][j] = p4[c4 + 4 * g0 + j];
-            }
-#pragma unroll
-            for (int gi = 0; gi < kDecChunk / 16; ++gi) {
-                if (gi + kDecAhead < kDecChunk / 16) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        R[(gi + kDecAhead) % (kDecAhead + 1)][j] = p4[c4 + 4 * (gi + kDecAhead) + j];
-                }
-                asm volatile("" : "+v"(acc)::"memory");  // the reads issue before the adds
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc += R[gi % (kDecAhead + 1)][j].x;
-                    acc += R[gi % (kDecAhead + 1)][j].y;
-                    acc += R[gi % (kDecAhead + 1)][j].z;
-                    acc += R[gi % (kDecAhead + 1)][j].w;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        mark<TRACE>(a, tr, u, 4 * kMaxW + d, 2);
-        if (lane == 0)
-            __hip_atomic_store(dres + (size_t)slot * kDecW + d, granule(tag, acc), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    // ---- waves 1..5: the dots (parity waves for the N-long ones) ----
+    auto buf = [&](int i) { return prb + (size_t)i * (nmax + 32); };
+    const long long ue = a.u0 + ((a.u0 & 1) ? 1 : 0);  // first even iterate
+    const long long uo = a.u0 + ((a.u0 & 1) ? 0 : 1);  // first odd iterate
+    switch (d) {
+        case 1: dec_dots<1, TRACE>(a, d, 1, buf(0), nullptr, ue, 2, dres); break;
+        case 2: dec_dots<1, TRACE>(a, d, 1, buf(1), nullptr, uo, 2, dres); break;
+        case 3: dec_dots<1, TRACE>(a, d, 4, buf(2), nullptr, ue, 2, dres); break;
+        case 4: dec_dots<1, TRACE>(a, d, 4, buf(3), nullptr, uo, 2, dres); break;
+        default: dec_dots<2, TRACE>(a, d, 2, buf(4), buf(5), a.u0, 1, dres); break;
     }
 }
 
@@ -702,6 +949,7 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
         return;
     }
     const int role = b < a.g1 ? kUpd : (b < a.g2 ? kT1 : (b < a.g3 ? kT2 : kT3));
+    if (PQP_CV_DIAG && PQP_CV_DIAG != 3 && role != kUpd && !(PQP_CV_DIAG == 2 && role == kT1)) return;
     const int g = b - (role == kUpd ? 0 : role == kT1 ? a.g1 : role == kT2 ? a.g2 : a.g3);
     const int K = (role == kUpd || role == kT1) ? a.N : a.M;
     const f4v* src = role == kUpd ? a.SPu : role == kT1 ? a.A1 : role == kT2 ? a.A2 : a.A3;
@@ -713,7 +961,7 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     {
         const f4v* s = src + (size_t)g * KB * kL;
         for (int e = tid; e < KP * kL; e += blockDim.x) qs[e] = (e < KB * kL) ? s[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-        for (int e = tid; e < kR * kMaxW * kHL; e += blockDim.x) hs[e] = 0ull;
+        for (int e = tid; e < kR * kMaxW * kL; e += blockDim.x) hs[e] = 0ull;
         // x past K (read by the last packet's products) stays +0: zeroed once in
         // both parity buffers
         for (int e = tid; e < 2 * (KPmax * 4 - K); e += blockDim.x) ysb[(e & 1) * KPmax * 4 + K + (e >> 1)] = 0.0f;
@@ -722,16 +970,15 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (w >= W) return;
     const int ny = KPmax * 4;
-#if PQP_CV_RTROLE
-    chain_wave<kUpd, TRACE>(a, g, w, K, qs, ysb, ny, hs, __builtin_amdgcn_readfirstlane(role));
-#else
-    switch (role) {
-        case kUpd: chain_wave<kUpd, TRACE>(a, g, w, K, qs, ysb, ny, hs, kUpd); break;
-        case kT1: chain_wave<kT1, TRACE>(a, g, w, K, qs, ysb, ny, hs, kT1); break;
-        case kT2: chain_wave<kT2, TRACE>(a, g, w, K, qs, ysb, ny, hs, kT2); break;
-        default: chain_wave<kT3, TRACE>(a, g, w, K, qs, ysb, ny, hs, kT3); break;
+    if (role == kUpd) {  // k_split_persist's update form
+        upd_wave<TRACE>(a, g, w, qs, ysb, ny, hs);
+        return;
     }
-#endif
+    switch (role) {
+        case kT1: chain_wave<kT1, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+        case kT2: chain_wave<kT2, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+        default: chain_wave<kT3, TRACE>(a, g, w, K, qs, ysb, ny, hs); break;
+    }
 }
 
 // packets of stage columns [col0, col0 + ncols): column j of the job is
@@ -789,8 +1036,8 @@ int converge_persist_wgs(int N, int M, int* g) {
 size_t converge_persist_lds_bytes(int N, int M) {
     const int Kmax = N > M ? N : M;
     const int KPmax = packets_of(waves_of(split_kblocks(Kmax)));
-    const size_t chain = sizeof(float) * ((size_t)KPmax * kL * 4 + (size_t)2 * KPmax * 4) + sizeof(u64) * kR * kMaxW * kHL;
-    const size_t dec = sizeof(float) * (size_t)(kDecW - 1) * (kDecChunk * cdiv_i(Kmax, kDecChunk) + 32) +
+    const size_t chain = sizeof(float) * ((size_t)KPmax * kL * 4 + (size_t)2 * KPmax * 4) + sizeof(u64) * kR * kMaxW * kL;
+    const size_t dec = sizeof(float) * (size_t)kDecBufs * (kDecChunk * cdiv_i(Kmax, kDecChunk) + 32) +
                        sizeof(u64) * kR * kDecW;
     return chain > dec ? chain : dec;
 }

@@ -13,6 +13,9 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
 ROLES = ("UPD", "T1", "T2", "T3")
+NIDS = 30  # 4 chain roles x 6 waves, then DEC's 6 waves (pqp_converge.hip kTraceIds)
+# DEC's waves: 0 decides; 1, 2 dot 1 (Fd.Y) of even / odd iterates; 3, 4 dot 4
+# ((Y'Qd).Y) of even / odd iterates; 5 dots 2 and 3 of every iterate
 
 
 def waves_of(K):
@@ -36,14 +39,14 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
     P = pb.problem(0)
     del pb
     L = pqp_amd.lib()
-    tr = torch.zeros(2 * n_trace * 29 * 4, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(2 * n_trace * NIDS * 4, dtype=torch.int64, device="cuda")
     with pqp_amd.Problem(P) as prob:
         prob.solve(max_updates=cap)
         L.pqp_tune_converge_trace(pqp_amd.C.c_void_p(tr.data_ptr()), n_trace)
         r = prob.solve(max_updates=cap)
         L.pqp_tune_converge_trace(None, 0)
     torch.cuda.synchronize()
-    both = tr.cpu().numpy().reshape(2, n_trace, 29, 4).astype(np.float64)
+    both = tr.cpu().numpy().reshape(2, n_trace, NIDS, 4).astype(np.float64)
     t = both[0] / 100.0  # us
     clk = both[1]  # shader clocks
     lo, hi = n_trace // 3, n_trace - 10
@@ -65,11 +68,13 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
     out["roles"]["DEC.w0 (decision)"] = {"period": med(np.diff(t[lo:hi + 1, 24, 0])),
                                          "feasibility": med(x[:, 1] - x[:, 0]), "dots_wait": med(x[:, 2] - x[:, 1]),
                                          "decide": med(x[:, 3] - x[:, 2])}
-    for d in range(1, 5):
+    for d in range(1, 6):
         i = 24 + d
         x = t[lo:hi, i]
-        out["roles"][f"DEC.w{d}"] = {"period": med(np.diff(t[lo:hi + 1, i, 0])), "gather": med(x[:, 1] - x[:, 0]),
-                                     "sum": med(x[:, 2] - x[:, 1])}
+        on = x[:, 0] > 0  # parity waves mark every other iterate
+        xs = x[on]
+        out["roles"][f"DEC.w{d}"] = {"period": med(np.diff(xs[:, 0])) if len(xs) > 1 else 0.0,
+                                     "gather": med(xs[:, 1] - xs[:, 0]), "sum": med(xs[:, 2] - xs[:, 1])}
     lastw = lambda role: ROLES.index(role) * 6 + W[role] - 1
     u = np.arange(lo, hi)
     out["handover"] = {
@@ -77,8 +82,8 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
         "UPD done u -> T1.w0 staged u+1": med(t[u + 1, 6, 1] - t[u, lastw("UPD"), 3]),
         "T1 done u -> T2.w0 staged u": med(t[u, 12, 1] - t[u, lastw("T1"), 3]),
         "T2 done u -> T3.w0 staged u": med(t[u, 18, 1] - t[u, lastw("T2"), 3]),
-        "T3 done u -> DEC.w2 gathered u": med(t[u, 26, 1] - t[u, lastw("T3"), 3]),
-        "T1 done u -> DEC.w4 gathered u": med(t[u, 28, 1] - t[u, lastw("T1"), 3]),
+        "T3 done u -> DEC.w5 gathered u": med(t[u, 29, 1] - t[u, lastw("T3"), 3]),
+        "T1 done u -> DEC dot-4 wave gathered u": med(np.maximum(t[u, 27, 1], t[u, 28, 1]) - t[u, lastw("T1"), 3]),
         "DEC decided u": med(t[u, 24, 3] - t[u, lastw("UPD"), 3]),
         "y_u published -> DEC decided u (latency)": med(t[u, 24, 3] - t[u - 1, lastw("UPD"), 3]),
         "DEC decided u-8 -> y_u published": med(t[u - 1, lastw("UPD"), 3] - t[u - 8, 24, 3]),
@@ -93,7 +98,8 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
               "T1.w0 staged": t[uu, 6, 1], "T1 last done": t[uu, lastw("T1"), 3],
               "T2.w0 staged": t[uu, 12, 1], "T2 last done": t[uu, lastw("T2"), 3],
               "T3.w0 staged": t[uu, 18, 1], "T3 last done": t[uu, lastw("T3"), 3],
-              "DEC.w4 gathered": t[uu, 28, 1], "DEC.w4 summed": t[uu, 28, 2], "DEC.w2 summed": t[uu, 26, 2],
+              "DEC dot-4 gathered": max(t[uu, 27, 1], t[uu, 28, 1]), "DEC dot-4 summed": max(t[uu, 27, 2], t[uu, 28, 2]),
+              "DEC.w5 summed": t[uu, 29, 2],
               "DEC.w0 feasibility": t[uu, 24, 1], "DEC.w0 dots in": t[uu, 24, 2],
               "DEC decided": t[uu, 24, 3]}
         sample[f"u={uu}"] = {k: round(float(v - base), 2) for k, v in ev.items()}

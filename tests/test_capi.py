@@ -91,6 +91,22 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
         assert n_fma == 5 * n_div, f"{name}: {n_fma} FMAs for {n_div} divisions"
 
 
+@pytest.mark.parametrize("src,name", [
+    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_i"),
+    ("pqp_converge.hip", "_ZN3pqp12_GLOBAL__N_118k_converge_persistILb0EEEvNS_6CvArgsE"),
+])
+def test_persistent_kernels_do_not_spill(src, name):
+    """The persistent launches hold a whole slice of products in registers
+    (up to 196 VGPRs) at 6 waves per workgroup, i.e. 256 VGPRs per lane: a
+    spill to scratch costs 0.3 us per update (measured on k_converge_persist),
+    so the default instantiations must have no scratch."""
+    asm = _gfx950_asm(src)
+    i = asm.index("\n" + name + ":")
+    m = re.search(r"; ScratchSize: (\d+)", asm[i:])
+    assert m, f"{name}: no ScratchSize note"
+    assert int(m.group(1)) == 0, f"{name} spills {m.group(1)} bytes per lane"
+
+
 def test_read_example_matches_oracle_loader(orc):
     import pqp_amd
 
