@@ -69,8 +69,11 @@ constexpr int kMaxW = 6;   // waves for K <= 1024
 #ifndef PQP_CV_DIAG  // timing diagnostic only (wrong results): 1 UPD alone, 2 UPD + T1, 3 UPD + T1-T3; DEC decides blind
 #define PQP_CV_DIAG 0
 #endif
+#ifndef PQP_CV_NOBP  // timing diagnostic only (with PQP_CV_DIAG): no backpressure check
+#define PQP_CV_NOBP 0
+#endif
 #ifndef PQP_CV_UPD_INPLACE  // upd_wave: later waves read their q while they wait for y
-#define PQP_CV_UPD_INPLACE 0
+#define PQP_CV_UPD_INPLACE 1
 #endif
 #ifndef PQP_CONVERGE_RING
 #define PQP_CONVERGE_RING 8
@@ -281,7 +284,8 @@ __device__ __forceinline__ int wait_sums(const CvArgs& a, const u64* src, unsign
 // multiply in place), the running sums through one 64-bit LDS word per lane
 // and update parity ([2][W][64] words inside the hand-off area), each chain
 // form running straight into its hand-off or epilogue; the last wave divides
-// and publishes y_{u+1} (tag u + 2) once slot (u + 1) % kR is free.  Waits
+// and publishes y_{u+1} (tag u + 2); its sweep also waits until slot
+// (u + 1) % kR is free.  Waits
 // also end when the launch has stopped (DEC finished or a role failed).
 template <bool TRACE>
 __device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4v* qs, float* ysb, int ny, u64* hs) {
@@ -304,9 +308,12 @@ __device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4
         const unsigned tag = (unsigned)(u + 1);
         const int rslot = (int)(u & (kR - 1));
         mark<TRACE>(a, tr, u, w, 0);
-        long long dec_seen = 0;
-        const bool need_bp = last && u + 1 - kR >= a.u0;
-        if (need_bp) dec_seen = __hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the last wave publishes y_{u+1} into slot (u + 1) % kR: free once DEC
+        // has decided u + 1 - kR.  Its sweep waits for that too (one more load
+        // in the same loop: off the critical path, since the last wave waits
+        // for its turn long after it has staged, and no loop of its own, which
+        // made the in-place products spill)
+        const bool need_bp = !PQP_CV_NOBP && last && u + 1 - kR >= a.u0;
         // ---- 1. y of this slice from the ring: every load in flight, one
         // wave-wide tag test, the exit straight into the LDS stores ----
         auto stage_y = [&]() -> bool {
@@ -327,7 +334,9 @@ __device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4
                 for (int m = 0; m < 4; ++m)
                     x[m] = __hip_atomic_load(gsrc + kk[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (last) xo = __hip_atomic_load(gsrc + rowc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = true;
+                long long dv = 0;
+                if (need_bp) dv = __hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = !need_bp || dv >= u + 1 - kR;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) ok &= (unsigned)(x[m] >> 32) == tag;
                 if (last) ok &= (unsigned)(xo >> 32) == tag;
@@ -346,9 +355,6 @@ __device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4
 #pragma unroll
             for (int m = 0; m < 4; ++m) ys[kk[m]] = __uint_as_float((unsigned)x[m]);
             if (last) yrow = __uint_as_float((unsigned)xo);
-            // the backpressure word (loaded before the sweep, so back by now) into scalars
-            if (need_bp) dec_seen = ((long long)__builtin_amdgcn_readfirstlane((int)(dec_seen >> 32)) << 32) |
-                                    (unsigned)__builtin_amdgcn_readfirstlane((int)dec_seen);
             mark<TRACE>(a, tr, u, w, 1);
             return true;
         };
@@ -379,18 +385,6 @@ __device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4
             const float v = acc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
             // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2)
             const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-            if (need_bp && dec_seen < u + 1 - kR) {
-                Deadline dl;
-                for (unsigned spins = 0;; ++spins) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (__hip_atomic_load(a.decided, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= u + 1 - kR) break;
-                    if (stopped(a)) return false;
-                    if ((spins & 63) == 63 && dl.expired()) {
-                        fail(a, 20);
-                        return false;
-                    }
-                }
-            }
             const float yn = v / den * yrow;  // updY :594
             if (!(p & 1) && live)
                 __hip_atomic_store((gu64*)a.ry + (size_t)((u + 1) & (kR - 1)) * N + row, granule(tag + 1, yn),

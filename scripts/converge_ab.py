@@ -33,8 +33,17 @@ def main(N: int = 1024, cap: int = 2000):
             r = prob.solve(max_updates=cap)
             ts.append((time.perf_counter() - t0) / (cap + 1) * 1e6)
         assert L.pqp_tune_last_path(None) == 3, "not the persistent converge launch"
+        # the launch's fixed cost: a 200-iteration solve beside the 2000 one
+        t200 = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            prob.solve(max_updates=200)
+            t200.append(time.perf_counter() - t0)
+        slope = (np.median(ts) * (cap + 1) * 1e-6 - np.median(t200)) / (cap - 200) * 1e6
+        fixed_us = np.median(t200) * 1e6 - 201 * slope
     h = hashlib.sha256(np.asarray(r["Y"], np.float32).tobytes() + np.asarray(r["U"], np.float32).tobytes())
     print(json.dumps({"n_dual": N, "median_us_per_iter": float(np.median(ts)), "all": ts, "h": r["h"],
+                      "slope_us_per_iter": float(slope), "per_solve_fixed_us": float(fixed_us),
                       "digest": h.hexdigest()[:16]}))
 
 
