@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import hashlib
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -24,6 +25,10 @@ def main(N: int = 1024, cap: int = 2000):
     pb = pqp_amd.ProblemBatch.synthetic(1, 0, 1, N, M)
     P = pb.problem(0)
     del pb
+    if os.environ.get("CONVERGE_AB_FEASIBLE"):
+        # every iterate feasible (Kp far above any Gp U): computeCost's four
+        # dots run on every iterate (the synthetic problem is infeasible)
+        P["Kp"] = np.full_like(np.asarray(P["Kp"], np.float32), 1e30)
     L = pqp_amd.lib()
     ts = []
     with pqp_amd.Problem(P) as prob:
