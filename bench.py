@@ -50,6 +50,7 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
@@ -100,6 +101,10 @@ def parse():
     ap.add_argument("--rowshard-updates", type=int, default=100)
     ap.add_argument("--rowshard-graph", action="store_true",
                     help="at N > 1, also time the row-sharded steps as hipGraph replays (update + RCCL all-gather)")
+    ap.add_argument("--leg-timeout", type=float, default=240.0,
+                    help="seconds an optional leg (gather, rowshard, ...) may run before the line is printed without it")
+    ap.add_argument("--dist-timeout", type=float, default=420.0,
+                    help="process-group timeout (s); longer than --leg-timeout")
     return ap.parse_args()
 
 
@@ -165,6 +170,20 @@ def cpu_baseline(n: int, seconds: float, instances: list, tol_cases: dict | None
         tb = sorted(times)[len(times) // 2]
         bundled = {"converge_h": h, "converge_ms": tb * 1e3, "iter_per_s": h / tb,
                    "what": "PQP_CPU.c solveQuadraticDual on the bundled example (configs[0]), 1 thread"}
+        # configs[0] as BASELINE states it, "1000 iters": the reference's
+        # fixed-iteration solve (the testing/ harness loop, 999 updateY2 calls
+        # from Y = 1000, PQP_CPU_test.c:714-744) over its own functions, median
+        # of 5 -- the like-for-like figure of the GPU's bundled.fixed1000_ms
+        runs = [ref.fixed_solve(B, 1000) for _ in range(5)]
+        tot = sorted(r[1] for r in runs)[2]
+        loop = sorted(r[2] for r in runs)[2]
+        yf = runs[0][0]
+        bundled["fixed1000"] = {"ms": tot * 1e3, "loop_ms": loop * 1e3, "iter_per_s": 999 / tot,
+                                "y_star_zeros": int((yf == 0).sum()), "y_star_1000": int((yf == 1000).sum()),
+                                "what": "oracle/_ref/libref_fixed.so: PQP_CPU.c's setup (:696-710) + 999 x "
+                                        "(updateY2 :603, copyMatrix) as the testing/ harness runs them, 1 thread, "
+                                        "median of 5; ms = setup + loop (the GPU's bundled.fixed1000_ms is one "
+                                        "pqp_problem_solve call), loop_ms = the updates alone"}
         # the reference's convertToDual of ONE N = 1024, M = 512 problem with a
         # dense Qp_inv (the setup_convert leg's problems), one thread
         sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
@@ -438,32 +457,77 @@ def single_converge_bench(pqp_amd, N: int = 1024, updates: int = 2000) -> dict:
                     "concurrent workgroup roles, terminate(Y_u) beside the update to Y_{u+1}"}
 
 
-def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: int, graph: bool = True) -> dict:
+def _sync(dev):
+    import torch
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+class _FaultyBlock:
+    """PQP_BENCH_FAULT=rowshard:<rank>: this rank's row block raises inside
+    the leg's first timed update (failure injection for the N > 1 tests)."""
+
+    def __init__(self, blk):
+        self.blk, self.row0, self.rows, self.calls = blk, blk.row0, blk.rows, 0
+
+    def update(self, Y, Y_rows):
+        self.calls += 1
+        if self.calls > 5:  # past the warm-up steps, inside the timed region
+            raise RuntimeError("injected row-block failure (PQP_BENCH_FAULT)")
+        self.blk.update(Y, Y_rows)
+
+
+def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: int, graph: bool = True,
+                   make_block=None) -> dict:
     """One synthetic problem of n_dual = N whose rows are spread over the
     ranks (pqp_amd.rowshard); fixed-mode updates, timed as the max over
-    ranks.  Every rank ends with the whole iterate."""
+    ranks.  Every rank ends with the whole iterate.  `make_block(N, row0,
+    rows)`: another block than the GPU RowBlock (the CPU tests)."""
     import torch
 
     from pqp_amd.rowshard import RowShardedSolver, row_plan
 
     R, plan = row_plan(N, world)
     row0, rows = plan[rank]
-    blk, _, _ = pqp_amd.RowBlock.synthetic(7, 0, N, row0, rows, device=dev)
+    # every rank builds its block; the ranks agree on the outcome before any
+    # collective of the leg, so a failed setup on one rank ends the leg on all
+    # of them instead of leaving its peers in an all-gather
+    blk, err = None, None
+    try:
+        blk = (make_block(N, row0, rows) if make_block else
+               pqp_amd.RowBlock.synthetic(7, 0, N, row0, rows, device=dev)[0])
+    except Exception as e:  # noqa: BLE001 -- reported below, on every rank
+        err = f"{type(e).__name__}: {e}"
+    if dist is not None:
+        flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag.item()) and err is None:
+            err = "row-block setup failed on another rank"
+    if err is not None:
+        raise RuntimeError(err)
+    if os.environ.get("PQP_BENCH_FAULT") == f"rowshard:{rank}":
+        blk = _FaultyBlock(blk)
     solver = RowShardedSolver(blk, N, dev, dist=dist)
 
     def timed(n):
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
         solver.advance(n)
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         if dist is not None:
             dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        solver.check()  # no expired in-kernel wait in any update (else this raises)
-        if dist is not None:
+        t = torch.tensor([time.perf_counter() - t0, 0.0], dtype=torch.float64, device=dev)
+        try:
+            solver.check()  # no expired in-kernel wait in any update of this rank's block
+        except Exception:  # noqa: BLE001 -- every rank learns of it from the all-reduce below
+            t[1] = 1.0
+        if dist is not None:  # the flag rides with the timing: no rank raises while a peer waits
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if float(t[1]):
+            raise RuntimeError("a row block's in-kernel hand-off wait expired (pqp_rowblock_check) on some rank")
         return float(t[0]) / n
 
     solver.Y.fill_(1000.0)
@@ -474,8 +538,7 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     # step, 16 steps per graph); not on gloo (rehearsal), see RowShardedSolver.capture
     G = 16
     # RowShardedSolver.capture is tested on a one-rank RCCL group only (one GPU
-    # per box); at N > 1 the bench captures only when asked (--rowshard-graph),
-    # so an unexpected capture failure cannot cost the job its JSON line
+    # per box); at N > 1 the bench captures only when asked (--rowshard-graph)
     graphed = solver.capture(G) if graph else False
     dt_graph, same = None, None
     if graphed:
@@ -486,15 +549,8 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
         dt_graph = timed(max(G, updates // G * G))
     dt = min(dt_eager, dt_graph) if dt_graph else dt_eager
     y = solver.Y[:N]
-    L = pqp_amd.lib()
-    lean_min = L.pqp_tune_lean_min_n(0)  # read the setting (and restore it)
-    L.pqp_tune_lean_min_n(lean_min)
-    lean = lean_min > 0 and rows * N >= lean_min * lean_min  # row blocks choose the lean relay by rows x N
-    bpe = 4 if lean else 8  # bytes per matrix entry the update streams
     out = {"n_dual": N, "ranks": world, "rows_per_rank": R, "updates": updates, "us_per_update": dt * 1e6,
            "iter_per_s": 1.0 / dt,
-           "layout": "Qd packets, k_lean_relay (4 B/entry)" if lean else "stored split matrices (8 B/entry)",
-           "alg_GBps": bpe * N * N / dt / 1e9,
            "finite_nonneg": bool(torch.isfinite(y).all().item()) and bool((y >= 0).all().item()),
            "us_per_update_eager": dt_eager * 1e6,
            "us_per_update_graph": dt_graph * 1e6 if dt_graph else None,
@@ -505,9 +561,74 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
                           f"not captured: {solver.capture_error or 'gloo group (rehearsal)'}"),
            "note": "us_per_update = the faster of eager launches (pqp_rowblock_update + all_gather_into_tensor per "
                    "update at N>1 ranks) and graph replays"}
+    if make_block is None:
+        L = pqp_amd.lib()
+        lean_min = L.pqp_tune_lean_min_n(0)  # read the setting (and restore it)
+        L.pqp_tune_lean_min_n(lean_min)
+        lean = lean_min > 0 and rows * N >= lean_min * lean_min  # row blocks choose the lean relay by rows x N
+        bpe = 4 if lean else 8  # bytes per matrix entry the update streams
+        out["layout"] = "Qd packets, k_lean_relay (4 B/entry)" if lean else "stored split matrices (8 B/entry)"
+        out["alg_GBps"] = bpe * N * N / dt / 1e9
     del solver, blk
-    torch.cuda.empty_cache()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
     return out
+
+
+class Emitter:
+    """Rank 0's one JSON line, printed exactly once.
+
+    The headline (`result`) is measured and held before any optional leg
+    runs.  Each leg then runs under :meth:`leg`: an exception becomes
+    ``{"error": ...}`` under the leg's key, and a leg still running after
+    `leg_timeout_s` (a collective whose peer never arrives) makes the
+    watchdog print the line with that leg marked as timed out and end the
+    process with status 0 -- on every rank, before the process group's own
+    timeout would abort it.  So no optional leg can cost the job its line."""
+
+    def __init__(self, rank: int, result: dict | None, leg_timeout_s: float):
+        import threading
+
+        self.rank, self.result, self.timeout = rank, result, float(leg_timeout_s)
+        self._lock = threading.Lock()
+        self._printed = False
+        self.failed = False
+
+    def emit(self):
+        with self._lock:
+            if self.rank == 0 and not self._printed and self.result is not None:
+                print(json.dumps(self.result), flush=True)
+            self._printed = True
+
+    def _expire(self, name: str):
+        with self._lock:
+            if self._printed:
+                return
+            if self.result is not None:
+                self.result[name] = {"error": f"timed out: no result within {self.timeout:.0f} s "
+                                              "(a peer rank never reached the collective?)"}
+        self.emit()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    def leg(self, name: str, fn):
+        import threading
+
+        t = threading.Timer(self.timeout, self._expire, args=(name,))
+        t.daemon = True
+        t.start()
+        try:
+            out = fn()
+        except Exception as e:  # noqa: BLE001 -- an optional leg never costs the headline
+            out = {"error": f"{type(e).__name__}: {e}"}
+            self.failed = True
+        finally:
+            t.cancel()
+        with self._lock:
+            if self.result is not None and not self._printed:
+                self.result[name] = out
+        return out
 
 
 def _free_port() -> int:
@@ -591,7 +712,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo" if rehearse else "nccl", device_id=None if rehearse else dev)
+        # an explicit timeout: a collective whose peer never arrives ends with an
+        # error (after the Emitter's leg watchdog has already printed the line)
+        dist.init_process_group("gloo" if rehearse else "nccl", device_id=None if rehearse else dev,
+                                timeout=timedelta(seconds=args.dist_timeout))
 
     N, B, K, W, C = args.n, args.batch, args.steps, args.warmup, max(1, args.chunk)
     # "scatter inputs": rank 0 hands each rank its (seed, first problem, count)
@@ -636,31 +760,67 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
 
-    # gather Y* to rank 0 over RCCL (reported separately, not in `value`)
-    gather_ms = None
-    gather_ok = None
-    if dist is not None:
-        y = batch.Y[:, :N].contiguous()
-        torch.cuda.synchronize(dev)
-        g0 = time.perf_counter()
-        full = gather_rows(dist, rank, world, y)
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - g0) * 1e3
-        if rank == 0:  # rank order = problem order: rank 0's own block leads
-            gather_ok = tuple(full.shape) == (B * world, N) and bool(torch.equal(full[:B], y))
     Yh = batch.Y[:, :N]
     finite = bool(torch.isfinite(Yh).all().item()) and bool((Yh >= 0).all().item())
 
-    rowshard = None
+    # The headline line is complete here; it is held (rank 0) while the
+    # optional legs run, each under the Emitter's guard.
+    result = headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse) \
+        if rank == 0 else None
+    em = Emitter(rank, result, args.leg_timeout)
+
+    if dist is not None:  # gather Y* to rank 0 over RCCL (reported separately, not in `value`)
+        def gather_leg():
+            y = batch.Y[:, :N].contiguous()
+            torch.cuda.synchronize(dev)
+            g0 = time.perf_counter()
+            full = gather_rows(dist, rank, world, y)
+            torch.cuda.synchronize(dev)
+            ok = None
+            if rank == 0:  # rank order = problem order: rank 0's own block leads
+                ok = tuple(full.shape) == (B * world, N) and bool(torch.equal(full[:B], y))
+            return {"ms": (time.perf_counter() - g0) * 1e3, "ok": ok}
+
+        g = em.leg("gather", gather_leg)
+        if result is not None:
+            result["gather_ms"], result["gather_ok"] = g.get("ms"), g.get("ok")
     if args.rowshard_n > 0:  # every rank takes part
-        rowshard = rowshard_bench(pqp_amd, dist, rank, world, dev, args.rowshard_n, args.rowshard_updates,
-                                  graph=world == 1 or args.rowshard_graph)
+        em.leg("rowshard", lambda: rowshard_bench(pqp_amd, dist, rank, world, dev, args.rowshard_n,
+                                                  args.rowshard_updates, graph=world == 1 or args.rowshard_graph))
+    if world == 1 and not args.no_bundled:
+        em.leg("bundled", lambda: bundled_bench(pqp_amd))
+        em.leg("mpc_batch", lambda: mpc_batch_bench(pqp_amd))
+        em.leg("single_n1024", lambda: single_bench(pqp_amd))
+        em.leg("single_converge", lambda: single_converge_bench(pqp_amd))
+        em.leg("setup_convert", lambda: setup_bench(pqp_amd))
+        em.leg("batch_converge", lambda: batch_converge_bench(pqp_amd))
+    tol_cases = None
+    if world == 1 and not args.no_bundled:
+        import tempfile
 
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+        with tempfile.TemporaryDirectory() as td:
+            tol_cases = tol_problems(pqp_amd, Path(td))
+        em.leg("iters_to_tol", lambda: iters_to_tol_bench(pqp_amd, tol_cases))
+    if world == 1 and not args.no_cpu_baseline:
+        # distinct problems of this very workload, from the GPU batch
+        inst = [(batch.qd_rowmajor(j), batch.Fd[j, :N].cpu().numpy()) for j in range(min(args.cpu_instances, B))]
+        cb = em.leg("cpu_baseline", lambda: cpu_baseline(N, args.cpu_seconds, inst, tol_cases))
+        ref_tol = cb.get("bundled", {}).get("iters_to_tol")
+        if ref_tol and "iters_to_tol" in result and "error" not in result["iters_to_tol"]:
+            result["iters_to_tol_identical_to_reference"] = all(
+                result["iters_to_tol"][k]["h"] == ref_tol[k]["h"] for k in ref_tol)
+    em.emit()
+    if dist is not None:
+        if em.failed:  # a peer may be stuck in the failed leg's collective: do not wait for it
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+        dist.destroy_process_group()
 
+
+def headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse) -> dict:
+    """The headline JSON object (rank 0): throughput of exactly K steps over
+    all ranks, the hot kernel's roofline, the result check."""
     per_launch_ms = kern_ms / launches
     achieved = alg_bytes(N) * B * C / (per_launch_ms * 1e-3) / 1e9 if launches else 0.0
     traffic, traffic_src = None, "no PMC record for this shape"
@@ -697,38 +857,12 @@ def main():
                      "kernel_src_sha256": khash, "kernel": KERNEL,
                      "alg_bytes_per_launch": alg_bytes(N) * B * C, "avg_launch_ms": per_launch_ms},
         "results_finite_nonneg": finite,
-        "gather_ms": gather_ms,
-        "gather_ok": gather_ok,
+        "gather_ms": None,
+        "gather_ok": None,
     }
     if rehearse:
         result["rehearsal"] = "all ranks on cuda:0 over gloo (PQP_BENCH_REHEARSE=1): control-flow check, not a measurement"
-    if rowshard is not None:
-        result["rowshard"] = rowshard
-    if world == 1 and not args.no_bundled:
-        result["bundled"] = bundled_bench(pqp_amd)
-        result["mpc_batch"] = mpc_batch_bench(pqp_amd)
-        result["single_n1024"] = single_bench(pqp_amd)
-        result["single_converge"] = single_converge_bench(pqp_amd)
-        result["setup_convert"] = setup_bench(pqp_amd)
-        result["batch_converge"] = batch_converge_bench(pqp_amd)
-    tol_cases = None
-    if world == 1 and not args.no_bundled:
-        import tempfile
-
-        with tempfile.TemporaryDirectory() as td:
-            tol_cases = tol_problems(pqp_amd, Path(td))
-        result["iters_to_tol"] = iters_to_tol_bench(pqp_amd, tol_cases)
-    if world == 1 and not args.no_cpu_baseline:
-        # distinct problems of this very workload, from the GPU batch
-        inst = [(batch.qd_rowmajor(j), batch.Fd[j, :N].cpu().numpy()) for j in range(min(args.cpu_instances, B))]
-        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, inst, tol_cases)
-        ref_tol = result["cpu_baseline"].get("bundled", {}).get("iters_to_tol")
-        if ref_tol and "iters_to_tol" in result:
-            result["iters_to_tol_identical_to_reference"] = all(
-                result["iters_to_tol"][k]["h"] == ref_tol[k]["h"] for k in ref_tol)
-    print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    return result
 
 
 if __name__ == "__main__":

@@ -27,6 +27,7 @@ ORACLE_SO = HERE / "_build" / "liboracle.so"
 REF_SO = HERE / "_ref" / "libpqp_ref.so"
 REF_BIN = HERE / "_ref" / "pqp_cpu_ref"
 REF_TEST_SO = HERE / "_ref" / "libpqp_ref_test.so"
+REF_FIXED_SO = HERE / "_ref" / "libref_fixed.so"
 
 # Bundled-example dimensions: PQP_CPU.c:13-17 (pHorizon=1, nState=29, nInput=7,
 # nOutput=7, nDis=1) -> M = 7 primal, N = 28 dual (PQP_CPU.c:940-941).
@@ -48,6 +49,30 @@ def f32(a) -> np.ndarray:
 def _p(a: np.ndarray):
     assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(_fp)
+
+
+def block_diag_problem(P: dict, k: int) -> dict:
+    """k copies of dual problem P on the diagonal (test data, numpy only):
+    Qd, Gp, Qp, Qp_inv block-diagonal, the vectors tiled, Md and Mp times k.
+    Rows of different blocks never meet in a product (the zero entries add
+    +0.0 to a sum that is never -0.0), so every block's iterate is P's own,
+    bit for bit, while terminate()'s dots run over all k*N (k*M) entries.
+    From the bundled example this gives large problems that STOP under the
+    reference's exact-float test (h = 313 up to n_dual 1008, 36 copies)."""
+    N, M = int(P["N"]), int(P["M"])
+
+    def bd(a, r, c):
+        out = np.zeros((k * r, k * c), np.float32)
+        a = np.asarray(a, np.float32).reshape(r, c)
+        for b in range(k):
+            out[b * r:(b + 1) * r, b * c:(b + 1) * c] = a
+        return out.reshape(-1)
+
+    tile = lambda a: np.tile(np.asarray(a, np.float32).reshape(-1), k)  # noqa: E731
+    return dict(Qd=bd(P["Qd"], N, N), Gp=bd(P["Gp"], N, M), Qp=bd(P["Qp"], M, M), Qp_inv=bd(P["Qp_inv"], M, M),
+                Fd=tile(P["Fd"]), Kp=tile(P["Kp"]), Fp=tile(P["Fp"]),
+                Md=(np.asarray(P["Md"], np.float32) * np.float32(k)).reshape(1),
+                Mp=(np.asarray(P["Mp"], np.float32) * np.float32(k)).reshape(1), N=k * N, M=k * M)
 
 
 class Oracle:
@@ -327,6 +352,24 @@ class Reference:
         self.lib.computeUfromY(_p(U), _p(f32(Y).copy()), _p(f32(P["Fp"]).copy()), _p(f32(P["Gp"]).copy()),
                                _p(f32(P["Qp_inv"]).copy()), P["N"], P["M"])
         return U
+
+    def fixed_solve(self, P, num_iter: int = 1000):
+        """The reference's fixed-iteration solve (oracle/ref_fixed.c over this
+        library's own setup/updateY2/copyMatrix; the testing/ harness loop,
+        PQP_CPU_test.c:714-744): Y after num_iter - 1 updates from Y = 1000.
+        Returns (Y, seconds of the whole call, seconds of the update loop)."""
+        if not hasattr(self, "_fixed"):
+            if not REF_FIXED_SO.exists():
+                raise FileNotFoundError(f"{REF_FIXED_SO} not built (needs /root/reference; run make -C oracle)")
+            self._fixed = C.CDLL(str(REF_FIXED_SO))
+            self._fixed.ref_fixed_solve.argtypes = [_fp, _fp, _fp, C.c_int, C.c_long, C.POINTER(C.c_double)]
+            self._fixed.ref_fixed_solve.restype = C.c_double
+        N = P["N"]
+        Y = np.zeros(N, np.float32)
+        loop = C.c_double(0.0)
+        total = self._fixed.ref_fixed_solve(_p(Y), _p(f32(P["Qd"]).copy()), _p(f32(P["Fd"]).copy()), N, num_iter,
+                                            C.byref(loop))
+        return Y, float(total), float(loop.value)
 
     def solve(self, P):
         """The reference solveQuadraticDual; returns (h, Y, U) with h parsed from

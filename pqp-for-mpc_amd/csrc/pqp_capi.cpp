@@ -1381,8 +1381,10 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
         path = 0;
     else if (solve_small_lds_bytes(N, M) <= kLdsBudget)
         path = 1;
-    else if (solve_single_lds_bytes(ldq, ldm, true) > kLdsBudget)
+    else if (solve_single_lds_bytes(ldq, ldm, false) > kLdsBudget)
         return set_error(PQP_ERR_ARG, "pqp_batch_solve: N=%d, M=%d exceeds the LDS budget", N, M);
+    // the fused Y'Qd pass needs one more ldq-long LDS vector: only where it fits
+    const bool fuse = path == 2 && (g_batch_opts & 1) && ldq == N && solve_single_lds_bytes(ldq, ldm, true) <= kLdsBudget;
     DevBuf QdT, theta, state, pending, Udummy, sym, GpT, QinvT;
     const float* qdt = nullptr;
     if (path == 2) {
@@ -1436,7 +1438,7 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
     a.Md = d_Md;
     a.Qp = d_Qp;
     a.Qinv = d_Qp_inv;
-    a.sym = (g_batch_opts & 1) ? static_cast<const int*>(sym.p) : nullptr;
+    a.sym = fuse ? static_cast<const int*>(sym.p) : nullptr;
     a.GpT = GpT.f();
     a.QinvT = QinvT.f();
     a.Fp = d_Fp;

@@ -16,12 +16,15 @@ Outputs (all small):
   synth_converge.npz    converge-mode (N, M, seed) cases that the reference solves
   synth_large.npz       N=1024/M=512 and N=1000/M=500: dual-data digests and Y
                         after a few reference updates
+  blocks.npz            the bundled example as k diagonal blocks (oracle.block_diag_problem,
+                        k = 9, 36: n_dual 252, 1008): the reference's h (313), Y*, U*, Jp, Jd --
+                        large problems that stop under the exact-float test, every iterate feasible
   dense_dual.npz        convertToDual with a DENSE Qp_inv (numpy-seeded,
                         pqp_amd.dense_qinv) at N=1024/M=512 and N=300/M=77: digests of
                         Qd, and Fd / Md (the general setup GEMM's parity case)
 
 Usage: python tests/golden/make_golden.py [part ...]   (parts: bundled converge
-       large testing dense; default all)
+       large testing dense blocks; default all)
 """
 from __future__ import annotations
 
@@ -34,7 +37,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "oracle"))
-from oracle import Oracle, Reference, ReferenceTesting, REF_BIN, build  # noqa: E402
+from oracle import Oracle, Reference, ReferenceTesting, REF_BIN, block_diag_problem, build  # noqa: E402
 
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 from pqp_amd import dense_qinv  # noqa: E402  (numpy only; the library is not loaded)
@@ -183,10 +186,27 @@ def testing_files(ref: Reference):
     print("testing/test2.txt: M", M, "N", N)
 
 
+BLOCK_CASES = (9, 36)
+
+
+def blocks(ref: Reference):
+    P = ref.bundled_problem(REFERENCE_DIR)
+    out = {"k": np.asarray(BLOCK_CASES, np.int64)}
+    for k in BLOCK_CASES:
+        Q = block_diag_problem(P, k)
+        h, Y, U = ref.solve(Q)
+        out[f"h{k}"] = np.int64(h)
+        out[f"Y{k}"], out[f"U{k}"] = Y, U
+        out[f"Jp{k}"] = np.float32(ref.cost(U, Q["Qp"], Q["Fp"], Q["Mp"], Q["M"]))
+        out[f"Jd{k}"] = np.float32(ref.cost(Y, Q["Qd"], Q["Fd"], Q["Md"], Q["N"]))
+        print(f"blocks k={k}: n_dual {Q['N']}, M {Q['M']}, h {h}")
+    np.savez(OUT / "blocks.npz", **out)
+
+
 def main(parts=None):
     build()
     ref, orc = Reference(), Oracle()
-    parts = set(parts or ("bundled", "converge", "large", "testing", "dense"))
+    parts = set(parts or ("bundled", "converge", "large", "testing", "dense", "blocks"))
     if "bundled" in parts:
         bundled(ref)
     if "converge" in parts:
@@ -197,6 +217,8 @@ def main(parts=None):
         testing_files(ref)
     if "dense" in parts:
         dense_dual(ref, orc)
+    if "blocks" in parts:
+        blocks(ref)
 
 
 if __name__ == "__main__":

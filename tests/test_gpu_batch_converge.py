@@ -82,3 +82,21 @@ def test_batch_mixed_symmetric_and_not(gpu_lib, orc, opts):
     for b, P in enumerate((P0, P1)):
         h, Y, U = orc.solve(P, max_updates=cap)
         _check(pb, b, h, Y, U, f"mixed {b}")
+
+
+@pytest.mark.parametrize("opts", [0, 1])
+def test_batch_fits_only_unfused(gpu_lib, orc, opts):
+    """n_dual 9600, M 4 fits the one-workgroup solver's LDS only
+    without the fused Y'Qd vector (3 ldq + 3 ldm floats <= 150 KiB < 4 ldq +
+    3 ldm).  It must solve in both settings (fusion turned off for the call
+    where it does not fit), bit for bit with the oracle."""
+    N, M, cap = 9600, 4, 2
+    L = gpu_lib.lib()
+    prev = L.pqp_tune_batch_converge(opts)
+    try:
+        pb = gpu_lib.ProblemBatch.synthetic(11, 0, 1, N, M).solve(max_updates=cap)
+    finally:
+        L.pqp_tune_batch_converge(prev)
+    P = orc.synth_problem(11, 0, N, M)
+    h, Y, U = orc.solve(P, max_updates=cap)
+    _check(pb, 0, h, Y, U, f"n_dual {N} opts={opts}")

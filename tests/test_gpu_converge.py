@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from conftest import CAP, assert_bitwise
+from conftest import CAP, GOLDEN, assert_bitwise
 
 pytestmark = pytest.mark.gpu
 
@@ -122,3 +122,70 @@ def test_persistent_testfile_vs_oracle(gpu_lib, orc, tmp_path):
     r = gpu_lib.solve_dual(P, max_updates=CAP)
     h, Y, U = orc.solve(P, max_updates=CAP)
     _same(r, h, Y, U, "test2")
+
+
+def _terminate_costs(orc, P, Y):
+    """(flag, Jp, Jd) of the reference's terminate() on iterate Y (oracle)."""
+    flag, _, Jp, Jd = orc.terminate(Y, P["Qd"], P["Fd"], P["Md"], P["Qp"], P["Qp_inv"], P["Fp"], P["Mp"], P["Gp"],
+                                    P["Kp"], P["N"], P["M"])
+    return flag, Jp, Jd
+
+
+# caps of both parities: DEC sums the N-long dots of even and odd iterates on
+# different waves (pqp_converge.hip)
+@pytest.mark.parametrize("N,M,cap", [(100, 50, 20), (100, 100, 21), (385, 192, 30), (385, 385, 31),
+                                     (1024, 512, 40), (1024, 512, 39), (1024, 1024, 22)])
+def test_persistent_feasible_iterates_vs_oracle(gpu_lib, orc, persistent, N, M, cap):
+    """VERDICT r2: every iterate feasible (Kp = 1e30 seen by checkFeas only;
+    Fd keeps the generator's Kp), so terminate() runs all of computeCost on
+    every iterate (PQP_CPU.c:648-666, :679-684): DEC's four dots, the M-long
+    ones included.  h, Y, U bit for bit, and the last terminate()'s Jp, Jd."""
+    P = orc.synth_problem(8, N % 3, N, M)
+    P["Kp"] = np.full(N, 1e30, np.float32)
+    r = gpu_lib.solve_dual(P, max_updates=cap)
+    assert gpu_lib.lib().pqp_tune_last_path(None) == 3, "not the persistent converge launch"
+    h, Y, U = orc.solve(P, max_updates=cap)
+    _same(r, h, Y, U, f"feasible N={N} M={M}")
+    flag, Jp, Jd = _terminate_costs(orc, P, Y)
+    assert flag == 0 and np.isfinite(Jp) and np.isfinite(Jd)
+    assert np.float32(r["Jp"]) == np.float32(Jp), (r["Jp"], Jp)
+    assert np.float32(r["Jd"]) == np.float32(Jd), (r["Jd"], Jd)
+
+
+@pytest.mark.parametrize("chunk", [0, 50, 7])
+@pytest.mark.parametrize("k", [9, 36])
+def test_persistent_large_problem_stops_like_reference(gpu_lib, golden_bundled, persistent, chunk, k):
+    """The bundled example as k diagonal blocks (n_dual 252 / 1008, every
+    iterate feasible) STOPS under the exact-float test at the reference's
+    h = 313 (tests/golden/blocks.npz, made by oracle/_ref): one launch, and
+    launches of 50 / 7 decided iterates, so the stop lands inside a chained
+    launch.  Y*, U*, Jp, Jd bit for bit."""
+    from oracle import block_diag_problem
+
+    g = np.load(GOLDEN / "blocks.npz")
+    P = {kk: np.ascontiguousarray(golden_bundled[kk], dtype=np.float32) for kk in
+         ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    P.update(N=int(golden_bundled["N"]), M=int(golden_bundled["M"]))
+    Q = block_diag_problem(P, k)
+    persistent.pqp_tune_converge_chunk(chunk)
+    r = gpu_lib.solve_dual(Q, max_updates=CAP)
+    assert gpu_lib.lib().pqp_tune_last_path(None) == 3, "not the persistent converge launch"
+    assert r["converged"] and r["h"] == int(g[f"h{k}"]) == 313
+    assert_bitwise(r["Y"], g[f"Y{k}"], "Y*")
+    assert_bitwise(r["U"], g[f"U{k}"], "U*")
+    assert np.float32(r["Jp"]) == g[f"Jp{k}"] and np.float32(r["Jd"]) == g[f"Jd{k}"]
+
+
+@pytest.mark.parametrize("chunk", [5, 8])
+def test_persistent_feasible_chunked(gpu_lib, orc, persistent, chunk):
+    """Feasible iterates at n_dual 1024 across chained launches of `chunk`
+    decided iterates: same h, Y, U, Jp, Jd as the oracle."""
+    N, M, cap = 1024, 512, 23
+    P = orc.synth_problem(8, 2, N, M)
+    P["Kp"] = np.full(N, 1e30, np.float32)
+    persistent.pqp_tune_converge_chunk(chunk)
+    r = gpu_lib.solve_dual(P, max_updates=cap)
+    h, Y, U = orc.solve(P, max_updates=cap)
+    _same(r, h, Y, U, f"feasible chunk={chunk}")
+    _, Jp, Jd = _terminate_costs(orc, P, Y)
+    assert np.float32(r["Jp"]) == np.float32(Jp) and np.float32(r["Jd"]) == np.float32(Jd)

@@ -12,7 +12,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import EXAMPLE_DIR, assert_bitwise
+from conftest import EXAMPLE_DIR, GOLDEN, assert_bitwise
 
 from oracle import REF_SO, Reference
 
@@ -203,3 +203,40 @@ def test_dense_qinv_duals_match_reference(orc, tag):
     assert hashlib.sha256(Qd.tobytes()).digest() == g[f"{tag}_Qd_sha256"].tobytes()
     assert_bitwise(Fd, g[f"{tag}_Fd"], "Fd")
     assert_bitwise(Md, g[f"{tag}_Md"], "Md")
+
+
+@needs_ref
+def test_reference_fixed_driver_matches_golden(golden_bundled):
+    """oracle/ref_fixed.c (bench.py's configs[0] fixed-1000 CPU baseline) runs
+    the reference's own functions: its Y after 999 updates is the golden
+    fixed-999 Y* (made by make_golden.py from the reference), bit for bit."""
+    from oracle import REF_FIXED_SO
+
+    if not REF_FIXED_SO.exists():
+        pytest.skip("oracle/_ref/libref_fixed.so not built")
+    ref = Reference()
+    P = {k: golden_bundled[k] for k in ("Qd", "Fd")}
+    P["N"] = int(golden_bundled["N"])
+    Y, total, loop = ref.fixed_solve(P, 1000)
+    assert np.array_equal(Y.view(np.uint32), golden_bundled["Y_fixed999"].astype(np.float32).view(np.uint32))
+    assert 0 < loop <= total
+
+
+@pytest.mark.parametrize("k", [9, 36])
+def test_block_problems_match_reference_golden(orc, golden_bundled, k):
+    """The restatement on the bundled example as k diagonal blocks (a large
+    problem that stops, every iterate feasible): the reference's h, Y*, U*,
+    Jp, Jd (tests/golden/blocks.npz, made by the reference)."""
+    from oracle import block_diag_problem
+
+    g = np.load(GOLDEN / "blocks.npz")
+    P = {kk: golden_bundled[kk] for kk in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+    P.update(N=int(golden_bundled["N"]), M=int(golden_bundled["M"]))
+    Q = block_diag_problem(P, k)
+    h, Y, U = orc.solve(Q, max_updates=5000)
+    assert h == int(g[f"h{k}"]) == 313
+    assert np.array_equal(Y.view(np.uint32), g[f"Y{k}"].view(np.uint32))
+    assert np.array_equal(U.view(np.uint32), g[f"U{k}"].view(np.uint32))
+    flag, _, Jp, Jd = orc.terminate(Y, Q["Qd"], Q["Fd"], Q["Md"], Q["Qp"], Q["Qp_inv"], Q["Fp"], Q["Mp"], Q["Gp"],
+                                    Q["Kp"], Q["N"], Q["M"])
+    assert flag == 1 and np.float32(Jp) == g[f"Jp{k}"] and np.float32(Jd) == g[f"Jd{k}"]
