@@ -135,6 +135,19 @@ typedef struct pqp_problem pqp_problem;
 int pqp_problem_create(const float *Qd, const float *Fd, const float *Md, const float *Qp, const float *Qp_inv,
                        const float *Fp, const float *Mp, const float *Gp, const float *Kp, int N, int M,
                        pqp_problem **out);
+/* The same on an explicit device (-1: the calling thread's current one) and
+ * stream (a hipStream_t of that device; NULL: the handle creates and owns
+ * one).  A handle is bound to its device and stream: every call on it runs
+ * there, whatever device the calling thread has current, and restores the
+ * caller's device before returning.  Calls on one handle are serialized by a
+ * lock of that handle; different handles (one host thread per GPU, or several
+ * per GPU) run concurrently -- the reference's solver keeps no globals
+ * (PQP_CPU.c:694) and neither does this one. */
+int pqp_problem_create_on(int device, void *stream, const float *Qd, const float *Fd, const float *Md,
+                          const float *Qp, const float *Qp_inv, const float *Fp, const float *Mp, const float *Gp,
+                          const float *Kp, int N, int M, pqp_problem **out);
+/* The device a handle is bound to. */
+int pqp_problem_device(const pqp_problem *p);
 int pqp_problem_solve(pqp_problem *p, int mode, long long num_iter, long long max_updates, float *Y, float *U,
                       long long *h_out, float *Jp_out, float *Jd_out);
 int pqp_problem_destroy(pqp_problem *p);

@@ -4,6 +4,7 @@
 // host: every drop-in function is computed on the GPU and fails loudly (status
 // code, or exit(EXIT_FAILURE) for the void drop-ins) when no gfx950 device or
 // kernel is available -- there is no CPU fallback.
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -20,8 +21,6 @@
 namespace pqp {
 
 namespace {
-
-std::mutex g_mu;  // drop-in calls share the library stream and are serialized
 
 inline int round4(int n) { return (n + 3) & ~3; }
 
@@ -89,14 +88,33 @@ int ensure_device() {
     return PQP_OK;
 }
 
+// The stream of the drop-ins and of handles made without one: one per host
+// thread and device, so calls from different threads never share a stream
+// (or a lock); the drop-ins keep no other state between calls.
 hipStream_t lib_stream() {
-    static hipStream_t streams[64] = {nullptr};
+    thread_local hipStream_t streams[64] = {nullptr};
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= 64) dev = 0;
     if (!streams[dev]) (void)hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
     return streams[dev];
 }
+
+// Make `dev` the calling thread's current device for a scope (a handle's calls
+// run on the device it was made on, whatever the caller has current), and
+// restore the caller's device after.
+struct DeviceGuard {
+    int prev = -1;
+    bool changed = false;
+    explicit DeviceGuard(int dev) {
+        if (dev >= 0 && hipGetDevice(&prev) == hipSuccess && prev != dev) changed = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (changed) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 
 int upload(DevBuf& d, const float* h, size_t n, hipStream_t s) {
     PQP_TRY(d.floats(n));
@@ -228,9 +246,16 @@ struct SolveOut {
 }  // namespace pqp
 
 // A dual problem resident in HBM, prepared once and solved any number of times
-// (include/pqp.h: pqp_problem_create / _solve / _destroy).
+// (include/pqp.h: pqp_problem_create / _solve / _destroy).  Bound to the
+// device it was made on and to its own stream; calls on one handle are
+// serialized by its own lock, calls on different handles run concurrently
+// (the reference's solver keeps no globals, PQP_CPU.c:694).
 struct pqp_problem {
     int N = 0, M = 0;
+    int dev = -1;                 // the device every call of this handle runs on
+    hipStream_t stream = nullptr; // the handle's stream (owned unless the caller passed one)
+    bool own_stream = false;
+    std::mutex mu;
     bool small = false;  // fits k_solve_small (everything staged in LDS)
     pqp::DevBuf Qd, Fd, Md, Qp, Qinv, Fp, Mp, Gp, Kp;  // row-major device copies
     pqp::DevBuf QdT, theta;                          // large path only
@@ -261,6 +286,7 @@ struct pqp_problem {
     float* hin = nullptr;                            // pinned staging of small problems' inputs
     size_t hin_floats = 0;
     ~pqp_problem() {
+        if (own_stream && stream) (void)hipStreamDestroy(stream);
         if (graph) (void)hipGraphExecDestroy(graph);
         if (chunk_graph) (void)hipGraphExecDestroy(chunk_graph);
         if (wgraph) (void)hipGraphExecDestroy(wgraph);
@@ -279,6 +305,7 @@ struct pqp_problem {
 // One row block of a large problem's stored split matrices (pqp_rowblock_*).
 struct pqp_rowblock {
     int N = 0, row0 = 0, rows = 0, lw = 64;
+    int dev = -1;  // the device it was made on (its calls run there)
     bool lean = false;  // SP holds Qd packets (k_lean_relay), fdpn the {Fdn, Fdp, Theta, 0} words
     pqp::DevBuf SP, fdpn;
     pqp::DevBuf err;    // sticky relay hand-off error word (pqp_rowblock_check)
@@ -533,11 +560,23 @@ int ensure_persist_split(pqp_problem& P, hipStream_t s) {
 enum SolvePath : int {
     kPathFixedPersist = 1, kPathFixedRelay = 2, kPathConvergePersist = 3, kPathConvergeWide = 4, kPathOneWorkgroup = 5
 };
-int g_last_path = 0;
-long long g_persist_fallbacks = 0;
+thread_local int g_last_path = 0;               // of the calling thread's last solve
+std::atomic<long long> g_persist_fallbacks{0};
 // problem_run_*_persist: a wait of the persistent launch expired (its
 // workgroups were not all resident); the caller falls back
 constexpr int kPersistStalled = 1;
+
+// A persistent launch needs every one of its workgroups resident at once (they
+// wait on each other).  Two of them from different handles on one device could
+// each get part of the CUs and wait for the rest until their deadline, so the
+// persistent launches of one device run one at a time; everything else of
+// different handles runs concurrently.
+std::mutex& persist_lock() {
+    static std::mutex mu[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return mu[dev >= 0 && dev < 64 ? dev : 0];
+}
 
 int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, hipStream_t s) {
     const int N = P.N;
@@ -545,6 +584,7 @@ int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, 
     auto* gran = static_cast<unsigned long long*>(P.gran.p);
     int* err = static_cast<int*>(P.perr.p);
     PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
+    std::lock_guard<std::mutex> one_at_a_time(persist_lock());
     for (long long done = 0; done < updates;) {
         const long long n = std::min(kPersistChunk, updates - done);
         // the launch reads its initial iterate from Yb while it writes P.Y
@@ -679,6 +719,7 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
     L.decided = reinterpret_cast<long long*>(words + 8);
     L.Y = P.Y.f();
     L.U = P.U.f();
+    std::lock_guard<std::mutex> one_at_a_time(persist_lock());
     for (long long u0 = 0;;) {
         L.u0 = u0;
         PQP_HIP(launch_converge_persist(L, s));
@@ -945,36 +986,54 @@ int pqp_version(void) { return 100; }
 // ---------------------------------------------------------------------------
 // 2a. status-returning host API
 // ---------------------------------------------------------------------------
-int pqp_problem_create(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
-                       const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M,
-                       pqp_problem** out) {
+int pqp_problem_create_on(int device, void* stream, const float* Qd, const float* Fd, const float* Md,
+                          const float* Qp, const float* Qp_inv, const float* Fp, const float* Mp, const float* Gp,
+                          const float* Kp, int N, int M, pqp_problem** out) {
     if (!out) return set_error(PQP_ERR_ARG, "pqp_problem_create: null handle pointer");
     *out = nullptr;
     PQP_TRY(check_dims(N, M));
     if (!Qd || !Fd || !Md || !Qp || !Qp_inv || !Fp || !Mp || !Gp || !Kp)
         return set_error(PQP_ERR_ARG, "pqp_problem_create: null input");
-    std::lock_guard<std::mutex> lk(g_mu);
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return set_error(PQP_ERR_NO_DEVICE, "libpqp: no HIP device visible");
+    if (device < 0 && hipGetDevice(&device) != hipSuccess)
+        return set_error(PQP_ERR_NO_DEVICE, "libpqp: cannot query the current device");
+    if (device >= n) return set_error(PQP_ERR_ARG, "pqp_problem_create_on: device %d of %d", device, n);
+    DeviceGuard on(device);
     PQP_TRY(ensure_device());
-    hipStream_t s = lib_stream();
-    pqp_problem* P = new pqp_problem();
+    std::unique_ptr<pqp_problem> P(new pqp_problem());
+    P->dev = device;
+    if (stream) {
+        P->stream = static_cast<hipStream_t>(stream);
+    } else {
+        PQP_HIP(hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking));
+        P->own_stream = true;
+    }
+    hipStream_t s = P->stream;
     int rc = problem_upload(*P, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s);
     if (rc == PQP_OK && hipStreamSynchronize(s) != hipSuccess) rc = set_error(PQP_ERR_HIP, "problem setup failed");
-    if (rc != PQP_OK) {
-        delete P;
-        return rc;
-    }
-    *out = P;
+    if (rc != PQP_OK) return rc;
+    *out = P.release();
     return PQP_OK;
 }
+
+int pqp_problem_create(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
+                       const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M,
+                       pqp_problem** out) {
+    return pqp_problem_create_on(-1, nullptr, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, out);
+}
+
+int pqp_problem_device(const pqp_problem* P) { return P ? P->dev : set_error(PQP_ERR_ARG, "pqp_problem_device: null handle"); }
 
 int pqp_problem_solve(pqp_problem* P, int mode, long long num_iter, long long max_updates, float* Y, float* U,
                       long long* h_out, float* Jp_out, float* Jd_out) {
     if (!P || !Y) return set_error(PQP_ERR_ARG, "pqp_problem_solve: null handle or Y");
     if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
         return set_error(PQP_ERR_ARG, "pqp_problem_solve: unknown mode %d", mode);
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> lk(P->mu);
+    DeviceGuard on(P->dev);
     PQP_TRY(ensure_device());
-    hipStream_t s = lib_stream();
+    hipStream_t s = P->stream;
     SolveOut o;
     PQP_TRY(problem_run(*P, mode == PQP_MODE_CONVERGE ? kModeConverge : kModeFixed, num_iter, max_updates, false, o,
                         s));
@@ -995,13 +1054,19 @@ int pqp_problem_solve(pqp_problem* P, int mode, long long num_iter, long long ma
 }
 
 int pqp_problem_destroy(pqp_problem* P) {
-    std::lock_guard<std::mutex> lk(g_mu);
+    if (!P) return PQP_OK;
+    {
+        std::lock_guard<std::mutex> lk(P->mu);  // a solve still running on another thread ends first
+        DeviceGuard on(P->dev);
+        if (P->stream) (void)hipStreamSynchronize(P->stream);
+    }
+    DeviceGuard on(P->dev);
     delete P;
     return PQP_OK;
 }
 
-static std::mutex g_oneshot_mu;        // guards g_oneshot (taken before g_mu)
-static pqp_problem* g_oneshot = nullptr;  // cached handle of pqp_solve_dual's tiny problems
+static std::mutex g_oneshot_mu;              // guards g_oneshot
+static pqp_problem* g_oneshot[64] = {nullptr};  // per device: cached handle of pqp_solve_dual's tiny problems
 
 int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const float* Qp, const float* Qp_inv,
                    const float* Fp, const float* Mp, const float* Gp, const float* Kp, int N, int M, int mode,
@@ -1015,18 +1080,21 @@ int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const floa
         // pattern, solveQuadraticDual per solve) reuses one cached handle: its
         // buffers are re-filled in place (no allocations), and these problems
         // build no derived per-problem data a new Qd could leave stale
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+            return set_error(PQP_ERR_NO_DEVICE, "libpqp: cannot query the current device");
         std::lock_guard<std::mutex> lk(g_oneshot_mu);
-        if (!g_oneshot) {
-            PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &g_oneshot));
+        pqp_problem*& h = g_oneshot[dev];
+        if (!h) {
+            PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &h));
         } else {
             if (!Qd || !Fd || !Md || !Qp || !Qp_inv || !Fp || !Mp || !Gp || !Kp)
                 return set_error(PQP_ERR_ARG, "pqp_solve_dual: null input");
-            std::lock_guard<std::mutex> lk2(g_mu);
+            std::lock_guard<std::mutex> lk2(h->mu);
             PQP_TRY(ensure_device());
-            hipStream_t s = lib_stream();
-            PQP_TRY(problem_upload(*g_oneshot, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, s));
+            PQP_TRY(problem_upload(*h, Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, h->stream));
         }
-        return pqp_problem_solve(g_oneshot, mode, num_iter, max_updates, Y, U, h_out, Jp_out, Jd_out);
+        return pqp_problem_solve(h, mode, num_iter, max_updates, Y, U, h_out, Jp_out, Jd_out);
     }
     pqp_problem* P = nullptr;
     PQP_TRY(pqp_problem_create(Qd, Fd, Md, Qp, Qp_inv, Fp, Mp, Gp, Kp, N, M, &P));
@@ -1040,7 +1108,6 @@ int pqp_solve_dual(const float* Qd, const float* Fd, const float* Md, const floa
 int pqp_update_host(const float* Qd, const float* theta_diag, const float* Fd, const float* Y, float* Y_next,
                     int N) {
     if (N <= 0 || !Qd || !theta_diag || !Fd || !Y || !Y_next) return set_error(PQP_ERR_ARG, "pqp_update_host");
-    std::lock_guard<std::mutex> lk(g_mu);
     PQP_TRY(ensure_device());
     hipStream_t s = lib_stream();
     const int ldq = round4(N);
@@ -1064,7 +1131,6 @@ int pqp_run_example(const char* dir, void* out_file) {
     const int m = kRefNInput * kRefPHorizon, nd = kRefNDis * kRefPHorizon, ns = kRefNState;
     PQP_TRY(read_example(dir, m, nd, ns, e));
     const int M = m, N = 4 * m;
-    std::lock_guard<std::mutex> lk(g_mu);
     PQP_TRY(ensure_device());
     hipStream_t s = lib_stream();
     DevBuf Qinv, Fp1, Fp2, Fp3, Mp1, Mp2, Mp3, Mp4, Mp5, Mp6, Gp, Kp, x, D;
@@ -1212,6 +1278,7 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
     PQP_TRY(ensure_device());
     hipStream_t s = static_cast<hipStream_t>(stream);
     std::unique_ptr<pqp_rowblock> b(new pqp_rowblock);
+    PQP_HIP(hipGetDevice(&b->dev));
     b->N = N;
     b->row0 = row0;
     b->rows = rows;
@@ -1248,6 +1315,7 @@ int pqp_rowblock_create(const float* d_Qd_rows, int ld, const float* d_Fd, int N
 int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void* stream) {
     if (!b || !d_Y || (b->rows > 0 && !d_Y_rows)) return set_error(PQP_ERR_ARG, "pqp_rowblock_update: null argument");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    DeviceGuard on(b->dev);
     int* err = static_cast<int*>(b->err.p);
     if (b->lean)
         PQP_HIP(launch_lean_update(b->SP.f(), b->fdpn.f(), b->N, b->rows, b->row0, b->lw, d_Y, d_Y_rows, s, nullptr, err));
@@ -1260,12 +1328,15 @@ int pqp_rowblock_update(pqp_rowblock* b, const float* d_Y, float* d_Y_rows, void
 int pqp_rowblock_check(pqp_rowblock* b, void* stream) {
     if (!b) return set_error(PQP_ERR_ARG, "pqp_rowblock_check: null block");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    DeviceGuard on(b->dev);
     int herr = 0;
     PQP_HIP(hipMemcpyAsync(&herr, b->err.p, sizeof herr, hipMemcpyDeviceToHost, s));
     return relay_error_check(b->err, &herr, s, "pqp_rowblock_update");
 }
 
 int pqp_rowblock_destroy(pqp_rowblock* b) {
+    if (!b) return PQP_OK;
+    DeviceGuard on(b->dev);
     delete b;
     return PQP_OK;
 }
@@ -1491,7 +1562,6 @@ void updateY2(float* Y_next, float* Y, float* Qdp_theta, float* Qdn_theta, float
     (void)Fd;
     auto run = [&]() -> int {
         if (N <= 0) return set_error(PQP_ERR_ARG, "updateY2: N must be positive");
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         const int ldq = round4(N);
@@ -1519,7 +1589,6 @@ int terminate(float* Y, float* Qd, float* Fd, float* Md, float* U, float* Qp, fl
     int result = 0;
     auto run = [&]() -> int {
         PQP_TRY(check_dims(N, M));
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         pqp_problem P;
@@ -1540,7 +1609,6 @@ void convertToDual(float* Qd, float* Fd, float* Md, float* Qp_inv, float* Gp, fl
                    int M) {
     auto run = [&]() -> int {
         PQP_TRY(check_dims(N, M));
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf qinv, gp, kp, fp, mp, qd, fd, md;
@@ -1565,7 +1633,6 @@ void convertToDual(float* Qd, float* Fd, float* Md, float* Qp_inv, float* Gp, fl
 void computeUfromY(float* U, float* Y, float* Fp, float* Gp, float* Qp_inv, int N, int M) {
     auto run = [&]() -> int {
         PQP_TRY(check_dims(N, M));
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf u, y, fp, gp, qinv;
@@ -1586,7 +1653,6 @@ float computeCost(float* Z, float* Q, float* F, float* Mc, int N) {
     float J = 0.0f;
     auto run = [&]() -> int {
         if (N <= 0) return set_error(PQP_ERR_ARG, "computeCost: N must be positive");
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf z, q, f, m, j;
@@ -1608,7 +1674,6 @@ int checkFeas(float* U, float* Gp, float* Kp, int N, int M) {
     int flag = 0;
     auto run = [&]() -> int {
         PQP_TRY(check_dims(N, M));
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf u, gp, kp;
@@ -1624,7 +1689,6 @@ int checkFeas(float* U, float* Gp, float* Kp, int N, int M) {
 void computeTheta(float* theta, float* Qd, int N) {
     auto run = [&]() -> int {
         if (N <= 0) return set_error(PQP_ERR_ARG, "computeTheta: N must be positive");
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf th, qd;
@@ -1641,7 +1705,6 @@ void computeTheta(float* theta, float* Qd, int N) {
 void matrixMultiply(float* output, float* mat1, int transpose1, float* mat2, int transpose2, int a, int b, int c) {
     auto run = [&]() -> int {
         if (a <= 0 || b < 0 || c <= 0) return set_error(PQP_ERR_ARG, "matrixMultiply: bad sizes");
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf A, B, O;
@@ -1659,7 +1722,6 @@ void matrixMultiply(float* output, float* mat1, int transpose1, float* mat2, int
 void Gauss_Jordan(float* A, float* res, int N) {
     auto run = [&]() -> int {
         if (N <= 0) return set_error(PQP_ERR_ARG, "Gauss_Jordan: N must be positive");
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf a, r;
@@ -1676,7 +1738,6 @@ void Gauss_Jordan(float* A, float* res, int N) {
 void computeFp(float* Fp, float* Fp1, float* Fp2, float* Fp3, float* D, float* x) {
     const int m = kRefNInput * kRefPHorizon, nd = kRefNDis * kRefPHorizon, ns = kRefNState;
     auto run = [&]() -> int {
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf fp, f1, f2, f3, d, xx;
@@ -1698,7 +1759,6 @@ void computeMp(float* Mp, float* Mp1, float* Mp2, float* Mp3, float* Mp4, float*
                float* x) {
     const int nd = kRefNDis * kRefPHorizon, ns = kRefNState;
     auto run = [&]() -> int {
-        std::lock_guard<std::mutex> lk(g_mu);
         PQP_TRY(ensure_device());
         hipStream_t s = lib_stream();
         DevBuf mp, m1, m2, m3, m4, m5, m6, d, xx;

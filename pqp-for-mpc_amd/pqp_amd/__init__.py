@@ -60,6 +60,8 @@ SIGNATURES = {
     "pqp_solve_dual": (C.c_int, [_fp] * 9 + [C.c_int] * 3 + [C.c_longlong] * 2 + [_fp, _fp,
                                                                                    C.POINTER(C.c_longlong), _fp, _fp]),
     "pqp_problem_create": (C.c_int, [_fp] * 9 + [C.c_int] * 2 + [C.POINTER(C.c_void_p)]),
+    "pqp_problem_create_on": (C.c_int, [C.c_int, _vp] + [_fp] * 9 + [C.c_int] * 2 + [C.POINTER(C.c_void_p)]),
+    "pqp_problem_device": (C.c_int, [_vp]),
     "pqp_problem_solve": (C.c_int, [_vp, C.c_int, C.c_longlong, C.c_longlong, _fp, _fp, C.POINTER(C.c_longlong), _fp,
                                     _fp]),
     "pqp_problem_destroy": (C.c_int, [_vp]),
@@ -248,16 +250,27 @@ def solve_dual(P: dict, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_upd
 
 class Problem:
     """A dual problem resident in HBM (pqp_problem_*): upload/prepare once,
-    solve repeatedly.  Keys of P: Qd Fd Md Qp Qp_inv Fp Mp Gp Kp N M."""
+    solve repeatedly.  Keys of P: Qd Fd Md Qp Qp_inv Fp Mp Gp Kp N M.
+    `device` (int) and `stream` (a hipStream_t of that device, as int or
+    torch stream) bind the handle (pqp_problem_create_on); by default the
+    current device and a stream of the handle's own.  Solves release the GIL
+    (ctypes), so handles may be solved from several threads at once."""
 
     KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 
-    def __init__(self, P: dict):
+    def __init__(self, P: dict, device: int | None = None, stream=None):
         self.N, self.M = int(P["N"]), int(P["M"])
         a = [_f32(P[k]) for k in self.KEYS]
         h = C.c_void_p()
-        _check(lib().pqp_problem_create(*[_buf(x) for x in a], self.N, self.M, C.byref(h)))
+        if stream is not None and not isinstance(stream, int):
+            stream = stream.cuda_stream
+        _check(lib().pqp_problem_create_on(-1 if device is None else int(device), stream, *[_buf(x) for x in a],
+                                           self.N, self.M, C.byref(h)))
         self._h = h
+
+    @property
+    def device(self) -> int:
+        return int(lib().pqp_problem_device(self._h))
 
     def solve(self, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0) -> dict:
         Y, U = np.zeros(self.N, np.float32), np.zeros(self.M, np.float32)

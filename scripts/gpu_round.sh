@@ -12,6 +12,9 @@ tail -1 gpurun_out/smoke_$TAG.log
 if [ -z "$SKIP_REHEARSE" ]; then
 PQP_BENCH_REHEARSE=1 timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --rowshard-updates 20 > gpurun_out/bench_rehearse2_$TAG.json 2> gpurun_out/bench_rehearse2_$TAG.err || { tail -30 gpurun_out/bench_rehearse2_$TAG.err; exit 1; }
 cat gpurun_out/bench_rehearse2_$TAG.json
+# the same with rank 1's row block failing inside the leg: the line must survive (rc 0)
+PQP_BENCH_REHEARSE=1 PQP_BENCH_FAULT=rowshard:1 timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --rowshard-updates 20 > gpurun_out/bench_rehearse2_fault_$TAG.json 2> gpurun_out/bench_rehearse2_fault_$TAG.err || { tail -30 gpurun_out/bench_rehearse2_fault_$TAG.err; exit 1; }
+cat gpurun_out/bench_rehearse2_fault_$TAG.json
 fi
 timeout -k 10 400 python -u bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
