@@ -252,6 +252,36 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
                     int mode, long long num_iter, long long max_updates, float *d_Y, float *d_U, long long *d_h,
                     int *d_status, void *stream);
 
+/* Which batched solver pqp_batch_solve uses for (N, M): 0 one wave or one small
+ * workgroup per problem (N, M <= 32), 1 the problem staged in LDS, 2 one
+ * workgroup per problem from HBM (k_solve_single; uses pqp_batch_prepare's
+ * data), or PQP_ERR_ARG when (N, M) exceeds every solver's LDS budget. */
+int pqp_batch_solve_path(int N, int M);
+
+/* pqp_batch_solve in two steps, so that what depends only on the problems is
+ * computed once per batch instead of once per call (path 2 above):
+ *   pqp_batch_prepare: per-problem bit-symmetry flags of Qd into d_sym [B]
+ *     (int), Theta (computeTheta, PQP_CPU.c:503-519) into d_theta [B][N], and
+ *     *all_sym_out = 1 when every Qd is bit-symmetric and N % 4 == 0 (Qd is
+ *     then its own column-major copy).  Otherwise the column-major copy goes to
+ *     d_QdT [B][N][round4(N)], which must then be given: with d_QdT NULL the
+ *     call returns PQP_ERR_ARG with *all_sym_out = 0 (d_sym filled) -- call
+ *     again with it.  Optional d_GpT [B][M][N] and d_QinvT [B][M][M] (with
+ *     d_Gp / d_Qp_inv) receive transposed copies: terminate()'s row walks of
+ *     Gp and Qp_inv (PQP_CPU.c:357, :635) then read coalesced.
+ *   pqp_batch_solve_prepared: pqp_batch_solve on those (d_QdT NULL when
+ *     *all_sym_out was 1; d_GpT / d_QinvT NULL when not prepared).  The
+ *     prepared data stay valid until Qd (or Gp, Qp_inv) change.
+ * Paths 0 and 1 need none of it (NULLs are fine there). */
+int pqp_batch_prepare(int B, int N, int M, const float *d_Qd, const float *d_Gp, const float *d_Qp_inv, float *d_QdT,
+                      float *d_theta, int *d_sym, float *d_GpT, float *d_QinvT, int *all_sym_out, void *stream);
+int pqp_batch_solve_prepared(int B, int N, int M, const float *d_Qd, const float *d_QdT, const float *d_theta,
+                             const int *d_sym, const float *d_GpT, const float *d_QinvT, const float *d_Fd,
+                             const float *d_Md, const float *d_Qp, const float *d_Qp_inv, const float *d_Fp,
+                             const float *d_Mp, const float *d_Gp, const float *d_Kp, int mode, long long num_iter,
+                             long long max_updates, float *d_Y, float *d_U, long long *d_h, int *d_status,
+                             void *stream);
+
 /* ----------------------------------------------------------------------
  * 2d. Row blocks of one large problem (a single problem
  * row-sharded across GPUs).  A pqp_rowblock holds rows [row0, row0+rows) of

@@ -318,8 +318,9 @@ constexpr size_t kLdsBudget = 150 * 1024;
 bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
 bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
 int g_wide_min_n = 384;       // converge mode: smallest N solved over many workgroups (problem_run_wide)
-int g_batch_opts = 0;         // tuning (pqp_tune_batch_converge): bit 0 fuse Y'Qd, bit 1 transposed Gp / Qp_inv
-                              // (bit 2, 4-byte loads only, is g_single_scalar)
+int g_batch_opts = 0;         // tuning (pqp_tune_batch_converge): bit 0 no fused Y'Qd pass, bit 1 pqp_batch_solve
+                              // makes transposed Gp / Qp_inv per call (bit 2, 4-byte loads only, is g_single_scalar)
+inline bool batch_unfused() { return (g_batch_opts & 1) != 0; }
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -1434,10 +1435,64 @@ int pqp_batch_compute_mp(int B, int nd, int ns, const float* d_Mp1, const float*
     return PQP_OK;
 }
 
-int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, const float* d_Md, const float* d_Qp,
-                    const float* d_Qp_inv, const float* d_Fp, const float* d_Mp, const float* d_Gp, const float* d_Kp,
-                    int mode, long long num_iter, long long max_updates, float* d_Y, float* d_U, long long* d_h,
-                    int* d_status, void* stream) {
+// Which batched solver a problem size takes: 0 one wave / tiny workgroup
+// (N, M <= 32), 1 everything staged in LDS, 2 one workgroup from global
+// memory (k_solve_single; needs the prepared data of pqp_batch_prepare), -1
+// too large for any.
+static int batch_path(int N, int M) {
+    if (N <= 32 && M <= 32 && !g_force_small) return 0;
+    if (solve_small_lds_bytes(N, M) <= kLdsBudget) return 1;
+    if (solve_single_lds_bytes(round4(N), round4(M), false) <= kLdsBudget) return 2;
+    return -1;
+}
+
+int pqp_batch_solve_path(int N, int M) {
+    if (N <= 0 || M <= 0) return set_error(PQP_ERR_ARG, "pqp_batch_solve_path: N and M must be positive");
+    const int p = batch_path(N, M);
+    return p < 0 ? set_error(PQP_ERR_ARG, "N=%d, M=%d exceeds the batched solvers' LDS budget", N, M) : p;
+}
+
+int pqp_batch_prepare(int B, int N, int M, const float* d_Qd, const float* d_Gp, const float* d_Qp_inv, float* d_QdT,
+                      float* d_theta, int* d_sym, float* d_GpT, float* d_QinvT, int* all_sym_out, void* stream) {
+    if (all_sym_out) *all_sym_out = 0;
+    if (B <= 0 || N <= 0 || M <= 0 || !d_Qd || !d_theta || !d_sym)
+        return set_error(PQP_ERR_ARG, "pqp_batch_prepare: bad arguments");
+    if ((d_GpT && !d_Gp) || (d_QinvT && !d_Qp_inv))
+        return set_error(PQP_ERR_ARG, "pqp_batch_prepare: a transposed copy needs its source");
+    PQP_TRY(ensure_device());
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int ldq = round4(N);
+    // Qd bit-symmetric in every problem (convertToDual's (Gp Qp_inv) Gp' is,
+    // for a diagonal Qp_inv) and N % 4 == 0: the row-major Qd is its own
+    // column-major copy, no packing pass.  The per-problem flags also gate the
+    // fused Y'Qd pass of converge mode.
+    PQP_HIP(launch_check_symmetric(B, d_Qd, N, d_sym, s));
+    std::vector<int> hs((size_t)B);
+    PQP_HIP(hipMemcpyAsync(hs.data(), d_sym, sizeof(int) * (size_t)B, hipMemcpyDeviceToHost, s));
+    PQP_HIP(hipStreamSynchronize(s));
+    bool all_sym = ldq == N;
+    for (int v : hs) all_sym = all_sym && v != 0;
+    if (all_sym_out) *all_sym_out = all_sym ? 1 : 0;
+    const float* qdt = d_Qd;
+    if (!all_sym) {
+        if (!d_QdT)
+            return set_error(PQP_ERR_ARG, "pqp_batch_prepare: some Qd is not bit-symmetric (or N %% 4 != 0): pass "
+                                          "d_QdT ([B][N][round4(N)] floats) for its column-major copy");
+        PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, d_QdT, ldq, (long long)N * ldq, s));
+        qdt = d_QdT;
+    }
+    PQP_HIP(launch_theta(B, qdt, ldq, (long long)N * ldq, N, d_theta, N, s));  // computeTheta :503-519
+    if (d_GpT) PQP_HIP(launch_transpose_b(B, d_Gp, N, M, d_GpT, s));
+    if (d_QinvT) PQP_HIP(launch_transpose_b(B, d_Qp_inv, M, M, d_QinvT, s));
+    return PQP_OK;
+}
+
+int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float* d_QdT, const float* d_theta,
+                             const int* d_sym, const float* d_GpT, const float* d_QinvT, const float* d_Fd,
+                             const float* d_Md, const float* d_Qp, const float* d_Qp_inv, const float* d_Fp,
+                             const float* d_Mp, const float* d_Gp, const float* d_Kp, int mode, long long num_iter,
+                             long long max_updates, float* d_Y, float* d_U, long long* d_h, int* d_status,
+                             void* stream) {
     if (B <= 0 || N <= 0 || M <= 0 || !d_Qd || !d_Fd || !d_Y)
         return set_error(PQP_ERR_ARG, "pqp_batch_solve: bad arguments");
     if (mode != PQP_MODE_CONVERGE && mode != PQP_MODE_FIXED)
@@ -1447,71 +1502,32 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
     PQP_TRY(ensure_device());
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int ldq = round4(N), ldm = round4(M);
-    int path = 2;
-    if (N <= 32 && M <= 32 && !g_force_small)
-        path = 0;
-    else if (solve_small_lds_bytes(N, M) <= kLdsBudget)
-        path = 1;
-    else if (solve_single_lds_bytes(ldq, ldm, false) > kLdsBudget)
-        return set_error(PQP_ERR_ARG, "pqp_batch_solve: N=%d, M=%d exceeds the LDS budget", N, M);
+    const int path = batch_path(N, M);
+    if (path < 0) return set_error(PQP_ERR_ARG, "pqp_batch_solve: N=%d, M=%d exceeds the LDS budget", N, M);
+    if (path == 2 && (!d_theta || !d_sym || (!d_QdT && ldq != N)))
+        return set_error(PQP_ERR_ARG, "pqp_batch_solve_prepared: N=%d, M=%d needs pqp_batch_prepare's theta, "
+                                      "symmetry flags and (unless every Qd is bit-symmetric) d_QdT", N, M);
     // the fused Y'Qd pass needs one more ldq-long LDS vector: only where it fits
-    const bool fuse = path == 2 && (g_batch_opts & 1) && ldq == N && solve_single_lds_bytes(ldq, ldm, true) <= kLdsBudget;
-    DevBuf QdT, theta, state, pending, Udummy, sym, GpT, QinvT;
-    const float* qdt = nullptr;
-    if (path == 2) {
-        // Qd bit-symmetric in every problem (convertToDual's (Gp Qp_inv) Gp'
-        // is, for a diagonal Qp_inv) and N % 4 == 0: the row-major Qd is its
-        // own column-major copy, no packing pass.  Optionally (tuning bit 0)
-        // converge mode then fuses terminate()'s Y'Qd into the update's pass.
-        bool all_sym = false;
-        if (ldq == N) {
-            PQP_TRY(sym.alloc(sizeof(int) * (size_t)B));
-            PQP_HIP(launch_check_symmetric(B, d_Qd, N, static_cast<int*>(sym.p), s));
-            std::vector<int> hs((size_t)B);
-            PQP_HIP(hipMemcpyAsync(hs.data(), sym.p, sizeof(int) * (size_t)B, hipMemcpyDeviceToHost, s));
-            PQP_HIP(hipStreamSynchronize(s));
-            all_sym = true;
-            for (int v : hs) all_sym = all_sym && v != 0;
-        }
-        if (all_sym && ldq == N) {
-            qdt = d_Qd;
-        } else {
-            PQP_TRY(QdT.floats((size_t)B * N * ldq));
-            PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, QdT.f(), ldq, (long long)N * ldq, s));
-            qdt = QdT.f();
-        }
-        PQP_TRY(theta.floats((size_t)B * N));
-        PQP_HIP(launch_theta(B, qdt, ldq, (long long)N * ldq, N, theta.f(), N, s));
-        if (mode == PQP_MODE_CONVERGE && (g_batch_opts & 2)) {  // coalesced row access of Gp, Qp_inv
-            PQP_TRY(GpT.floats((size_t)B * N * M));
-            PQP_TRY(QinvT.floats((size_t)B * M * M));
-            PQP_HIP(launch_transpose_b(B, d_Gp, N, M, GpT.f(), s));
-            PQP_HIP(launch_transpose_b(B, d_Qp_inv, M, M, QinvT.f(), s));
-        }
-    }
+    const bool fuse = path == 2 && !batch_unfused() && ldq == N && solve_single_lds_bytes(ldq, ldm, true) <= kLdsBudget;
+    DevBuf state, pending, Udummy;
     if (!d_U) {
         PQP_TRY(Udummy.floats((size_t)B * M));
         d_U = Udummy.f();
     }
     PQP_TRY(state.alloc(sizeof(SolveState) * (size_t)B));
     PQP_TRY(pending.alloc(sizeof(int)));
-    std::vector<SolveState> init((size_t)B);
-    for (auto& st : init) {
-        st = SolveState{};
-        st.h = 1;
-    }
-    PQP_HIP(hipMemcpyAsync(state.p, init.data(), sizeof(SolveState) * (size_t)B, hipMemcpyHostToDevice, s));
+    PQP_HIP(launch_state_init(B, static_cast<SolveState*>(state.p), s));
     SolveArgs a{};
-    a.QdT = qdt;
+    a.QdT = path == 2 ? (d_QdT ? d_QdT : d_Qd) : nullptr;
     a.Qd = d_Qd;
-    a.theta = theta.f();
+    a.theta = path == 2 ? d_theta : nullptr;
     a.Fd = d_Fd;
     a.Md = d_Md;
     a.Qp = d_Qp;
     a.Qinv = d_Qp_inv;
-    a.sym = fuse ? static_cast<const int*>(sym.p) : nullptr;
-    a.GpT = GpT.f();
-    a.QinvT = QinvT.f();
+    a.sym = fuse ? d_sym : nullptr;
+    a.GpT = path == 2 && mode == PQP_MODE_CONVERGE ? d_GpT : nullptr;
+    a.QinvT = path == 2 && mode == PQP_MODE_CONVERGE ? d_QinvT : nullptr;
     a.Fp = d_Fp;
     a.Mp = d_Mp;
     a.Gp = d_Gp;
@@ -1541,6 +1557,39 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
     PQP_HIP(launch_extract_state(B, st, d_h, d_status, s));
     PQP_HIP(hipStreamSynchronize(s));
     return PQP_OK;
+}
+
+int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, const float* d_Md, const float* d_Qp,
+                    const float* d_Qp_inv, const float* d_Fp, const float* d_Mp, const float* d_Gp, const float* d_Kp,
+                    int mode, long long num_iter, long long max_updates, float* d_Y, float* d_U, long long* d_h,
+                    int* d_status, void* stream) {
+    if (B <= 0 || N <= 0 || M <= 0 || !d_Qd || !d_Fd || !d_Y)
+        return set_error(PQP_ERR_ARG, "pqp_batch_solve: bad arguments");
+    const int path = batch_path(N, M);
+    if (path < 0) return set_error(PQP_ERR_ARG, "pqp_batch_solve: N=%d, M=%d exceeds the LDS budget", N, M);
+    DevBuf QdT, theta, sym, GpT, QinvT;
+    if (path == 2) {  // the per-problem setup, for this call only (pqp_batch_prepare keeps it across calls)
+        PQP_TRY(ensure_device());
+        PQP_TRY(theta.floats((size_t)B * N));
+        PQP_TRY(sym.alloc(sizeof(int) * (size_t)B));
+        if ((g_batch_opts & 2) && mode == PQP_MODE_CONVERGE && d_Gp && d_Qp_inv) {
+            PQP_TRY(GpT.floats((size_t)B * N * M));
+            PQP_TRY(QinvT.floats((size_t)B * M * M));
+        }
+        int all_sym = 0;
+        int* ps = static_cast<int*>(sym.p);
+        const int rc = pqp_batch_prepare(B, N, M, d_Qd, d_Gp, d_Qp_inv, nullptr, theta.f(), ps, GpT.f(), QinvT.f(),
+                                         &all_sym, stream);
+        if (rc != PQP_OK && (all_sym || !sym.p)) return rc;
+        if (rc != PQP_OK) {  // some Qd not bit-symmetric: the column-major copy
+            PQP_TRY(QdT.floats((size_t)B * N * round4(N)));
+            PQP_TRY(pqp_batch_prepare(B, N, M, d_Qd, d_Gp, d_Qp_inv, QdT.f(), theta.f(), ps, GpT.f(), QinvT.f(),
+                                      &all_sym, stream));
+        }
+    }
+    return pqp_batch_solve_prepared(B, N, M, d_Qd, QdT.f(), theta.f(), static_cast<const int*>(sym.p), GpT.f(),
+                                    QinvT.f(), d_Fd, d_Md, d_Qp, d_Qp_inv, d_Fp, d_Mp, d_Gp, d_Kp, mode, num_iter,
+                                    max_updates, d_Y, d_U, d_h, d_status, stream);
 }
 
 // ---------------------------------------------------------------------------

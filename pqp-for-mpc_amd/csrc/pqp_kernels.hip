@@ -1533,19 +1533,42 @@ __global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* _
             __syncthreads();
             // row access of Qp_inv / Gp through their transposes when given (lane
             // i walks column i of QinvT / GpT: coalesced), else row by row
-            for (int i = tid; i < M; i += NT)
-                Us[i] = -(A.QinvT ? seq_dot<kSU>(A.QinvT + i, M, tM, M)
-                          : VEC   ? row_dot4<4>(A.Qinv + (size_t)i * M, tM, M)
-                                  : seq_dot<kSU>(A.Qinv + (size_t)i * M, 1, tM, M));
+            // (VEC with the transposes: four adjacent rows per lane, 16-byte
+            // coalesced loads of the transposed copy, each row's sum in j order)
+            if (VEC && A.QinvT) {
+                for (int i0 = 4 * tid; i0 < M; i0 += 4 * NT) {
+                    float t[4];
+                    col_dotv<4, kSU4>(A.QinvT + i0, M, tM, M, t);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) Us[i0 + c] = -t[c];
+                }
+            } else {
+                for (int i = tid; i < M; i += NT)
+                    Us[i] = -(A.QinvT ? seq_dot<kSU>(A.QinvT + i, M, tM, M)
+                              : VEC   ? row_dot4<4>(A.Qinv + (size_t)i * M, tM, M)
+                                      : seq_dot<kSU>(A.Qinv + (size_t)i * M, 1, tM, M));
+            }
             __syncthreads();
             // checkFeas :632-641
             int bad = 0;
-            for (int i = tid; i < N; i += NT) {
-                const float s = A.GpT ? seq_dot<kSU>(A.GpT + i, N, Us, M)
-                                : VEC   ? row_dot4<4>(A.Gp + (size_t)i * M, Us, M)
-                                        : seq_dot<kSU>(A.Gp + (size_t)i * M, 1, Us, M);
-                const float kp = A.Kp[i];
-                if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+            if (VEC && A.GpT) {
+                for (int i0 = 4 * tid; i0 < N; i0 += 4 * NT) {
+                    float t[4];
+                    col_dotv<4, kSU4>(A.GpT + i0, N, Us, M, t);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float kp = A.Kp[i0 + c];
+                        if (t[c] > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                    }
+                }
+            } else {
+                for (int i = tid; i < N; i += NT) {
+                    const float s = A.GpT ? seq_dot<kSU>(A.GpT + i, N, Us, M)
+                                    : VEC   ? row_dot4<4>(A.Gp + (size_t)i * M, Us, M)
+                                            : seq_dot<kSU>(A.Gp + (size_t)i * M, 1, Us, M);
+                    const float kp = A.Kp[i];
+                    if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                }
             }
             const int infeasible = __syncthreads_or(bad);
             was_feasible = !infeasible;
@@ -2774,7 +2797,8 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
     // wide loads need every row and column start 16-byte aligned: N, M
     // multiples of 4 and 16-byte-aligned arrays (null ones are not read)
     const bool vec = !g_single_scalar && a.N % 4 == 0 && a.M % 4 == 0 && aligned16(a.QdT) && aligned16(a.Qd) &&
-                     aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
+                     aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && aligned16(a.GpT) &&
+                     aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
     if (a.N <= 64) {
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
@@ -2906,6 +2930,18 @@ __global__ void k_extract_state(int B, const SolveState* __restrict__ st, long l
     if (b >= B) return;
     if (h) h[b] = st[b].h;
     if (status) status[b] = st[b].status;
+}
+// every problem at the reference's start: h = 1, nothing decided (SolveState{})
+__global__ void k_init_state(int B, SolveState* __restrict__ st) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    SolveState z{};
+    z.h = 1;
+    st[b] = z;
+}
+hipError_t launch_state_init(int B, SolveState* st, hipStream_t s) {
+    hipLaunchKernelGGL(k_init_state, dim3(cdiv(B, 256)), dim3(256), 0, s, B, st);
+    return hipGetLastError();
 }
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s) {
     hipLaunchKernelGGL(k_extract_state, dim3(cdiv(B, 256)), dim3(256), 0, s, B, st, h, status);

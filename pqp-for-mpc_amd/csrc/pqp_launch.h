@@ -119,6 +119,7 @@ extern int g_wave_pipe_max_b; // tuning: largest batch whose k_solve_wave launch
 extern int g_wave_min_b;     // tuning: smallest batch whose converge-mode tiny solves run one wave per problem
 // batched forms: grid = B problems (states st[0..B-1])
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
+hipError_t launch_state_init(int B, SolveState* st, hipStream_t s);
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);
 extern int g_matmul_tiled_off;  // tuning: force k_matmul_seq for every product
 hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const float* Bm, int tB, int a, int b,

@@ -83,6 +83,10 @@ SIGNATURES = {
     "pqp_batch_compute_mp": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [_vp]),
     "pqp_batch_solve": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [C.c_int, C.c_longlong, C.c_longlong] + [_vp] * 4
                         + [_vp]),
+    "pqp_batch_solve_path": (C.c_int, [C.c_int, C.c_int]),
+    "pqp_batch_prepare": (C.c_int, [C.c_int] * 3 + [_vp] * 8 + [C.POINTER(C.c_int), _vp]),
+    "pqp_batch_solve_prepared": (C.c_int, [C.c_int] * 3 + [_vp] * 15 + [C.c_int, C.c_longlong, C.c_longlong]
+                                 + [_vp] * 4 + [_vp]),
     "pqp_rowblock_create": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(C.c_void_p)]),
     "pqp_rowblock_update": (C.c_int, [_vp, _vp, _vp, _vp]),
     "pqp_rowblock_check": (C.c_int, [_vp, _vp]),
@@ -497,11 +501,13 @@ class ProblemBatch:
     PRIMAL = ("Qp_inv", "Gp", "Kp", "Fp", "Mp")
     DUAL = ("Qd", "Fd", "Md")
 
-    def __init__(self, B: int, N: int, M: int, device=None):
+    def __init__(self, B: int, N: int, M: int, device=None, transposes: bool = True):
         import torch
 
         self.torch = torch
         self.B, self.N, self.M = int(B), int(N), int(M)
+        self.transposes = bool(transposes)  # prepare() keeps Gp', Qp_inv' for coalesced row walks (path 2)
+        self._prep = None  # pqp_batch_prepare's per-problem data, until Qd / Gp / Qp_inv change
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         f = dict(dtype=torch.float32, device=self.device)
         B, N, M = self.B, self.N, self.M
@@ -531,11 +537,12 @@ class ProblemBatch:
         return pb
 
     @classmethod
-    def synthetic(cls, seed: int, inst0: int, B: int, N: int, M: int | None = None, device=None) -> "ProblemBatch":
+    def synthetic(cls, seed: int, inst0: int, B: int, N: int, M: int | None = None, device=None,
+                  transposes: bool = True) -> "ProblemBatch":
         """Synthetic problems inst0..inst0+B-1 of `seed` (the primal behind
         Batch.generate), with Qp and the duals built on the device."""
         M = int(M) if M else max(1, int(N) // 2)
-        pb = cls(B, N, M, device)
+        pb = cls(B, N, M, device, transposes=transposes)
         _check(lib().pqp_batch_synth_primal(seed, inst0, pb.B, pb.N, pb.M, *[pb._p(getattr(pb, k)) for k in
                                                                             cls.PRIMAL], pb._s()))
         return pb.gauss_jordan().convert_to_dual()
@@ -551,6 +558,45 @@ class ProblemBatch:
         t = getattr(self, name)
         t.copy_(self.torch.as_tensor(np.asarray(values, np.float32) if not self.torch.is_tensor(values) else values,
                                      device=self.device).reshape(t.shape))
+        if name in ("Qd", "Gp", "Qp_inv"):
+            self.invalidate()
+        return self
+
+    def invalidate(self):
+        """Drop the prepared per-problem data (call after writing Qd, Gp or
+        Qp_inv in place; set() and convert_to_dual() do it themselves)."""
+        self._prep = None
+        return self
+
+    def prepare(self):
+        """pqp_batch_prepare: what the solver derives from the problems alone
+        (symmetry flags, Theta, column-major Qd if needed, Gp' and Qp_inv'),
+        computed once and kept for every later solve()."""
+        torch = self.torch
+        path = lib().pqp_batch_solve_path(self.N, self.M)
+        if path < 0:
+            _check(path)
+        prep = {"path": path}
+        if path == 2:
+            B, N, M = self.B, self.N, self.M
+            f = dict(dtype=torch.float32, device=self.device)
+            prep["theta"] = torch.empty(B, N, **f)
+            prep["sym"] = torch.empty(B, dtype=torch.int32, device=self.device)
+            prep["QdT"] = None
+            prep["GpT"] = torch.empty(B, M * N, **f) if self.transposes else None
+            prep["QinvT"] = torch.empty(B, M * M, **f) if self.transposes else None
+            p = lambda t: self._p(t) if t is not None else None  # noqa: E731
+            all_sym = C.c_int(0)
+            args = lambda qdt: (B, N, M, self._p(self.Qd), self._p(self.Gp), self._p(self.Qp_inv), qdt,  # noqa: E731
+                                self._p(prep["theta"]), self._p(prep["sym"]), p(prep["GpT"]), p(prep["QinvT"]),
+                                C.byref(all_sym), self._s())
+            rc = lib().pqp_batch_prepare(*args(None))
+            if rc != PQP_OK and not all_sym.value and rc == PQP_ERR_ARG and "d_QdT" in last_error():
+                prep["QdT"] = torch.empty(B, N * round_up(N, 4), **f)
+                rc = lib().pqp_batch_prepare(*args(self._p(prep["QdT"])))
+            _check(rc)
+            prep["all_sym"] = bool(all_sym.value)
+        self._prep = prep
         return self
 
     def gauss_jordan(self):
@@ -562,15 +608,29 @@ class ProblemBatch:
         """Qd, Fd, Md from the primal data (convertToDual, PQP_CPU.c:489)."""
         _check(lib().pqp_batch_convert_to_dual(self.B, self.N, self.M, *[self._p(getattr(self, k)) for k in
                                                                          self.PRIMAL + self.DUAL], self._s()))
-        return self
+        return self.invalidate()
 
-    def solve(self, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0):
-        """solveQuadraticDual for every problem; fills Y, U, h, status."""
-        _check(lib().pqp_batch_solve(self.B, self.N, self.M, *[self._p(getattr(self, k)) for k in
-                                                              ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp",
-                                                               "Kp")],
-                                     mode, num_iter, max_updates, self._p(self.Y), self._p(self.U), self._p(self.h),
-                                     self._p(self.status), self._s()))
+    def solve(self, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0, prepared: bool = True):
+        """solveQuadraticDual for every problem; fills Y, U, h, status.  The
+        per-problem setup is prepared on the first call and reused
+        (prepared=False: pqp_batch_solve, which redoes it every call)."""
+        if not prepared:
+            _check(lib().pqp_batch_solve(self.B, self.N, self.M, *[self._p(getattr(self, k)) for k in
+                                                                  ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp",
+                                                                   "Gp", "Kp")],
+                                         mode, num_iter, max_updates, self._p(self.Y), self._p(self.U),
+                                         self._p(self.h), self._p(self.status), self._s()))
+            return self
+        if self._prep is None:
+            self.prepare()
+        P = self._prep
+        p = lambda k: self._p(P[k]) if P.get(k) is not None else None  # noqa: E731
+        _check(lib().pqp_batch_solve_prepared(self.B, self.N, self.M, self._p(self.Qd), p("QdT"), p("theta"), p("sym"),
+                                              p("GpT"), p("QinvT"),
+                                              *[self._p(getattr(self, k)) for k in
+                                                ("Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")],
+                                              mode, num_iter, max_updates, self._p(self.Y), self._p(self.U),
+                                              self._p(self.h), self._p(self.status), self._s()))
         return self
 
 

@@ -1,5 +1,8 @@
 """One batched converge-mode call at n_dual 1024 x 4096 problems (the bench's
-batch_converge leg), for kernel traces: python scripts/batch_converge_one.py [K]"""
+batch_converge leg), for kernel traces: python scripts/batch_converge_one.py [K]
+FEASIBLE=1: every iterate feasible (Kp = 1e30 seen by checkFeas only), so
+terminate() runs all of computeCost; PQP_BATCH_OPTS: pqp_tune_batch_converge."""
+import os
 import sys
 import time
 from pathlib import Path
@@ -14,6 +17,10 @@ def main():
 
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     pb = pqp_amd.ProblemBatch.synthetic(3, 0, 4096, 1024, 512)
+    if os.environ.get("FEASIBLE"):
+        pb.Kp.fill_(1e30)
+    if os.environ.get("PQP_BATCH_OPTS"):
+        pqp_amd.lib().pqp_tune_batch_converge(int(os.environ["PQP_BATCH_OPTS"]))
     pb.solve(max_updates=1)
     torch.cuda.synchronize()
     for k in (K, 3 * K):

@@ -1,12 +1,14 @@
 """Batched converge mode at larger sizes: pqp_batch_solve,
 one workgroup per problem from global memory (k_solve_single).  Problems whose
 Qd is bit-symmetric (diagonal Qp_inv: the synthetic and testing/ problems)
-skip the column-major copy; optionally (tuning) terminate()'s Y'Qd
+skip the column-major copy; after a feasible terminate() the next Y'Qd
 (PQP_CPU.c:648-653) rides in the same pass over Qd as the speculative update
-to Y_{h+1} (:603-618), and Gp / Qp_inv are read through transposes.  Bar: the
-reference's h, Y and U bit for bit (oracle) in every setting, and a batch
-mixing both kinds of Qd.  N and M multiples of 4 take the 8/16-byte load
-forms of k_solve_single; opts bit 2 (and ragged N, M) the 4-byte form."""
+to Y_{h+1} (:603-618) (opts bit 0 turns that off), and Gp / Qp_inv are read
+through transposes (prepared once per ProblemBatch; opts bit 1: made per
+call by the unprepared pqp_batch_solve).  Bar: the reference's h, Y and U bit
+for bit (oracle) in every setting, and a batch mixing both kinds of Qd.  N and
+M multiples of 4 take the 8/16-byte load forms of k_solve_single; opts bit 2
+(and ragged N, M) the 4-byte form."""
 from __future__ import annotations
 
 import numpy as np
@@ -24,8 +26,9 @@ def _check(pb, b, h, Y, U, what):
     assert_bitwise(pb.U[b].cpu().numpy(), U, f"{what} U")
 
 
-@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4])
-def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts):
+@pytest.mark.parametrize("opts,tr,prep", [(0, True, True), (0, False, True), (1, True, True), (4, True, True),
+                                           (0, False, False), (2, False, False), (3, False, False), (6, False, False)])
+def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts, tr, prep):
     from test_gpu_wide import _testing_file
 
     L = gpu_lib.lib()
@@ -33,30 +36,43 @@ def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts):
     h, Y, U = orc.solve(P, max_updates=CAP)
     prev = L.pqp_tune_batch_converge(opts)
     try:
-        pb = gpu_lib.ProblemBatch.replicate(P, 3).solve(max_updates=CAP)
+        pb = gpu_lib.ProblemBatch.replicate(P, 3)
+        pb.transposes = tr
+        pb.solve(max_updates=CAP, prepared=prep)
+        if prep:
+            pb.solve(max_updates=CAP)  # again on the kept prepared data
     finally:
         L.pqp_tune_batch_converge(prev)
     for b in range(3):
-        _check(pb, b, h, Y, U, f"test2 copy {b} opts={opts}")
+        _check(pb, b, h, Y, U, f"test2 copy {b} opts={opts} transposes={tr} prepared={prep}")
 
 
-@pytest.mark.parametrize("opts,N,M", [(0, 256, 128), (3, 256, 128), (4, 256, 128), (0, 201, 61), (0, 204, 62)])
-def test_batch_synthetic_capped_vs_oracle(gpu_lib, orc, opts, N, M):
+@pytest.mark.parametrize("opts,tr,N,M", [(0, True, 256, 128), (0, False, 256, 128), (1, True, 256, 128),
+                                         (4, True, 256, 128), (0, True, 201, 61), (0, True, 204, 62)])
+@pytest.mark.parametrize("feasible", [False, True])
+def test_batch_synthetic_capped_vs_oracle(gpu_lib, orc, opts, tr, N, M, feasible):
+    """Capped solves; `feasible`: Kp = 1e30 seen by checkFeas only, so every
+    iterate runs all of computeCost (and the fused Y'Qd pass where enabled)."""
     L = gpu_lib.lib()
     B, cap = 3, 6
     prev = L.pqp_tune_batch_converge(opts)
     try:
-        pb = gpu_lib.ProblemBatch.synthetic(9, 4, B, N, M).solve(max_updates=cap)
+        pb = gpu_lib.ProblemBatch.synthetic(9, 4, B, N, M, transposes=tr)
+        if feasible:
+            pb.Kp.fill_(1e30)
+        pb.solve(max_updates=cap)
     finally:
         L.pqp_tune_batch_converge(prev)
     for b in range(B):
         P = orc.synth_problem(9, 4 + b, N, M)
+        if feasible:
+            P["Kp"] = np.full(N, 1e30, np.float32)
         h, Y, U = orc.solve(P, max_updates=cap)
-        _check(pb, b, h, Y, U, f"synthetic {b} opts={opts}")
+        _check(pb, b, h, Y, U, f"synthetic {b} opts={opts} transposes={tr} feasible={feasible}")
 
 
-@pytest.mark.parametrize("opts", [0, 1])
-def test_batch_mixed_symmetric_and_not(gpu_lib, orc, opts):
+@pytest.mark.parametrize("opts,prep", [(0, True), (1, True), (0, False)])
+def test_batch_mixed_symmetric_and_not(gpu_lib, orc, opts, prep):
     """Problem 0's Qd is bit-symmetric (diagonal Qp_inv), problem 1's is not
     (dense Qp_inv): one launch, the packed column-major copy, and (opts 1) a
     per-problem choice of the fused pass."""
@@ -76,9 +92,11 @@ def test_batch_mixed_symmetric_and_not(gpu_lib, orc, opts):
     L = gpu_lib.lib()
     prev = L.pqp_tune_batch_converge(opts)
     try:
-        pb.solve(max_updates=cap)
+        pb.solve(max_updates=cap, prepared=prep)
     finally:
         L.pqp_tune_batch_converge(prev)
+    if prep:
+        assert pb._prep["QdT"] is not None and not pb._prep["all_sym"]
     for b, P in enumerate((P0, P1)):
         h, Y, U = orc.solve(P, max_updates=cap)
         _check(pb, b, h, Y, U, f"mixed {b}")
@@ -100,3 +118,21 @@ def test_batch_fits_only_unfused(gpu_lib, orc, opts):
     P = orc.synth_problem(11, 0, N, M)
     h, Y, U = orc.solve(P, max_updates=cap)
     _check(pb, 0, h, Y, U, f"n_dual {N} opts={opts}")
+
+
+def test_prepared_data_follow_new_qd(gpu_lib, orc):
+    """A solve, new problems written through set() (the prepared Theta and
+    flags are dropped and rebuilt), a solve: the second problem set's bits."""
+    N, M, cap = 256, 128, 5
+    pb = gpu_lib.ProblemBatch.synthetic(12, 0, 2, N, M)
+    pb.solve(max_updates=cap)
+    first = pb._prep
+    other = [orc.synth_problem(12, 5 + b, N, M) for b in range(2)]
+    for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
+        pb.set(k, np.stack([np.asarray(P[k], np.float32).reshape(-1) for P in other]))
+    assert pb._prep is None
+    pb.solve(max_updates=cap)
+    assert pb._prep is not first
+    for b, P in enumerate(other):
+        h, Y, U = orc.solve(P, max_updates=cap)
+        _check(pb, b, h, Y, U, f"reloaded {b}")
