@@ -59,15 +59,21 @@ int pqp_tune_relay_spin_max(int polls);
 int pqp_tune_matmul_tiled(int off);
 
 /* Batched converge mode (pqp_batch_solve: one workgroup per problem, operands
- * from global memory).  opts bit 0: for problems whose Qd is bit-symmetric,
- * fuse terminate()'s Y'Qd into the update's pass over Qd after a feasible
- * terminate() (the update runs first, speculatively); bit 1: read Gp and
- * Qp_inv row by row through transposed copies made per call.  Both measured
- * slower at n_dual 1024 x 4096 problems and are off by default;
- * bit 2: 4-byte loads only (the 8/16-byte load forms, used by default when N
- * and M are multiples of 4 and the arrays 16-byte aligned, are turned off).
- * Every setting is bit-identical.  Returns the previous value. */
+ * from global memory).  By default, for problems whose Qd is bit-symmetric,
+ * terminate()'s Y'Qd rides in the update's pass over Qd after a feasible
+ * terminate() (the update runs first, speculatively); opts bit 0 turns that
+ * off.  bit 1: the unprepared pqp_batch_solve makes transposed copies of Gp
+ * and Qp_inv per call (pqp_batch_prepare makes them once when asked); bit 2:
+ * 4-byte loads only (the 8/16-byte load forms, used by default when N and M
+ * are multiples of 4 and the arrays 16-byte aligned, are turned off).  Every
+ * setting is bit-identical.  Returns the previous value. */
 int pqp_tune_batch_converge(int opts);
+
+/* Batched Gauss_Jordan (n <= 1024): the blocked kernel (one read and write of
+ * the augmented matrix per 16 or 8 pivots) by default; off != 0 takes the
+ * one-pivot-per-sweep kernel (A/B timing; both bit-identical to PQP_CPU.c).
+ * Returns the previous value. */
+int pqp_tune_gj_blocked(int off);
 
 /* The persistent single-problem launches (fixed mode: k_split_persist; converge
  * mode: k_converge_persist) need all their workgroups resident at once.  Before

@@ -227,7 +227,7 @@ int dev_compute_mp(float* Mp, const float* Mp1, const float* Mp2, const float* M
 // Gauss_Jordan (PQP_CPU.c:251-326)
 int dev_gauss_jordan(float* res, const float* A, int n, hipStream_t s) {
     DevBuf aug, fac;
-    PQP_TRY(aug.floats((size_t)2 * n * n));
+    PQP_TRY(aug.floats(gauss_jordan_aug_floats(n)));
     PQP_TRY(fac.floats(n));
     PQP_HIP(launch_gauss_jordan(A, aug.f(), fac.f(), res, n, s));
     PQP_HIP(hipStreamSynchronize(s));
@@ -1361,7 +1361,7 @@ int pqp_batch_gauss_jordan(int B, int n, const float* d_A, float* d_res, void* s
     PQP_TRY(ensure_device());
     hipStream_t s = static_cast<hipStream_t>(stream);
     DevBuf aug, fac;
-    PQP_TRY(aug.floats((size_t)B * 2 * n * n));
+    PQP_TRY(aug.floats((size_t)B * gauss_jordan_aug_floats(n)));
     PQP_TRY(fac.floats((size_t)B * n));
     PQP_HIP(launch_gauss_jordan_b(B, d_A, aug.f(), fac.f(), d_res, n, s));
     PQP_HIP(hipStreamSynchronize(s));
@@ -1911,6 +1911,12 @@ extern "C" int pqp_tune_batch_converge(int opts) {
 extern "C" int pqp_tune_matmul_tiled(int off) {
     const int old = pqp::g_matmul_tiled_off;
     pqp::g_matmul_tiled_off = off ? 1 : 0;
+    return old;
+}
+
+extern "C" int pqp_tune_gj_blocked(int off) {
+    const int old = pqp::g_gj_blocked_off;
+    pqp::g_gj_blocked_off = off ? 1 : 0;
     return old;
 }
 

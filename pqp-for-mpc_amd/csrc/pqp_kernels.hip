@@ -2744,6 +2744,208 @@ hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp
     if (B > 0) hipLaunchKernelGGL(k_mp_finish, dim3(B), dim3(1), 0, s, t, Mp6, Mp, sMp6);
     return hipGetLastError();
 }
+// ---------------------------------------------------------------------------
+// Blocked Gauss_Jordan (PQP_CPU.c:251-326) of many matrices, one workgroup
+// each, the pivots taken kGJB at a time.  Element (j,k) of the reference's
+// augmented matrix sees, at pivot step i (j != i),
+//     t = m_ji / m_ii;  m_jk = m_jk - m_ik * t          (:296-302, no FMA)
+// with row i's values "at step i" (after steps 0..i-1) and row j's own m_ji
+// read before the step touches row j.  Rows never read each other within a
+// step except the pivot row, so the order in which ROWS are processed is
+// free; only each element's own sequence of steps is fixed.  Per panel of
+// pivots [p0, p0 + nb):
+//   1. wave 0 forms the pivot rows "at their step", P_s = row p0+s with steps
+//      p0 .. p0+s-1 applied (from P_0 .. P_{s-1}), into LDS;
+//   2. every row j (pivot rows included, their own step skipped) is loaded
+//      once, takes the nb steps in order from the LDS panel, and is stored.
+// Each element thus sees exactly the reference's operations, in its order,
+// on the reference's operand values: bit-identical, with one read and one
+// write of the matrix per kGJB pivots instead of one per pivot.  A row lives
+// in one wave: lane l holds columns 256c + 4l + e (c < C, e < 4), so the
+// broadcast of m_ji is one v_readlane and no barrier is needed inside a row's
+// steps.  The last panel ends with the row scaling (:307-314) and writes the
+// right half straight into res (:316-322).
+// ---------------------------------------------------------------------------
+template <int C>
+__device__ __forceinline__ void gj_load(const float* __restrict__ row, int lane, float (&v)[4 * C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const sf4 q = *reinterpret_cast<const sf4*>(row + 256 * c + 4 * lane);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * c + e] = q[e];
+    }
+}
+template <int C>
+__device__ __forceinline__ void gj_store(float* __restrict__ row, int lane, const float (&v)[4 * C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        sf4 q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = v[4 * c + e];
+        *reinterpret_cast<sf4*>(row + 256 * c + 4 * lane) = q;
+    }
+}
+// m_{row, 256*CP + 4*lo + e}, broadcast from the lane that holds it
+template <int C, int CP, int E>
+__device__ __forceinline__ float gj_col(const float (&v)[4 * C], int lo) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[4 * CP + E]), lo));
+}
+// Steps p0 + s, s in [0, ns) (ns <= NB), of the panel whose pivot rows "at
+// their step" are P[s][.] (LDS, row stride W) with diagonal Pd[s]; the step of
+// pivot row `skip` (this row's own index) is left out.  The panel's pivot
+// columns lie in column block CP (p0 % NB == 0, NB divides 256).
+template <int C, int NB, int CP>
+__device__ __forceinline__ void gj_steps(float (&v)[4 * C], const float* __restrict__ P, const float* __restrict__ Pd,
+                                         int W, int p0, int ns, int skip, int lane) {
+    const int lo0 = (p0 & 255) >> 2;
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+        if (s < ns && p0 + s != skip) {
+            float mji;
+            switch (s & 3) {
+                case 0: mji = gj_col<C, CP, 0>(v, lo0 + (s >> 2)); break;
+                case 1: mji = gj_col<C, CP, 1>(v, lo0 + (s >> 2)); break;
+                case 2: mji = gj_col<C, CP, 2>(v, lo0 + (s >> 2)); break;
+                default: mji = gj_col<C, CP, 3>(v, lo0 + (s >> 2)); break;
+            }
+            const float t = mji / Pd[s];  // temp (:298)
+            const float* prow = P + (size_t)s * W;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const sf4 q = *reinterpret_cast<const sf4*>(prow + 256 * c + 4 * lane);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[4 * c + e] -= q[e] * t;  // (:301)
+            }
+        }
+    }
+}
+template <int C, int NB>
+__device__ __forceinline__ void gj_steps_any(float (&v)[4 * C], const float* P, const float* Pd, int W, int p0, int ns,
+                                             int skip, int lane) {
+    switch (p0 >> 8) {  // the pivot column block: compile-time register indices
+        case 0: gj_steps<C, NB, 0>(v, P, Pd, W, p0, ns, skip, lane); break;
+        case 1: if constexpr (C > 1) gj_steps<C, NB, 1>(v, P, Pd, W, p0, ns, skip, lane); break;
+        case 2: if constexpr (C > 2) gj_steps<C, NB, 2>(v, P, Pd, W, p0, ns, skip, lane); break;
+        case 3: if constexpr (C > 3) gj_steps<C, NB, 3>(v, P, Pd, W, p0, ns, skip, lane); break;
+        default: break;  // pivots lie in the left half: column blocks < C / 2 <= 3 for C <= 8
+    }
+}
+// m_{row, col} of the row held in v (any col), broadcast to the whole wave
+template <int C>
+__device__ __forceinline__ float gj_any_col(const float (&v)[4 * C], int col) {
+    const int idx = 4 * (col >> 8) + (col & 3);
+    float x = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4 * C; ++r) x = (r == idx) ? v[r] : x;
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), (col & 255) >> 2));
+}
+
+template <int C, int NB>
+__global__ void __launch_bounds__(256) k_gj_blocked(const float* __restrict__ A, float* __restrict__ aug,
+                                                    float* __restrict__ res, int n) {
+    constexpr int W = 256 * C;  // padded row of the augmented matrix
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* P = lds;             // [NB][W] pivot rows at their step
+    float* Pd = lds + NB * W;   // [NB] their diagonals
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    {
+        const size_t b = blockIdx.x;
+        A += b * n * n;
+        res += b * n * n;
+        aug += b * (size_t)n * W;
+    }
+    // the one bubble pass on column 0 (:280-289) as a row order, then [A | I]
+    // in that order (:262-276), zero-padded to W columns
+    int* perm = reinterpret_cast<int*>(P);
+    float* col0 = P + n;
+    for (int r = tid; r < n; r += 256) col0[r] = A[(size_t)r * n];
+    __syncthreads();
+    if (tid == 0) {
+        for (int r = 0; r < n; ++r) perm[r] = r;
+        for (int r = n - 1; r > 0; --r)
+            if (col0[perm[r - 1]] < col0[perm[r]]) {
+                const int t = perm[r];
+                perm[r] = perm[r - 1];
+                perm[r - 1] = t;
+            }
+    }
+    __syncthreads();
+    for (int r = wv; r < n; r += 4) {
+        const int src = perm[r];
+        float v[4 * C];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = 256 * c + 4 * lane + e;
+                v[4 * c + e] = k < n ? A[(size_t)src * n + k] : (k == n + src ? 1.0f : 0.0f);
+            }
+        gj_store<C>(aug + (size_t)r * W, lane, v);
+    }
+    __syncthreads();
+    for (int p0 = 0; p0 < n; p0 += NB) {
+        const int ns = n - p0 < NB ? n - p0 : NB;
+        if (wv == 0) {  // 1. the pivot rows at their step
+            for (int s = 0; s < ns; ++s) {
+                float v[4 * C];
+                gj_load<C>(aug + (size_t)(p0 + s) * W, lane, v);
+                gj_steps_any<C, NB>(v, P, Pd, W, p0, s, -1, lane);
+                gj_store<C>(P + (size_t)s * W, lane, v);
+                const float d = gj_any_col<C>(v, p0 + s);
+                if (lane == 0) Pd[s] = d;
+            }
+        }
+        __syncthreads();
+        const bool last = p0 + NB >= n;
+        for (int j = wv; j < n; j += 4) {  // 2. every row takes the panel's steps
+            float v[4 * C];
+            gj_load<C>(aug + (size_t)j * W, lane, v);
+            gj_steps_any<C, NB>(v, P, Pd, W, p0, ns, j, lane);
+            if (!last) {
+                gj_store<C>(aug + (size_t)j * W, lane, v);
+            } else {  // temp = m_jj; the row / temp; its right half is res's row j
+                const float d = gj_any_col<C>(v, j);
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int k = 256 * c + 4 * lane + e;
+                        if (k >= n && k < 2 * n) res[(size_t)j * n + (k - n)] = v[4 * c + e] / d;
+                    }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// padded row width and panel of the blocked kernel for an n x n matrix (0: not handled)
+static int gj_blocked_c(int n) { return n >= 1 && n <= 1024 ? (2 * n + 255) / 256 : 0; }
+size_t gauss_jordan_aug_floats(int n) {
+    const int c = gj_blocked_c(n);
+    return c ? (size_t)n * 256 * c : (size_t)2 * n * n;
+}
+int g_gj_blocked_off = 0;  // tuning: the one-pivot-per-sweep kernel instead (A/B)
+template <int C>
+static void launch_gj_blocked_c(int B, const float* A, float* aug, float* res, int n, hipStream_t s) {
+    constexpr int NB = C <= 4 ? 16 : 8;
+    const size_t lds = sizeof(float) * ((size_t)NB * 256 * C + NB);
+    hipLaunchKernelGGL((k_gj_blocked<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
+}
+static hipError_t launch_gj_blocked(int B, const float* A, float* aug, float* res, int n, hipStream_t s) {
+    switch (gj_blocked_c(n)) {
+        case 1: launch_gj_blocked_c<1>(B, A, aug, res, n, s); break;
+        case 2: launch_gj_blocked_c<2>(B, A, aug, res, n, s); break;
+        case 3: launch_gj_blocked_c<3>(B, A, aug, res, n, s); break;
+        case 4: launch_gj_blocked_c<4>(B, A, aug, res, n, s); break;
+        case 5: launch_gj_blocked_c<5>(B, A, aug, res, n, s); break;
+        case 6: launch_gj_blocked_c<6>(B, A, aug, res, n, s); break;
+        case 7: launch_gj_blocked_c<7>(B, A, aug, res, n, s); break;
+        case 8: launch_gj_blocked_c<8>(B, A, aug, res, n, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (n >= kGaussJordanWideMin && B <= 8) {  // few large matrices: each over many workgroups
@@ -2755,6 +2957,7 @@ hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, 
         }
         return hipSuccess;
     }
+    if (!g_gj_blocked_off && gj_blocked_c(n)) return launch_gj_blocked(B, A, aug, res, n, s);
     hipLaunchKernelGGL(k_gauss_jordan, dim3(B), dim3(256), 0, s, A, aug, fac, res, n);
     return hipGetLastError();
 }

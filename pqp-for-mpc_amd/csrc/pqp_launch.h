@@ -129,6 +129,9 @@ hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, lo
 hipError_t launch_negate_b(int B, float* A, int n, long long sA, hipStream_t s);
 hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp, long long sMp6, hipStream_t s);
 hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
+// floats of one matrix's augmented workspace (`aug` holds B of them)
+size_t gauss_jordan_aug_floats(int n);
+extern int g_gj_blocked_off;
 // ---- converge mode of one large problem over many workgroups (pqp_wide.hip)
 enum GemvEpi : int { kEpiPlain = 0, kEpiAdd = 1, kEpiNeg = 2, kEpiFeas = 3 };
 // out[j] = epi( sum_k A[k * lda + j] * x[k] ), j < n_out, k = 0..n_in-1 in order

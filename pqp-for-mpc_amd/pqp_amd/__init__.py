@@ -101,6 +101,7 @@ SIGNATURES = {
     "pqp_tune_lean_min_n": (C.c_int, [C.c_int]),
     "pqp_tune_relay_spin_max": (C.c_int, [C.c_int]),
     "pqp_tune_matmul_tiled": (C.c_int, [C.c_int]),
+    "pqp_tune_gj_blocked": (C.c_int, [C.c_int]),
     "pqp_tune_batch_converge": (C.c_int, [C.c_int]),
     "pqp_tune_persist_fit_cus": (C.c_int, [C.c_int]),
     "pqp_tune_last_path": (C.c_int, [C.POINTER(C.c_longlong)]),

@@ -162,3 +162,40 @@ def test_problem_beyond_one_workgroup_budget(gpu_lib, orc):
     assert_bitwise(r["Y"], Y, "converge Y")
     assert_bitwise(r["U"], U, "converge U")
     assert_bitwise(f["Y"], orc.iterate(P["Qd"], P["Fd"], N, 2), "fixed-mode Y")
+
+
+@pytest.mark.parametrize("n,B", [(1, 3), (7, 5), (15, 2), (16, 2), (17, 2), (63, 2), (100, 3), (256, 2), (300, 2),
+                                 (385, 1), (512, 2), (640, 1), (1024, 1)])
+@pytest.mark.parametrize("blocked", [1, 0])
+def test_gauss_jordan_blocked_vs_oracle(gpu_lib, orc, n, B, blocked):
+    """The blocked batched Gauss_Jordan (pivots 16 or 8 at a time, one pass
+    over the augmented matrix per panel) and the one-pivot-per-sweep kernel:
+    bit-identical to the reference's restatement (PQP_CPU.c:251-326),
+    including the bubble pass (column 0 random, rows swapped), ragged panels
+    and both register layouts (n <= 512: 16-pivot panels, above: 8)."""
+    import torch
+
+    if n >= 640 and not blocked:
+        pytest.skip("the per-sweep kernel at this size only costs time")
+    rng = np.random.default_rng(1000 + n)
+    A = rng.standard_normal((B, n, n)).astype(np.float32)
+    A += np.eye(n, dtype=np.float32)[None] * n  # well conditioned
+    dA = torch.from_numpy(A.reshape(B, -1)).cuda()
+    dR = torch.zeros_like(dA)
+    L = gpu_lib.lib()
+    prev = L.pqp_tune_gj_blocked(0 if blocked else 1)
+    try:
+        # B > 8 keeps large n off the one-launch-per-pivot path: replicate
+        reps = 9 if n >= 64 else 1
+        dA9 = dA.repeat(reps, 1)
+        dR9 = torch.zeros_like(dA9)
+        gpu_lib._check(L.pqp_batch_gauss_jordan(B * reps, n, gpu_lib.C.c_void_p(dA9.data_ptr()),
+                                                gpu_lib.C.c_void_p(dR9.data_ptr()),
+                                                gpu_lib.C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    finally:
+        L.pqp_tune_gj_blocked(prev)
+    got = dR9.cpu().numpy()
+    for b in range(B):
+        want = orc.gauss_jordan(A[b].reshape(-1), n)
+        for r in range(reps):
+            assert_bitwise(got[r * B + b], want, f"inverse {b} copy {r}")
