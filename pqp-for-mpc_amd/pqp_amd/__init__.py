@@ -85,7 +85,7 @@ SIGNATURES = {
                         + [_vp]),
     "pqp_batch_solve_path": (C.c_int, [C.c_int, C.c_int]),
     "pqp_batch_prepare": (C.c_int, [C.c_int] * 3 + [_vp] * 8 + [C.POINTER(C.c_int), _vp]),
-    "pqp_batch_solve_prepared": (C.c_int, [C.c_int] * 3 + [_vp] * 15 + [C.c_int, C.c_longlong, C.c_longlong]
+    "pqp_batch_solve_prepared": (C.c_int, [C.c_int] * 3 + [_vp] * 14 + [C.c_int, C.c_longlong, C.c_longlong]
                                  + [_vp] * 4 + [_vp]),
     "pqp_rowblock_create": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(C.c_void_p)]),
     "pqp_rowblock_update": (C.c_int, [_vp, _vp, _vp, _vp]),

@@ -49,6 +49,28 @@ def test_python_mirror_binds_every_symbol():
     assert L.pqp_version() >= 100
 
 
+def declared_arity() -> dict[str, int]:
+    """name -> number of parameters of every prototype in include/*.h."""
+    text = "\n".join(h.read_text() for h in HEADERS)
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s*([A-Za-z_][A-Za-z0-9_]*)\s*\(([^)]*)\)\s*;",
+                         text, re.M):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_python_mirror_arity_matches_header():
+    """Every ctypes binding takes exactly the parameters its prototype declares."""
+    import pqp_amd
+
+    arity = declared_arity()
+    assert set(arity) == set(pqp_amd.SIGNATURES)
+    bad = {n: (len(pqp_amd.SIGNATURES[n][1]), k) for n, k in arity.items() if len(pqp_amd.SIGNATURES[n][1]) != k}
+    assert not bad, bad
+
+
 def _gfx950_asm(name: str) -> str:
     import tempfile
 
