@@ -1902,9 +1902,10 @@ extern "C" int pqp_tune_last_path(long long* fallbacks) {
 }
 
 extern "C" int pqp_tune_batch_converge(int opts) {
-    const int old = pqp::g_batch_opts | (pqp::g_single_scalar ? 4 : 0);
+    const int old = pqp::g_batch_opts | (pqp::g_single_scalar ? 4 : 0) | (pqp::g_single_occ4 ? 8 : 0);
     pqp::g_batch_opts = opts & 3;
     pqp::g_single_scalar = (opts & 4) ? 1 : 0;
+    pqp::g_single_occ4 = (opts & 8) ? 1 : 0;
     return old;
 }
 

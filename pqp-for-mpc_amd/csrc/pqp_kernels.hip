@@ -1357,7 +1357,8 @@ template <> struct SVec<2> { typedef sf2 t; };
 template <> struct SVec<4> { typedef sf4 t; };
 
 // s[c] = sum_k A[k * lda + c] * x[k], c < V (V adjacent columns of a
-// row-major matrix), k = 0..n-1 in order, U rows of loads in flight
+// row-major matrix), k = 0..n-1 in order, U rows of loads in flight (the
+// matrix is streamed once per pass: non-temporal loads)
 template <int V, int U>
 __device__ __forceinline__ void col_dotv(const float* __restrict__ A, int lda, const float* x, int n, float (&s)[V]) {
     typedef typename SVec<V>::t vt;
@@ -1369,7 +1370,7 @@ __device__ __forceinline__ void col_dotv(const float* __restrict__ A, int lda, c
         float xv[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            a[j] = *reinterpret_cast<const vt*>(A + (size_t)(k + j) * lda);
+            a[j] = __builtin_nontemporal_load(reinterpret_cast<const vt*>(A + (size_t)(k + j) * lda));
             xv[j] = x[k + j];
         }
 #pragma unroll
@@ -1432,7 +1433,7 @@ __device__ __forceinline__ void single_update4(const SolveArgs& A, const float* 
             float yv[kSU4];
 #pragma unroll
             for (int j = 0; j < kSU4; ++j) {
-                q[j] = *reinterpret_cast<const sf4*>(col + (size_t)(k + j) * ldq);
+                q[j] = __builtin_nontemporal_load(reinterpret_cast<const sf4*>(col + (size_t)(k + j) * ldq));
                 yv[j] = cur[k + j];
             }
 #pragma unroll
@@ -1472,8 +1473,8 @@ __device__ __forceinline__ void single_update4(const SolveArgs& A, const float* 
     }
 }
 
-template <int NT, bool VEC>
-__global__ void __launch_bounds__(NT) k_solve_single(SolveArgs A0, SolveState* __restrict__ st0) {
+template <int NT, bool VEC, int MINB = 1>
+__global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
     SolveState* st = st0 + blockIdx.x;
@@ -2994,6 +2995,7 @@ size_t solve_single_lds_bytes(int ldq, int ldm, bool fused) {
 }
 
 int g_single_scalar = 0;  // tuning: k_solve_single with 4-byte loads only
+int g_single_occ4 = 0;    // tuning: k_solve_single compiled for 4 workgroups per CU (<= 128 VGPRs)
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
@@ -3005,6 +3007,8 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
     if (a.N <= 64) {
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
+    } else if (vec && g_single_occ4) {
+        hipLaunchKernelGGL((k_solve_single<256, true, 4>), dim3(B), dim3(256), lds, s, a, st);
     } else {
         if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<256, false>), dim3(B), dim3(256), lds, s, a, st);

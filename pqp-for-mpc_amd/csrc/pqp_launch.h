@@ -198,5 +198,6 @@ extern int g_converge_trace_n;
 
 hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s);
 extern int g_single_scalar;  // tuning: k_solve_single with 4-byte loads only (no 8/16-byte forms)
+extern int g_single_occ4;    // tuning: k_solve_single built for 4 workgroups per CU
 
 }  // namespace pqp

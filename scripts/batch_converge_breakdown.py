@@ -6,8 +6,9 @@ for: fixed mode (the update pass alone), converge mode on infeasible iterates
 checkFeas only: all of computeCost runs), each under the batch-converge
 tuning options.  Prints one JSON line.
 Usage: python scripts/batch_converge_breakdown.py [N B K [variant,...]]
-(variants: fused_T unfused_T fused unfused -- the fused Y'Qd pass on / off,
-with / without the prepared transposes of Gp and Qp_inv)"""
+(variants: fused_T unfused_T fused unfused fused_T_occ4 unfused_T_occ4 -- the
+fused Y'Qd pass on / off, with / without the prepared transposes of Gp and
+Qp_inv, k_solve_single built for 4 workgroups per CU)"""
 from __future__ import annotations
 
 import json
@@ -45,7 +46,8 @@ def main(N=1024, B=4096, K=4):
 
     out = {"n_dual": N, "m": M, "problems": B, "K": K}
     GB = B * 1e-9
-    variants = {"fused_T": (0, True), "unfused_T": (1, True), "fused": (0, False), "unfused": (1, False)}
+    variants = {"fused_T": (0, True), "unfused_T": (1, True), "fused": (0, False), "unfused": (1, False),
+                "fused_T_occ4": (8, True), "unfused_T_occ4": (9, True)}
     names = sys.argv[4].split(",") if len(sys.argv) > 4 else list(variants)
     for name in names:
         opts, tr = variants[name]
