@@ -65,11 +65,17 @@ def hot_kernel_hash() -> str:
     <hot-kernel> markers of pqp_kernels.hip, plus the library's compile flags.
     profiles/pmc_traffic.json records carry the hash they were measured with;
     a record whose hash differs is stale and is not reported as `traffic`."""
+    return kernel_src_hash("hot-kernel")
+
+
+def kernel_src_hash(marker: str) -> str:
+    """SHA-256 (16 hex) of the text between pqp_kernels.hip's <marker> and
+    </marker> comments plus the library's compile flags."""
     import hashlib
     import re
 
     src = (ROOT / "pqp-for-mpc_amd" / "csrc" / "pqp_kernels.hip").read_text()
-    m = re.search(r"// <hot-kernel>.*?// </hot-kernel>", src, re.S)
+    m = re.search(rf"// <{marker}>.*?// </{marker}>", src, re.S)
     flags = [ln for ln in (ROOT / "pqp-for-mpc_amd" / "Makefile").read_text().splitlines()
              if ln.startswith("HIPFLAGS")]
     text = (m.group(0) if m else src) + "\n".join(flags)
@@ -357,14 +363,22 @@ def setup_bench(pqp_amd, N: int = 1024, M: int = 512, B: int = 64) -> dict:
 
 def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> dict:
     """converge mode of B synthetic problems at once
-    (pqp_batch_solve, terminate() before every update), capped at K updates
-    (the synthetic problems do not meet the exact gap test at this size).
-    One iteration = terminate() + updateY2 (PQP_CPU.c:716-725).  Qd is
-    bit-symmetric here, so the row-major Qd serves as its own column-major copy."""
+    (ProblemBatch over pqp_batch_prepare + pqp_batch_solve_prepared,
+    terminate() before every update), capped at K updates (the synthetic
+    problems do not meet the exact gap test at this size).  One iteration =
+    terminate() + updateY2 (PQP_CPU.c:716-725).  Two cases: the generator's
+    problems, whose iterates fail checkFeas (terminate() stops there: no Y'Qd,
+    no U'Qp), and the same problems with Kp = 1e30 seen by checkFeas only, so
+    every iterate runs all of computeCost (PQP_CPU.c:648-666)."""
     import torch
 
     pb = pqp_amd.ProblemBatch.synthetic(1, 0, B, N)
     M = pb.M
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pb.prepare()  # once per batch: symmetry flags, Theta, Gp' and Qp_inv'
+    torch.cuda.synchronize()
+    prep_ms = (time.perf_counter() - t0) * 1e3
     pb.solve(max_updates=1)  # warm
 
     def call(k):
@@ -374,29 +388,41 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    dt = call(K)
-    ok = bool((pb.h == K + 1).all().item())
-    dt3 = call(3 * K)  # the same call with 3K updates: the difference is 2K iterations without the per-call setup
-    ok = ok and bool((pb.h == 3 * K + 1).all().item())
+    rec = {}
+    tf = ROOT / "profiles" / "pmc_traffic.json"
+    db = json.loads(tf.read_text()) if tf.exists() else {}
+    khash = kernel_src_hash("solve-single")
+    # bytes per problem-iteration: Qd once (the update; on feasible iterates
+    # Y'Qd rides in the same pass), Gp twice (Gp'Y, Gp U: 8NM), Qp_inv once,
+    # and on feasible iterates Qp once (U'Qp)
+    for case, alg in (("infeasible", 4.0 * N * N + 8.0 * N * M + 4.0 * M * M),
+                      ("feasible", 4.0 * N * N + 8.0 * N * M + 8.0 * M * M)):
+        if case == "feasible":
+            pb.Kp.fill_(1e30)
+            pb.solve(max_updates=1)
+        dt = call(K)
+        ok = bool((pb.h == K + 1).all().item())
+        dt3 = call(3 * K)  # the same call with 3K updates: the difference is 2K iterations, no per-call cost
+        ok = ok and bool((pb.h == 3 * K + 1).all().item())
+        per_iter = (dt3 - dt) / (2 * K)
+        gbs = alg * B / per_iter / 1e9
+        r = {"ms_per_iteration": per_iter * 1e3, "instance_iter_per_s": B / per_iter,
+             "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
+             "call_ms": dt * 1e3, "call_instance_iter_per_s": B * K / dt, "all_capped": ok}
+        pmc = db.get(f"k_solve_single_{case}")
+        if pmc and pmc.get("kernel_src_sha256") == khash:
+            r["traffic_ratio"] = pmc["traffic_ratio"]
+            r["traffic_source"] = f"profiles/pmc_traffic.json k_solve_single_{case}"
+        else:
+            r["traffic_ratio"] = None
+            r["traffic_source"] = "no PMC record for this kernel source (scripts/gpu_batch_converge.sh)"
+        rec[case] = r
     del pb
     torch.cuda.empty_cache()
-    # algorithmic bytes per problem-iteration: Qd once (the update), Gp twice
-    # (Gp'Y, Gp U), Qp_inv once -- terminate() of these iterates stops at
-    # checkFeas (infeasible), so Y'Qd and U'Qp are never formed
-    alg = 4.0 * N * N + 8.0 * N * M + 4.0 * M * M
-    gbs = alg * B * K / dt / 1e9
-    per_iter = (dt3 - dt) / (2 * K)
-    ss_gbs = alg * B / per_iter / 1e9
-    return {"problems": B, "n_dual": N, "m": M, "updates": K, "ms": dt * 1e3, "instance_iter_per_s": B * K / dt,
-            "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS, "all_capped": ok,
-            "steady_state": {"ms_per_iteration": per_iter * 1e3, "instance_iter_per_s": B / per_iter,
-                             "alg_GBps": ss_gbs, "frac_of_hbm_peak": ss_gbs / HBM_PEAK_GBS,
-                             "per_call_setup_ms": (dt - K * per_iter) * 1e3,
-                             "note": f"(time of a {3 * K}-update call - time of a {K}-update call) / {2 * K}: the "
-                                     "iterations alone; the per-call setup (symmetry check, Theta, state upload and "
-                                     "readback) is per_call_setup_ms"},
-            "note": "k_solve_single, one workgroup per problem; the timed call includes the per-call setup and the "
-                    "state readback"}
+    return {"problems": B, "n_dual": N, "m": M, "updates": K, "prepare_ms": prep_ms, **rec,
+            "note": "k_solve_single, one workgroup per problem; ms_per_iteration = (time of a 3K-update call - time "
+                    "of a K-update call) / 2K, the iterations alone; call_ms = one K-update call (K + 1 terminate() "
+                    "+ K updates, state init and readback); prepare_ms = pqp_batch_prepare, once per batch"}
 
 
 def _testing_file(name: str, tmpdir: Path) -> Path:

@@ -1266,6 +1266,7 @@ __device__ __forceinline__ SolveArgs problem_at(SolveArgs A, int b) {
     return A;
 }
 
+// <solve-single> (bench.py hashes the text up to </solve-single>: k_solve_single PMC records are keyed by it)
 // ---------------------------------------------------------------------------
 // k_solve_single: the whole solveQuadraticDual (PQP_CPU.c:694-750) in ONE
 // persistent workgroup: terminate() before every update, bit-exact, no host
@@ -1536,12 +1537,19 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
             // i walks column i of QinvT / GpT: coalesced), else row by row
             // (VEC with the transposes: four adjacent rows per lane, 16-byte
             // coalesced loads of the transposed copy, each row's sum in j order)
-            if (VEC && A.QinvT) {
+            if (VEC && A.QinvT && M >= 4 * NT) {
                 for (int i0 = 4 * tid; i0 < M; i0 += 4 * NT) {
                     float t[4];
                     col_dotv<4, kSU4>(A.QinvT + i0, M, tM, M, t);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) Us[i0 + c] = -t[c];
+                }
+            } else if (VEC && A.QinvT) {  // M < 4 NT: two rows per lane keep more lanes loading
+                for (int i0 = 2 * tid; i0 < M; i0 += 2 * NT) {
+                    float t[2];
+                    col_dotv<2, kSU>(A.QinvT + i0, M, tM, M, t);
+                    Us[i0] = -t[0];
+                    Us[i0 + 1] = -t[1];
                 }
             } else {
                 for (int i = tid; i < M; i += NT)
@@ -1682,6 +1690,8 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
         if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
     }
 }
+
+// </solve-single>
 
 // ---------------------------------------------------------------------------
 // k_solve_small: solveQuadraticDual for problems that fit in LDS (the bundled
