@@ -26,9 +26,10 @@ Extra keys:
   single_n1024  configs[2]: one n_dual=1024 problem, 1000 fixed iterations
   single_converge  the same problem size in the reference's converge mode
                 (terminate() before every update), capped at 2000 updates
-  rowshard      one large problem (n_dual = 16384) row-sharded over the job's
-                ranks: per update, every rank updates its
-                rows and an RCCL all-gather assembles y (all ranks take part)
+  rowshard      one large problem (n_dual = 32768; rowshard_16384 beside it)
+                row-sharded over the job's ranks: per update,
+                every rank updates its rows and an RCCL all-gather assembles y
+                (all ranks take part)
   gather_ms     RCCL gather of every rank's Y* to rank 0 (outside the timed
                 region)
   iters_to_tol  converge mode on the problems the reference converges on (the
@@ -103,7 +104,9 @@ def parse():
                     help="distinct problems the CPU baseline cycles through (>= 8, DRAM-resident)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bundled", action="store_true")
-    ap.add_argument("--rowshard-n", type=int, default=16384, help="n_dual of the row-sharded leg (0: skip)")
+    ap.add_argument("--rowshard-n", default="32768,16384",
+                    help="n_dual of the row-sharded legs, comma-separated (the first is `rowshard`, the others "
+                         "`rowshard_<n>`; 0 or empty: skip)")
     ap.add_argument("--rowshard-updates", type=int, default=100)
     ap.add_argument("--rowshard-graph", action="store_true",
                     help="at N > 1, also time the row-sharded steps as hipGraph replays (update + RCCL all-gather)")
@@ -810,9 +813,11 @@ def main():
         g = em.leg("gather", gather_leg)
         if result is not None:
             result["gather_ms"], result["gather_ok"] = g.get("ms"), g.get("ok")
-    if args.rowshard_n > 0:  # every rank takes part
-        em.leg("rowshard", lambda: rowshard_bench(pqp_amd, dist, rank, world, dev, args.rowshard_n,
-                                                  args.rowshard_updates, graph=world == 1 or args.rowshard_graph))
+    sizes = [int(v) for v in str(args.rowshard_n).split(",") if v.strip() and int(v) > 0]
+    for i, n_rs in enumerate(sizes):  # every rank takes part
+        em.leg("rowshard" if i == 0 else f"rowshard_{n_rs}",
+               lambda n_rs=n_rs: rowshard_bench(pqp_amd, dist, rank, world, dev, n_rs, args.rowshard_updates,
+                                                graph=world == 1 or args.rowshard_graph))
     if world == 1 and not args.no_bundled:
         em.leg("bundled", lambda: bundled_bench(pqp_amd))
         em.leg("mpc_batch", lambda: mpc_batch_bench(pqp_amd))

@@ -58,6 +58,16 @@ int pqp_tune_relay_spin_max(int polls);
  * timing; both are bit-identical to PQP_CPU.c).  Returns the previous value. */
 int pqp_tune_matmul_tiled(int off);
 
+/* Error-path tests of the persistent launches: workgroup `wg` of every
+ * persistent launch (k_split_persist, k_converge_persist) returns at once, as
+ * if it were never resident, so the other workgroups' waits expire (2 s) and
+ * the solve falls back to the graph-replayed relay / chain path, from the
+ * reference's start (pqp_tune_last_path tells which path ran and counts the
+ * fallbacks).  wg < 0 turns it off.  Returns the previous value. */
+int pqp_tune_persist_stall(int wg);
+/* Workgroups of the persistent converge launch for (N, M) (0: not used). */
+int pqp_tune_converge_grid(int N, int M);
+
 /* Batched converge mode (pqp_batch_solve: one workgroup per problem, operands
  * from global memory).  By default, for problems whose Qd is bit-symmetric,
  * terminate()'s Y'Qd rides in the update's pass over Qd after a feasible

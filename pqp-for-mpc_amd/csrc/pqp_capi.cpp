@@ -278,7 +278,7 @@ struct pqp_problem {
     hipStream_t side = nullptr;                      // capture-time fork for the speculative update
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     long long wgraph_key = -1;
-    int graph_variant = -1;                          // g_split_u the graph was captured with
+    long long graph_variant = -1;                    // the settings the fixed-mode graphs were captured with
     pqp::DevBuf Y, U, state;
     pqp::SolveState* hst = nullptr;                  // pinned host mirror of `state`
     float* hio = nullptr;                            // pinned staging of Y (N floats) then U (M floats)
@@ -621,8 +621,10 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     }
     const int lw = pick_lw(N);
     PQP_TRY(ensure_split(P, lw, s));
-    const int variant = g_split_u | (g_split_kind << 4) | (lw << 8) | ((int)use_lean(N, N) << 16) |
-                        ((int)(g_relay_spin_max != kRelaySpinMax) << 20);
+    // every setting the captured launches bake in as an argument, the relay
+    // wait budget's value included
+    const long long variant = (long long)g_split_u | ((long long)g_split_kind << 4) | ((long long)lw << 8) |
+                              ((long long)use_lean(N, N) << 16) | ((long long)(unsigned)g_relay_spin_max << 24);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
         P.chunk_ready = false;
@@ -778,8 +780,11 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     int* flag = static_cast<int*>(P.wflag.p);
     long long* cap = static_cast<long long*>(P.wcap.p);
-    const long long key = ((long long)(g_relay_spin_max != kRelaySpinMax) << 32) ^ ((long long)use_lean(N, N) << 24) ^
-                          ((long long)g_wide_flags << 16) ^ ((long long)g_split_kind << 8) ^ lw;  // cap: device word
+    // every launch argument the capture bakes in (cap: a device word)
+    const long long key = (long long)(((unsigned long long)(unsigned)g_relay_spin_max << 32) |
+                                      ((unsigned long long)use_lean(N, N) << 24) |
+                                      ((unsigned long long)(g_wide_flags & 0xff) << 16) |
+                                      ((unsigned long long)(g_split_kind & 0xff) << 8) | (unsigned long long)(lw & 0xff));
     int* rerr = static_cast<int*>(P.rerr.p);
     if (!P.wgraph || P.wgraph_key != key) {
         if (P.wgraph) {
@@ -1890,6 +1895,14 @@ extern "C" int pqp_tune_persist_trace(void* d_trace, int updates) {
     return PQP_OK;
 }
 
+extern "C" int pqp_tune_persist_stall(int wg) {
+    const int old = pqp::g_persist_stall_wg;
+    pqp::g_persist_stall_wg = wg >= 0 ? wg : -1;
+    return old;
+}
+
+extern "C" int pqp_tune_converge_grid(int N, int M) { return pqp::converge_persist_wgs(N, M, nullptr); }
+
 extern "C" int pqp_tune_persist_fit_cus(int cus) {
     const int old = pqp::g_persist_fit_cus;
     pqp::g_persist_fit_cus = cus > 0 ? cus : 0;
@@ -1923,7 +1936,9 @@ extern "C" int pqp_tune_gj_blocked(int off) {
 
 extern "C" int pqp_tune_relay_spin_max(int polls) {
     const int old = pqp::g_relay_spin_max;
-    pqp::g_relay_spin_max = polls == 0 ? pqp::kRelaySpinMax : polls;
+    // clamped: a budget near INT_MAX would let a broken hand-off spin until its
+    // counter overflows
+    pqp::g_relay_spin_max = polls == 0 ? pqp::kRelaySpinMax : (polls > (1 << 30) ? (1 << 30) : polls);
     return old;
 }
 

@@ -207,6 +207,7 @@ struct CvArgs {
     float *Yout, *Uout;
     u64* trace;           // tuning: [2][iterate][29][4] s_memrealtime, then s_memtime marks of workgroup 0 of each role
     int trace_n;
+    int stall_wg;  // tuning: this workgroup never runs (error-path tests; -1: none)
 };
 
 namespace {
@@ -938,6 +939,7 @@ template <bool TRACE>
 __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.x, tid = threadIdx.x;
+    if (b == a.stall_wg) return;  // as if not resident: the other roles' waits expire into err
     if (b >= a.g4) {
         decide_role<TRACE>(a, lds);
         return;
@@ -1126,6 +1128,7 @@ hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s) {
     a.Uout = L.U;
     a.trace = g_converge_trace;
     a.trace_n = g_converge_trace_n;
+    a.stall_wg = g_persist_stall_wg;
     hipError_t e = hipMemsetAsync(ring, 0, sizeof(u64) * converge_ring_words(L.N, L.M), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_converge_init, dim3(4), dim3(256), 0, s, L.Y, L.N, L.u0, a.ry, L.ctl, L.decided, L.err);

@@ -193,6 +193,7 @@ hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Q
                                 float* A1, float* A2, float* A3, hipStream_t s);
 hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s);
 extern int g_converge_persist_off;
+extern int g_persist_stall_wg;  // tuning: workgroup of each persistent launch that never runs (-1: none)
 extern unsigned long long* g_converge_trace;  // tuning: [iterate][29][4] words (pqp_tune_converge_trace)
 extern int g_converge_trace_n;
 

@@ -196,6 +196,7 @@ __device__ __forceinline__ void slice_products(f4v (&prod)[NP], const f4v* qw, c
 }  // namespace
 
 int g_persist_off = 0;
+int g_persist_stall_wg = -1;  // tuning: workgroup of each persistent launch that never runs (-1: none)
 unsigned long long* g_persist_trace = nullptr;  // tuning: timeline of workgroup 0 (pqp_tune_persist_trace)
 int g_persist_trace_n = 0;
 
@@ -228,8 +229,11 @@ template <bool TRACE>
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     k_split_persist(const float* __restrict__ SP, const float* __restrict__ fdpn, int N, int updates,
                     const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err, u64* trace,
-                    int trace_n) {
+                    int trace_n, int stall_wg) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    // tuning (error-path tests): this workgroup never runs, as if it were not
+    // resident; every other one's waits expire and report through err
+    if ((int)blockIdx.x == stall_wg) return;
     gu64* gran = (gu64*)gran_;
     const int KB = split_kblocks(N);
     const int W = persist_waves_of(KB);
@@ -487,10 +491,10 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
     if (e != hipSuccess) return e;
     if (g_persist_trace)
         hipLaunchKernelGGL(k_split_persist<true>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
-                           updates, Y0, Yout, gran, err, g_persist_trace, g_persist_trace_n);
+                           updates, Y0, Yout, gran, err, g_persist_trace, g_persist_trace_n, g_persist_stall_wg);
     else
         hipLaunchKernelGGL(k_split_persist<false>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
-                           updates, Y0, Yout, gran, err, nullptr, 0);
+                           updates, Y0, Yout, gran, err, nullptr, 0, g_persist_stall_wg);
     return hipGetLastError();
 }
 

@@ -104,6 +104,8 @@ SIGNATURES = {
     "pqp_tune_gj_blocked": (C.c_int, [C.c_int]),
     "pqp_tune_batch_converge": (C.c_int, [C.c_int]),
     "pqp_tune_persist_fit_cus": (C.c_int, [C.c_int]),
+    "pqp_tune_persist_stall": (C.c_int, [C.c_int]),
+    "pqp_tune_converge_grid": (C.c_int, [C.c_int, C.c_int]),
     "pqp_tune_last_path": (C.c_int, [C.POINTER(C.c_longlong)]),
     "pqp_tune_converge_chunk": (C.c_int, [C.c_int]),
     "pqp_tune_converge_trace": (C.c_int, [_vp, C.c_int]),

@@ -114,7 +114,7 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
 
 
 @pytest.mark.parametrize("src,name", [
-    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_i"),
+    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_ii"),
     ("pqp_converge.hip", "_ZN3pqp12_GLOBAL__N_118k_converge_persistILb0EEEvNS_6CvArgsE"),
 ])
 def test_persistent_kernels_do_not_spill(src, name):
