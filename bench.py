@@ -110,9 +110,9 @@ def parse():
     ap.add_argument("--rowshard-updates", type=int, default=100)
     ap.add_argument("--rowshard-graph", action="store_true",
                     help="at N > 1, also time the row-sharded steps as hipGraph replays (update + RCCL all-gather)")
-    ap.add_argument("--leg-timeout", type=float, default=240.0,
+    ap.add_argument("--leg-timeout", type=float, default=150.0,
                     help="seconds an optional leg (gather, rowshard, ...) may run before the line is printed without it")
-    ap.add_argument("--dist-timeout", type=float, default=420.0,
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="process-group timeout (s); longer than --leg-timeout")
     return ap.parse_args()
 
@@ -613,12 +613,18 @@ class Emitter:
     `leg_timeout_s` (a collective whose peer never arrives) makes the
     watchdog print the line with that leg marked as timed out and end the
     process with status 0 -- on every rank, before the process group's own
-    timeout would abort it.  So no optional leg can cost the job its line."""
+    timeout would abort it.  So no optional leg can cost the job its line.
+    `abort_on_failure` (multi-rank jobs): a leg that fails ends the process
+    at once, after rank 0 has printed: a peer may still be inside one of that
+    leg's collectives, and any later leg's collectives would meet it there
+    out of order -- leaving, the rank unblocks gloo peers at once (the
+    connection closes); RCCL peers end by their own watchdog."""
 
-    def __init__(self, rank: int, result: dict | None, leg_timeout_s: float):
+    def __init__(self, rank: int, result: dict | None, leg_timeout_s: float, abort_on_failure: bool = False):
         import threading
 
         self.rank, self.result, self.timeout = rank, result, float(leg_timeout_s)
+        self.abort = bool(abort_on_failure)
         self._lock = threading.Lock()
         self._printed = False
         self.failed = False
@@ -644,6 +650,7 @@ class Emitter:
     def leg(self, name: str, fn):
         import threading
 
+        print(f"bench: rank {self.rank}: {name} ...", file=sys.stderr, flush=True)  # progress (stderr)
         t = threading.Timer(self.timeout, self._expire, args=(name,))
         t.daemon = True
         t.start()
@@ -657,6 +664,11 @@ class Emitter:
         with self._lock:
             if self.result is not None and not self._printed:
                 self.result[name] = out
+        if self.failed and self.abort:
+            self.emit()
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
         return out
 
 
@@ -796,7 +808,7 @@ def main():
     # optional legs run, each under the Emitter's guard.
     result = headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse) \
         if rank == 0 else None
-    em = Emitter(rank, result, args.leg_timeout)
+    em = Emitter(rank, result, args.leg_timeout, abort_on_failure=world > 1)
 
     if dist is not None:  # gather Y* to rank 0 over RCCL (reported separately, not in `value`)
         def gather_leg():

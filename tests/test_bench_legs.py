@@ -156,3 +156,44 @@ def test_emitter_prints_once_and_records_errors(capsys):
     em1.leg("x", lambda: {})
     em1.emit()
     assert capsys.readouterr().out == ""
+
+
+def test_failed_leg_ends_every_rank_before_the_next_leg(tmp_path):
+    """Two collective legs, rank 1 failing inside the first (abort_on_failure,
+    as bench.main runs N > 1): rank 0 prints the line with the first leg's
+    error, nobody meets a peer inside the wrong leg's collectives, and the job
+    ends quickly with status 0."""
+    code = f"""
+import os, sys
+sys.path.insert(0, {str(ROOT)!r}); sys.path.insert(0, {str(ROOT / 'tests')!r})
+sys.path.insert(0, {str(ROOT / 'pqp-for-mpc_amd')!r})
+from datetime import timedelta
+import torch, torch.distributed as dist
+import bench
+from test_bench_legs import _HalfBlock
+rank = int(os.environ['RANK'])
+os.environ['PQP_BENCH_FAULT'] = 'rowshard:1'
+dist.init_process_group('gloo', timeout=timedelta(seconds=60))
+em = bench.Emitter(rank, {{'value': 5.0}} if rank == 0 else None, 60, abort_on_failure=True)
+for name, n in (('rowshard', 16), ('rowshard_8', 8)):
+    em.leg(name, lambda n=n: bench.rowshard_bench(None, dist, rank, 2, torch.device('cpu'), n, 20, graph=False,
+                                                  make_block=_HalfBlock))
+em.emit()
+dist.destroy_process_group()
+"""
+    out_file = tmp_path / "out.txt"
+    bench = _bench()
+    t0 = time.monotonic()
+    with open(out_file, "w") as f:
+        old = os.dup(1)
+        os.dup2(f.fileno(), 1)
+        try:
+            rc = bench.launch_ranks(2, [sys.executable, "-c", code], grace_s=30)
+        finally:
+            os.dup2(old, 1)
+            os.close(old)
+    assert rc == 0 and time.monotonic() - t0 < 90
+    lines = [ln for ln in out_file.read_text().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, lines
+    rec = json.loads(lines[0])
+    assert rec["value"] == 5.0 and "error" in rec["rowshard"] and "rowshard_8" not in rec
