@@ -65,7 +65,7 @@ constexpr int kLateGate = 1;
 #endif
 constexpr int kTPollSleep = PQP_T_POLL_SLEEP;  // s_sleep units (64 clocks) between the T roles' and DEC's sweeps
 static_assert(kP0 <= 64 && kP1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");  // waves 4, 5 (sharing SIMDs with 0, 1) form products once this wave is done
-constexpr int kMaxW = 6;   // waves for K <= 1024
+constexpr int kMaxW = 7;   // waves per workgroup: the chain roles use up to 6 (K <= 1024), DEC 7
 #ifndef PQP_CV_DIAG  // timing diagnostic only (wrong results): 1 UPD alone, 2 UPD + T1, 3 UPD + T1-T3; DEC decides blind
 #define PQP_CV_DIAG 0
 #endif
@@ -80,9 +80,9 @@ constexpr int kMaxW = 6;   // waves for K <= 1024
 #endif
 constexpr int kR = PQP_CONVERGE_RING;  // ring depth (iterates in flight), a power of 2
 static_assert((kR & (kR - 1)) == 0, "ring slots are iterate & (kR - 1)");
-constexpr int kDecW = 6;     // DEC's waves: the decision, then the dot waves (dec_dots)
+constexpr int kDecW = 7;     // DEC's waves: the decision, then the dot waves (dec_dots)
 constexpr int kDots = 4;     // computeCost's dots, hand-off word 1..4 of a ring slot
-constexpr int kDecBufs = 6;  // product buffers: waves 1-4 one each, wave 5 two
+constexpr int kDecBufs = 8;  // product buffers: waves 1-4 one each, waves 5 and 6 two each
 constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
 constexpr int kDecChunk = 256;  // dot terms per unrolled chunk
 constexpr int kDecAhead = 4;    // groups of 16 terms read ahead of the adds
@@ -205,7 +205,7 @@ struct CvArgs {
     long long* decided;   // last iterate DEC let through
     int* err;
     float *Yout, *Uout;
-    u64* trace;           // tuning: [2][iterate][29][4] s_memrealtime, then s_memtime marks of workgroup 0 of each role
+    u64* trace;           // tuning: [2][iterate][kTraceIds][4] s_memrealtime, then s_memtime marks of workgroup 0 of each role
     int trace_n;
     int stall_wg;  // tuning: this workgroup never runs (error-path tests; -1: none)
 };
@@ -669,8 +669,9 @@ __device__ bool ring_copy(const CvArgs& a, const u64* ring, int n, int slot, uns
 // LDS word).  ND = 1: dot `dot0` (1: Fd.Y, 4: (Y'Qd).Y; N terms) of every
 // ustep-th iterate from ustart -- two waves per dot take the even and the odd
 // iterates, so each has two periods for its gather and its N-long sum.  ND = 2:
-// dots 2 ((U'Qp).U) and 3 (Fp.U) of every iterate, one U stream, their two
-// M-long chains side by side.
+// dots 2 ((U'Qp).U) and 3 (Fp.U), one U stream, their two M-long chains side
+// by side -- also on two waves, the even and the odd iterates (one wave for
+// both parities was the bound of an all-feasible solve).
 template <int ND, bool TRACE>
 __device__ __forceinline__ void dec_dots(const CvArgs& a, int d, int dot0, float* pr0, float* pr1, long long ustart,
                                          int ustep, u64* dres) {
@@ -822,7 +823,7 @@ __device__ __forceinline__ void dec_dots(const CvArgs& a, int d, int dot0, float
 }
 
 // DEC: wave 0 gathers the feasibility words of T3, receives the four dots
-// from waves 1-5 (dec_dots) and decides (terminate :673-687, loop control
+// from waves 1-6 (dec_dots) and decides (terminate :673-687, loop control
 // :716-724), so the decision of iterate u overlaps the dots of u + 1.
 template <bool TRACE>
 __device__ void decide_role(const CvArgs& a, float* lds) {
@@ -920,7 +921,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
         }
         return;
     }
-    // ---- waves 1..5: the dots (parity waves for the N-long ones) ----
+    // ---- waves 1..6: the dots, each on two parity waves ----
     auto buf = [&](int i) { return prb + (size_t)i * (nmax + 32); };
     const long long ue = a.u0 + ((a.u0 & 1) ? 1 : 0);  // first even iterate
     const long long uo = a.u0 + ((a.u0 & 1) ? 0 : 1);  // first odd iterate
@@ -929,7 +930,8 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
         case 2: dec_dots<1, TRACE>(a, d, 1, buf(1), nullptr, uo, 2, dres); break;
         case 3: dec_dots<1, TRACE>(a, d, 4, buf(2), nullptr, ue, 2, dres); break;
         case 4: dec_dots<1, TRACE>(a, d, 4, buf(3), nullptr, uo, 2, dres); break;
-        default: dec_dots<2, TRACE>(a, d, 2, buf(4), buf(5), a.u0, 1, dres); break;
+        case 5: dec_dots<2, TRACE>(a, d, 2, buf(4), buf(5), ue, 2, dres); break;
+        default: dec_dots<2, TRACE>(a, d, 2, buf(6), buf(7), uo, 2, dres); break;
     }
 }
 

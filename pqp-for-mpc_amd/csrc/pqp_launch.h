@@ -194,7 +194,7 @@ hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Q
 hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s);
 extern int g_converge_persist_off;
 extern int g_persist_stall_wg;  // tuning: workgroup of each persistent launch that never runs (-1: none)
-extern unsigned long long* g_converge_trace;  // tuning: [iterate][29][4] words (pqp_tune_converge_trace)
+extern unsigned long long* g_converge_trace;  // tuning: [iterate][4 * 7 + 7][4] words (pqp_tune_converge_trace)
 extern int g_converge_trace_n;
 
 hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s);

@@ -13,7 +13,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
 ROLES = ("UPD", "T1", "T2", "T3")
-NIDS = 30  # 4 chain roles x 6 waves, then DEC's 6 waves (pqp_converge.hip kTraceIds)
+KW = 7  # wave slots per role (pqp_converge.hip kMaxW)
+NIDS = 5 * KW  # 4 chain roles x KW wave slots, then DEC's kDecW = KW waves (pqp_converge.hip kTraceIds)
 # DEC's waves: 0 decides; 1, 2 dot 1 (Fd.Y) of even / odd iterates; 3, 4 dot 4
 # ((Y'Qd).Y) of even / odd iterates; 5 dots 2 and 3 of every iterate
 
@@ -54,28 +55,28 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
     med = lambda x: float(np.median(x))
     out = {"n_dual": N, "m": M, "h": r["h"], "iterates": [lo, hi], "roles": {}}
     # the shader clock the launch ran at: clocks over chip time, per role's wave 0
-    out["clock_GHz"] = {role: float((clk[hi, ri * 6, 0] - clk[lo, ri * 6, 0]) / ((t[hi, ri * 6, 0] - t[lo, ri * 6, 0]) * 1e3))
+    out["clock_GHz"] = {role: float((clk[hi, ri * KW, 0] - clk[lo, ri * KW, 0]) / ((t[hi, ri * KW, 0] - t[lo, ri * KW, 0]) * 1e3))
                         for ri, role in enumerate(ROLES)}
     for ri, role in enumerate(ROLES):
         for w in range(W[role]):
-            i = ri * 6 + w
+            i = ri * KW + w
             x = t[lo:hi, i]
             out["roles"][f"{role}.w{w}"] = {
                 "period": med(np.diff(t[lo:hi + 1, i, 0])), "stage": med(x[:, 1] - x[:, 0]),
                 "turn_wait": med(x[:, 2] - x[:, 1]) if w else 0.0, "adds": med(x[:, 3] - x[:, 2]) if w else
                 med(x[:, 3] - x[:, 1])}
-    x = t[lo:hi, 24]
-    out["roles"]["DEC.w0 (decision)"] = {"period": med(np.diff(t[lo:hi + 1, 24, 0])),
+    x = t[lo:hi, 4 * KW]
+    out["roles"]["DEC.w0 (decision)"] = {"period": med(np.diff(t[lo:hi + 1, 4 * KW, 0])),
                                          "feasibility": med(x[:, 1] - x[:, 0]), "dots_wait": med(x[:, 2] - x[:, 1]),
                                          "decide": med(x[:, 3] - x[:, 2])}
     for d in range(1, 6):
-        i = 24 + d
+        i = 4 * KW + d
         x = t[lo:hi, i]
         on = x[:, 0] > 0  # parity waves mark every other iterate
         xs = x[on]
         out["roles"][f"DEC.w{d}"] = {"period": med(np.diff(xs[:, 0])) if len(xs) > 1 else 0.0,
                                      "gather": med(xs[:, 1] - xs[:, 0]), "sum": med(xs[:, 2] - xs[:, 1])}
-    lastw = lambda role: ROLES.index(role) * 6 + W[role] - 1
+    lastw = lambda role: ROLES.index(role) * KW + W[role] - 1
     u = np.arange(lo, hi)
     out["handover"] = {
         "UPD done u -> UPD.w0 staged u+1": med(t[u + 1, 0, 1] - t[u, lastw("UPD"), 3]),
@@ -84,10 +85,10 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
         "T2 done u -> T3.w0 staged u": med(t[u, 18, 1] - t[u, lastw("T2"), 3]),
         "T3 done u -> DEC.w5 gathered u": med(t[u, 29, 1] - t[u, lastw("T3"), 3]),
         "T1 done u -> DEC dot-4 wave gathered u": med(np.maximum(t[u, 27, 1], t[u, 28, 1]) - t[u, lastw("T1"), 3]),
-        "DEC decided u": med(t[u, 24, 3] - t[u, lastw("UPD"), 3]),
-        "y_u published -> DEC decided u (latency)": med(t[u, 24, 3] - t[u - 1, lastw("UPD"), 3]),
+        "DEC decided u": med(t[u, 4 * KW, 3] - t[u, lastw("UPD"), 3]),
+        "y_u published -> DEC decided u (latency)": med(t[u, 4 * KW, 3] - t[u - 1, lastw("UPD"), 3]),
         "DEC decided u-8 -> y_u published": med(t[u - 1, lastw("UPD"), 3] - t[u - 8, 24, 3]),
-        "UPD ahead of DEC (iterates)": med(np.searchsorted(t[:, lastw("UPD"), 3], t[u, 24, 3]) - u),
+        "UPD ahead of DEC (iterates)": med(np.searchsorted(t[:, lastw("UPD"), 3], t[u, 4 * KW, 3]) - u),
     }
     # absolute timeline of a few iterates, relative to DEC's decision of u - 8
     # (the decision that lets y_u be published)
