@@ -69,7 +69,7 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
     out["roles"]["DEC.w0 (decision)"] = {"period": med(np.diff(t[lo:hi + 1, 4 * KW, 0])),
                                          "feasibility": med(x[:, 1] - x[:, 0]), "dots_wait": med(x[:, 2] - x[:, 1]),
                                          "decide": med(x[:, 3] - x[:, 2])}
-    for d in range(1, 6):
+    for d in range(1, KW):
         i = 4 * KW + d
         x = t[lo:hi, i]
         on = x[:, 0] > 0  # parity waves mark every other iterate
@@ -87,22 +87,22 @@ def main(N: int = 1024, cap: int = 200, n_trace: int = 120):
         "T1 done u -> DEC dot-4 wave gathered u": med(np.maximum(t[u, 27, 1], t[u, 28, 1]) - t[u, lastw("T1"), 3]),
         "DEC decided u": med(t[u, 4 * KW, 3] - t[u, lastw("UPD"), 3]),
         "y_u published -> DEC decided u (latency)": med(t[u, 4 * KW, 3] - t[u - 1, lastw("UPD"), 3]),
-        "DEC decided u-8 -> y_u published": med(t[u - 1, lastw("UPD"), 3] - t[u - 8, 24, 3]),
+        "DEC decided u-8 -> y_u published": med(t[u - 1, lastw("UPD"), 3] - t[u - 8, 4 * KW, 3]),
         "UPD ahead of DEC (iterates)": med(np.searchsorted(t[:, lastw("UPD"), 3], t[u, 4 * KW, 3]) - u),
     }
     # absolute timeline of a few iterates, relative to DEC's decision of u - 8
     # (the decision that lets y_u be published)
     sample = {}
     for uu in range(lo, lo + 4):
-        base = t[uu - 8, 24, 3]
+        base = t[uu - 8, 4 * KW, 3]
         ev = {"y_u published (UPD last wave)": t[uu - 1, lastw("UPD"), 3],
               "T1.w0 staged": t[uu, 6, 1], "T1 last done": t[uu, lastw("T1"), 3],
               "T2.w0 staged": t[uu, 12, 1], "T2 last done": t[uu, lastw("T2"), 3],
               "T3.w0 staged": t[uu, 18, 1], "T3 last done": t[uu, lastw("T3"), 3],
               "DEC dot-4 gathered": max(t[uu, 27, 1], t[uu, 28, 1]), "DEC dot-4 summed": max(t[uu, 27, 2], t[uu, 28, 2]),
               "DEC.w5 summed": t[uu, 29, 2],
-              "DEC.w0 feasibility": t[uu, 24, 1], "DEC.w0 dots in": t[uu, 24, 2],
-              "DEC decided": t[uu, 24, 3]}
+              "DEC.w0 feasibility": t[uu, 4 * KW, 1], "DEC.w0 dots in": t[uu, 4 * KW, 2],
+              "DEC decided": t[uu, 4 * KW, 3]}
         sample[f"u={uu}"] = {k: round(float(v - base), 2) for k, v in ev.items()}
     out["timeline_from_decision_u-8"] = sample
     print(json.dumps(out, indent=1))
