@@ -75,8 +75,11 @@ int pqp_tune_converge_grid(int N, int M);
  * off.  bit 1: the unprepared pqp_batch_solve makes transposed copies of Gp
  * and Qp_inv per call (pqp_batch_prepare makes them once when asked); bit 2:
  * 4-byte loads only (the 8/16-byte load forms, used by default when N and M
- * are multiples of 4 and the arrays 16-byte aligned, are turned off).  Every
- * setting is bit-identical.  Returns the previous value. */
+ * are multiples of 4 and the arrays 16-byte aligned, are turned off); bit 3:
+ * the solver built for four workgroups per CU; bit 4: checkFeas sums every
+ * row (by default, with the transposes, it sums the first 256 rows and stops
+ * there when one is over its bound -- terminate() returns 0 either way).
+ * Every setting is bit-identical.  Returns the previous value. */
 int pqp_tune_batch_converge(int opts);
 
 /* Batched Gauss_Jordan (n <= 1024): the blocked kernel (one read and write of

@@ -319,7 +319,8 @@ bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead 
 bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
 int g_wide_min_n = 384;       // converge mode: smallest N solved over many workgroups (problem_run_wide)
 int g_batch_opts = 0;         // tuning (pqp_tune_batch_converge): bit 0 no fused Y'Qd pass, bit 1 pqp_batch_solve
-                              // makes transposed Gp / Qp_inv per call (bit 2, 4-byte loads only, is g_single_scalar)
+                              // makes transposed Gp / Qp_inv per call, bit 4 checkFeas over every row (bit 2,
+                              // 4-byte loads only, is g_single_scalar; bit 3 the 4-per-CU build, g_single_occ4)
 inline bool batch_unfused() { return (g_batch_opts & 1) != 0; }
 
 // Allocate the per-problem work buffers and, for the large path, the
@@ -1533,6 +1534,7 @@ int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float
     a.sym = fuse ? d_sym : nullptr;
     a.GpT = path == 2 && mode == PQP_MODE_CONVERGE ? d_GpT : nullptr;
     a.QinvT = path == 2 && mode == PQP_MODE_CONVERGE ? d_QinvT : nullptr;
+    a.feas_split = (g_batch_opts & 16) ? 0 : 1;
     a.Fp = d_Fp;
     a.Mp = d_Mp;
     a.Gp = d_Gp;
@@ -1916,7 +1918,7 @@ extern "C" int pqp_tune_last_path(long long* fallbacks) {
 
 extern "C" int pqp_tune_batch_converge(int opts) {
     const int old = pqp::g_batch_opts | (pqp::g_single_scalar ? 4 : 0) | (pqp::g_single_occ4 ? 8 : 0);
-    pqp::g_batch_opts = opts & 3;
+    pqp::g_batch_opts = opts & 19;
     pqp::g_single_scalar = (opts & 4) ? 1 : 0;
     pqp::g_single_occ4 = (opts & 8) ? 1 : 0;
     return old;

@@ -1560,7 +1560,31 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
             __syncthreads();
             // checkFeas :632-641
             int bad = 0;
-            if (VEC && A.GpT) {
+            int infeasible = 0;
+            if (VEC && A.GpT && A.feas_split && N > NT) {
+                // first NT rows (one per lane), then the rest only if none of them
+                // is over its bound: terminate() returns 0 on ANY row over its
+                // bound (:677), so a violation among the first rows decides the
+                // iterate and the other rows' sums change nothing observable
+                // (checkFeas's products are used for nothing else)
+                {
+                    const float s0 = seq_dot<kSU>(A.GpT + tid, N, Us, M);
+                    const float kp = A.Kp[tid];
+                    if (s0 > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                }
+                infeasible = __syncthreads_or(bad);
+                if (!infeasible) {
+                    for (int i0 = NT + 4 * tid; i0 < N; i0 += 4 * NT) {
+                        float t[4];
+                        col_dotv<4, kSU4>(A.GpT + i0, N, Us, M, t);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const float kp = A.Kp[i0 + c];
+                            if (t[c] > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                        }
+                    }
+                }
+            } else if (VEC && A.GpT) {
                 for (int i0 = 4 * tid; i0 < N; i0 += 4 * NT) {
                     float t[4];
                     col_dotv<4, kSU4>(A.GpT + i0, N, Us, M, t);
@@ -1579,7 +1603,7 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
                     if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
                 }
             }
-            const int infeasible = __syncthreads_or(bad);
+            infeasible = __syncthreads_or(bad);
             was_feasible = !infeasible;
             int stop = 0;
             if (!infeasible) {

@@ -32,6 +32,7 @@ struct SolveArgs {
     int* pending;  // optional: +1 per problem still running when a launch ends
     const int* sym;  // optional (k_solve_single): sym[b] != 0 when problem b's Qd is bit-symmetric
     const float *GpT, *QinvT;  // optional (k_solve_single): transposes of Gp (M x N) and Qp_inv, per problem
+    int feas_split;  // k_solve_single with GpT: checkFeas decides on its first rows when one is over its bound
 };
 hipError_t launch_transpose_b(int B, const float* src, int rows, int cols, float* dst, hipStream_t s);
 // sym[b] = nonzero iff problem b's row-major Qd equals its transpose bit for bit

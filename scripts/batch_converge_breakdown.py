@@ -47,7 +47,7 @@ def main(N=1024, B=4096, K=4):
     out = {"n_dual": N, "m": M, "problems": B, "K": K}
     GB = B * 1e-9
     variants = {"fused_T": (0, True), "unfused_T": (1, True), "fused": (0, False), "unfused": (1, False),
-                "fused_T_occ4": (8, True), "unfused_T_occ4": (9, True)}
+                "fused_T_occ4": (8, True), "unfused_T_occ4": (9, True), "fused_T_fullfeas": (16, True)}
     names = sys.argv[4].split(",") if len(sys.argv) > 4 else list(variants)
     for name in names:
         opts, tr = variants[name]

@@ -48,7 +48,8 @@ def test_batch_testfile_converges_like_reference(gpu_lib, orc, tmp_path, opts, t
 
 
 @pytest.mark.parametrize("opts,tr,N,M", [(0, True, 256, 128), (0, False, 256, 128), (1, True, 256, 128),
-                                         (4, True, 256, 128), (0, True, 201, 61), (0, True, 204, 62)])
+                                         (4, True, 256, 128), (16, True, 256, 128), (0, True, 512, 64),
+                                         (16, True, 512, 64), (0, True, 201, 61), (0, True, 204, 62)])
 @pytest.mark.parametrize("feasible", [False, True])
 def test_batch_synthetic_capped_vs_oracle(gpu_lib, orc, opts, tr, N, M, feasible):
     """Capped solves; `feasible`: Kp = 1e30 seen by checkFeas only, so every
