@@ -591,9 +591,7 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
            "note": "us_per_update = the faster of eager launches (pqp_rowblock_update + all_gather_into_tensor per "
                    "update at N>1 ranks) and graph replays"}
     if make_block is None:
-        L = pqp_amd.lib()
-        lean_min = L.pqp_tune_lean_min_n(0)  # read the setting (and restore it)
-        L.pqp_tune_lean_min_n(lean_min)
+        lean_min = pqp_amd.tune_get("lean_min_n")
         lean = lean_min > 0 and rows * N >= lean_min * lean_min  # row blocks choose the lean relay by rows x N
         bpe = 4 if lean else 8  # bytes per matrix entry the update streams
         out["layout"] = "Qd packets, k_lean_relay (4 B/entry)" if lean else "stored split matrices (8 B/entry)"

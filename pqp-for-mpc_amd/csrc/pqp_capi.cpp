@@ -312,16 +312,12 @@ struct pqp_rowblock {
 };
 
 namespace pqp {
+Tuning g_tune;
+
 namespace {
 
 constexpr size_t kLdsBudget = 150 * 1024;
-bool g_force_small = false;   // tuning: route N <= 32 to k_solve_small instead of k_solve_tiny
-bool g_force_single = false;  // tuning: fixed mode of a large problem on one workgroup (k_solve_single)
-int g_wide_min_n = 384;       // converge mode: smallest N solved over many workgroups (problem_run_wide)
-int g_batch_opts = 0;         // tuning (pqp_tune_batch_converge): bit 0 no fused Y'Qd pass, bit 1 pqp_batch_solve
-                              // makes transposed Gp / Qp_inv per call, bit 4 checkFeas over every row (bit 2,
-                              // 4-byte loads only, is g_single_scalar; bit 3 the 4-per-CU build, g_single_occ4)
-inline bool batch_unfused() { return (g_batch_opts & 1) != 0; }
+inline bool batch_unfused() { return (g_tune.batch_opts & 1) != 0; }
 
 // Allocate the per-problem work buffers and, for the large path, the
 // column-major copy and theta.  The nine input buffers must already hold the
@@ -444,7 +440,7 @@ int pick_lw(int N) { return use_lean(N, N) ? lean_pick_lw(N) : split_pick_lw(N);
 
 // The relay update's operand of the whole problem (rows 0..N-1), built on
 // first use (and rebuilt if lw or the layout changes): the stored split
-// matrices with lw row sides per workgroup, or, from n_dual >= g_lean_min_n,
+// matrices with lw row sides per workgroup, or, from n_dual >= g_tune.lean_min_n,
 // Qd itself with lw rows per workgroup (k_lean_relay, half the bytes).
 int ensure_split(pqp_problem& P, int lw, hipStream_t s) {
     const int N = P.N;
@@ -615,7 +611,7 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     // one persistent launch when its workgroups can all be resident; if one of
     // its waits still expires (CUs held by other work), the solve restarts on
     // the graph-replayed relay below (fixed mode restarts from Y = 1000)
-    if (!g_persist_off && N <= persist_max_n() && split_persist_fits(N)) {
+    if (!g_tune.persist_off && N <= persist_max_n() && split_persist_fits(N)) {
         const int rc = problem_run_fixed_persist(P, updates, out, s);
         if (rc != kPersistStalled) return rc;
         ++g_persist_fallbacks;
@@ -624,8 +620,8 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     PQP_TRY(ensure_split(P, lw, s));
     // every setting the captured launches bake in as an argument, the relay
     // wait budget's value included
-    const long long variant = (long long)g_split_u | ((long long)g_split_kind << 4) | ((long long)lw << 8) |
-                              ((long long)use_lean(N, N) << 16) | ((long long)(unsigned)g_relay_spin_max << 24);
+    const long long variant = (long long)g_tune.split_u | ((long long)g_tune.split_kind << 4) | ((long long)lw << 8) |
+                              ((long long)use_lean(N, N) << 16) | ((long long)(unsigned)g_tune.relay_spin_max << 24);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
         P.chunk_ready = false;
@@ -660,10 +656,9 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
 // Converge mode of a problem with N, M <= 1024 as ONE persistent launch
 // (pqp_converge.hip): the update and the stages of terminate() run as
 // concurrent roles, terminate(Y_u) beside the update to Y_{u+1}.  Launches
-// decide at most g_converge_chunk iterates each and are chained through P.Y.
-long long g_converge_chunk = 1 << 16;  // tuning: iterates decided per launch
+// decide at most g_tune.converge_chunk iterates each and are chained through P.Y.
 bool converge_persist_fits(int N, int M) {
-    if (g_converge_persist_off) return false;
+    if (g_tune.converge_persist_off) return false;
     const int G = converge_persist_wgs(N, M, nullptr);
     if (G == 0) return false;
     int dev = 0, cus = 0, lds = 0;
@@ -671,7 +666,7 @@ bool converge_persist_fits(int N, int M) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) return false;
     if (converge_persist_lds_bytes(N, M) > (size_t)lds) return false;
-    if (g_persist_fit_cus > 0) cus = g_persist_fit_cus;
+    if (g_tune.persist_fit_cus > 0) cus = g_tune.persist_fit_cus;
     // every workgroup of the launch resident at once (its roles wait on each other)
     return (long long)converge_persist_per_cu(N, M) * cus >= G;
 }
@@ -704,7 +699,7 @@ int problem_run_converge_persist(pqp_problem& P, long long max_updates, SolveOut
     ConvergeLaunch L{};
     L.N = N;
     L.M = M;
-    L.chunk = g_converge_chunk;
+    L.chunk = g_tune.converge_chunk;
     L.cap = max_updates;
     L.SP = P.SPp.f();
     L.A1 = P.CA1.f();
@@ -782,10 +777,10 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     int* flag = static_cast<int*>(P.wflag.p);
     long long* cap = static_cast<long long*>(P.wcap.p);
     // every launch argument the capture bakes in (cap: a device word)
-    const long long key = (long long)(((unsigned long long)(unsigned)g_relay_spin_max << 32) |
+    const long long key = (long long)(((unsigned long long)(unsigned)g_tune.relay_spin_max << 32) |
                                       ((unsigned long long)use_lean(N, N) << 24) |
-                                      ((unsigned long long)(g_wide_flags & 0xff) << 16) |
-                                      ((unsigned long long)(g_split_kind & 0xff) << 8) | (unsigned long long)(lw & 0xff));
+                                      ((unsigned long long)(g_tune.wide_flags & 0xff) << 16) |
+                                      ((unsigned long long)(g_tune.split_kind & 0xff) << 8) | (unsigned long long)(lw & 0xff));
     int* rerr = static_cast<int*>(P.rerr.p);
     if (!P.wgraph || P.wgraph_key != key) {
         if (P.wgraph) {
@@ -802,7 +797,7 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
         // (tuning bit; measured slower as a graph branch): if the iteration
         // stops or hits the cap, its result in `nxt` is not used, and the next
         // iteration's launches, gated on the status, do nothing.
-        const bool fork = (g_wide_flags & 1) != 0;
+        const bool fork = (g_tune.wide_flags & 1) != 0;
         auto iteration = [&](const float* cur, float* nxt) -> hipError_t {
             hipError_t e = hipSuccess;
             if (fork) {
@@ -896,13 +891,13 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
 int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_updates, bool resume, SolveOut& out,
                 hipStream_t s) {
     const int N = P.N, M = P.M;
-    if (mode == kModeFixed && !P.small && !g_force_single && !resume) return problem_run_fixed_split(P, num_iter, out, s);
-    if (mode == kModeConverge && !g_force_single && !resume) {
+    if (mode == kModeFixed && !P.small && !g_tune.force_single && !resume) return problem_run_fixed_split(P, num_iter, out, s);
+    if (mode == kModeConverge && !g_tune.force_single && !resume) {
         // the one-wave solver stays fastest for N, M <= 32 (0.65 us per iteration
         // at 32/16 against 2.3 on the persistent launch); from n_dual 48 up the
         // persistent launch wins (scripts/converge_crossover.py)
-        const bool tiny = N <= 32 && M <= 32 && !g_force_small;
-        const bool wide_ok = N >= g_wide_min_n && (!P.small || g_wide_min_n <= 0);
+        const bool tiny = N <= 32 && M <= 32 && !g_tune.force_small;
+        const bool wide_ok = N >= g_tune.wide_min_n && (!P.small || g_tune.wide_min_n <= 0);
         if (!tiny && converge_persist_fits(N, M)) {
             const int rc = problem_run_converge_persist(P, max_updates, out, s);
             if (rc != kPersistStalled) return rc;
@@ -944,7 +939,7 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
     a.chunk = chunk < 1 ? 1 : chunk;
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     for (;;) {
-        if (P.N <= 32 && P.M <= 32 && !g_force_small)
+        if (P.N <= 32 && P.M <= 32 && !g_tune.force_small)
             PQP_HIP(launch_solve_tiny(a, dst, s));
         else if (P.small)
             PQP_HIP(launch_solve_small(a, dst, s));
@@ -1446,7 +1441,7 @@ int pqp_batch_compute_mp(int B, int nd, int ns, const float* d_Mp1, const float*
 // memory (k_solve_single; needs the prepared data of pqp_batch_prepare), -1
 // too large for any.
 static int batch_path(int N, int M) {
-    if (N <= 32 && M <= 32 && !g_force_small) return 0;
+    if (N <= 32 && M <= 32 && !g_tune.force_small) return 0;
     if (solve_small_lds_bytes(N, M) <= kLdsBudget) return 1;
     if (solve_single_lds_bytes(round4(N), round4(M), false) <= kLdsBudget) return 2;
     return -1;
@@ -1534,7 +1529,7 @@ int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float
     a.sym = fuse ? d_sym : nullptr;
     a.GpT = path == 2 && mode == PQP_MODE_CONVERGE ? d_GpT : nullptr;
     a.QinvT = path == 2 && mode == PQP_MODE_CONVERGE ? d_QinvT : nullptr;
-    a.feas_split = (g_batch_opts & 16) ? 0 : 1;
+    a.feas_split = (g_tune.batch_opts & 16) ? 0 : 1;
     a.Fp = d_Fp;
     a.Mp = d_Mp;
     a.Gp = d_Gp;
@@ -1579,7 +1574,7 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
         PQP_TRY(ensure_device());
         PQP_TRY(theta.floats((size_t)B * N));
         PQP_TRY(sym.alloc(sizeof(int) * (size_t)B));
-        if ((g_batch_opts & 2) && mode == PQP_MODE_CONVERGE && d_Gp && d_Qp_inv) {
+        if ((g_tune.batch_opts & 2) && mode == PQP_MODE_CONVERGE && d_Gp && d_Qp_inv) {
             PQP_TRY(GpT.floats((size_t)B * N * M));
             PQP_TRY(QinvT.floats((size_t)B * M * M));
         }
@@ -1851,139 +1846,104 @@ void input(float* qp_inv, float* Fp1, float* Fp2, float* Fp3, float* Mp1, float*
 // ---------------------------------------------------------------------------
 #include "../../include/pqp_tuning.h"
 
-extern "C" int pqp_tune_set_variant(int variant) {
-    const int old = (pqp::g_force_small ? 0x100 : 0) | (pqp::g_force_single ? 0x200 : 0) |
-                    (pqp::g_fixed_tiny_old ? 0x400 : 0) |
-                    (pqp::g_split_u << 12) | (pqp::g_split_kind << 14) |
-                    ((pqp::g_split_lw ? __builtin_ctz(pqp::g_split_lw) - 2 : 0) << 17);
-    pqp::g_split_u = (variant >> 12) & 3;
-    pqp::g_split_kind = (variant >> 14) & 7;
-    const int lwsel = (variant >> 17) & 7;  // 0 auto, 1: 8, 2: 16, 3: 32, 4: 64 lanes per workgroup
-    pqp::g_split_lw = (lwsel >= 1 && lwsel <= 4) ? (4 << lwsel) : 0;
-    pqp::g_force_small = (variant & 0x100) != 0;
-    pqp::g_fixed_tiny_old = (variant & 0x400) != 0;
-    pqp::g_force_single = (variant & 0x200) != 0;
-    return old;
+namespace {
+// key -> knob of pqp::g_tune (pqp_tune / pqp_tune_get)
+struct KnobRef {
+    const char* key;
+    int* i;
+    bool* b;
+    long long* ll;
+};
+const KnobRef* find_knob(const char* key) {
+    using pqp::g_tune;
+    static const KnobRef knobs[] = {
+        {"relay_spin_max", &g_tune.relay_spin_max, nullptr, nullptr},
+        {"lean_min_n", &g_tune.lean_min_n, nullptr, nullptr},
+        {"split_u", &g_tune.split_u, nullptr, nullptr},
+        {"split_lw", &g_tune.split_lw, nullptr, nullptr},
+        {"split_kind", &g_tune.split_kind, nullptr, nullptr},
+        {"wave_pipe_max_b", &g_tune.wave_pipe_max_b, nullptr, nullptr},
+        {"fixed_tiny_old", &g_tune.fixed_tiny_old, nullptr, nullptr},
+        {"fixed_rl_max_b", &g_tune.fixed_rl_max_b, nullptr, nullptr},
+        {"wave_min_b", &g_tune.wave_min_b, nullptr, nullptr},
+        {"matmul_tiled_off", &g_tune.matmul_tiled_off, nullptr, nullptr},
+        {"gj_blocked_off", &g_tune.gj_blocked_off, nullptr, nullptr},
+        {"single_scalar", &g_tune.single_scalar, nullptr, nullptr},
+        {"single_occ4", &g_tune.single_occ4, nullptr, nullptr},
+        {"persist_off", &g_tune.persist_off, nullptr, nullptr},
+        {"persist_stall_wg", &g_tune.persist_stall_wg, nullptr, nullptr},
+        {"persist_fit_cus", &g_tune.persist_fit_cus, nullptr, nullptr},
+        {"wide_flags", &g_tune.wide_flags, nullptr, nullptr},
+        {"converge_persist_off", &g_tune.converge_persist_off, nullptr, nullptr},
+        {"force_small", nullptr, &g_tune.force_small, nullptr},
+        {"force_single", nullptr, &g_tune.force_single, nullptr},
+        {"wide_min_n", &g_tune.wide_min_n, nullptr, nullptr},
+        {"batch_opts", &g_tune.batch_opts, nullptr, nullptr},
+        {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
+    };
+    for (const KnobRef& k : knobs)
+        if (std::strcmp(k.key, key) == 0) return &k;
+    return nullptr;
 }
+long long knob_value(const KnobRef& k) { return k.i ? *k.i : (k.b ? (long long)*k.b : *k.ll); }
+}  // namespace
 
-extern "C" int pqp_tune_fixed_rl_max_b(int b) {
-    const int old = pqp::g_fixed_rl_max_b;
-    pqp::g_fixed_rl_max_b = b;
-    return old;
-}
-
-extern "C" int pqp_tune_wave_min_b(int b) {
-    const int old = pqp::g_wave_min_b;
-    pqp::g_wave_min_b = b;
-    return old;
-}
-
-extern "C" int pqp_tune_wave_pipe_max_b(int b) {
-    const int old = pqp::g_wave_pipe_max_b;
-    pqp::g_wave_pipe_max_b = b;
-    return old;
-}
-
-extern "C" int pqp_tune_persist(int off) {
-    const int old = pqp::g_persist_off;
-    pqp::g_persist_off = off ? 1 : 0;
-    return old;
-}
-
-extern "C" int pqp_tune_persist_trace(void* d_trace, int updates) {
-    if (updates < 0 || (updates > 0 && !d_trace)) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_persist_trace: bad arguments");
-    pqp::g_persist_trace = updates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
-    pqp::g_persist_trace_n = updates;
+extern "C" int pqp_tune(const char* key, long long value, long long* old_value) {
+    const KnobRef* k = key ? find_knob(key) : nullptr;
+    if (!k) return pqp::set_error(PQP_ERR_ARG, "pqp_tune: unknown key '%s'", key ? key : "(null)");
+    if (old_value) *old_value = knob_value(*k);
+    if (std::strcmp(key, "relay_spin_max") == 0) {
+        // 0 restores the default; clamped: a budget near INT_MAX would let a
+        // broken hand-off spin until its counter overflows
+        value = value == 0 ? pqp::kRelaySpinMax : (value > (1 << 30) ? (1 << 30) : value);
+    } else if (std::strcmp(key, "converge_chunk") == 0) {
+        value = value > 0 ? value : (1 << 16);
+    } else if (std::strcmp(key, "persist_stall_wg") == 0) {
+        value = value >= 0 ? value : -1;
+    }
+    if (k->i) *k->i = (int)value;
+    else if (k->b) *k->b = value != 0;
+    else *k->ll = value;
     return PQP_OK;
 }
 
-extern "C" int pqp_tune_persist_stall(int wg) {
-    const int old = pqp::g_persist_stall_wg;
-    pqp::g_persist_stall_wg = wg >= 0 ? wg : -1;
-    return old;
-}
-
-extern "C" int pqp_tune_converge_grid(int N, int M) { return pqp::converge_persist_wgs(N, M, nullptr); }
-
-extern "C" int pqp_tune_persist_fit_cus(int cus) {
-    const int old = pqp::g_persist_fit_cus;
-    pqp::g_persist_fit_cus = cus > 0 ? cus : 0;
-    return old;
-}
-
-extern "C" int pqp_tune_last_path(long long* fallbacks) {
-    if (fallbacks) *fallbacks = pqp::g_persist_fallbacks;
-    return pqp::g_last_path;
-}
-
-extern "C" int pqp_tune_batch_converge(int opts) {
-    const int old = pqp::g_batch_opts | (pqp::g_single_scalar ? 4 : 0) | (pqp::g_single_occ4 ? 8 : 0);
-    pqp::g_batch_opts = opts & 19;
-    pqp::g_single_scalar = (opts & 4) ? 1 : 0;
-    pqp::g_single_occ4 = (opts & 8) ? 1 : 0;
-    return old;
-}
-
-extern "C" int pqp_tune_matmul_tiled(int off) {
-    const int old = pqp::g_matmul_tiled_off;
-    pqp::g_matmul_tiled_off = off ? 1 : 0;
-    return old;
-}
-
-extern "C" int pqp_tune_gj_blocked(int off) {
-    const int old = pqp::g_gj_blocked_off;
-    pqp::g_gj_blocked_off = off ? 1 : 0;
-    return old;
-}
-
-extern "C" int pqp_tune_relay_spin_max(int polls) {
-    const int old = pqp::g_relay_spin_max;
-    // clamped: a budget near INT_MAX would let a broken hand-off spin until its
-    // counter overflows
-    pqp::g_relay_spin_max = polls == 0 ? pqp::kRelaySpinMax : (polls > (1 << 30) ? (1 << 30) : polls);
-    return old;
-}
-
-extern "C" int pqp_tune_lean_min_n(int n) {
-    const int old = pqp::g_lean_min_n;
-    pqp::g_lean_min_n = n;
-    return old;
-}
-
-extern "C" int pqp_tune_converge_persist(int off) {
-    const int old = pqp::g_converge_persist_off;
-    pqp::g_converge_persist_off = off ? 1 : 0;
-    return old;
-}
-
-extern "C" int pqp_tune_converge_trace(void* d_trace, int iterates) {
-    if (iterates < 0 || (iterates > 0 && !d_trace))
-        return pqp::set_error(PQP_ERR_ARG, "pqp_tune_converge_trace: bad arguments");
-    pqp::g_converge_trace = iterates > 0 ? static_cast<unsigned long long*>(d_trace) : nullptr;
-    pqp::g_converge_trace_n = iterates;
+extern "C" int pqp_tune_get(const char* key, long long* value) {
+    if (!key || !value) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_get: null argument");
+    if (std::strcmp(key, "last_path") == 0) {
+        *value = pqp::g_last_path;
+        return PQP_OK;
+    }
+    if (std::strcmp(key, "persist_fallbacks") == 0) {
+        *value = pqp::g_persist_fallbacks;
+        return PQP_OK;
+    }
+    if (std::strcmp(key, "converge_grid") == 0) {  // in: N << 32 | M
+        const long long v = *value;
+        *value = pqp::converge_persist_wgs((int)(v >> 32), (int)(v & 0xffffffff), nullptr);
+        return PQP_OK;
+    }
+    const KnobRef* k = find_knob(key);
+    if (!k) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_get: unknown key '%s'", key);
+    *value = knob_value(*k);
     return PQP_OK;
 }
 
-extern "C" int pqp_tune_converge_chunk(int iterates) {
-    const int old = (int)pqp::g_converge_chunk;
-    pqp::g_converge_chunk = iterates > 0 ? iterates : (1 << 16);
-    return old;
-}
-
-extern "C" int pqp_tune_wide_flags(int flags) {
-    const int old = pqp::g_wide_flags;
-    pqp::g_wide_flags = flags;
-    return old;
-}
-
-extern "C" int pqp_tune_wide_min_n(int n) {
-    const int old = pqp::g_wide_min_n;
-    pqp::g_wide_min_n = n;
-    return old;
+extern "C" int pqp_tune_trace(const char* what, void* d_buf, int n) {
+    if (!what || n < 0 || (n > 0 && !d_buf)) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_trace: bad arguments");
+    auto* buf = n > 0 ? static_cast<unsigned long long*>(d_buf) : nullptr;
+    if (std::strcmp(what, "persist") == 0) {
+        pqp::g_tune.persist_trace = buf;
+        pqp::g_tune.persist_trace_n = n;
+    } else if (std::strcmp(what, "converge") == 0) {
+        pqp::g_tune.converge_trace = buf;
+        pqp::g_tune.converge_trace_n = n;
+    } else {
+        return pqp::set_error(PQP_ERR_ARG, "pqp_tune_trace: unknown timeline '%s'", what);
+    }
+    return PQP_OK;
 }
 
 extern "C" int pqp_tune_glibc_rand(int n, int* out) {
     if (n < 0 || (n > 0 && !out)) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_glibc_rand: bad arguments");
     return pqp::glibc_rand_sequence(n, out);
 }
-

@@ -41,6 +41,7 @@
 // host checks the count against the device's CUs.
 #include "pqp_device.h"
 #include "pqp_launch.h"
+#include "pqp_chain.h"
 
 #include <type_traits>
 
@@ -50,12 +51,8 @@ namespace pqp {
 
 namespace {
 
-typedef unsigned long long u64;
-typedef __attribute__((address_space(1))) u64 gu64;
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef float f2v __attribute__((ext_vector_type(2)));
 
-constexpr int kL = 32;     // output columns (update: row sides) per workgroup
+constexpr int kL = kSliceLanes;  // output columns (update: row sides) per workgroup
 constexpr int kP0 = 24;    // packets (4 values of k) of wave 0's slice, multiplied inside its chain
 constexpr int kP1 = 36;    // packets of wave 1's slice: its products must be ready when wave 0 is done
 constexpr int kPW = 49;    // packets per later slice, products formed ahead in 4 kPW VGPRs
@@ -86,25 +83,8 @@ constexpr int kDecBufs = 8;  // product buffers: waves 1-4 one each, waves 5 and
 constexpr int kDecPer = 16;  // dot terms per lane (n <= 1024)
 constexpr int kDecChunk = 256;  // dot terms per unrolled chunk
 constexpr int kDecAhead = 4;    // groups of 16 terms read ahead of the adds
-constexpr long long kTimeoutTicks = 200000000LL;  // s_memrealtime at 100 MHz: 2 s
 enum Role : int { kUpd = 0, kT1 = 1, kT2 = 2, kT3 = 3, kDec = 4 };
 
-__device__ __forceinline__ u64 rt_now() { return __builtin_amdgcn_s_memrealtime(); }
-// A wait's time limit.  The clock is read only once the wait has spun:
-// s_memrealtime is a scalar memory access counted by lgkmcnt, so reading it at
-// the start of every wait delays the first LDS poll (which waits on lgkmcnt
-// too) by the clock's round trip.
-struct Deadline {
-    u64 t0 = 0;
-    __device__ __forceinline__ bool expired() {
-        const u64 now = rt_now();
-        if (t0 == 0) {
-            t0 = now;
-            return false;
-        }
-        return (long long)(now - t0) > kTimeoutTicks;
-    }
-};
 // slices of kP0, kP1, then kPW packets (as k_split_persist)
 __host__ __device__ inline int slice0_of(int w) { return w == 0 ? 0 : (w == 1 ? kP0 : kP0 + kP1 + (w - 2) * kPW); }
 __host__ __device__ inline int packets_of(int W) { return slice0_of(W); }
@@ -116,77 +96,8 @@ __host__ __device__ inline int waves_of(int KB) {
 __host__ __device__ inline int cdiv_i(int a, int b) { return (a + b - 1) / b; }
 __device__ __forceinline__ u64 granule(unsigned tag, float v) { return ((u64)tag << 32) | __float_as_uint(v); }
 
-// Products of one slice, prod[j] = q[j] * y[j] (each rounded as the
-// reference's q * y), the reads of packet j + D issued before packet j is
-// multiplied (q into prod[j + D], y into a ring of D + 1): the LDS latency is
-// paid about once per slice (pqp_persist.hip's slice_products).
-template <int NP>
-__device__ __forceinline__ void slice_products(f4v (&prod)[NP], const f4v* qw, const f4v* yw) {
-    constexpr int D = NP < 6 ? NP : 6;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        prod[j] = qw[j * kL];
-        yr[j] = yw[j];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) {
-            prod[j + D] = qw[(j + D) * kL];
-            yr[(j + D) % (D + 1)] = yw[j + D];
-        }
-        const f4v q = prod[j], y = yr[j % (D + 1)];
-        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
 
-// prod[j] = prod[j] * y[j] with the slice's q already in prod (read while the
-// wave waited for y): only y is read, D packets ahead (as pqp_persist.hip).
-template <int NP>
-__device__ __forceinline__ void slice_products_inplace(f4v (&prod)[NP], const f4v* yw) {
-    constexpr int D = NP < 6 ? NP : 6;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) yr[j] = yw[j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
-        const f4v q = prod[j], y = yr[j % (D + 1)];
-        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
 
-// Wave 0's slice with its q already in registers: one LDS read (y) per
-// packet, D packets ahead, each packet added as soon as it is formed.
-template <int NP>
-__device__ __forceinline__ float chain_qreg(float acc, const f4v (&q)[NP], const f4v* yw) {
-    constexpr int D = NP < 12 ? NP : 12;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) yr[j] = yw[j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
-        const f4v y = yr[j % (D + 1)];
-        const f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
-        acc += lo.x;  // matrixMultiply :88-100 / updateY2 :608-609, k in order
-        acc += lo.y;
-        acc += hi.x;
-        acc += hi.y;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return acc;
-}
 
 }  // namespace
 
@@ -1011,9 +922,6 @@ __global__ void k_converge_init(const float* __restrict__ Y, int N, long long u0
 
 }  // namespace
 
-int g_converge_persist_off = 0;
-unsigned long long* g_converge_trace = nullptr;
-int g_converge_trace_n = 0;
 
 // Geometry of the launch for (N, M); 0 when it does not apply.
 int converge_persist_wgs(int N, int M, int* g) {
@@ -1080,7 +988,7 @@ int converge_persist_per_cu(int N, int M) {
     const int W = waves_of(split_kblocks(N > M ? N : M));
     const int threads = 64 * (W > kDecW ? W : kDecW);
     int per = 0;
-    const void* kern = g_converge_trace ? reinterpret_cast<const void*>(&k_converge_persist<true>)
+    const void* kern = g_tune.converge_trace ? reinterpret_cast<const void*>(&k_converge_persist<true>)
                                         : reinterpret_cast<const void*>(&k_converge_persist<false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, converge_persist_lds_bytes(N, M)) !=
         hipSuccess)
@@ -1128,9 +1036,9 @@ hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s) {
     a.err = L.err;
     a.Yout = L.Y;
     a.Uout = L.U;
-    a.trace = g_converge_trace;
-    a.trace_n = g_converge_trace_n;
-    a.stall_wg = g_persist_stall_wg;
+    a.trace = g_tune.converge_trace;
+    a.trace_n = g_tune.converge_trace_n;
+    a.stall_wg = g_tune.persist_stall_wg;
     hipError_t e = hipMemsetAsync(ring, 0, sizeof(u64) * converge_ring_words(L.N, L.M), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_converge_init, dim3(4), dim3(256), 0, s, L.Y, L.N, L.u0, a.ry, L.ctl, L.decided, L.err);

@@ -729,10 +729,8 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
     relay_report(stale, err, lane);
 }
 
-int g_relay_spin_max = kRelaySpinMax;  // tuning: hand-off wait budget (< 0 expires every wait: error-path tests)
-int g_lean_min_n = 4096;  // tuning: k_lean_relay for blocks of rows x N >= g_lean_min_n^2 entries
 bool use_lean(int N, int rows) {
-    return g_lean_min_n > 0 && (long long)rows * N >= (long long)g_lean_min_n * g_lean_min_n;
+    return g_tune.lean_min_n > 0 && (long long)rows * N >= (long long)g_tune.lean_min_n * g_tune.lean_min_n;
 }
 // lw = row SIDES per workgroup (as for the split matrices): lw / 2 rows
 size_t lean_floats(int N, int rows, int lw) { return (size_t)cdiv(2LL * rows, lw) * split_kblocks(N) * (lw / 2) * 4; }
@@ -758,19 +756,17 @@ hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows
     const int G = (split_kblocks(N) + S - 1) / S;
     const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);
     hipLaunchKernelGGL((k_lean_relay<W, S>), dim3(cdiv(2LL * rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows, row0,
-                       lw, Yin, Yout, gate, err, g_relay_spin_max);
+                       lw, Yin, Yout, gate, err, g_tune.relay_spin_max);
     return hipGetLastError();
 }
 
-int g_split_u = 0;  // tuning: k_split_update stage depth (0: 16, 1: 8, 2: 24)
 size_t split_floats(int N, int rows, int lw) { return (size_t)split_wgs(rows, lw) * split_kblocks(N) * lw * 4; }
 // LDS of the split updates (the full y, padded to a whole relay segment of up
 // to 64 packets, plus the relay's hand-off words)
 size_t split_lds_bytes(int N) { return sizeof(float) * ((size_t)4 * (split_kblocks(N) + 64) + 128); }
 
-int g_split_lw = 0;  // tuning: lanes per workgroup (0 auto, else 8/16/32/64)
 int split_pick_lw(int rows) {
-    if (g_split_lw == 8 || g_split_lw == 16 || g_split_lw == 32 || g_split_lw == 64) return g_split_lw;
+    if (g_tune.split_lw == 8 || g_tune.split_lw == 16 || g_tune.split_lw == 32 || g_tune.split_lw == 64) return g_tune.split_lw;
     // about one workgroup per CU: 2 rows / lw ~ 256
     int lw = 8;
     while (lw < 64 && 2LL * rows > 256LL * lw) lw *= 2;
@@ -791,7 +787,6 @@ hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* th
     return hipGetLastError();
 }
 
-int g_split_kind = 0;  // tuning: 0 auto (relay W8 S16), 1 k_split_update, 2 relay W4 S64, 3 W8 S32, 4 W16 S16, 5 W8 S16
 
 template <int W, int S>
 static void launch_relay(const float* SP, const float* fdpn, int N, int rows, int row0, int lw, const float* Yin,
@@ -799,13 +794,13 @@ static void launch_relay(const float* SP, const float* fdpn, int N, int rows, in
     const int G = (split_kblocks(N) + S - 1) / S;
     const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);  // y to the end of the last segment
     hipLaunchKernelGGL((k_split_relay<W, S>), dim3(split_wgs(rows, lw)), dim3(64 * W), lds, s, SP, fdpn, N, rows,
-                       row0, lw, Yin, Yout, gate, err, g_relay_spin_max);
+                       row0, lw, Yin, Yout, gate, err, g_tune.relay_spin_max);
 }
 
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
                                const float* Yin, float* Yout, hipStream_t s, const int* gate, int* err) {
     if (rows <= 0) return hipSuccess;
-    switch (g_split_kind) {
+    switch (g_tune.split_kind) {
         case 1: break;
         case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
         case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
@@ -816,7 +811,7 @@ hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int ro
     // one wave per CU with most of the register file as a 2-stage load buffer:
     // a lane's packet stream is latency-bound (Little's law) with few in flight
     const dim3 grid(split_wgs(rows, lw));
-    switch (g_split_u) {
+    switch (g_tune.split_u) {
         case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
         case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
         default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
@@ -2558,7 +2553,6 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
 // slot at once, so the pipelined form's shorter iterations win; beyond that
 // the plain form's smaller register file (3 vs 2 problems per SIMD at the
 // bundled size) wins on throughput.
-int g_wave_pipe_max_b = 4096;
 template <int NMAX, bool PIPE>
 static void launch_wave_mp(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     if (a.M <= 8)
@@ -2570,7 +2564,7 @@ static void launch_wave_mp(int B, const SolveArgs& a, SolveState* st, hipStream_
 }
 template <int NMAX>
 static void launch_wave_m(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
-    if (B <= g_wave_pipe_max_b) launch_wave_mp<NMAX, true>(B, a, st, s);
+    if (B <= g_tune.wave_pipe_max_b) launch_wave_mp<NMAX, true>(B, a, st, s);
     else launch_wave_mp<NMAX, false>(B, a, st, s);
 }
 
@@ -2584,8 +2578,6 @@ static void launch_tiny_m(int B, const SolveArgs& a, SolveState* st, int threads
         hipLaunchKernelGGL((k_solve_tiny<NMAX, 32>), dim3(B), dim3(threads), 0, s, a, st);
 }
 
-int g_fixed_tiny_old = 0;  // tuning: fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
-int g_fixed_rl_max_b = 1024;  // tuning: largest batch whose k_fixed_tiny keeps y in registers (RL; 16384 bundled problems: 2.47 ms vs 1.76 through LDS)
 template <bool RL>
 static void launch_fixed_tiny(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     if (a.N <= 8) hipLaunchKernelGGL((k_fixed_tiny<8, RL>), dim3(B), dim3(64), 0, s, a, st);
@@ -2594,17 +2586,16 @@ static void launch_fixed_tiny(int B, const SolveArgs& a, SolveState* st, hipStre
     else if (a.N <= 28) hipLaunchKernelGGL((k_fixed_tiny<28, RL>), dim3(B), dim3(64), 0, s, a, st);
     else hipLaunchKernelGGL((k_fixed_tiny<32, RL>), dim3(B), dim3(64), 0, s, a, st);
 }
-int g_wave_min_b = 1;  // tuning: converge mode of N, M <= 32 on k_solve_wave from this many problems on
 
 static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the
     // sequential chain is the critical path, so keep the padding small
-    if (a.mode == kModeFixed && !g_fixed_tiny_old) {
-        if (B <= g_fixed_rl_max_b) launch_fixed_tiny<true>(B, a, st, s);
+    if (a.mode == kModeFixed && !g_tune.fixed_tiny_old) {
+        if (B <= g_tune.fixed_rl_max_b) launch_fixed_tiny<true>(B, a, st, s);
         else launch_fixed_tiny<false>(B, a, st, s);
         return hipGetLastError();
     }
-    if (a.mode == kModeConverge && B >= g_wave_min_b && a.N + a.M < 64) {  // many problems: one wave each
+    if (a.mode == kModeConverge && B >= g_tune.wave_min_b && a.N + a.M < 64) {  // many problems: one wave each
         if (a.N <= 8) launch_wave_m<8>(B, a, st, s);
         else if (a.N <= 16) launch_wave_m<16>(B, a, st, s);
         else if (a.N <= 24) launch_wave_m<24>(B, a, st, s);
@@ -2744,8 +2735,7 @@ hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, flo
     return hipGetLastError();
 }
 
-int g_matmul_tiled_off = 0;  // tuning: every product through k_matmul_seq (A/B of the tiled setup GEMM)
-static bool use_tiled(int a, int c) { return !g_matmul_tiled_off && a >= 32 && c >= 32; }
+static bool use_tiled(int a, int c) { return !g_tune.matmul_tiled_off && a >= 32 && c >= 32; }
 
 hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c,
                              hipStream_t s) {
@@ -2959,7 +2949,6 @@ size_t gauss_jordan_aug_floats(int n) {
     const int c = gj_blocked_c(n);
     return c ? (size_t)n * 256 * c : (size_t)2 * n * n;
 }
-int g_gj_blocked_off = 0;  // tuning: the one-pivot-per-sweep kernel instead (A/B)
 template <int C>
 static void launch_gj_blocked_c(int B, const float* A, float* aug, float* res, int n, hipStream_t s) {
     constexpr int NB = C <= 4 ? 16 : 8;
@@ -2992,7 +2981,7 @@ hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, 
         }
         return hipSuccess;
     }
-    if (!g_gj_blocked_off && gj_blocked_c(n)) return launch_gj_blocked(B, A, aug, res, n, s);
+    if (!g_tune.gj_blocked_off && gj_blocked_c(n)) return launch_gj_blocked(B, A, aug, res, n, s);
     hipLaunchKernelGGL(k_gauss_jordan, dim3(B), dim3(256), 0, s, A, aug, fac, res, n);
     return hipGetLastError();
 }
@@ -3028,20 +3017,18 @@ size_t solve_single_lds_bytes(int ldq, int ldm, bool fused) {
     return sizeof(float) * ((size_t)(fused ? 4 : 3) * ldq + (size_t)3 * ldm);
 }
 
-int g_single_scalar = 0;  // tuning: k_solve_single with 4-byte loads only
-int g_single_occ4 = 0;    // tuning: k_solve_single compiled for 4 workgroups per CU (<= 128 VGPRs)
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
     // wide loads need every row and column start 16-byte aligned: N, M
     // multiples of 4 and 16-byte-aligned arrays (null ones are not read)
-    const bool vec = !g_single_scalar && a.N % 4 == 0 && a.M % 4 == 0 && aligned16(a.QdT) && aligned16(a.Qd) &&
+    const bool vec = !g_tune.single_scalar && a.N % 4 == 0 && a.M % 4 == 0 && aligned16(a.QdT) && aligned16(a.Qd) &&
                      aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && aligned16(a.GpT) &&
                      aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
     if (a.N <= 64) {
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
-    } else if (vec && g_single_occ4) {
+    } else if (vec && g_tune.single_occ4) {
         hipLaunchKernelGGL((k_solve_single<256, true, 4>), dim3(B), dim3(256), lds, s, a, st);
     } else {
         if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);

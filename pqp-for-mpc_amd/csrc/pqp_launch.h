@@ -77,7 +77,36 @@ hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int ro
                                const float* Yin, float* Yout, hipStream_t s, const int* gate = nullptr,
                                int* err = nullptr);
 constexpr int kRelaySpinMax = 1 << 20;  // relay hand-off wait budget in polls (~0.1-1 s)
-extern int g_relay_spin_max;            // tuning: the budget in use
+struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuning.h); defaults = production
+    int relay_spin_max = kRelaySpinMax;  // relay hand-off wait budget in polls (< 0: every wait expires at once)
+    int lean_min_n = 4096;  // k_lean_relay for row blocks of rows x N >= lean_min_n^2 entries
+    int split_u = 0;  // k_split_update stage depth (0: 16, 1: 8, 2: 24)
+    int split_lw = 0;  // relay lanes per workgroup (0 auto, else 8/16/32/64)
+    int split_kind = 0;  // 0 auto (relay W8 S16), 1 k_split_update, 2 relay W4 S64, 3 W8 S32, 4 W16 S16, 5 W8 S16
+    int wave_pipe_max_b = 4096;  // largest batch whose k_solve_wave launch is the software-pipelined form
+    int fixed_tiny_old = 0;  // fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
+    int fixed_rl_max_b = 1024;  // largest batch whose k_fixed_tiny keeps y in registers
+    int wave_min_b = 1;  // converge mode of N, M <= 32 on k_solve_wave from this many problems on
+    int matmul_tiled_off = 0;  // every product through k_matmul_seq
+    int gj_blocked_off = 0;  // Gauss_Jordan through the one-pivot-per-sweep kernel
+    int single_scalar = 0;  // k_solve_single with 4-byte loads only
+    int single_occ4 = 0;  // k_solve_single built for 4 workgroups per CU
+    int persist_off = 0;  // fixed mode of n_dual <= 1024 through the graph-replayed relay
+    int persist_stall_wg = -1;  // workgroup of each persistent launch that never runs (error-path tests; -1: none)
+    unsigned long long* persist_trace = nullptr;  // k_split_persist timeline buffer (device)
+    int persist_trace_n = 0;  // updates the timeline buffer holds
+    int persist_fit_cus = 0;  // CU count the residency checks assume (0: the device's)
+    int wide_flags = 0;  // converge chain: bit 0 update on a forked graph branch, bit 1 gemv segments of 64
+    int converge_persist_off = 0;  // converge mode through the graph chain instead of the persistent launch
+    unsigned long long* converge_trace = nullptr;  // k_converge_persist timeline buffer (device)
+    int converge_trace_n = 0;  // iterates the timeline buffer holds
+    bool force_small = false;  // route N <= 32 to k_solve_small instead of k_solve_tiny
+    bool force_single = false;  // fixed mode of a large problem on one workgroup (k_solve_single)
+    int wide_min_n = 384;  // converge mode: smallest N solved over many workgroups
+    int batch_opts = 0;  // pqp_batch_solve: bit 0 no fused Y'Qd, bit 1 per-call transposes, bit 4 checkFeas over every row
+    long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
+};
+extern Tuning g_tune;
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
 // packets of 4 k per row side in the split layout (k padded to a multiple of 4)
 __host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }
@@ -87,16 +116,11 @@ int persist_max_n();
 size_t persist_lds_bytes(int N);
 hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,
                                 unsigned long long* gran, int* err, hipStream_t s);
-extern int g_persist_off;
 bool split_persist_fits(int N);  // all of k_split_persist's workgroups co-resident on this device
-extern int g_persist_fit_cus;    // tuning: CU count the residency checks assume (0: the device's)
-extern unsigned long long* g_persist_trace;  // tuning: device buffer of 12 * waves * g_persist_trace_n words
-extern int g_persist_trace_n;  // tuning: 1 = fixed mode of large problems through the graph-replayed relay instead
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
 // lean relay (k_lean_relay): Qd packets (4 B per entry, lw / 2 rows per
 // workgroup) and aux[row] = {Fdn, Fdp, Theta, 0} + NaN flags; used for blocks
-// of rows x N >= g_lean_min_n^2 entries
-extern int g_lean_min_n;
+// of rows x N >= g_tune.lean_min_n^2 entries
 bool use_lean(int N, int rows);
 size_t lean_floats(int N, int rows, int lw);
 size_t lean_aux_floats(int N, int rows, int lw);  // per-row words + per-(workgroup, segment) NaN flags
@@ -111,18 +135,10 @@ size_t split_lds_bytes(int N);         // k_split_update's LDS (the full y)
 // columns [N, ld) zeroed) and, if Fd, its full Fd (and Md)
 hipError_t launch_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float* Qrows, int ld,
                              float* Fd, float* Md, hipStream_t s);
-extern int g_split_u;        // tuning: k_split_update stage depth selector
-extern int g_split_kind;     // tuning: relay / stream kernel selector
-extern int g_split_lw;       // tuning: lanes per workgroup override (0 = auto)
-extern int g_fixed_tiny_old; // tuning: fixed mode of tiny problems on k_solve_tiny
-extern int g_fixed_rl_max_b; // tuning: largest batch whose k_fixed_tiny keeps the iterate in registers
-extern int g_wave_pipe_max_b; // tuning: largest batch whose k_solve_wave launch is the software-pipelined form
-extern int g_wave_min_b;     // tuning: smallest batch whose converge-mode tiny solves run one wave per problem
 // batched forms: grid = B problems (states st[0..B-1])
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_state_init(int B, SolveState* st, hipStream_t s);
 hipError_t launch_extract_state(int B, const SolveState* st, long long* h, int* status, hipStream_t s);
-extern int g_matmul_tiled_off;  // tuning: force k_matmul_seq for every product
 hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const float* Bm, int tB, int a, int b,
                                int c, long long sA, long long sB, long long sO, hipStream_t s);
 hipError_t launch_axpy_b(int B, float* A, const float* Bv, float sign, int n, long long sA, long long sB,
@@ -132,7 +148,6 @@ hipError_t launch_mp_finish_b(int B, const float* t, const float* Mp6, float* Mp
 hipError_t launch_gauss_jordan_b(int B, const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
 // floats of one matrix's augmented workspace (`aug` holds B of them)
 size_t gauss_jordan_aug_floats(int n);
-extern int g_gj_blocked_off;
 // ---- converge mode of one large problem over many workgroups (pqp_wide.hip)
 enum GemvEpi : int { kEpiPlain = 0, kEpiAdd = 1, kEpiNeg = 2, kEpiFeas = 3 };
 // out[j] = epi( sum_k A[k * lda + j] * x[k] ), j < n_out, k = 0..n_in-1 in order
@@ -156,11 +171,10 @@ struct GemvJobs {
     const int* gate;         // optional: skip unless *gate == kStatusContinue
     int* flag;               // kEpiFeas: cleared to 0 by an infeasible row
     int* err;                // optional sticky word: an expired hand-off wait ORs 1 into it
-    int spin_max;            // set by the launcher (g_relay_spin_max)
+    int spin_max;            // set by the launcher (g_tune.relay_spin_max)
 };
 hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s);
 hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s);
-extern int g_wide_flags;  // tuning (pqp_tune_wide_flags)
 hipError_t launch_wide_decide(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_init(SolveState* st, int* flag, long long* cap, long long max_updates, float* Y, int N,
                             hipStream_t s);
@@ -193,13 +207,7 @@ size_t converge_stage_floats(int N, int M, int stage);  // stage 1..3 packet arr
 hipError_t launch_converge_pack(const float* Qd, const float* Gp, const float* Qinv, const float* Qp, int N, int M,
                                 float* A1, float* A2, float* A3, hipStream_t s);
 hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s);
-extern int g_converge_persist_off;
-extern int g_persist_stall_wg;  // tuning: workgroup of each persistent launch that never runs (-1: none)
-extern unsigned long long* g_converge_trace;  // tuning: [iterate][4 * 7 + 7][4] words (pqp_tune_converge_trace)
-extern int g_converge_trace_n;
 
 hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s);
-extern int g_single_scalar;  // tuning: k_solve_single with 4-byte loads only (no 8/16-byte forms)
-extern int g_single_occ4;    // tuning: k_solve_single built for 4 workgroups per CU
 
 }  // namespace pqp

@@ -41,6 +41,7 @@
 // by their LDS; G <= 64 of the 256 CUs).
 #include "pqp_device.h"
 #include "pqp_launch.h"
+#include "pqp_chain.h"
 
 #include <type_traits>
 
@@ -48,12 +49,8 @@ namespace pqp {
 
 namespace {
 
-typedef unsigned long long u64;
-typedef __attribute__((address_space(1))) u64 gu64;
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef float f2v __attribute__((ext_vector_type(2)));
 
-constexpr int kPLanes = 32;  // row sides per workgroup
+constexpr int kPLanes = kSliceLanes;  // row sides per workgroup
 #ifndef PQP_PERSIST_SLICES  // A/B builds: -DPQP_PERSIST_SLICES=P0,P1,PW
 #define PQP_PERSIST_SLICES 24, 36, 49
 #endif
@@ -65,24 +62,7 @@ static_assert(kPW0 + kPW1 + 4 * kPW >= 256, "six waves must cover n_dual 1024");
 static_assert(kPW0 <= 64 && kPW1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");
 constexpr int kLateGate = 1; // waves 4, 5 form their products once this wave has handed on its sums
 constexpr int kPMaxWaves = 6;
-constexpr long long kPTimeoutTicks = 200000000LL;  // s_memrealtime runs at 100 MHz: 2 s
 
-__device__ __forceinline__ u64 rt_now() { return __builtin_amdgcn_s_memrealtime(); }
-// A wait's time limit.  The clock is read only once the wait has spun:
-// s_memrealtime is a scalar memory access counted by lgkmcnt, so reading it at
-// the start of every wait delays the first LDS poll (which waits on lgkmcnt
-// too) by the clock's round trip.
-struct Deadline {
-    u64 t0 = 0;
-    __device__ __forceinline__ bool expired() {
-        const u64 now = rt_now();
-        if (t0 == 0) {
-            t0 = now;
-            return false;
-        }
-        return (long long)(now - t0) > kPTimeoutTicks;
-    }
-};
 
 __device__ __forceinline__ void fail(int* err, int code) {
     __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -118,87 +98,11 @@ __device__ __forceinline__ bool lds_wait_sums(u64* word, unsigned want, u64& h) 
     return spins < kHandoffSpins;
 }
 
-// Wave 0's slice: its split entries were read into registers ahead (during
-// its wait for y), so each packet needs one LDS read (y, D packets ahead);
-// the packet's products are added as soon as they are formed, so the chain
-// starts with the first packet instead of after the whole slice.
-template <int NP>
-__device__ __forceinline__ float chain_qreg(float acc, const f4v (&q)[NP], const f4v* yw) {
-    constexpr int D = NP < 12 ? NP : 12;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) yr[j] = yw[j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
-        const f4v y = yr[j % (D + 1)];
-        const f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
-        acc += lo.x;  // :608-609, k in order
-        acc += lo.y;
-        acc += hi.x;
-        acc += hi.y;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return acc;
-}
 
-// prod[j] = prod[j] * y[j] with the slice's q already in prod (read ahead,
-// while the wave waited for y): only y is read, D packets ahead.
-template <int NP>
-__device__ __forceinline__ void slice_products_inplace(f4v (&prod)[NP], const f4v* yw) {
-    constexpr int D = NP < 6 ? NP : 6;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) yr[j] = yw[j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
-        const f4v q = prod[j], y = yr[j % (D + 1)];
-        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
 
-// Products of one slice, prod[j] = q[j] * y[j] (each product rounded as the
-// reference's q * y), with the reads of packet j + D issued before packet j
-// is multiplied (q straight into prod[j + D], y into a ring of D + 1): the
-// LDS latency is paid about once per slice instead of once per packet (the
-// compiler's own schedule kept two packets in flight, ~48 clocks each).
-template <int NP>
-__device__ __forceinline__ void slice_products(f4v (&prod)[NP], const f4v* qw, const f4v* yw) {
-    constexpr int D = NP < 6 ? NP : 6;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        prod[j] = qw[j * kPLanes];
-        yr[j] = yw[j];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) {
-            prod[j + D] = qw[(j + D) * kPLanes];
-            yr[(j + D) % (D + 1)] = yw[j + D];
-        }
-        const f4v q = prod[j], y = yr[j % (D + 1)];
-        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-        prod[j] = f4v{lo.x, lo.y, hi.x, hi.y};
-        __builtin_amdgcn_sched_barrier(0);  // keep the reads D packets ahead of their use
-    }
-}
 
 }  // namespace
 
-int g_persist_off = 0;
-int g_persist_stall_wg = -1;  // tuning: workgroup of each persistent launch that never runs (-1: none)
-unsigned long long* g_persist_trace = nullptr;  // tuning: timeline of workgroup 0 (pqp_tune_persist_trace)
-int g_persist_trace_n = 0;
 
 // waves: slices of kPW0, kPW1, then kPW packets
 __host__ __device__ inline int persist_slice0(int w) { return w == 0 ? 0 : (w == 1 ? kPW0 : kPW0 + kPW1 + (w - 2) * kPW); }
@@ -461,7 +365,6 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     if (last && updates > 0 && !(p & 1) && live) Yout[row] = yn;
 }
 
-int g_persist_fit_cus = 0;  // tuning: CU count the residency check assumes (0: the device's)
 
 // Can all G workgroups of k_split_persist be resident at once?  The launch's
 // waits need every producer running; a grid that cannot be co-resident would
@@ -473,8 +376,8 @@ bool split_persist_fits(int N) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    if (g_persist_fit_cus > 0) cus = g_persist_fit_cus;
-    const void* kern = g_persist_trace ? reinterpret_cast<const void*>(&k_split_persist<true>)
+    if (g_tune.persist_fit_cus > 0) cus = g_tune.persist_fit_cus;
+    const void* kern = g_tune.persist_trace ? reinterpret_cast<const void*>(&k_split_persist<true>)
                                        : reinterpret_cast<const void*>(&k_split_persist<false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, persist_lds_bytes(N)) != hipSuccess)
         return false;
@@ -489,12 +392,12 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
     hipError_t e = hipMemsetAsync(gran, 0, sizeof(u64) * 2 * N, s);
     if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    if (g_persist_trace)
+    if (g_tune.persist_trace)
         hipLaunchKernelGGL(k_split_persist<true>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
-                           updates, Y0, Yout, gran, err, g_persist_trace, g_persist_trace_n, g_persist_stall_wg);
+                           updates, Y0, Yout, gran, err, g_tune.persist_trace, g_tune.persist_trace_n, g_tune.persist_stall_wg);
     else
         hipLaunchKernelGGL(k_split_persist<false>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
-                           updates, Y0, Yout, gran, err, nullptr, 0, g_persist_stall_wg);
+                           updates, Y0, Yout, gran, err, nullptr, 0, g_tune.persist_stall_wg);
     return hipGetLastError();
 }
 

@@ -280,7 +280,6 @@ hipError_t launch_transpose(const float* src, int rows, int cols, float* dst, hi
     return hipGetLastError();
 }
 
-int g_wide_flags = 0;  // tuning: bit 0 update on a forked graph branch, bit 1 gemv segments of 64 (default 32)
 
 template <int W, int S>
 static hipError_t gemv_launch(GemvJobs J, int n_in, hipStream_t s) {
@@ -293,10 +292,10 @@ static hipError_t gemv_launch(GemvJobs J, int n_in, hipStream_t s) {
 hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s) {
     GemvJobs J = jobs;
     J.wgs0 = cdivw(J.job[0].n_out, 64);
-    J.spin_max = g_relay_spin_max;
+    J.spin_max = g_tune.relay_spin_max;
     int n_in = J.job[0].n_in;
     if (J.job[1].A && J.job[1].n_in > n_in) n_in = J.job[1].n_in;
-    return (g_wide_flags & 2) ? gemv_launch<8, 64>(J, n_in, s) : gemv_launch<8, 32>(J, n_in, s);
+    return (g_tune.wide_flags & 2) ? gemv_launch<8, 64>(J, n_in, s) : gemv_launch<8, 32>(J, n_in, s);
 }
 
 

@@ -93,27 +93,10 @@ SIGNATURES = {
     "pqp_rowblock_destroy": (C.c_int, [_vp]),
     "pqp_synth_rows": (C.c_int, [C.c_uint32, C.c_longlong] + [C.c_int] * 4 + [_vp, C.c_int, _vp, _vp, _vp]),
     # include/pqp_tuning.h
-    "pqp_tune_set_variant": (C.c_int, [C.c_int]),
+    "pqp_tune": (C.c_int, [C.c_char_p, C.c_longlong, C.POINTER(C.c_longlong)]),
+    "pqp_tune_get": (C.c_int, [C.c_char_p, C.POINTER(C.c_longlong)]),
+    "pqp_tune_trace": (C.c_int, [C.c_char_p, _vp, C.c_int]),
     "pqp_tune_glibc_rand": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
-    "pqp_tune_wide_min_n": (C.c_int, [C.c_int]),
-    "pqp_tune_persist": (C.c_int, [C.c_int]),
-    "pqp_tune_converge_persist": (C.c_int, [C.c_int]),
-    "pqp_tune_lean_min_n": (C.c_int, [C.c_int]),
-    "pqp_tune_relay_spin_max": (C.c_int, [C.c_int]),
-    "pqp_tune_matmul_tiled": (C.c_int, [C.c_int]),
-    "pqp_tune_gj_blocked": (C.c_int, [C.c_int]),
-    "pqp_tune_batch_converge": (C.c_int, [C.c_int]),
-    "pqp_tune_persist_fit_cus": (C.c_int, [C.c_int]),
-    "pqp_tune_persist_stall": (C.c_int, [C.c_int]),
-    "pqp_tune_converge_grid": (C.c_int, [C.c_int, C.c_int]),
-    "pqp_tune_last_path": (C.c_int, [C.POINTER(C.c_longlong)]),
-    "pqp_tune_converge_chunk": (C.c_int, [C.c_int]),
-    "pqp_tune_converge_trace": (C.c_int, [_vp, C.c_int]),
-    "pqp_tune_wave_min_b": (C.c_int, [C.c_int]),
-    "pqp_tune_fixed_rl_max_b": (C.c_int, [C.c_int]),
-    "pqp_tune_wave_pipe_max_b": (C.c_int, [C.c_int]),
-    "pqp_tune_persist_trace": (C.c_int, [_vp, C.c_int]),
-    "pqp_tune_wide_flags": (C.c_int, [C.c_int]),
 }
 
 
@@ -149,7 +132,80 @@ def lib() -> C.CDLL:
             fn.restype = res
             fn.argtypes = args
         _LIB = L
+        if hasattr(L, "pqp_tune"):
+            _attach_knobs(L)
     return _LIB
+
+
+# ---------------------------------------------------------------------------
+# tuning knobs (include/pqp_tuning.h): one keyed C entry point; Python names
+# ---------------------------------------------------------------------------
+def tune(key: str, value: int) -> int:
+    """pqp_tune: set knob `key`, return its previous value."""
+    old = C.c_longlong(0)
+    _check(lib().pqp_tune(key.encode(), int(value), C.byref(old)))
+    return int(old.value)
+
+
+def tune_get(key: str, arg: int = 0) -> int:
+    """pqp_tune_get: a knob's value or a diagnostic (last_path,
+    persist_fallbacks, converge_grid with arg = N << 32 | M)."""
+    v = C.c_longlong(int(arg))
+    _check(lib().pqp_tune_get(key.encode(), C.byref(v)))
+    return int(v.value)
+
+
+# L.pqp_tune_<name>(value) -> previous value, for the knobs the tests and
+# scripts set (one C entry point behind them all)
+_KNOB_NAMES = {"persist": "persist_off", "converge_persist": "converge_persist_off", "wide_min_n": "wide_min_n",
+               "lean_min_n": "lean_min_n", "relay_spin_max": "relay_spin_max", "matmul_tiled": "matmul_tiled_off",
+               "gj_blocked": "gj_blocked_off", "persist_fit_cus": "persist_fit_cus",
+               "persist_stall": "persist_stall_wg", "converge_chunk": "converge_chunk", "wave_min_b": "wave_min_b",
+               "fixed_rl_max_b": "fixed_rl_max_b", "wave_pipe_max_b": "wave_pipe_max_b", "wide_flags": "wide_flags"}
+
+
+def _set_variant(variant: int) -> int:
+    """The packed kernel-variant word of the round-1 tuning API: 0x100
+    force_small, 0x200 force_single, 0x400 fixed_tiny_old, bits 12-13 split_u,
+    14-16 split_kind, 17-19 split_lw (1: 8 ... 4: 64)."""
+    lw_old = tune_get("split_lw")
+    old = ((0x100 if tune_get("force_small") else 0) | (0x200 if tune_get("force_single") else 0)
+           | (0x400 if tune_get("fixed_tiny_old") else 0) | (tune_get("split_u") << 12)
+           | (tune_get("split_kind") << 14) | (((lw_old.bit_length() - 3) if lw_old else 0) << 17))
+    sel = (variant >> 17) & 7
+    tune("split_u", (variant >> 12) & 3)
+    tune("split_kind", (variant >> 14) & 7)
+    tune("split_lw", 4 << sel if 1 <= sel <= 4 else 0)
+    tune("force_small", 1 if variant & 0x100 else 0)
+    tune("force_single", 1 if variant & 0x200 else 0)
+    tune("fixed_tiny_old", 1 if variant & 0x400 else 0)
+    return old
+
+
+def _batch_converge(opts: int) -> int:
+    """batch_opts plus the k_solve_single build bits (2: 4-byte loads, 3: four
+    workgroups per CU) in one word."""
+    old = tune("batch_opts", opts & 19) | (4 if tune("single_scalar", 1 if opts & 4 else 0) else 0)
+    return old | (8 if tune("single_occ4", 1 if opts & 8 else 0) else 0)
+
+
+def _last_path(fallbacks=None) -> int:
+    """Solver path of this thread's last solve; the fallback count goes to
+    `fallbacks` (a c_longlong or byref() of one) when given."""
+    if fallbacks is not None:
+        getattr(fallbacks, "_obj", fallbacks).value = tune_get("persist_fallbacks")
+    return tune_get("last_path")
+
+
+def _attach_knobs(L):
+    for name, key in _KNOB_NAMES.items():
+        setattr(L, f"pqp_tune_{name}", lambda v, key=key: tune(key, v))
+    L.pqp_tune_set_variant = _set_variant
+    L.pqp_tune_batch_converge = _batch_converge
+    L.pqp_tune_last_path = _last_path
+    L.pqp_tune_converge_grid = lambda N, M: tune_get("converge_grid", (int(N) << 32) | int(M))
+    L.pqp_tune_persist_trace = lambda buf, n: L.pqp_tune_trace(b"persist", buf, n)
+    L.pqp_tune_converge_trace = lambda buf, n: L.pqp_tune_trace(b"converge", buf, n)
 
 
 def last_error() -> str:

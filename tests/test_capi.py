@@ -205,3 +205,33 @@ def test_dropin_input_reads_example_from_cwd(tmp_path, monkeypatch, orc):
     for k in ("Fp1", "Fp2", "Fp3", "Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "Gp", "Kp", "x", "D"):
         assert_bitwise(A[k], exp[k], k)
     assert A["Z"].any()  # read although unused by the solver (PQP_CPU.c:889-899)
+
+
+def test_tuning_knobs_roundtrip():
+    """The keyed tuning interface (include/pqp_tuning.h): every knob sets and
+    reads back, the previous value is returned, unknown keys are errors, and
+    the Python knob names map onto it.  Host-only (no GPU work)."""
+    import ctypes as C
+
+    import pqp_amd
+
+    L = pqp_amd.lib()
+    for key in ("persist_off", "lean_min_n", "batch_opts", "split_kind", "converge_chunk", "wide_min_n"):
+        old = pqp_amd.tune_get(key)
+        assert pqp_amd.tune(key, old + 3) == old
+        assert pqp_amd.tune_get(key) == old + 3
+        assert pqp_amd.tune(key, old) == old + 3
+    assert pqp_amd.tune("relay_spin_max", 2**40) == 1 << 20 and pqp_amd.tune_get("relay_spin_max") == 1 << 30
+    pqp_amd.tune("relay_spin_max", 0)
+    assert pqp_amd.tune_get("relay_spin_max") == 1 << 20
+    with pytest.raises(pqp_amd.PQPError):
+        pqp_amd.tune("no_such_knob", 1)
+    prev = L.pqp_tune_set_variant((3 << 17) | (2 << 14) | 0x200)
+    assert pqp_amd.tune_get("split_lw") == 32 and pqp_amd.tune_get("split_kind") == 2
+    assert pqp_amd.tune_get("force_single") == 1
+    assert L.pqp_tune_set_variant(prev) == (3 << 17) | (2 << 14) | 0x200
+    assert L.pqp_tune_batch_converge(1 | 4 | 16) == 0 and pqp_amd.tune_get("single_scalar") == 1
+    assert L.pqp_tune_batch_converge(0) == 1 | 4 | 16
+    fb = C.c_longlong(-1)
+    assert L.pqp_tune_last_path(C.byref(fb)) == 0 and fb.value == 0
+    assert L.pqp_tune_converge_grid(1024, 512) > 0 and L.pqp_tune_converge_grid(28, 7) > 0
