@@ -396,9 +396,13 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
     db = json.loads(tf.read_text()) if tf.exists() else {}
     khash = kernel_src_hash("solve-single")
     # bytes per problem-iteration: Qd once (the update; on feasible iterates
-    # Y'Qd rides in the same pass), Gp twice (Gp'Y, Gp U: 8NM), Qp_inv once,
-    # and on feasible iterates Qp once (U'Qp)
-    for case, alg in (("infeasible", 4.0 * N * N + 8.0 * N * M + 4.0 * M * M),
+    # Y'Qd rides in the same pass), Gp for Gp'Y (4NM), Qp_inv once, Gp again for
+    # checkFeas's Gp U -- on these infeasible iterates only its first 256 rows
+    # (a row over its bound there decides terminate(), the rest is skipped;
+    # the every-row setting, tuning bit 4, reads all 4NM) -- and on feasible
+    # iterates Qp once (U'Qp)
+    first = 4.0 * min(N, 256) * M
+    for case, alg in (("infeasible", 4.0 * N * N + 4.0 * N * M + first + 4.0 * M * M),
                       ("feasible", 4.0 * N * N + 8.0 * N * M + 8.0 * M * M)):
         if case == "feasible":
             pb.Kp.fill_(1e30)
@@ -411,6 +415,7 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         gbs = alg * B / per_iter / 1e9
         r = {"ms_per_iteration": per_iter * 1e3, "instance_iter_per_s": B / per_iter,
              "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
+             "full_pass_bytes_per_iter": 4.0 * N * N + 8.0 * N * M + 4.0 * M * M * (2 if case == "feasible" else 1),
              "call_ms": dt * 1e3, "call_instance_iter_per_s": B * K / dt, "all_capped": ok}
         pmc = db.get(f"k_solve_single_{case}")
         if pmc and pmc.get("kernel_src_sha256") == khash:

@@ -30,8 +30,9 @@ def dispatches(path: str, counter: str) -> list[float]:
 def design_bytes(case: str) -> float:
     """Bytes per problem the 8-update dispatch moves by design."""
     q, g, qi, qp = 4.0 * N * N, 4.0 * N * M, 4.0 * M * M, 4.0 * M * M
-    if case == "infeasible":  # 8 updates; 9 terminates stopping at checkFeas (Gp'Y, Qp_inv, Gp U)
-        return K * q + (K + 1) * (2 * g + qi)
+    if case == "infeasible":  # 8 updates; 9 terminates stopping at checkFeas (Gp'Y, Qp_inv, and Gp U
+        # over its first 256 rows, where a row over its bound decides the iterate)
+        return K * q + (K + 1) * (g + 4.0 * min(N, 256) * M + qi)
     # feasible: terminate 1 reads Qd for Y'Qd, then update 1 (unfused), then
     # 8 fused passes (update + Y'Qd, the last one speculative); Qp for U'Qp each time
     return (K + 2) * q + (K + 1) * (2 * g + qi + qp)
