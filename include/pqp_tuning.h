@@ -38,8 +38,6 @@ extern "C" {
  *                          (0: auto; 8, 16, 32 or 64)
  *   lean_min_n [4096]      row blocks of rows x N >= lean_min_n^2 use the lean
  *                          relay over Qd (k_lean_relay); 0 turns it off
- *   lean_s [16]            k_lean_relay segment length in packets (16 or 32;
- *                          one hand-off between waves per segment)
  *   matmul_tiled_off [0]   every setup product through k_matmul_seq
  *   gj_blocked_off [0]     batched Gauss_Jordan through the one-pivot-per-sweep
  *                          kernel instead of the blocked one (n <= 1024)

@@ -1859,7 +1859,6 @@ const KnobRef* find_knob(const char* key) {
     static const KnobRef knobs[] = {
         {"relay_spin_max", &g_tune.relay_spin_max, nullptr, nullptr},
         {"lean_min_n", &g_tune.lean_min_n, nullptr, nullptr},
-        {"lean_s", &g_tune.lean_s, nullptr, nullptr},
         {"split_u", &g_tune.split_u, nullptr, nullptr},
         {"split_lw", &g_tune.split_lw, nullptr, nullptr},
         {"split_kind", &g_tune.split_kind, nullptr, nullptr},

@@ -610,7 +610,7 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
     };
     if (w < G) load_seg(w);
     const f4v ax = live ? *reinterpret_cast<const f4v*>(aux + 4 * (size_t)r) : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-    const int* segnan = reinterpret_cast<const int*>(aux + 4 * (size_t)gridDim.x * rp);  // [wg][G16] NaN flags
+    const int* segnan = reinterpret_cast<const int*>(aux + 4 * (size_t)gridDim.x * rp);  // [wg][G] NaN flags
     {
         const int t = threadIdx.x, n_lds = 4 * G * S;
         for (int b = 0; b < n_lds; b += 64 * W * 8) {
@@ -641,16 +641,7 @@ __global__ void __launch_bounds__(64 * W) k_lean_relay(const float* __restrict__
     for (int g = w; g < G; g += W) {
         const int kbase = 4 * g * S;
         const bool lit = kbase < d0 + rp && kbase + 4 * S > d0;  // a diagonal of this workgroup is in here
-        // a NaN of Qd is in here (the builder flags kLeanS-packet segments)
-        bool nan_seg = false;
-        if (!lit) {
-            const int GF = (KB + kLeanS - 1) / kLeanS;
-#pragma unroll
-            for (int f = 0; f < S / kLeanS; ++f) {
-                const int gf = g * (S / kLeanS) + f;
-                nan_seg |= gf < GF && segnan[(size_t)blockIdx.x * GF + gf] != 0;
-            }
-        }
+        const bool nan_seg = !lit && segnan[(size_t)blockIdx.x * G + g] != 0;  // a NaN of Qd is in here
         // the terms replace the packets in place; the branch is per segment,
         // each side one straight-line unrolled loop (2: literal, 1: lean with
         // compares, 0: lean by max)
@@ -761,16 +752,11 @@ hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const 
 hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows, int row0, int lw, const float* Yin,
                               float* Yout, hipStream_t s, const int* gate, int* err) {
     if (rows <= 0) return hipSuccess;
-    constexpr int W = 8;
-    const int S = g_tune.lean_s == 32 ? 32 : kLeanS;  // packets per segment: 16, or 32 (half the hand-offs)
+    constexpr int W = 8, S = kLeanS;
     const int G = (split_kblocks(N) + S - 1) / S;
     const size_t lds = sizeof(float) * ((size_t)4 * G * S + 128);
-    if (S == 32)
-        hipLaunchKernelGGL((k_lean_relay<W, 32>), dim3(cdiv(2LL * rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows,
-                           row0, lw, Yin, Yout, gate, err, g_tune.relay_spin_max);
-    else
-        hipLaunchKernelGGL((k_lean_relay<W, kLeanS>), dim3(cdiv(2LL * rows, lw)), dim3(64 * W), lds, s, LP, aux, N,
-                           rows, row0, lw, Yin, Yout, gate, err, g_tune.relay_spin_max);
+    hipLaunchKernelGGL((k_lean_relay<W, S>), dim3(cdiv(2LL * rows, lw)), dim3(64 * W), lds, s, LP, aux, N, rows, row0,
+                       lw, Yin, Yout, gate, err, g_tune.relay_spin_max);
     return hipGetLastError();
 }
 

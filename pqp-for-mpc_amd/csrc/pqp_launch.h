@@ -80,7 +80,6 @@ constexpr int kRelaySpinMax = 1 << 20;  // relay hand-off wait budget in polls (
 struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuning.h); defaults = production
     int relay_spin_max = kRelaySpinMax;  // relay hand-off wait budget in polls (< 0: every wait expires at once)
     int lean_min_n = 4096;  // k_lean_relay for row blocks of rows x N >= lean_min_n^2 entries
-    int lean_s = 16;  // k_lean_relay segment: 16 or 32 packets (one hand-off per segment)
     int split_u = 0;  // k_split_update stage depth (0: 16, 1: 8, 2: 24)
     int split_lw = 0;  // relay lanes per workgroup (0 auto, else 8/16/32/64)
     int split_kind = 0;  // 0 auto (relay W8 S16), 1 k_split_update, 2 relay W4 S64, 3 W8 S32, 4 W16 S16, 5 W8 S16

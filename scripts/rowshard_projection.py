@@ -56,8 +56,6 @@ def time_block(N: int, world: int, updates: int = 200) -> dict:
 
 def main():
     Ns = [int(a) for a in sys.argv[1:]] or [16384, 32768]
-    if os.environ.get("LEAN_S"):  # k_lean_relay segment length (tuning knob lean_s)
-        pqp_amd.tune("lean_s", int(os.environ["LEAN_S"]))
     out = {"note": "rank 0's row block on one GPU; the all-gather of 4N bytes per update is not included", "runs": []}
     for N in Ns:
         for world in (1, 2, 4, 8):

@@ -146,30 +146,3 @@ def test_lean_matches_split_relay_large(gpu_lib):
         del blocks
     assert_bitwise(got["lean"], got["split"], "lean vs split")
     assert np.all(np.isfinite(got["lean"]))
-
-
-@pytest.mark.parametrize("N,rows", [(4100, 4100), (8192, 2100), (5000, 3400)])
-def test_lean_relay_32_packet_segments(gpu_lib, orc, N, rows):
-    """k_lean_relay with 32-packet segments (tuning lean_s = 32: half the
-    hand-offs) gives the same rows as the oracle's updateY2, NaN segments
-    included (the builder flags 16-packet segments; a 32-packet segment is
-    NaN-flagged when either half is).  rows x N >= 4096^2: the lean form."""
-    import torch
-
-    P = orc.synth_problem(31, 0, N, 8, with_qp=False)
-    Qd = np.asarray(P["Qd"], np.float32).reshape(N, N).copy()
-    row0 = N - rows
-    Qd[row0 + 3, 4 * 16 * 3 + 5] = np.nan  # the second half of a 32-packet segment of the block's row 3
-    Fd = np.asarray(P["Fd"], np.float32)
-    prev = gpu_lib.tune("lean_s", 32)
-    try:
-        blk = gpu_lib.RowBlock(torch.from_numpy(Qd[row0:].copy()).cuda(), torch.from_numpy(Fd).cuda(), N, row0, rows)
-        Y = torch.full((N,), 1000.0, device="cuda")
-        out = torch.empty(rows, device="cuda")
-        blk.update(Y, out)
-        blk.check()
-    finally:
-        gpu_lib.tune("lean_s", prev)
-    th = orc.theta(Qd.reshape(-1), N)
-    want = orc.update(np.full(N, 1000.0, np.float32), Qd.reshape(-1), th, Fd, N)[row0:]
-    assert_bitwise(out.cpu().numpy(), want, f"N={N} rows={rows}")
