@@ -553,7 +553,7 @@ int ensure_persist_split(pqp_problem& P, hipStream_t s) {
     return PQP_OK;
 }
 
-// Which solver the last single-problem solve ran (pqp_tune_last_path), and
+// Which solver the last single-problem solve ran (pqp_tune_get("last_path")), and
 // how many persistent launches fell back to the relay / graph path.
 enum SolvePath : int {
     kPathFixedPersist = 1, kPathFixedRelay = 2, kPathConvergePersist = 3, kPathConvergeWide = 4, kPathOneWorkgroup = 5

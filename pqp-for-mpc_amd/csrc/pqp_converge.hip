@@ -846,7 +846,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
     }
 }
 
-// TRACE: the timeline instantiation (pqp_tune_converge_trace); the default one
+// TRACE: the timeline instantiation (pqp_tune_trace("converge", ...)); the default one
 // carries no trace branches.
 template <bool TRACE>
 __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {

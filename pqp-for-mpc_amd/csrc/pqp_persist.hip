@@ -127,7 +127,7 @@ size_t persist_lds_bytes(int N) {
 
 // SP: the k_build_split layout with lw = 32 (workgroup-major packets).
 // gran: 2 * N granules, zeroed before the launch.  err: zeroed before the launch.
-// TRACE: the timeline instantiation (pqp_tune_persist_trace); the default one
+// TRACE: the timeline instantiation (pqp_tune_trace("persist", ...)); the default one
 // carries no trace branches on its critical path.
 template <bool TRACE>
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
