@@ -1006,6 +1006,11 @@ int pqp_problem_create_on(int device, void* stream, const float* Qd, const float
     std::unique_ptr<pqp_problem> P(new pqp_problem());
     P->dev = device;
     if (stream) {
+        hipDevice_t sdev = -1;
+        PQP_HIP(hipStreamGetDevice(static_cast<hipStream_t>(stream), &sdev));
+        if (sdev != device)
+            return set_error(PQP_ERR_ARG, "pqp_problem_create_on: the stream belongs to device %d, not %d", (int)sdev,
+                             device);
         P->stream = static_cast<hipStream_t>(stream);
     } else {
         PQP_HIP(hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking));
