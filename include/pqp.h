@@ -253,9 +253,12 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
                     int *d_status, void *stream);
 
 /* Which batched solver pqp_batch_solve uses for (N, M): 0 one wave or one small
- * workgroup per problem (N, M <= 32), 1 the problem staged in LDS, 2 one
- * workgroup per problem from HBM (k_solve_single; uses pqp_batch_prepare's
- * data), or PQP_ERR_ARG when (N, M) exceeds every solver's LDS budget. */
+ * workgroup per problem (N, M <= 32), 3 one workgroup per problem with each
+ * matrix held in LDS once (k_solve_mid: mid-size, about N <= 165 at M = N/4),
+ * 1 the problem staged in LDS with its split copies (k_solve_small; only with
+ * the mid_off knob), 2 one workgroup per problem from HBM (k_solve_single;
+ * uses pqp_batch_prepare's data), or PQP_ERR_ARG when (N, M) exceeds every
+ * solver's LDS budget. */
 int pqp_batch_solve_path(int N, int M);
 
 /* pqp_batch_solve in two steps, so that what depends only on the problems is

@@ -47,6 +47,11 @@ extern "C" {
  *                          row (by default it stops after its first 256 rows
  *                          when one is over its bound: terminate() returns 0
  *                          either way)
+ *   mid_off [0]            batched solves of mid-size problems through
+ *                          k_solve_small / k_solve_single instead of the
+ *                          LDS-resident k_solve_mid (path 3)
+ *   batch_chunk [0]        iterates per problem per batched-solve launch
+ *                          (0: sized from N and M)
  *   single_scalar [0]      k_solve_single with 4-byte loads only
  *   single_occ4 [0]        k_solve_single built for 4 workgroups per CU
  *   wide_min_n [384]       converge mode: smallest N solved over many workgroups

@@ -1442,11 +1442,13 @@ int pqp_batch_compute_mp(int B, int nd, int ns, const float* d_Mp1, const float*
 }
 
 // Which batched solver a problem size takes: 0 one wave / tiny workgroup
-// (N, M <= 32), 1 everything staged in LDS, 2 one workgroup from global
-// memory (k_solve_single; needs the prepared data of pqp_batch_prepare), -1
-// too large for any.
+// (N, M <= 32), 3 every matrix once in LDS (k_solve_mid), 1 everything
+// staged in LDS with the split copies (k_solve_small; mid_off), 2 one
+// workgroup from global memory (k_solve_single; needs the prepared data of
+// pqp_batch_prepare), -1 too large for any.
 static int batch_path(int N, int M) {
     if (N <= 32 && M <= 32 && !g_tune.force_small) return 0;
+    if (!g_tune.mid_off && solve_mid_lds_bytes(N, M, true) <= kLdsBudget) return 3;
     if (solve_small_lds_bytes(N, M) <= kLdsBudget) return 1;
     if (solve_single_lds_bytes(round4(N), round4(M), false) <= kLdsBudget) return 2;
     return -1;
@@ -1550,7 +1552,7 @@ int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float
     a.max_updates = max_updates;
     const double per_update = (double)N * N * 3.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
     const long long chunk = (long long)((double)(1 << 26) / per_update);
-    a.chunk = chunk < 1 ? 1 : chunk;
+    a.chunk = g_tune.batch_chunk > 0 ? g_tune.batch_chunk : (chunk < 1 ? 1 : chunk);
     a.pending = static_cast<int*>(pending.p);
     SolveState* st = static_cast<SolveState*>(state.p);
     for (;;) {
@@ -1884,6 +1886,8 @@ const KnobRef* find_knob(const char* key) {
         {"force_single", nullptr, &g_tune.force_single, nullptr},
         {"wide_min_n", &g_tune.wide_min_n, nullptr, nullptr},
         {"batch_opts", &g_tune.batch_opts, nullptr, nullptr},
+        {"mid_off", &g_tune.mid_off, nullptr, nullptr},
+        {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},
         {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
     };
     for (const KnobRef& k : knobs)

@@ -2613,6 +2613,447 @@ static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hi
 }
 hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) { return launch_tiny_grid(1, a, st, s); }
 
+// ---------------------------------------------------------------------------
+// k_solve_mid: solveQuadraticDual (PQP_CPU.c:694-750) for mid-size problems
+// -- the MPC plant over a few horizon steps, N ~ 33..165 -- one 256-thread
+// workgroup per problem with Qd, Gp, Qp_inv and Qp each held in LDS ONCE (no
+// split copies: the update forms its split entries from Qd on the fly, as
+// k_solve_single does from HBM), so the problem is read from HBM once per
+// launch and every iteration runs out of LDS.  Matrix rows are laid out with
+// an ODD stride: a lane-per-row walk (row i at i*ld + k) and a lane-per-column
+// walk (column j at k*ld + j) are then both free of bank conflicts with
+// 4-byte reads, so each matrix serves both of its access directions.  Shared
+// vectors are 16-byte aligned and read as 16-byte broadcasts.
+//
+// One iteration (terminate(Y_h), then the update from Y_h, computed
+// speculatively and dropped when terminate() stops -- every value is the
+// reference's):
+//   phase A  update rows i < N (one lane each; with Y'Qd fused in once an
+//            iterate was feasible and Qd is bit-symmetric), tM = Gp'Y + Fp
+//            (one lane per column), and -- Qd not symmetric, previous iterate
+//            feasible -- the Y'Qd columns, on separate waves at once
+//   phase B  U = -Qp_inv tM          (computeUfromY :352-360)
+//   phase C  checkFeas, any row over its bound -> infeasible (:632-641)
+//   phase D  (feasible) the terms of the four dot products of computeCost
+//   phase E  (feasible) lanes 0-3 of wave 0 sum the four in k order, Jp, Jd
+//            and the three gap tests (:648-687)
+// Chunked and resumable like k_solve_small (state in SolveState).
+// ---------------------------------------------------------------------------
+struct MidLayout {
+    int ldn, ldm;
+    int ya, yb, tq, fy, tM, Us, tu, fu, Fp, dP, dN, Fdp, Fdn, Fd, Kp, sc, Qd, Gp, Qi, Qp, total;
+};
+__host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv) {
+    MidLayout L;
+    L.ldn = N | 1;
+    L.ldm = M | 1;
+    int o = 0;
+    L.ya = o;  o += align4(N);
+    L.yb = o;  o += align4(N);
+    L.tq = o;  o += align4(N);
+    L.fy = o;  o += align4(N);
+    L.dP = o;  o += align4(N);
+    L.dN = o;  o += align4(N);
+    L.Fdp = o; o += align4(N);
+    L.Fdn = o; o += align4(N);
+    L.Fd = o;  o += align4(N);
+    L.sc = o;  o += 8;
+    if (conv) {
+        L.tM = o;  o += align4(M);
+        L.Us = o;  o += align4(M);
+        L.tu = o;  o += align4(M);
+        L.fu = o;  o += align4(M);
+        L.Fp = o;  o += align4(M);
+        L.Kp = o;  o += align4(N);
+    } else {
+        L.tM = L.Us = L.tu = L.fu = L.Fp = L.Kp = 0;
+    }
+    L.Qd = o;  o += N * L.ldn;
+    if (conv) {
+        L.Gp = o;  o += N * L.ldm;
+        L.Qi = o;  o += M * L.ldm;
+        L.Qp = o;  o += M * L.ldm;
+    } else {
+        L.Gp = L.Qi = L.Qp = 0;
+    }
+    L.total = o;
+    return L;
+}
+
+// Blocks of 8 terms, software-pipelined: the LDS loads of block b+1 are
+// issued before block b's arithmetic, so an iteration's dependent sums wait
+// on LDS latency once per pass instead of once per block (with one or two
+// workgroups per CU there are too few other waves to hide it).
+struct MidBlk {
+    float a[8];
+    sf4 b0, b1;
+};
+__device__ __forceinline__ void mid_load(MidBlk& B, const float* a, int as, const float* b, int k) {
+    B.b0 = *reinterpret_cast<const sf4*>(b + k);
+    B.b1 = *reinterpret_cast<const sf4*>(b + k + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) B.a[j] = a[(k + j) * as];
+}
+
+// s = sum_k a[k * as] * b[k], k = 0..n-1 in the reference's order (product
+// rounded before each add); b a 16-byte-aligned LDS vector every lane reads
+// at the same address (16-byte broadcasts)
+__device__ __forceinline__ float mid_dot(const float* a, int as, const float* b, int n) {
+    float s = 0.0f;
+    const int nb = n & ~7;
+    if (nb > 0) {
+        MidBlk c, x;
+        mid_load(c, a, as, b, 0);
+        for (int k = 8; k < nb; k += 8) {
+            mid_load(x, a, as, b, k);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += c.a[j] * (j < 4 ? c.b0[j] : c.b1[j - 4]);
+            c = x;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += c.a[j] * (j < 4 ? c.b0[j] : c.b1[j - 4]);
+    }
+    for (int k = nb; k < n; ++k) s += a[k * as] * b[k];
+    return s;
+}
+
+// The split entries of one off-diagonal Qd value q in max form, qp =
+// (q<0?0:q) and qn = (q>0?0:-q) (bit-identical to the reference's
+// max(0,+-q)+0.0f products).  FAST (the problem's Qd holds no NaN,
+// checked when it is staged): one v_max_f32 each.  v_max_f32 differs from the
+// selects only on a NaN and in the sign of a zero result, and a signed zero
+// does not change a sum that starts at +0.0f and only ever adds products of
+// non-negative values (never -0).  Inline asm: the compiler's own fmaxf
+// quiets each operand first (one more instruction per value).
+template <bool FAST>
+__device__ __forceinline__ void split_q(float q, float& qp, float& qn) {
+    if constexpr (FAST) {
+        asm("v_max_f32 %0, %1, 0" : "=v"(qp) : "v"(q));
+        asm("v_max_f32_e64 %0, -%1, 0" : "=v"(qn) : "v"(q));
+    } else {
+        qp = (q < 0.0f) ? 0.0f : q;
+        qn = (q > 0.0f) ? 0.0f : -q;
+    }
+}
+
+// terms k..k+7 of row i of updateY2 over the loaded block (Qd[i][k..k+7] and
+// y_k..y_k+7).  (ap, an) ride as one packed pair: one v_pk_mul_f32 and one
+// v_pk_add_f32 per k (each half of a packed op rounds as the scalar op).
+// DIAG: the block holds the diagonal k = i of some lanes' rows, where the
+// literal max(0,+-q_ii)+Theta_i (dp, dn) replaces the split entries.  FUSE
+// adds aq += y_k Qd[i][k] (Y'Qd's column i when Qd is bit-symmetric,
+// computeCost :652, :110).
+template <bool DIAG, bool FUSE, bool FAST>
+__device__ __forceinline__ void mid_block(const MidBlk& B, int k, int i, float dp, float dn, sf2& acc, float& aq) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float yk = j < 4 ? B.b0[j] : B.b1[j - 4];
+        float qp, qn;
+        split_q<FAST>(B.a[j], qp, qn);
+        if constexpr (DIAG) {
+            const bool d = (k + j == i);
+            qp = d ? dp : qp;
+            qn = d ? dn : qn;
+        }
+        acc += sf2{qp, qn} * sf2{yk, yk};
+        if constexpr (FUSE) aq += yk * B.a[j];
+    }
+}
+
+// row i of updateY2 (PQP_CPU.c:603-618) over the LDS row q = Qd[i][.], k =
+// 0..N-1 in order; the diagonal test only in the blocks of the 64 columns
+// that hold the diagonal of this wave's rows
+template <bool FUSE, bool FAST>
+__device__ __forceinline__ void mid_row(const float* q, const float* y, int N, int i, float dp, float dn, float& ap,
+                                        float& an, float& aq) {
+    const int w0 = __builtin_amdgcn_readfirstlane(i & ~63);  // rows of a wave share it
+    const int w1 = w0 + 64;
+    sf2 acc = {0.0f, 0.0f};
+    aq = 0.0f;
+    const int nb = N & ~7;
+    if (nb > 0) {
+        MidBlk c, x;
+        mid_load(c, q, 1, y, 0);
+        int k = 0;
+        for (; k + 8 < nb; k += 8) {
+            mid_load(x, q, 1, y, k + 8);
+            if (k >= w0 && k < w1) mid_block<true, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
+            else mid_block<false, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
+            c = x;
+        }
+        if (k >= w0 && k < w1) mid_block<true, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
+        else mid_block<false, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
+    }
+    ap = acc.x;
+    an = acc.y;
+    for (int k = nb; k < N; ++k) {
+        const float qk = q[k], yk = y[k];
+        float qp, qn;
+        split_q<FAST>(qk, qp, qn);
+        qp = (k == i) ? dp : qp;
+        qn = (k == i) ? dn : qn;
+        ap += qp * yk;
+        an += qn * yk;
+        if constexpr (FUSE) aq += yk * qk;
+    }
+}
+
+// one update row (and with FUSE its Y'Qd column) into nxt / tq
+template <bool FUSE, bool FAST>
+__device__ __forceinline__ void mid_update(const float* Qd, int ldn, const float* cur, float* nxt, float* tq,
+                                           const float* dP, const float* dN, const float* Fdn, const float* Fdp,
+                                           int N, int i) {
+    float ap, an, aq;
+    mid_row<FUSE, FAST>(Qd + i * ldn, cur, N, i, dP[i], dN[i], ap, an, aq);
+    if constexpr (FUSE) tq[i] = aq;
+    const float num = an + 1.0f * Fdn[i];  // :611
+    const float den = ap + 1.0f * Fdp[i];  // :612
+    nxt[i] = num / den * cur[i];           // :594
+}
+
+__global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __restrict__ st0) {
+    constexpr int NT = 256;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;
+    const int N = A.N, M = A.M;
+    const bool conv = (A.mode != kModeFixed);
+    const MidLayout L = mid_layout(N, M, conv);
+    const int ldn = L.ldn, ldm = L.ldm;
+    float* Qd = lds + L.Qd;
+    float* Gp = lds + L.Gp;
+    float* Qi = lds + L.Qi;
+    float* Qp = lds + L.Qp;
+    float* tq = lds + L.tq;
+    float* fy = lds + L.fy;
+    float* tM = lds + L.tM;
+    float* Us = lds + L.Us;
+    float* tu = lds + L.tu;
+    float* fu = lds + L.fu;
+    float* Fp = lds + L.Fp;
+    float* dP = lds + L.dP;
+    float* dN = lds + L.dN;
+    float* Fdp = lds + L.Fdp;
+    float* Fdn = lds + L.Fdn;
+    float* Fd = lds + L.Fd;
+    float* Kp = lds + L.Kp;
+    float* sc = lds + L.sc;  // [0] stop
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+    // ---- stage the problem (once per launch) ----
+    for (int e = tid; e < N * N; e += NT) {
+        const int i = e / N, k = e - i * N;
+        Qd[i * ldn + k] = A.Qd[e];
+    }
+    for (int i = tid; i < N; i += NT) {
+        const float f = A.Fd[i];
+        Fd[i] = f;
+        Fdp[i] = max_ref(0.0f, f);   // matrixPos(Fdp, Fd) :703
+        Fdn[i] = max_ref(0.0f, -f);  // matrixNeg(Fdn, Fd) :704
+    }
+    if (conv) {
+        for (int e = tid; e < N * M; e += NT) {
+            const int i = e / M, j = e - i * M;
+            Gp[i * ldm + j] = A.Gp[e];
+        }
+        for (int e = tid; e < M * M; e += NT) {
+            const int i = e / M, j = e - i * M;
+            Qi[i * ldm + j] = A.Qinv[e];
+            Qp[i * ldm + j] = A.Qp[e];
+        }
+        for (int i = tid; i < N; i += NT) Kp[i] = A.Kp[i];
+        for (int j = tid; j < M; j += NT) Fp[j] = A.Fp[j];
+    }
+    float* cur = lds + L.ya;
+    float* nxt = lds + L.yb;
+    for (int i = tid; i < align4(N); i += NT) {
+        cur[i] = i < N ? (st->resume ? A.Y[i] : 1000.0f) : 0.0f;  // initMat(Y,1000) :710
+        nxt[i] = 0.0f;
+    }
+    __syncthreads();
+    // computeTheta (:503-519) and the diagonal literals of computeQdp_theta /
+    // computeQdn_theta (:524-537); Qd bit-symmetric?  any NaN in it?
+    int asym = 0, nan = 0;
+    for (int i = tid; i < N; i += NT) {
+        const float* row = Qd + i * ldn;
+        float s = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            s += max_ref(0.0f, -row[k]) * 1.0f;
+            if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
+            if (row[k] != row[k]) nan = 1;
+        }
+        const float th = max_ref(s, 5.0f), qii = row[i];
+        dP[i] = max_ref(0.0f, qii) + 1.0f * th;
+        dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
+    }
+    const bool sym = !__syncthreads_or(asym);
+    const bool fast = !__syncthreads_or(nan);
+    const float Md = conv ? A.Md[0] : 0.0f, Mp = conv ? A.Mp[0] : 0.0f;
+
+    const bool may_update = (A.mode != kModeTerminate);
+    const int nR = may_update ? (N + 63) & ~63 : 0;  // update-row items (whole waves)
+    const int nT = conv ? (M + 63) & ~63 : 0;        // tM items
+    long long h = st->h;
+    long long done_here = 0;
+    int status = kStatusContinue;
+    bool was_feasible = false;
+    for (;;) {
+        const bool fuse = conv && was_feasible && sym;    // Y'Qd inside the update rows
+        const bool spec = conv && was_feasible && !sym;   // Y'Qd columns beside them
+        // ---------------- phase A ----------------
+        const int nA = nR + nT + (spec ? nR : 0);
+        for (int it = tid; it < nA; it += NT) {
+            if (it < nR) {
+                const int i = it;
+                if (i < N) {
+                    if (fast) {
+                        if (fuse) mid_update<true, true>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
+                        else mid_update<false, true>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
+                    } else {
+                        if (fuse) mid_update<true, false>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
+                        else mid_update<false, false>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
+                    }
+                }
+            } else if (it < nR + nT) {
+                const int j = it - nR;
+                if (j < M) tM[j] = mid_dot(Gp + j, ldm, cur, N) + 1.0f * Fp[j];  // :355-356
+            } else {
+                const int j = it - nR - nT;
+                if (j < N) tq[j] = mid_dot(Qd + j, ldn, cur, N);  // Y'Qd, column access :110
+            }
+        }
+        __syncthreads();
+        if (conv) {
+            // ---------------- phase B: U = -Qp_inv tM ----------------
+            for (int i = tid; i < M; i += NT) Us[i] = -mid_dot(Qi + i * ldm, 1, tM, M);  // :357-358
+            __syncthreads();
+            // ---------------- phase C: checkFeas ----------------
+            int bad = 0;
+            for (int i = tid; i < N; i += NT) {
+                const float s = mid_dot(Gp + i * ldm, 1, Us, M);
+                const float kp = Kp[i];
+                if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+            }
+            const bool infeasible = __syncthreads_or(bad);
+            int stop = 0;
+            if (!infeasible) {
+                // ------------ phase D: the dot products' terms ------------
+                const bool have_tq = fuse || spec;
+                const int nN = (N + 63) & ~63;
+                for (int it = tid; it < nN + nT; it += NT) {
+                    if (it < nN) {
+                        const int j = it;
+                        if (j < N) {
+                            const float t = have_tq ? tq[j] : mid_dot(Qd + j, ldn, cur, N);
+                            tq[j] = t * cur[j];   // (Y'Qd).Y terms :652-655
+                            fy[j] = Fd[j] * cur[j];  // Fd'Y terms :656-657
+                        }
+                    } else {
+                        const int j = it - nN;
+                        if (j < M) {
+                            tu[j] = mid_dot(Qp + j, ldm, Us, M) * Us[j];  // (U'Qp).U
+                            fu[j] = Fp[j] * Us[j];                        // Fp'U
+                        }
+                    }
+                }
+                __syncthreads();
+                // ------------ phase E: the four sums, the costs, the tests ------------
+                if (wave == 0) {
+                    float s = 0.0f;
+                    if (lane < 4) {
+                        const float* v = lane == 0 ? tq : lane == 1 ? fy : lane == 2 ? tu : fu;
+                        const int n = lane < 2 ? N : M;
+                        const int nb = n & ~7;
+                        if (nb > 0) {  // loads of the next 8 terms in flight
+                            sf4 c0 = *reinterpret_cast<const sf4*>(v), c1 = *reinterpret_cast<const sf4*>(v + 4);
+                            for (int k = 8; k < nb; k += 8) {
+                                const sf4 x0 = *reinterpret_cast<const sf4*>(v + k);
+                                const sf4 x1 = *reinterpret_cast<const sf4*>(v + k + 4);
+                                s += c0.x; s += c0.y; s += c0.z; s += c0.w;
+                                s += c1.x; s += c1.y; s += c1.z; s += c1.w;
+                                c0 = x0;
+                                c1 = x1;
+                            }
+                            s += c0.x; s += c0.y; s += c0.z; s += c0.w;
+                            s += c1.x; s += c1.y; s += c1.z; s += c1.w;
+                        }
+                        for (int k = nb; k < n; ++k) s += v[k];
+                    }
+                    const float quad_d = rdl(s, 0), lin_d = rdl(s, 1), quad_p = rdl(s, 2), lin_p = rdl(s, 3);
+                    float Jd = 0.0f;
+                    Jd = (float)((double)Jd + 0.5 * (double)quad_d);
+                    Jd += lin_d;
+                    Jd += Md / 2;
+                    float Jp = 0.0f;
+                    Jp = (float)((double)Jp + 0.5 * (double)quad_p);
+                    Jp += lin_p;
+                    Jp += Mp / 2;
+                    int sp = 1;
+                    if (Jp > -Jd) sp = 0;
+                    if ((double)(Jp + Jd) > kTol) sp = 0;
+                    if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) sp = 0;
+                    if (lane == 0) {
+                        sc[0] = (float)sp;
+                        st->Jp = Jp;
+                        st->Jd = Jd;
+                        st->have_costs = 1;
+                    }
+                }
+                __syncthreads();
+                stop = sc[0] != 0.0f;
+            }
+            was_feasible = !infeasible;
+            if (A.mode == kModeTerminate) {
+                if (tid == 0) st->last_stop = stop;
+                status = kStatusDone;
+                break;
+            }
+            if (stop) {
+                status = kStatusDone;
+                break;
+            }
+            if (A.max_updates > 0 && h - 1 >= A.max_updates) {
+                status = kStatusCapped;
+                break;
+            }
+        } else if (h >= A.num_iter) {  // while(h < NUM_ITER)
+            status = kStatusDone;
+            break;
+        }
+        if (done_here >= A.chunk) {
+            status = kStatusContinue;
+            break;
+        }
+        // accept the update computed in phase A.  The next phase A reads cur
+        // (written before the last barrier) and writes nxt (read by nobody
+        // until after the next barrier); tq/fy/tu/fu of phase D were last read
+        // in phase E, behind a barrier.
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+        ++h;
+        ++done_here;
+    }
+    for (int i = tid; i < N; i += NT) A.Y[i] = cur[i];
+    if (conv)
+        for (int i = tid; i < M; i += NT) A.U[i] = Us[i];
+    if (tid == 0) {
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
+    }
+}
+
+size_t solve_mid_lds_bytes(int N, int M, bool conv) { return sizeof(float) * (size_t)mid_layout(N, M, conv).total; }
+
+static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    hipLaunchKernelGGL(k_solve_mid, dim3(B), dim3(256), solve_mid_lds_bytes(a.N, a.M, a.mode != kModeFixed), s, a,
+                       st);
+    return hipGetLastError();
+}
+
 size_t solve_small_lds_bytes(int N, int M) { return sizeof(float) * (size_t)small_layout(N, M).total; }
 
 static hipError_t launch_small_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
@@ -3040,10 +3481,12 @@ hipError_t launch_solve_single(const SolveArgs& a, SolveState* st, hipStream_t s
     return launch_single_grid(1, a, st, s);
 }
 
-// path: 0 tiny (N, M <= 32), 1 LDS-staged small, 2 global-memory single
+// path: 0 tiny (N, M <= 32), 1 LDS-staged small, 2 global-memory single,
+// 3 LDS-resident mid-size
 hipError_t launch_solve_batch(int B, int path, const SolveArgs& a, SolveState* st, hipStream_t s) {
     if (path == 0) return launch_tiny_grid(B, a, st, s);
     if (path == 1) return launch_small_grid(B, a, st, s);
+    if (path == 3) return launch_mid_grid(B, a, st, s);
     return launch_single_grid(B, a, st, s);
 }
 

@@ -680,8 +680,8 @@ class ProblemBatch:
                                          mode, num_iter, max_updates, self._p(self.Y), self._p(self.U),
                                          self._p(self.h), self._p(self.status), self._s()))
             return self
-        if self._prep is None:
-            self.prepare()
+        if self._prep is None or self._prep["path"] != lib().pqp_batch_solve_path(self.N, self.M):
+            self.prepare()  # first solve, new data, or a tuning knob moved the size to another solver
         P = self._prep
         p = lambda k: self._p(P[k]) if P.get(k) is not None else None  # noqa: E731
         _check(lib().pqp_batch_solve_prepared(self.B, self.N, self.M, self._p(self.Qd), p("QdT"), p("theta"), p("sym"),

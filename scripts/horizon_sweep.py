@@ -44,6 +44,21 @@ def main(Hs):
         # iterates: Qd (update, Y'Qd fused), Gp twice, Qp_inv, Qp
         alg = 4.0 * N * N + 8.0 * N * M + 8.0 * M * M
         it = float(h.sum())
+        ab = {}
+        if path == 3:  # the same batch with k_solve_mid turned off: time and bits
+            Y3 = pb.Y.clone()
+            old = pqp_amd.tune("mid_off", 1)
+            try:
+                pb.solve(max_updates=200000)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                pb.solve(max_updates=200000)
+                torch.cuda.synchronize()
+                ab = {"mid_off_path": pqp_amd.lib().pqp_batch_solve_path(N, M),
+                      "mid_off_batch_ms": (time.perf_counter() - t0) * 1e3,
+                      "mid_off_same_bits": bool(torch.equal(pb.Y.view(torch.int32), Y3.view(torch.int32)))}
+            finally:
+                pqp_amd.tune("mid_off", old)
         with pqp_amd.Problem(P) as prob:
             prob.solve(max_updates=200000)
             ts = []
@@ -55,7 +70,7 @@ def main(Hs):
         print(json.dumps({"H": H, "n_dual": N, "m": M, "batch": B, "batch_path": path, "all_h_313": ok,
                           "batch_ms": dt * 1e3, "qp_solves_per_s": B / dt, "instance_iter_per_s": it / dt,
                           "alg_GBps": alg * it / dt / 1e9, "single_h": r["h"], "single_ms": single * 1e3,
-                          "single_us_per_iter": single / r["h"] * 1e6}), flush=True)
+                          "single_us_per_iter": single / r["h"] * 1e6, **ab}), flush=True)
         del pb
         torch.cuda.empty_cache()
 

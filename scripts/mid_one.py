@@ -1,0 +1,39 @@
+"""One k_solve_mid workload for profiling: the bundled plant as H diagonal
+blocks, B copies, in the mode named by MODE (fixed | infeasible | feasible),
+solved twice (the second is the one to read).  Usage:
+MODE=fixed python scripts/mid_one.py [H] [B]"""
+from __future__ import annotations
+
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+
+def main():
+    import torch
+
+    import pqp_amd
+    from oracle import Oracle, block_diag_problem
+
+    H = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    mode = os.environ.get("MODE", "fixed")
+    P = block_diag_problem(Oracle().bundled_problem(ROOT / "tests" / "golden" / "example"), H)
+    pb = pqp_amd.ProblemBatch.replicate(P, B)
+    if mode == "infeasible":
+        pb.Kp.fill_(-1e30)
+    for _ in range(2):
+        if mode == "fixed":
+            pb.solve(pqp_amd.MODE_FIXED, num_iter=314)
+        else:
+            pb.solve(max_updates=312 if mode == "infeasible" else 200000)
+    torch.cuda.synchronize()
+    print(mode, H, B, int(pb.h.min()), int(pb.h.max()))
+
+
+if __name__ == "__main__":
+    main()
