@@ -1537,6 +1537,8 @@ int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float
     a.GpT = path == 2 && mode == PQP_MODE_CONVERGE ? d_GpT : nullptr;
     a.QinvT = path == 2 && mode == PQP_MODE_CONVERGE ? d_QinvT : nullptr;
     a.feas_split = (g_tune.batch_opts & 16) ? 0 : 1;
+    a.trace = g_tune.mid_trace;
+    a.trace_n = g_tune.mid_trace_n;
     a.Fp = d_Fp;
     a.Mp = d_Mp;
     a.Gp = d_Gp;
@@ -1943,6 +1945,9 @@ extern "C" int pqp_tune_trace(const char* what, void* d_buf, int n) {
     if (std::strcmp(what, "persist") == 0) {
         pqp::g_tune.persist_trace = buf;
         pqp::g_tune.persist_trace_n = n;
+    } else if (std::strcmp(what, "mid") == 0) {
+        pqp::g_tune.mid_trace = buf;
+        pqp::g_tune.mid_trace_n = n;
     } else if (std::strcmp(what, "converge") == 0) {
         pqp::g_tune.converge_trace = buf;
         pqp::g_tune.converge_trace_n = n;

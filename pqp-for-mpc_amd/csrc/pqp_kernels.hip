@@ -2615,105 +2615,151 @@ hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) 
 
 // ---------------------------------------------------------------------------
 // k_solve_mid: solveQuadraticDual (PQP_CPU.c:694-750) for mid-size problems
-// -- the MPC plant over a few horizon steps, N ~ 33..165 -- one 256-thread
-// workgroup per problem with Qd, Gp, Qp_inv and Qp each held in LDS ONCE (no
-// split copies: the update forms its split entries from Qd on the fly, as
-// k_solve_single does from HBM), so the problem is read from HBM once per
-// launch and every iteration runs out of LDS.  Matrix rows are laid out with
-// an ODD stride: a lane-per-row walk (row i at i*ld + k) and a lane-per-column
-// walk (column j at k*ld + j) are then both free of bank conflicts with
-// 4-byte reads, so each matrix serves both of its access directions.  Shared
-// vectors are 16-byte aligned and read as 16-byte broadcasts.
+// -- the MPC plant over a few horizon steps, N ~ 33..165 -- one workgroup
+// per problem with Qd, Gp, Qp_inv and Qp each held in LDS ONCE (no split
+// copies: the update forms its split entries from Qd on the fly), so a
+// problem is read from HBM once per launch and every iteration runs out of
+// LDS.  Layout: Qd rows 16-byte aligned with a stride of 4 (mod 8) dwords
+// (ldn = round8(N) + 4): a lane-per-row walk reads 16 bytes per lane
+// conflict-free and a lane-per-column walk reads consecutive dwords; Gp,
+// Qp_inv, Qp with an ODD stride (4-byte reads, conflict-free both ways).
+// Every dimension is padded to a multiple of 8 with zeros, so each walk is
+// whole blocks of 8 terms: a padded term adds +0 (or -0) to a sum that starts
+// at +0.0f and therefore is never -0, which leaves it unchanged.  Shared
+// vectors are 16-byte aligned and read as 16-byte broadcasts.  The blocks of
+// a walk are software-pipelined two deep (loads of block b+1 issued before
+// block b's arithmetic): with one or two workgroups per CU there are too few
+// waves to hide LDS latency otherwise.
 //
 // One iteration (terminate(Y_h), then the update from Y_h, computed
 // speculatively and dropped when terminate() stops -- every value is the
 // reference's):
-//   phase A  update rows i < N (one lane each; with Y'Qd fused in once an
-//            iterate was feasible and Qd is bit-symmetric), tM = Gp'Y + Fp
-//            (one lane per column), and -- Qd not symmetric, previous iterate
-//            feasible -- the Y'Qd columns, on separate waves at once
-//   phase B  U = -Qp_inv tM          (computeUfromY :352-360)
+//   phase A  update rows i < N (one lane each; Y'Qd's column i and its
+//            product with y_i fused in once an iterate was feasible and Qd is
+//            bit-symmetric), tM = Gp'Y + Fp (one lane per column) and Fd.Y
+//            (one more lane), and -- Qd not symmetric, previous iterate
+//            feasible -- the Y'Qd columns, on separate waves
+//   phase B  U = -Qp_inv tM (computeUfromY :352-360); a spare wave sums the
+//            (Y'Qd).Y terms when phase A formed them
 //   phase C  checkFeas, any row over its bound -> infeasible (:632-641)
-//   phase D  (feasible) the terms of the four dot products of computeCost
-//   phase E  (feasible) lanes 0-3 of wave 0 sum the four in k order, Jp, Jd
+//   phase D  (feasible) the (U'Qp).U and Fp.U terms (and the (Y'Qd).Y terms
+//            when phase A did not form them)
+//   phase E  (feasible) lanes of wave 0 sum what is left in k order; Jp, Jd
 //            and the three gap tests (:648-687)
 // Chunked and resumable like k_solve_small (state in SolveState).
 // ---------------------------------------------------------------------------
+__host__ __device__ inline int round8(int n) { return (n + 7) & ~7; }
 struct MidLayout {
-    int ldn, ldm;
-    int ya, yb, tq, fy, tM, Us, tu, fu, Fp, dP, dN, Fdp, Fdn, Fd, Kp, sc, Qd, Gp, Qi, Qp, total;
+    int nk, mk;    // N, M rounded up to 8
+    int ldn, ldm;  // row strides of Qd (nk + 4) and of Gp / Qp_inv / Qp (mk + 1)
+    int ya, yb, tq, dP, dN, Fdp, Fdn, Fd, Kp, tM, Us, tu, fu, Fp, sc, Qd, Gp, Qi, Qp, total;
 };
 __host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv) {
     MidLayout L;
-    L.ldn = N | 1;
-    L.ldm = M | 1;
+    L.nk = round8(N);
+    L.mk = round8(M);
+    L.ldn = L.nk + 4;
+    L.ldm = L.mk + 1;
     int o = 0;
-    L.ya = o;  o += align4(N);
-    L.yb = o;  o += align4(N);
-    L.tq = o;  o += align4(N);
-    L.fy = o;  o += align4(N);
-    L.dP = o;  o += align4(N);
-    L.dN = o;  o += align4(N);
-    L.Fdp = o; o += align4(N);
-    L.Fdn = o; o += align4(N);
-    L.Fd = o;  o += align4(N);
+    L.ya = o;  o += L.nk;
+    L.yb = o;  o += L.nk;
+    L.tq = o;  o += L.nk;
+    L.dP = o;  o += L.nk;
+    L.dN = o;  o += L.nk;
+    L.Fdp = o; o += L.nk;
+    L.Fdn = o; o += L.nk;
+    L.Fd = o;  o += L.nk;
     L.sc = o;  o += 8;
     if (conv) {
-        L.tM = o;  o += align4(M);
-        L.Us = o;  o += align4(M);
-        L.tu = o;  o += align4(M);
-        L.fu = o;  o += align4(M);
-        L.Fp = o;  o += align4(M);
-        L.Kp = o;  o += align4(N);
+        L.Kp = o;  o += L.nk;
+        L.tM = o;  o += L.mk;
+        L.Us = o;  o += L.mk;
+        L.tu = o;  o += L.mk;
+        L.fu = o;  o += L.mk;
+        L.Fp = o;  o += L.mk;
     } else {
-        L.tM = L.Us = L.tu = L.fu = L.Fp = L.Kp = 0;
+        L.Kp = L.tM = L.Us = L.tu = L.fu = L.Fp = 0;
     }
-    L.Qd = o;  o += N * L.ldn;
+    L.Qd = o;  o += L.nk * L.ldn;
     if (conv) {
-        L.Gp = o;  o += N * L.ldm;
-        L.Qi = o;  o += M * L.ldm;
-        L.Qp = o;  o += M * L.ldm;
+        L.Gp = o;  o += L.nk * L.ldm;
+        L.Qi = o;  o += L.mk * L.ldm;
+        L.Qp = o;  o += L.mk * L.ldm;
     } else {
         L.Gp = L.Qi = L.Qp = 0;
     }
     L.total = o;
     return L;
 }
+// threads of the k_solve_mid workgroup: enough waves for phase A at once
+__host__ __device__ inline int mid_threads(int N, int M, bool conv) {
+    const int w = (N + 63) / 64 + (conv ? (M + 64) / 64 : 0);
+    return w <= 2 ? 128 : (w <= 4 ? 256 : 512);
+}
 
-// Blocks of 8 terms, software-pipelined: the LDS loads of block b+1 are
-// issued before block b's arithmetic, so an iteration's dependent sums wait
-// on LDS latency once per pass instead of once per block (with one or two
-// workgroups per CU there are too few other waves to hide it).
+// 8 terms of a strided walk: a[(k + j) * as] (per-lane a and as) and the
+// broadcast b[k + j]
 struct MidBlk {
     float a[8];
     sf4 b0, b1;
 };
 __device__ __forceinline__ void mid_load(MidBlk& B, const float* a, int as, const float* b, int k) {
-    B.b0 = *reinterpret_cast<const sf4*>(b + k);
-    B.b1 = *reinterpret_cast<const sf4*>(b + k + 4);
 #pragma unroll
     for (int j = 0; j < 8; ++j) B.a[j] = a[(k + j) * as];
+    B.b0 = *reinterpret_cast<const sf4*>(b + k);
+    B.b1 = *reinterpret_cast<const sf4*>(b + k + 4);
 }
-
-// s = sum_k a[k * as] * b[k], k = 0..n-1 in the reference's order (product
-// rounded before each add); b a 16-byte-aligned LDS vector every lane reads
-// at the same address (16-byte broadcasts)
-__device__ __forceinline__ float mid_dot(const float* a, int as, const float* b, int n) {
+__device__ __forceinline__ void mid_acc(float& s, const MidBlk& B) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += B.a[j] * (j < 4 ? B.b0[j] : B.b1[j - 4]);
+}
+// s = sum_k a[k * as] * b[k], k = 0..n8-1 (n8 a multiple of 8) in the
+// reference's order, product rounded before each add
+__device__ __forceinline__ float mid_dot(const float* a, int as, const float* b, int n8) {
     float s = 0.0f;
-    const int nb = n & ~7;
-    if (nb > 0) {
-        MidBlk c, x;
-        mid_load(c, a, as, b, 0);
-        for (int k = 8; k < nb; k += 8) {
-            mid_load(x, a, as, b, k);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s += c.a[j] * (j < 4 ? c.b0[j] : c.b1[j - 4]);
-            c = x;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += c.a[j] * (j < 4 ? c.b0[j] : c.b1[j - 4]);
+    MidBlk c, x;
+    mid_load(c, a, as, b, 0);
+    int k = 0;
+    for (; k + 16 < n8; k += 16) {
+        mid_load(x, a, as, b, k + 8);
+        mid_acc(s, c);
+        mid_load(c, a, as, b, k + 16);
+        mid_acc(s, x);
     }
-    for (int k = nb; k < n; ++k) s += a[k * as] * b[k];
+    if (k + 8 < n8) {
+        mid_load(x, a, as, b, k + 8);
+        mid_acc(s, c);
+        mid_acc(s, x);
+    } else {
+        mid_acc(s, c);
+    }
+    return s;
+}
+// s = sum_k v[k], k = 0..n8-1 in order (v 16-byte aligned, per lane)
+__device__ __forceinline__ void mid_add8(float& s, sf4 a, sf4 b) {
+    s += a.x; s += a.y; s += a.z; s += a.w;
+    s += b.x; s += b.y; s += b.z; s += b.w;
+}
+__device__ __forceinline__ float mid_sum(const float* v, int n8) {
+    float s = 0.0f;
+    sf4 c0 = *reinterpret_cast<const sf4*>(v), c1 = *reinterpret_cast<const sf4*>(v + 4), x0, x1;
+    int k = 0;
+    for (; k + 16 < n8; k += 16) {
+        x0 = *reinterpret_cast<const sf4*>(v + k + 8);
+        x1 = *reinterpret_cast<const sf4*>(v + k + 12);
+        mid_add8(s, c0, c1);
+        c0 = *reinterpret_cast<const sf4*>(v + k + 16);
+        c1 = *reinterpret_cast<const sf4*>(v + k + 20);
+        mid_add8(s, x0, x1);
+    }
+    if (k + 8 < n8) {
+        x0 = *reinterpret_cast<const sf4*>(v + k + 8);
+        x1 = *reinterpret_cast<const sf4*>(v + k + 12);
+        mid_add8(s, c0, c1);
+        mid_add8(s, x0, x1);
+    } else {
+        mid_add8(s, c0, c1);
+    }
     return s;
 }
 
@@ -2736,83 +2782,84 @@ __device__ __forceinline__ void split_q(float q, float& qp, float& qn) {
     }
 }
 
-// terms k..k+7 of row i of updateY2 over the loaded block (Qd[i][k..k+7] and
-// y_k..y_k+7).  (ap, an) ride as one packed pair: one v_pk_mul_f32 and one
-// v_pk_add_f32 per k (each half of a packed op rounds as the scalar op).
-// DIAG: the block holds the diagonal k = i of some lanes' rows, where the
-// literal max(0,+-q_ii)+Theta_i (dp, dn) replaces the split entries.  FUSE
-// adds aq += y_k Qd[i][k] (Y'Qd's column i when Qd is bit-symmetric,
-// computeCost :652, :110).
+// 8 terms of an update row: Qd[i][k..k+7] (16-byte loads of the row) and the
+// broadcast y_k..y_k+7
+struct RowBlk {
+    sf4 q0, q1, y0, y1;
+};
+__device__ __forceinline__ void row_load(RowBlk& B, const float* q, const float* y, int k) {
+    B.q0 = *reinterpret_cast<const sf4*>(q + k);
+    B.q1 = *reinterpret_cast<const sf4*>(q + k + 4);
+    B.y0 = *reinterpret_cast<const sf4*>(y + k);
+    B.y1 = *reinterpret_cast<const sf4*>(y + k + 4);
+}
+// (ap, an) ride as one packed pair: one v_pk_mul_f32 and one v_pk_add_f32 per
+// k (each half of a packed op rounds as the scalar op).  DIAG: the block
+// holds the diagonal k = i of some lanes' rows, where the literal
+// max(0,+-q_ii)+Theta_i (dp, dn) replaces the split entries.  FUSE adds aq +=
+// y_k Qd[i][k] (Y'Qd's column i when Qd is bit-symmetric, computeCost :652,
+// :110).
 template <bool DIAG, bool FUSE, bool FAST>
-__device__ __forceinline__ void mid_block(const MidBlk& B, int k, int i, float dp, float dn, sf2& acc, float& aq) {
+__device__ __forceinline__ void row_block(const RowBlk& B, int k, int i, float dp, float dn, sf2& acc, float& aq) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float yk = j < 4 ? B.b0[j] : B.b1[j - 4];
+        const float q = j < 4 ? B.q0[j] : B.q1[j - 4];
+        const float yk = j < 4 ? B.y0[j] : B.y1[j - 4];
         float qp, qn;
-        split_q<FAST>(B.a[j], qp, qn);
+        split_q<FAST>(q, qp, qn);
         if constexpr (DIAG) {
             const bool d = (k + j == i);
             qp = d ? dp : qp;
             qn = d ? dn : qn;
         }
         acc += sf2{qp, qn} * sf2{yk, yk};
-        if constexpr (FUSE) aq += yk * B.a[j];
+        if constexpr (FUSE) aq += yk * q;
     }
 }
-
-// row i of updateY2 (PQP_CPU.c:603-618) over the LDS row q = Qd[i][.], k =
-// 0..N-1 in order; the diagonal test only in the blocks of the 64 columns
-// that hold the diagonal of this wave's rows
 template <bool FUSE, bool FAST>
-__device__ __forceinline__ void mid_row(const float* q, const float* y, int N, int i, float dp, float dn, float& ap,
-                                        float& an, float& aq) {
-    const int w0 = __builtin_amdgcn_readfirstlane(i & ~63);  // rows of a wave share it
-    const int w1 = w0 + 64;
-    sf2 acc = {0.0f, 0.0f};
-    aq = 0.0f;
-    const int nb = N & ~7;
-    if (nb > 0) {
-        MidBlk c, x;
-        mid_load(c, q, 1, y, 0);
-        int k = 0;
-        for (; k + 8 < nb; k += 8) {
-            mid_load(x, q, 1, y, k + 8);
-            if (k >= w0 && k < w1) mid_block<true, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
-            else mid_block<false, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
-            c = x;
-        }
-        if (k >= w0 && k < w1) mid_block<true, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
-        else mid_block<false, FUSE, FAST>(c, k, i, dp, dn, acc, aq);
-    }
-    ap = acc.x;
-    an = acc.y;
-    for (int k = nb; k < N; ++k) {
-        const float qk = q[k], yk = y[k];
-        float qp, qn;
-        split_q<FAST>(qk, qp, qn);
-        qp = (k == i) ? dp : qp;
-        qn = (k == i) ? dn : qn;
-        ap += qp * yk;
-        an += qn * yk;
-        if constexpr (FUSE) aq += yk * qk;
-    }
+__device__ __forceinline__ void row_step(const RowBlk& B, int k, int w0, int i, float dp, float dn, sf2& acc,
+                                         float& aq) {
+    if (k >= w0 && k < w0 + 64) row_block<true, FUSE, FAST>(B, k, i, dp, dn, acc, aq);
+    else row_block<false, FUSE, FAST>(B, k, i, dp, dn, acc, aq);
 }
 
-// one update row (and with FUSE its Y'Qd column) into nxt / tq
+// update row i (updateY2, PQP_CPU.c:603-618) into nxt[i], k = 0..nk-1 in
+// order, the diagonal test only in the blocks of the 64 columns that hold the
+// diagonal of this wave's rows; FUSE: tq[i] = (Y'Qd)_i * y_i as well
 template <bool FUSE, bool FAST>
-__device__ __forceinline__ void mid_update(const float* Qd, int ldn, const float* cur, float* nxt, float* tq,
+__device__ __forceinline__ void mid_update(const float* Qd, int ldn, int nk, const float* cur, float* nxt, float* tq,
                                            const float* dP, const float* dN, const float* Fdn, const float* Fdp,
-                                           int N, int i) {
-    float ap, an, aq;
-    mid_row<FUSE, FAST>(Qd + i * ldn, cur, N, i, dP[i], dN[i], ap, an, aq);
-    if constexpr (FUSE) tq[i] = aq;
-    const float num = an + 1.0f * Fdn[i];  // :611
-    const float den = ap + 1.0f * Fdp[i];  // :612
-    nxt[i] = num / den * cur[i];           // :594
+                                           int i) {
+    const float* q = Qd + i * ldn;
+    const float dp = dP[i], dn = dN[i];
+    const int w0 = __builtin_amdgcn_readfirstlane(i & ~63);  // rows of a wave share it
+    sf2 acc = {0.0f, 0.0f};
+    float aq = 0.0f;
+    RowBlk c, x;
+    row_load(c, q, cur, 0);
+    int k = 0;
+    for (; k + 16 < nk; k += 16) {
+        row_load(x, q, cur, k + 8);
+        row_step<FUSE, FAST>(c, k, w0, i, dp, dn, acc, aq);
+        row_load(c, q, cur, k + 16);
+        row_step<FUSE, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
+    }
+    if (k + 8 < nk) {
+        row_load(x, q, cur, k + 8);
+        row_step<FUSE, FAST>(c, k, w0, i, dp, dn, acc, aq);
+        row_step<FUSE, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
+    } else {
+        row_step<FUSE, FAST>(c, k, w0, i, dp, dn, acc, aq);
+    }
+    const float y = cur[i];
+    if constexpr (FUSE) tq[i] = aq * y;   // (Y'Qd)_i * Y_i, computeCost :652-655
+    const float num = acc.y + 1.0f * Fdn[i];  // :611
+    const float den = acc.x + 1.0f * Fdp[i];  // :612
+    nxt[i] = num / den * y;                   // :594
 }
 
-__global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __restrict__ st0) {
-    constexpr int NT = 256;
+template <int NT>
+__global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
     SolveState* st = st0 + blockIdx.x;
@@ -2820,13 +2867,12 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
     const int N = A.N, M = A.M;
     const bool conv = (A.mode != kModeFixed);
     const MidLayout L = mid_layout(N, M, conv);
-    const int ldn = L.ldn, ldm = L.ldm;
+    const int ldn = L.ldn, ldm = L.ldm, nk = L.nk, mk = L.mk;
     float* Qd = lds + L.Qd;
     float* Gp = lds + L.Gp;
     float* Qi = lds + L.Qi;
     float* Qp = lds + L.Qp;
     float* tq = lds + L.tq;
-    float* fy = lds + L.fy;
     float* tM = lds + L.tM;
     float* Us = lds + L.Us;
     float* tu = lds + L.tu;
@@ -2838,10 +2884,12 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
     float* Fdn = lds + L.Fdn;
     float* Fd = lds + L.Fd;
     float* Kp = lds + L.Kp;
-    float* sc = lds + L.sc;  // [0] stop
+    float* sc = lds + L.sc;  // [0] (Y'Qd).Y  [1] Fd.Y  [2] stop
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
-    // ---- stage the problem (once per launch) ----
+    // ---- stage the problem (once per launch; padding zero) ----
+    for (int e = tid; e < L.total; e += NT) lds[e] = 0.0f;
+    __syncthreads();
     for (int e = tid; e < N * N; e += NT) {
         const int i = e / N, k = e - i * N;
         Qd[i * ldn + k] = A.Qd[e];
@@ -2867,10 +2915,7 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
     }
     float* cur = lds + L.ya;
     float* nxt = lds + L.yb;
-    for (int i = tid; i < align4(N); i += NT) {
-        cur[i] = i < N ? (st->resume ? A.Y[i] : 1000.0f) : 0.0f;  // initMat(Y,1000) :710
-        nxt[i] = 0.0f;
-    }
+    for (int i = tid; i < N; i += NT) cur[i] = st->resume ? A.Y[i] : 1000.0f;  // initMat(Y,1000) :710
     __syncthreads();
     // computeTheta (:503-519) and the diagonal literals of computeQdp_theta /
     // computeQdn_theta (:524-537); Qd bit-symmetric?  any NaN in it?
@@ -2893,14 +2938,22 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
 
     const bool may_update = (A.mode != kModeTerminate);
     const int nR = may_update ? (N + 63) & ~63 : 0;  // update-row items (whole waves)
-    const int nT = conv ? (M + 63) & ~63 : 0;        // tM items
+    const int nT = conv ? (M + 64) & ~63 : 0;        // tM items, and Fd.Y on item M
+    const int nU = (M + 63) & ~63;                   // U (and later (U'Qp).U) items
+    const bool quadB = nU < NT;                      // a wave free for the (Y'Qd).Y sum in phase B
     long long h = st->h;
     long long done_here = 0;
     int status = kStatusContinue;
     bool was_feasible = false;
+    // timing trace (pqp_tune_trace "mid"): wave 0's phase totals, each wave's
+    // phase-A busy time, in shader cycles
+    const bool tr = A0.trace && (int)blockIdx.x < A0.trace_n;
+    unsigned long long t_top = 0, t_ph = 0, acc_busyA = 0, acc_ph[4] = {0, 0, 0, 0}, n_it = 0;
     for (;;) {
-        const bool fuse = conv && was_feasible && sym;    // Y'Qd inside the update rows
-        const bool spec = conv && was_feasible && !sym;   // Y'Qd columns beside them
+        if (tr) t_top = t_ph = __builtin_amdgcn_s_memtime();
+        const bool fuse = conv && was_feasible && sym;   // (Y'Qd).Y terms inside the update rows
+        const bool spec = conv && was_feasible && !sym;  // ... in columns beside them
+        const bool have_tq = fuse || spec;
         // ---------------- phase A ----------------
         const int nA = nR + nT + (spec ? nR : 0);
         for (int it = tid; it < nA; it += NT) {
@@ -2908,79 +2961,84 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
                 const int i = it;
                 if (i < N) {
                     if (fast) {
-                        if (fuse) mid_update<true, true>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
-                        else mid_update<false, true>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
+                        if (fuse) mid_update<true, true>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
+                        else mid_update<false, true>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
                     } else {
-                        if (fuse) mid_update<true, false>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
-                        else mid_update<false, false>(Qd, ldn, cur, nxt, tq, dP, dN, Fdn, Fdp, N, i);
+                        if (fuse) mid_update<true, false>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
+                        else mid_update<false, false>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
                     }
                 }
             } else if (it < nR + nT) {
                 const int j = it - nR;
-                if (j < M) tM[j] = mid_dot(Gp + j, ldm, cur, N) + 1.0f * Fp[j];  // :355-356
+                if (j <= M) {  // tM_j = Gp'Y + Fp (:355-356); item M: Fd.Y (:656-657)
+                    const float s = mid_dot(j < M ? Gp + j : Fd, j < M ? ldm : 1, cur, nk);
+                    if (j < M) tM[j] = s + 1.0f * Fp[j];
+                    else sc[1] = s;
+                }
             } else {
                 const int j = it - nR - nT;
-                if (j < N) tq[j] = mid_dot(Qd + j, ldn, cur, N);  // Y'Qd, column access :110
+                if (j < N) tq[j] = mid_dot(Qd + j, ldn, cur, nk) * cur[j];  // Y'Qd, column access :110
             }
         }
+        if (tr) acc_busyA += __builtin_amdgcn_s_memtime() - t_top;
         __syncthreads();
+        if (tr) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc_ph[0] += t - t_ph;
+            t_ph = t;
+            ++n_it;
+        }
         if (conv) {
-            // ---------------- phase B: U = -Qp_inv tM ----------------
-            for (int i = tid; i < M; i += NT) Us[i] = -mid_dot(Qi + i * ldm, 1, tM, M);  // :357-358
+            // ------- phase B: U = -Qp_inv tM; (Y'Qd).Y on a free wave -------
+            if (tid < nU) {
+                for (int i = tid; i < M; i += NT) Us[i] = -mid_dot(Qi + i * ldm, 1, tM, mk);  // :357-358
+            } else if (have_tq && tid == nU) {
+                sc[0] = mid_sum(tq, nk);
+            }
             __syncthreads();
+            if (tr) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                acc_ph[1] += t - t_ph;
+                t_ph = t;
+            }
             // ---------------- phase C: checkFeas ----------------
             int bad = 0;
             for (int i = tid; i < N; i += NT) {
-                const float s = mid_dot(Gp + i * ldm, 1, Us, M);
+                const float s = mid_dot(Gp + i * ldm, 1, Us, mk);
                 const float kp = Kp[i];
                 if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
             }
             const bool infeasible = __syncthreads_or(bad);
+            if (tr) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                acc_ph[2] += t - t_ph;
+                t_ph = t;
+            }
             int stop = 0;
             if (!infeasible) {
                 // ------------ phase D: the dot products' terms ------------
-                const bool have_tq = fuse || spec;
-                const int nN = (N + 63) & ~63;
-                for (int it = tid; it < nN + nT; it += NT) {
-                    if (it < nN) {
+                const int nN = have_tq ? 0 : (N + 63) & ~63;
+                for (int it = tid; it < nU + nN; it += NT) {
+                    if (it < nU) {
                         const int j = it;
-                        if (j < N) {
-                            const float t = have_tq ? tq[j] : mid_dot(Qd + j, ldn, cur, N);
-                            tq[j] = t * cur[j];   // (Y'Qd).Y terms :652-655
-                            fy[j] = Fd[j] * cur[j];  // Fd'Y terms :656-657
+                        if (j < M) {
+                            tu[j] = mid_dot(Qp + j, ldm, Us, mk) * Us[j];  // (U'Qp).U
+                            fu[j] = Fp[j] * Us[j];                         // Fp'U
                         }
                     } else {
-                        const int j = it - nN;
-                        if (j < M) {
-                            tu[j] = mid_dot(Qp + j, ldm, Us, M) * Us[j];  // (U'Qp).U
-                            fu[j] = Fp[j] * Us[j];                        // Fp'U
-                        }
+                        const int j = it - nU;
+                        if (j < N) tq[j] = mid_dot(Qd + j, ldn, cur, nk) * cur[j];  // (Y'Qd).Y
                     }
                 }
                 __syncthreads();
-                // ------------ phase E: the four sums, the costs, the tests ------------
+                // ------------ phase E: the sums left, the costs, the tests ------------
                 if (wave == 0) {
                     float s = 0.0f;
-                    if (lane < 4) {
-                        const float* v = lane == 0 ? tq : lane == 1 ? fy : lane == 2 ? tu : fu;
-                        const int n = lane < 2 ? N : M;
-                        const int nb = n & ~7;
-                        if (nb > 0) {  // loads of the next 8 terms in flight
-                            sf4 c0 = *reinterpret_cast<const sf4*>(v), c1 = *reinterpret_cast<const sf4*>(v + 4);
-                            for (int k = 8; k < nb; k += 8) {
-                                const sf4 x0 = *reinterpret_cast<const sf4*>(v + k);
-                                const sf4 x1 = *reinterpret_cast<const sf4*>(v + k + 4);
-                                s += c0.x; s += c0.y; s += c0.z; s += c0.w;
-                                s += c1.x; s += c1.y; s += c1.z; s += c1.w;
-                                c0 = x0;
-                                c1 = x1;
-                            }
-                            s += c0.x; s += c0.y; s += c0.z; s += c0.w;
-                            s += c1.x; s += c1.y; s += c1.z; s += c1.w;
-                        }
-                        for (int k = nb; k < n; ++k) s += v[k];
-                    }
-                    const float quad_d = rdl(s, 0), lin_d = rdl(s, 1), quad_p = rdl(s, 2), lin_p = rdl(s, 3);
+                    if (lane == 0 && !(have_tq && quadB)) s = mid_sum(tq, nk);
+                    else if (lane == 1) s = mid_sum(tu, mk);
+                    else if (lane == 2) s = mid_sum(fu, mk);
+                    const float quad_d = (have_tq && quadB) ? sc[0] : rdl(s, 0);
+                    const float lin_d = sc[1], quad_p = rdl(s, 1), lin_p = rdl(s, 2);
                     float Jd = 0.0f;
                     Jd = (float)((double)Jd + 0.5 * (double)quad_d);
                     Jd += lin_d;
@@ -2994,14 +3052,15 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
                     if ((double)(Jp + Jd) > kTol) sp = 0;
                     if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) sp = 0;
                     if (lane == 0) {
-                        sc[0] = (float)sp;
+                        sc[2] = (float)sp;
                         st->Jp = Jp;
                         st->Jd = Jd;
                         st->have_costs = 1;
                     }
                 }
                 __syncthreads();
-                stop = sc[0] != 0.0f;
+                stop = sc[2] != 0.0f;
+                if (tr) acc_ph[3] += __builtin_amdgcn_s_memtime() - t_ph;
             }
             was_feasible = !infeasible;
             if (A.mode == kModeTerminate) {
@@ -3026,9 +3085,9 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
             break;
         }
         // accept the update computed in phase A.  The next phase A reads cur
-        // (written before the last barrier) and writes nxt (read by nobody
-        // until after the next barrier); tq/fy/tu/fu of phase D were last read
-        // in phase E, behind a barrier.
+        // (written before the last barrier) and writes nxt and tq (read by
+        // nobody until after the next barrier: tq's last readers, in phases B
+        // and E, are behind one).
         float* t = cur;
         cur = nxt;
         nxt = t;
@@ -3038,6 +3097,14 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
     for (int i = tid; i < N; i += NT) A.Y[i] = cur[i];
     if (conv)
         for (int i = tid; i < M; i += NT) A.U[i] = Us[i];
+    if (tr && lane == 0) {  // totals over the launches of a solve
+        unsigned long long* T = A0.trace + 16 * (size_t)blockIdx.x;
+        if (wave < 8) T[8 + wave] += acc_busyA;
+        if (wave == 0) {
+            for (int p = 0; p < 4; ++p) T[p] += acc_ph[p];
+            T[4] += n_it;
+        }
+    }
     if (tid == 0) {
         st->h = h;
         st->status = status;
@@ -3049,8 +3116,12 @@ __global__ void __launch_bounds__(256) k_solve_mid(SolveArgs A0, SolveState* __r
 size_t solve_mid_lds_bytes(int N, int M, bool conv) { return sizeof(float) * (size_t)mid_layout(N, M, conv).total; }
 
 static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
-    hipLaunchKernelGGL(k_solve_mid, dim3(B), dim3(256), solve_mid_lds_bytes(a.N, a.M, a.mode != kModeFixed), s, a,
-                       st);
+    const bool conv = a.mode != kModeFixed;
+    const size_t lds = solve_mid_lds_bytes(a.N, a.M, conv);
+    const int nt = mid_threads(a.N, a.M, conv);
+    if (nt == 128) hipLaunchKernelGGL(k_solve_mid<128>, dim3(B), dim3(128), lds, s, a, st);
+    else if (nt == 256) hipLaunchKernelGGL(k_solve_mid<256>, dim3(B), dim3(256), lds, s, a, st);
+    else hipLaunchKernelGGL(k_solve_mid<512>, dim3(B), dim3(512), lds, s, a, st);
     return hipGetLastError();
 }
 

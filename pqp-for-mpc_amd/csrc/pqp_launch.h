@@ -33,6 +33,8 @@ struct SolveArgs {
     const int* sym;  // optional (k_solve_single): sym[b] != 0 when problem b's Qd is bit-symmetric
     const float *GpT, *QinvT;  // optional (k_solve_single): transposes of Gp (M x N) and Qp_inv, per problem
     int feas_split;  // k_solve_single with GpT: checkFeas decides on its first rows when one is over its bound
+    unsigned long long* trace;  // optional (k_solve_mid): 16 words of phase cycle totals per traced problem
+    int trace_n;                // problems traced (workgroups 0..trace_n-1)
 };
 hipError_t launch_transpose_b(int B, const float* src, int rows, int cols, float* dst, hipStream_t s);
 // sym[b] = nonzero iff problem b's row-major Qd equals its transpose bit for bit
@@ -99,6 +101,8 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int persist_fit_cus = 0;  // CU count the residency checks assume (0: the device's)
     int wide_flags = 0;  // converge chain: bit 0 update on a forked graph branch, bit 1 gemv segments of 64
     int converge_persist_off = 0;  // converge mode through the graph chain instead of the persistent launch
+    unsigned long long* mid_trace = nullptr;  // k_solve_mid phase totals buffer (device)
+    int mid_trace_n = 0;  // problems it holds
     unsigned long long* converge_trace = nullptr;  // k_converge_persist timeline buffer (device)
     int converge_trace_n = 0;  // iterates the timeline buffer holds
     bool force_small = false;  // route N <= 32 to k_solve_small instead of k_solve_tiny
