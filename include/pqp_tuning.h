@@ -88,7 +88,10 @@ int pqp_tune_get(const char *key, long long *value);
 /* Record an on-device timeline (s_memrealtime / s_memtime marks) of the
  * persistent launches into the device buffer d_buf ("persist": 12 * waves * n
  * words for n updates of k_split_persist; "converge": 2 * n * 35 * 4 words for
- * n iterates of k_converge_persist).  n = 0 turns it off.  Timing only. */
+ * n iterates of k_converge_persist; "mid": 16 words per problem for the first
+ * n problems of a batched k_solve_mid solve -- phase A/B/C/D+E clock totals,
+ * iterations, then each wave's phase-A busy clocks, added to what the buffer
+ * holds).  n = 0 turns it off.  Timing only. */
 int pqp_tune_trace(const char *what, void *d_buf, int n);
 
 /* The first n values of glibc's unseeded rand() sequence (the testing/
