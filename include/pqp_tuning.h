@@ -50,6 +50,8 @@ extern "C" {
  *   mid_off [0]            batched solves of mid-size problems through
  *                          k_solve_small / k_solve_single instead of the
  *                          LDS-resident k_solve_mid (path 3)
+ *   mid_split [0]          1: k_solve_mid holds the stored split matrices
+ *                          (Qdp_theta, Qdn_theta) instead of Qd where they fit
  *   batch_chunk [0]        iterates per problem per batched-solve launch
  *                          (0: sized from N and M)
  *   single_scalar [0]      k_solve_single with 4-byte loads only

@@ -1889,6 +1889,7 @@ const KnobRef* find_knob(const char* key) {
         {"wide_min_n", &g_tune.wide_min_n, nullptr, nullptr},
         {"batch_opts", &g_tune.batch_opts, nullptr, nullptr},
         {"mid_off", &g_tune.mid_off, nullptr, nullptr},
+        {"mid_split", &g_tune.mid_split, nullptr, nullptr},
         {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},
         {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
     };

@@ -2651,15 +2651,21 @@ hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) 
 __host__ __device__ inline int round8(int n) { return (n + 7) & ~7; }
 struct MidLayout {
     int nk, mk;    // N, M rounded up to 8
-    int ldn, ldm;  // row strides of Qd (nk + 4) and of Gp / Qp_inv / Qp (mk + 1)
-    int ya, yb, tq, dP, dN, Fdp, Fdn, Fd, Kp, tM, Us, tu, fu, Fp, sc, Qd, Gp, Qi, Qp, total;
+    int ldn, ldm;  // row strides of Qd (nk + 4; split: 2 nk + 4) and of Qp (mk + 1)
+    int ldg, ldi;  // row strides of Gp' (nk + 4; rows 0..mk-1 the columns of Gp, row mk Fd) and Qp_inv (mk + 4)
+    int ya, yb, tq, dP, dN, Fdp, Fdn, Fd, Kp, tM, Us, tu, fu, Fp, sc, qg, Qd, Gp, Qi, Qp, total;
 };
-__host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv) {
+// split: the Qd region holds the reference's stored split matrices instead,
+// row i = {Qdp_theta[i][k], Qdn_theta[i][k]} pairs (computeQdp_theta /
+// computeQdn_theta, PQP_CPU.c:524-537), and qg the diagonal of Qd
+__host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv, bool split = false) {
     MidLayout L;
     L.nk = round8(N);
     L.mk = round8(M);
-    L.ldn = L.nk + 4;
+    L.ldn = split ? 2 * L.nk + 4 : L.nk + 4;
     L.ldm = L.mk + 1;
+    L.ldg = L.nk + 4;
+    L.ldi = L.mk + 4;
     int o = 0;
     L.ya = o;  o += L.nk;
     L.yb = o;  o += L.nk;
@@ -2670,6 +2676,7 @@ __host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv) {
     L.Fdn = o; o += L.nk;
     L.Fd = o;  o += L.nk;
     L.sc = o;  o += 8;
+    L.qg = o;  o += split ? L.nk : 0;
     if (conv) {
         L.Kp = o;  o += L.nk;
         L.tM = o;  o += L.mk;
@@ -2682,8 +2689,8 @@ __host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv) {
     }
     L.Qd = o;  o += L.nk * L.ldn;
     if (conv) {
-        L.Gp = o;  o += L.nk * L.ldm;
-        L.Qi = o;  o += L.mk * L.ldm;
+        L.Gp = o;  o += (L.mk + 1) * L.ldg;
+        L.Qi = o;  o += L.mk * L.ldi;
         L.Qp = o;  o += L.mk * L.ldm;
     } else {
         L.Gp = L.Qi = L.Qp = 0;
@@ -2735,6 +2742,42 @@ __device__ __forceinline__ float mid_dot(const float* a, int as, const float* b,
     }
     return s;
 }
+// s = sum_k a[k] * b[k] over a 16-byte-aligned LDS row a (per lane, 16-byte
+// loads) and the broadcast b, k = 0..n8-1 in order
+struct RowDotBlk {
+    sf4 a0, a1, b0, b1;
+};
+__device__ __forceinline__ void rowdot_load(RowDotBlk& B, const float* a, const float* b, int k) {
+    B.a0 = *reinterpret_cast<const sf4*>(a + k);
+    B.a1 = *reinterpret_cast<const sf4*>(a + k + 4);
+    B.b0 = *reinterpret_cast<const sf4*>(b + k);
+    B.b1 = *reinterpret_cast<const sf4*>(b + k + 4);
+}
+__device__ __forceinline__ void rowdot_acc(float& s, const RowDotBlk& B) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += (j < 4 ? B.a0[j] : B.a1[j - 4]) * (j < 4 ? B.b0[j] : B.b1[j - 4]);
+}
+__device__ __forceinline__ float mid_dot_row(const float* a, const float* b, int n8) {
+    float s = 0.0f;
+    RowDotBlk c, x;
+    rowdot_load(c, a, b, 0);
+    int k = 0;
+    for (; k + 16 < n8; k += 16) {
+        rowdot_load(x, a, b, k + 8);
+        rowdot_acc(s, c);
+        rowdot_load(c, a, b, k + 16);
+        rowdot_acc(s, x);
+    }
+    if (k + 8 < n8) {
+        rowdot_load(x, a, b, k + 8);
+        rowdot_acc(s, c);
+        rowdot_acc(s, x);
+    } else {
+        rowdot_acc(s, c);
+    }
+    return s;
+}
+
 // s = sum_k v[k], k = 0..n8-1 in order (v 16-byte aligned, per lane)
 __device__ __forceinline__ void mid_add8(float& s, sf4 a, sf4 b) {
     s += a.x; s += a.y; s += a.z; s += a.w;
@@ -2858,7 +2901,92 @@ __device__ __forceinline__ void mid_update(const float* Qd, int ldn, int nk, con
     nxt[i] = num / den * y;                   // :594
 }
 
-template <int NT>
+// ---- the stored-split form (SPLIT): per k one packed multiply and one
+// packed add on the {Qdp_theta, Qdn_theta} pair, the diagonal literal stored
+// (scripts/microbench/chain_mb.hip: 24 clocks per k against 34 for the max
+// form and 50 in its diagonal blocks); twice the LDS of Qd
+struct SplitBlk {
+    sf4 s[4];  // {p, n} pairs of k .. k+7
+    sf4 y0, y1;
+};
+__device__ __forceinline__ void split_load(SplitBlk& B, const float* r, const float* y, int k) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) B.s[m] = *reinterpret_cast<const sf4*>(r + 2 * k + 4 * m);
+    B.y0 = *reinterpret_cast<const sf4*>(y + k);
+    B.y1 = *reinterpret_cast<const sf4*>(y + k + 4);
+}
+// FUSE: aq += y_k Qd[i][k], with Qd[i][k] = p - n off the diagonal (exact:
+// one of them is +0, and a zero's sign cannot change a sum that is never -0)
+// and qii on it (DIAG: the block holds the diagonal of some lanes' rows)
+template <bool FUSE, bool DIAG>
+__device__ __forceinline__ void split_block(const SplitBlk& B, int k, int i, float qii, sf2& acc, float& aq) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const sf4 v = B.s[j >> 1];
+        const float p = (j & 1) ? v.z : v.x, n = (j & 1) ? v.w : v.y;
+        const float yk = j < 4 ? B.y0[j] : B.y1[j - 4];
+        acc += sf2{p, n} * sf2{yk, yk};
+        if constexpr (FUSE) {
+            float q = p - n;
+            if constexpr (DIAG) q = (k + j == i) ? qii : q;
+            aq += yk * q;
+        }
+    }
+}
+template <bool FUSE>
+__device__ __forceinline__ void split_step(const SplitBlk& B, int k, int w0, int i, float qii, sf2& acc, float& aq) {
+    if (FUSE && k >= w0 && k < w0 + 64) split_block<FUSE, true>(B, k, i, qii, acc, aq);
+    else split_block<FUSE, false>(B, k, i, qii, acc, aq);
+}
+template <bool FUSE>
+__device__ __forceinline__ void mid_update_split(const float* S, int ld2, int nk, const float* cur, float* nxt,
+                                                 float* tq, const float* qg, const float* Fdn, const float* Fdp,
+                                                 int i) {
+    const float* r = S + i * ld2;
+    const float qii = FUSE ? qg[i] : 0.0f;
+    const int w0 = __builtin_amdgcn_readfirstlane(i & ~63);
+    sf2 acc = {0.0f, 0.0f};
+    float aq = 0.0f;
+    SplitBlk c, x;
+    split_load(c, r, cur, 0);
+    int k = 0;
+    for (; k + 16 < nk; k += 16) {
+        split_load(x, r, cur, k + 8);
+        split_step<FUSE>(c, k, w0, i, qii, acc, aq);
+        split_load(c, r, cur, k + 16);
+        split_step<FUSE>(x, k + 8, w0, i, qii, acc, aq);
+    }
+    if (k + 8 < nk) {
+        split_load(x, r, cur, k + 8);
+        split_step<FUSE>(c, k, w0, i, qii, acc, aq);
+        split_step<FUSE>(x, k + 8, w0, i, qii, acc, aq);
+    } else {
+        split_step<FUSE>(c, k, w0, i, qii, acc, aq);
+    }
+    const float y = cur[i];
+    if constexpr (FUSE) tq[i] = aq * y;       // (Y'Qd)_i * Y_i, computeCost :652-655
+    const float num = acc.y + 1.0f * Fdn[i];  // :611
+    const float den = acc.x + 1.0f * Fdp[i];  // :612
+    nxt[i] = num / den * y;                   // :594
+}
+// sum_k y_k Qd[k][j] from the pairs of column j (k in order), Qd[j][j] = qjj
+__device__ __forceinline__ float mid_col_split(const float* S, int ld2, int j, float qjj, const float* y, int nk) {
+    float s = 0.0f;
+    for (int k = 0; k < nk; k += 8) {
+        sf2 v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = *reinterpret_cast<const sf2*>(S + (k + m) * ld2 + 2 * j);
+        const sf4 y0 = *reinterpret_cast<const sf4*>(y + k), y1 = *reinterpret_cast<const sf4*>(y + k + 4);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const float q = (k + m == j) ? qjj : v[m].x - v[m].y;
+            s += (m < 4 ? y0[m] : y1[m - 4]) * q;
+        }
+    }
+    return s;
+}
+
+template <int NT, bool SPLIT>
 __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
@@ -2866,9 +2994,10 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     if (st->status == kStatusDone || st->status == kStatusCapped) return;
     const int N = A.N, M = A.M;
     const bool conv = (A.mode != kModeFixed);
-    const MidLayout L = mid_layout(N, M, conv);
-    const int ldn = L.ldn, ldm = L.ldm, nk = L.nk, mk = L.mk;
-    float* Qd = lds + L.Qd;
+    const MidLayout L = mid_layout(N, M, conv, SPLIT);
+    const int ldn = L.ldn, ldm = L.ldm, ldg = L.ldg, ldi = L.ldi, nk = L.nk, mk = L.mk;
+    float* Qd = lds + L.Qd;  // SPLIT: the {Qdp_theta, Qdn_theta} pairs
+    float* qg = lds + L.qg;
     float* Gp = lds + L.Gp;
     float* Qi = lds + L.Qi;
     float* Qp = lds + L.Qp;
@@ -2892,7 +3021,17 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     __syncthreads();
     for (int e = tid; e < N * N; e += NT) {
         const int i = e / N, k = e - i * N;
-        Qd[i * ldn + k] = A.Qd[e];
+        const float q = A.Qd[e];
+        if constexpr (SPLIT) {  // off the diagonal max(0,+-q) + 1.0f*0.0f (:524-537); the diagonal below
+            if (i != k) {
+                Qd[i * ldn + 2 * k] = max_ref(0.0f, q) + 1.0f * 0.0f;
+                Qd[i * ldn + 2 * k + 1] = max_ref(0.0f, -q) + 1.0f * 0.0f;
+            } else {
+                qg[i] = q;
+            }
+        } else {
+            Qd[i * ldn + k] = q;
+        }
     }
     for (int i = tid; i < N; i += NT) {
         const float f = A.Fd[i];
@@ -2901,13 +3040,14 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
         Fdn[i] = max_ref(0.0f, -f);  // matrixNeg(Fdn, Fd) :704
     }
     if (conv) {
-        for (int e = tid; e < N * M; e += NT) {
+        for (int e = tid; e < N * M; e += NT) {  // Gp' (Gp'Y walks rows of it with 16-byte loads)
             const int i = e / M, j = e - i * M;
-            Gp[i * ldm + j] = A.Gp[e];
+            Gp[j * ldg + i] = A.Gp[e];
         }
+        for (int i = tid; i < N; i += NT) Gp[mk * ldg + i] = A.Fd[i];  // Fd.Y rides as row mk
         for (int e = tid; e < M * M; e += NT) {
             const int i = e / M, j = e - i * M;
-            Qi[i * ldm + j] = A.Qinv[e];
+            Qi[i * ldi + j] = A.Qinv[e];
             Qp[i * ldm + j] = A.Qp[e];
         }
         for (int i = tid; i < N; i += NT) Kp[i] = A.Kp[i];
@@ -2923,14 +3063,30 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     for (int i = tid; i < N; i += NT) {
         const float* row = Qd + i * ldn;
         float s = 0.0f;
-        for (int k = 0; k < N; ++k) {
-            s += max_ref(0.0f, -row[k]) * 1.0f;
-            if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
-            if (row[k] != row[k]) nan = 1;
+        if constexpr (SPLIT) {
+            // the stored max(0,-q)+0.0f is max(0,-q)*1.0f but for a zero's
+            // sign, which cannot change this sum; symmetry compares the pairs
+            // (equal pairs give equal p - n, the value the fused Y'Qd uses)
+            const float qii = qg[i];
+            for (int k = 0; k < N; ++k) {
+                s += (k == i) ? max_ref(0.0f, -qii) * 1.0f : row[2 * k + 1];
+                if (k > i && (__float_as_uint(row[2 * k]) != __float_as_uint(Qd[k * ldn + 2 * i]) ||
+                              __float_as_uint(row[2 * k + 1]) != __float_as_uint(Qd[k * ldn + 2 * i + 1])))
+                    asym = 1;
+            }
+            const float th = max_ref(s, 5.0f);
+            Qd[i * ldn + 2 * i] = max_ref(0.0f, qii) + 1.0f * th;
+            Qd[i * ldn + 2 * i + 1] = max_ref(0.0f, -qii) + 1.0f * th;
+        } else {
+            for (int k = 0; k < N; ++k) {
+                s += max_ref(0.0f, -row[k]) * 1.0f;
+                if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
+                if (row[k] != row[k]) nan = 1;
+            }
+            const float th = max_ref(s, 5.0f), qii = row[i];
+            dP[i] = max_ref(0.0f, qii) + 1.0f * th;
+            dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
         }
-        const float th = max_ref(s, 5.0f), qii = row[i];
-        dP[i] = max_ref(0.0f, qii) + 1.0f * th;
-        dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
     }
     const bool sym = !__syncthreads_or(asym);
     const bool fast = !__syncthreads_or(nan);
@@ -2940,7 +3096,13 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     const int nR = may_update ? (N + 63) & ~63 : 0;  // update-row items (whole waves)
     const int nT = conv ? (M + 64) & ~63 : 0;        // tM items, and Fd.Y on item M
     const int nU = (M + 63) & ~63;                   // U (and later (U'Qp).U) items
-    const bool quadB = nU < NT;                      // a wave free for the (Y'Qd).Y sum in phase B
+    // M < 64: the tM wave goes straight on to U = -Qp_inv tM in phase A (it
+    // finishes long before the update rows), so phase B and its barrier vanish
+    const bool uInA = conv && M < 64 && nR + 64 <= NT;
+    const int nRC = (N + 63) & ~63;                  // checkFeas row items
+    const bool quadC = nRC < NT;                     // a wave free for the (Y'Qd).Y sum in phase C
+    float Jp_last = 0.0f, Jd_last = 0.0f;            // costs of the last feasible terminate() (wave 0)
+    bool costs = false;
     long long h = st->h;
     long long done_here = 0;
     int status = kStatusContinue;
@@ -2960,7 +3122,10 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
             if (it < nR) {
                 const int i = it;
                 if (i < N) {
-                    if (fast) {
+                    if constexpr (SPLIT) {
+                        if (fuse) mid_update_split<true>(Qd, ldn, nk, cur, nxt, tq, qg, Fdn, Fdp, i);
+                        else mid_update_split<false>(Qd, ldn, nk, cur, nxt, tq, qg, Fdn, Fdp, i);
+                    } else if (fast) {
                         if (fuse) mid_update<true, true>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
                         else mid_update<false, true>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
                     } else {
@@ -2971,14 +3136,23 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
             } else if (it < nR + nT) {
                 const int j = it - nR;
                 if (j <= M) {  // tM_j = Gp'Y + Fp (:355-356); item M: Fd.Y (:656-657)
-                    const float s = mid_dot(j < M ? Gp + j : Fd, j < M ? ldm : 1, cur, nk);
+                    const float s = mid_dot_row(Gp + (j < M ? j : mk) * ldg, cur, nk);
                     if (j < M) tM[j] = s + 1.0f * Fp[j];
                     else sc[1] = s;
                 }
             } else {
                 const int j = it - nR - nT;
-                if (j < N) tq[j] = mid_dot(Qd + j, ldn, cur, nk) * cur[j];  // Y'Qd, column access :110
+                if (j < N)  // Y'Qd, column access :110
+                    tq[j] = (SPLIT ? mid_col_split(Qd, ldn, j, qg[j], cur, nk) : mid_dot(Qd + j, ldn, cur, nk)) *
+                            cur[j];
             }
+        }
+        if (uInA && tid >= nR && tid < nR + 64) {
+            // the tM wave: its own tM stores are visible to its own later LDS
+            // reads (a wave's LDS accesses complete in order)
+            __builtin_amdgcn_wave_barrier();
+            const int i = tid - nR;
+            if (i < M) Us[i] = -mid_dot_row(Qi + i * ldi, tM, mk);  // :357-358
         }
         if (tr) acc_busyA += __builtin_amdgcn_s_memtime() - t_top;
         __syncthreads();
@@ -2989,24 +3163,26 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
             ++n_it;
         }
         if (conv) {
-            // ------- phase B: U = -Qp_inv tM; (Y'Qd).Y on a free wave -------
-            if (tid < nU) {
-                for (int i = tid; i < M; i += NT) Us[i] = -mid_dot(Qi + i * ldm, 1, tM, mk);  // :357-358
-            } else if (have_tq && tid == nU) {
-                sc[0] = mid_sum(tq, nk);
+            // ---------------- phase B: U = -Qp_inv tM (M >= 64) ----------------
+            if (!uInA) {
+                for (int i = tid; i < M; i += NT) Us[i] = -mid_dot_row(Qi + i * ldi, tM, mk);  // :357-358
+                __syncthreads();
             }
-            __syncthreads();
             if (tr) {
                 const unsigned long long t = __builtin_amdgcn_s_memtime();
                 acc_ph[1] += t - t_ph;
                 t_ph = t;
             }
-            // ---------------- phase C: checkFeas ----------------
+            // ------- phase C: checkFeas; (Y'Qd).Y on a free wave -------
             int bad = 0;
-            for (int i = tid; i < N; i += NT) {
-                const float s = mid_dot(Gp + i * ldm, 1, Us, mk);
-                const float kp = Kp[i];
-                if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+            if (tid < nRC) {
+                for (int i = tid; i < N; i += NT) {
+                    const float s = mid_dot(Gp + i, ldg, Us, mk);  // row i of Gp: column i of Gp'
+                    const float kp = Kp[i];
+                    if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                }
+            } else if (have_tq && tid == nRC) {
+                sc[0] = mid_sum(tq, nk);
             }
             const bool infeasible = __syncthreads_or(bad);
             if (tr) {
@@ -3027,17 +3203,19 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
                         }
                     } else {
                         const int j = it - nU;
-                        if (j < N) tq[j] = mid_dot(Qd + j, ldn, cur, nk) * cur[j];  // (Y'Qd).Y
+                        if (j < N)  // (Y'Qd).Y
+                            tq[j] = (SPLIT ? mid_col_split(Qd, ldn, j, qg[j], cur, nk)
+                                           : mid_dot(Qd + j, ldn, cur, nk)) *
+                                    cur[j];
                     }
                 }
                 __syncthreads();
                 // ------------ phase E: the sums left, the costs, the tests ------------
                 if (wave == 0) {
                     float s = 0.0f;
-                    if (lane == 0 && !(have_tq && quadB)) s = mid_sum(tq, nk);
-                    else if (lane == 1) s = mid_sum(tu, mk);
-                    else if (lane == 2) s = mid_sum(fu, mk);
-                    const float quad_d = (have_tq && quadB) ? sc[0] : rdl(s, 0);
+                    if (lane < 3 && (lane > 0 || !(have_tq && quadC)))  // one instruction stream
+                        s = mid_sum(lane == 0 ? tq : (lane == 1 ? tu : fu), lane == 0 ? nk : mk);
+                    const float quad_d = (have_tq && quadC) ? sc[0] : rdl(s, 0);
                     const float lin_d = sc[1], quad_p = rdl(s, 1), lin_p = rdl(s, 2);
                     float Jd = 0.0f;
                     Jd = (float)((double)Jd + 0.5 * (double)quad_d);
@@ -3051,12 +3229,12 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
                     if (Jp > -Jd) sp = 0;
                     if ((double)(Jp + Jd) > kTol) sp = 0;
                     if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) sp = 0;
-                    if (lane == 0) {
-                        sc[2] = (float)sp;
-                        st->Jp = Jp;
-                        st->Jd = Jd;
-                        st->have_costs = 1;
-                    }
+                    if (lane == 0) sc[2] = (float)sp;
+                    // to SolveState once, at the end: a global store here would
+                    // hold the barrier below for its round trip every iterate
+                    Jp_last = Jp;
+                    Jd_last = Jd;
+                    costs = true;
                 }
                 __syncthreads();
                 stop = sc[2] != 0.0f;
@@ -3106,6 +3284,11 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
         }
     }
     if (tid == 0) {
+        if (costs) {
+            st->Jp = Jp_last;
+            st->Jd = Jd_last;
+            st->have_costs = 1;
+        }
         st->h = h;
         st->status = status;
         st->resume = 1;
@@ -3113,15 +3296,33 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     }
 }
 
-size_t solve_mid_lds_bytes(int N, int M, bool conv) { return sizeof(float) * (size_t)mid_layout(N, M, conv).total; }
+size_t solve_mid_lds_bytes(int N, int M, bool conv, bool split) {
+    return sizeof(float) * (size_t)mid_layout(N, M, conv, split).total;
+}
+constexpr size_t kMidLdsBudget = 150 * 1024;
+// the stored-split form (pqp_tune "mid_split" 1, where its LDS fits): half
+// the update's instructions per k, but twice Qd's LDS, so half the resident
+// problems per CU, and no gain on feasible iterates (the fused Y'Qd term needs
+// q = p - n and the diagonal select again).  On the horizon sweep (every
+// iterate feasible) it lost at every H (profiles/r03/horizon_split_vs_qd.txt),
+// so it is off by default.
+bool mid_use_split(int N, int M, bool conv) {
+    return g_tune.mid_split == 1 && solve_mid_lds_bytes(N, M, conv, true) <= kMidLdsBudget;
+}
 
+template <bool SPLIT>
+static void launch_mid_t(int B, const SolveArgs& a, SolveState* st, hipStream_t s, size_t lds, int nt) {
+    if (nt == 128) hipLaunchKernelGGL((k_solve_mid<128, SPLIT>), dim3(B), dim3(128), lds, s, a, st);
+    else if (nt == 256) hipLaunchKernelGGL((k_solve_mid<256, SPLIT>), dim3(B), dim3(256), lds, s, a, st);
+    else hipLaunchKernelGGL((k_solve_mid<512, SPLIT>), dim3(B), dim3(512), lds, s, a, st);
+}
 static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const bool conv = a.mode != kModeFixed;
-    const size_t lds = solve_mid_lds_bytes(a.N, a.M, conv);
+    const bool split = mid_use_split(a.N, a.M, conv);
+    const size_t lds = solve_mid_lds_bytes(a.N, a.M, conv, split);
     const int nt = mid_threads(a.N, a.M, conv);
-    if (nt == 128) hipLaunchKernelGGL(k_solve_mid<128>, dim3(B), dim3(128), lds, s, a, st);
-    else if (nt == 256) hipLaunchKernelGGL(k_solve_mid<256>, dim3(B), dim3(256), lds, s, a, st);
-    else hipLaunchKernelGGL(k_solve_mid<512>, dim3(B), dim3(512), lds, s, a, st);
+    if (split) launch_mid_t<true>(B, a, st, s, lds, nt);
+    else launch_mid_t<false>(B, a, st, s, lds, nt);
     return hipGetLastError();
 }
 

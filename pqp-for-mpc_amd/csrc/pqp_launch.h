@@ -65,7 +65,7 @@ hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStre
 hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
 size_t solve_single_lds_bytes(int ldq, int ldm, bool fused = false);
 size_t solve_small_lds_bytes(int N, int M);
-size_t solve_mid_lds_bytes(int N, int M, bool conv);
+size_t solve_mid_lds_bytes(int N, int M, bool conv, bool split = false);
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);  // N, M <= 32
 // row block [row0, row0 + rows) of one large problem, fixed mode,
@@ -109,7 +109,8 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     bool force_single = false;  // fixed mode of a large problem on one workgroup (k_solve_single)
     int wide_min_n = 384;  // converge mode: smallest N solved over many workgroups
     long long batch_chunk = 0;  // iterates per problem per batched-solve launch (0: sized from N, M)
-    int mid_off = 0;  // batched solves of mid-size N through k_solve_small / k_solve_single instead of k_solve_mid
+    int mid_off = 0;
+    int mid_split = 0;  // 1: k_solve_mid's stored-split form where its LDS fits  // batched solves of mid-size N through k_solve_small / k_solve_single instead of k_solve_mid
     int batch_opts = 0;  // pqp_batch_solve: bit 0 no fused Y'Qd, bit 1 per-call transposes, bit 4 checkFeas over every row
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
 };

@@ -7,6 +7,7 @@ from the LDS footprint).  Usage: python scripts/mid_phases.py [H ...]"""
 from __future__ import annotations
 
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -34,6 +35,7 @@ def main(Hs):
 
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    pqp_amd.tune("mid_split", int(os.environ.get("MID_SPLIT", "0")))
     for H in Hs:
         P = block_diag_problem(base, H)
         N, M = P["N"], P["M"]

@@ -1,7 +1,8 @@
 """Batched solves of mid-size problems on k_solve_mid: one
-workgroup per problem with Qd, Gp, Qp_inv and Qp each held in LDS once (odd
-row strides), the update's split entries formed from Qd on the fly (v_max_f32
-form when the problem's Qd holds no NaN, the reference's selects otherwise).
+workgroup per problem with Gp, Qp_inv, Qp and either the reference's stored
+split matrices (where they fit, about N <= 100) or Qd held in LDS once, the
+update's split entries then formed on the fly (v_max_f32 form when the
+problem's Qd holds no NaN, the reference's selects otherwise).
 Bar: the oracle's h, Y and U bit for bit -- the bundled plant over H horizon
 blocks (stops at the reference's h = 313), synthetic problems capped with
 infeasible and all-feasible iterates, ragged sizes, a non-symmetric Qd, a NaN
@@ -55,8 +56,8 @@ def _bundled(golden_bundled):
 
 
 @pytest.mark.parametrize("H", [2, 3, 4, 5])
-@pytest.mark.parametrize("mid_off", [0, 1])
-def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off):
+@pytest.mark.parametrize("mid_off,split", [(0, 0), (0, 1), (1, 0)])
+def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off, split):
     """The bundled plant as H diagonal blocks (n_dual 28 H) stops at h = 313
     (the oracle's, itself pinned to oracle/_ref for 9 and 36 blocks): 8 copies
     in one launch, every value bit for bit."""
@@ -64,6 +65,7 @@ def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs,
 
     Q = block_diag_problem(_bundled(golden_bundled), H)
     knobs("mid_off", mid_off)
+    knobs("mid_split", split)
     if not mid_off:
         assert gpu_lib.lib().pqp_batch_solve_path(Q["N"], Q["M"]) == MID
     pb = _batch(gpu_lib, [Q] * 8).solve(max_updates=CAP)
@@ -89,10 +91,13 @@ def test_horizon_blocks_chunked(gpu_lib, golden_bundled, orc, knobs, chunk):
 
 @pytest.mark.parametrize("N,M", [(33, 5), (40, 20), (57, 57), (64, 16), (100, 50), (127, 31), (150, 40)])
 @pytest.mark.parametrize("feasible", [False, True])
-def test_synthetic_capped_vs_oracle(gpu_lib, orc, N, M, feasible):
+@pytest.mark.parametrize("split", [0, 1])
+def test_synthetic_capped_vs_oracle(gpu_lib, orc, knobs, N, M, feasible, split):
     """Capped solves of synthetic problems; `feasible`: Kp = 1e30, so every
     iterate runs all of computeCost and, from the second on, the Y'Qd sums
-    ride in the update rows."""
+    ride in the update rows.  split 1: the stored-split form where its LDS
+    fits (N <~ 100), 0: the Qd form (default)."""
+    knobs("mid_split", split)
     assert gpu_lib.lib().pqp_batch_solve_path(N, M) == MID
     B, cap = 3, 9
     Ps = [orc.synth_problem(31, b, N, M) for b in range(B)]
@@ -106,7 +111,9 @@ def test_synthetic_capped_vs_oracle(gpu_lib, orc, N, M, feasible):
 
 
 @pytest.mark.parametrize("N,M", [(48, 24), (101, 25)])
-def test_fixed_mode_vs_oracle(gpu_lib, orc, N, M):
+@pytest.mark.parametrize("split", [0, 1])
+def test_fixed_mode_vs_oracle(gpu_lib, orc, knobs, N, M, split):
+    knobs("mid_split", split)
     Ps = [orc.synth_problem(32, b, N, M) for b in range(4)]
     pb = _batch(gpu_lib, Ps).solve(gpu_lib.MODE_FIXED, num_iter=40)
     assert np.all(pb.h.cpu().numpy() == 40)
@@ -116,11 +123,13 @@ def test_fixed_mode_vs_oracle(gpu_lib, orc, N, M):
 
 
 @pytest.mark.parametrize("feasible", [False, True])
-def test_non_symmetric_qd_mixed(gpu_lib, orc, feasible):
+@pytest.mark.parametrize("split", [0, 1])
+def test_non_symmetric_qd_mixed(gpu_lib, orc, knobs, feasible, split):
     """Problem 0's Qd is bit-symmetric, problem 1's is not (dense Qp_inv):
     the Y'Qd columns then run beside the update rows instead of inside them."""
     from pqp_amd import dense_qinv
 
+    knobs("mid_split", split)
     N, M, cap = 96, 24, 7
     P0 = orc.synth_problem(33, 0, N, M)
     P1 = orc.synth_primal(33, 1, N, M)
@@ -139,11 +148,14 @@ def test_non_symmetric_qd_mixed(gpu_lib, orc, feasible):
         _check(pb, b, h, Y, U, f"problem {b} feasible={feasible}")
 
 
-def test_nan_in_qd_takes_the_select_form(gpu_lib, orc):
+@pytest.mark.parametrize("split", [0, 1])
+def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, split):
     """One NaN off the diagonal of row 5: the reference's selects keep it
     (row 5's sums turn NaN), a v_max_f32 form would drop it.  Fixed mode, one
     and two updates: NaN where the oracle has NaN, every other value bit for
-    bit; problem 1 (no NaN) unaffected."""
+    bit; problem 1 (no NaN) unaffected.  (The stored-split form keeps the
+    reference's literal entries, NaN included.)"""
+    knobs("mid_split", split)
     N, M = 48, 12
     P0 = orc.synth_problem(34, 0, N, M)
     P1 = orc.synth_problem(34, 1, N, M)
