@@ -314,6 +314,50 @@ def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
                     "on device, excluded from the timing; each solve bit-exact with PQP_CPU.c (tests)"}
 
 
+def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
+    """The bundled plant over H horizon blocks (oracle.block_diag_problem:
+    n_dual 28 H, M 7 H; every iterate feasible, the reference stops at h =
+    313), B copies solved at once (ProblemBatch; k_solve_mid, one workgroup per
+    problem, each matrix once in LDS), and beside it the reference's own
+    solveQuadraticDual on one copy, one host thread (oracle/_ref, median of
+    3).  Timed: the batched solve only."""
+    import torch
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from oracle import REF_SO, Oracle, Reference, block_diag_problem
+
+    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    ref = Reference() if REF_SO.exists() else None
+    out = {}
+    for H in Hs:
+        P = block_diag_problem(base, H)
+        pb = pqp_amd.ProblemBatch.replicate(P, B)
+        pb.solve(max_updates=200000)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pb.solve(max_updates=200000)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        h = pb.h.cpu().numpy()
+        row = {"n_dual": int(P["N"]), "m": int(P["M"]), "problems": B,
+               "path": int(pqp_amd.lib().pqp_batch_solve_path(P["N"], P["M"])), "converge_ms": dt * 1e3,
+               "qp_solves_per_s": B / dt, "iterations_per_s": float(h.sum()) / dt,
+               "all_h_313": bool((h == 313).all())}
+        if ref is not None:
+            ts = []
+            for _ in range(3):
+                tb = time.perf_counter()
+                hr, _, _ = ref.solve(P)
+                ts.append(time.perf_counter() - tb)
+            tr = sorted(ts)[1]
+            row["ref_cpu"] = {"h": hr, "ms": tr * 1e3, "qp_solves_per_s": 1.0 / tr, "cores": 1,
+                              "what": "PQP_CPU.c solveQuadraticDual (oracle/_ref), one copy, 1 thread, median of 3"}
+        out[f"H{H}"] = row
+        del pb
+        torch.cuda.empty_cache()
+    return out
+
+
 def single_bench(pqp_amd, N: int = 1024, iters: int = 1000) -> dict:
     """configs[2]: ONE synthetic n_dual=1024 problem, 1000 fixed-mode
     iterations, through pqp_problem_solve (multi-workgroup k_split_update,
@@ -839,6 +883,7 @@ def main():
     if world == 1 and not args.no_bundled:
         em.leg("bundled", lambda: bundled_bench(pqp_amd))
         em.leg("mpc_batch", lambda: mpc_batch_bench(pqp_amd))
+        em.leg("horizon", lambda: horizon_bench(pqp_amd))
         em.leg("single_n1024", lambda: single_bench(pqp_amd))
         em.leg("single_converge", lambda: single_converge_bench(pqp_amd))
         em.leg("setup_convert", lambda: setup_bench(pqp_amd))
