@@ -69,17 +69,21 @@ def hot_kernel_hash() -> str:
     return kernel_src_hash("hot-kernel")
 
 
-def kernel_src_hash(marker: str) -> str:
+def kernel_src_hash(*markers: str) -> str:
     """SHA-256 (16 hex) of the text between pqp_kernels.hip's <marker> and
-    </marker> comments plus the library's compile flags."""
+    </marker> comments (each marker's region, in order) plus the library's
+    compile flags."""
     import hashlib
     import re
 
     src = (ROOT / "pqp-for-mpc_amd" / "csrc" / "pqp_kernels.hip").read_text()
-    m = re.search(rf"// <{marker}>.*?// </{marker}>", src, re.S)
+    text = ""
+    for marker in markers:
+        m = re.search(rf"// <{marker}>.*?// </{marker}>", src, re.S)
+        text += m.group(0) if m else src
     flags = [ln for ln in (ROOT / "pqp-for-mpc_amd" / "Makefile").read_text().splitlines()
              if ln.startswith("HIPFLAGS")]
-    text = (m.group(0) if m else src) + "\n".join(flags)
+    text += "\n".join(flags)
     return hashlib.sha256(text.encode()).hexdigest()[:16]
 
 
@@ -435,19 +439,23 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    pipe = pqp_amd.tune_get("last_batch_kernel") == 1
+    kname = "k_solve_pipe" if pipe else "k_solve_single"
     rec = {}
     tf = ROOT / "profiles" / "pmc_traffic.json"
     db = json.loads(tf.read_text()) if tf.exists() else {}
-    khash = kernel_src_hash("solve-single")
-    # bytes per problem-iteration: Qd once (the update; on feasible iterates
-    # Y'Qd rides in the same pass), Gp for Gp'Y (4NM), Qp_inv once, Gp again for
-    # checkFeas's Gp U -- on these infeasible iterates only its first 256 rows
-    # (a row over its bound there decides terminate(), the rest is skipped;
-    # the every-row setting, tuning bit 4, reads all 4NM) -- and on feasible
-    # iterates Qp once (U'Qp)
+    khash = kernel_src_hash("solve-single", "solve-pipe") if pipe else kernel_src_hash("solve-single")
+    # algorithmic bytes per problem-iteration: every matrix terminate() and
+    # updateY2 read, once -- Qd (the update; on feasible iterates Y'Qd rides in
+    # the same pass), Gp (Gp'Y and checkFeas's Gp U), Qp_inv, and on feasible
+    # iterates Qp (U'Qp).  k_solve_pipe moves exactly these.  k_solve_single
+    # (pipe_off) reads Gp twice: the second time, on these infeasible
+    # iterates, only its first 256 rows (a row over its bound there decides
+    # terminate(); tuning bit 4 reads all 4NM) -- its `design_bytes_per_iter`
     first = 4.0 * min(N, 256) * M
-    for case, alg in (("infeasible", 4.0 * N * N + 4.0 * N * M + first + 4.0 * M * M),
-                      ("feasible", 4.0 * N * N + 8.0 * N * M + 8.0 * M * M)):
+    for case, alg in (("infeasible", 4.0 * N * N + 4.0 * N * M + 4.0 * M * M),
+                      ("feasible", 4.0 * N * N + 4.0 * N * M + 8.0 * M * M)):
+        design = alg if pipe else alg + (first if case == "infeasible" else 4.0 * N * M)
         if case == "feasible":
             pb.Kp.fill_(1e30)
             pb.solve(max_updates=1)
@@ -459,12 +467,12 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         gbs = alg * B / per_iter / 1e9
         r = {"ms_per_iteration": per_iter * 1e3, "instance_iter_per_s": B / per_iter,
              "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
-             "full_pass_bytes_per_iter": 4.0 * N * N + 8.0 * N * M + 4.0 * M * M * (2 if case == "feasible" else 1),
+             "design_bytes_per_iter": design, "design_GBps": design * B / per_iter / 1e9,
              "call_ms": dt * 1e3, "call_instance_iter_per_s": B * K / dt, "all_capped": ok}
-        pmc = db.get(f"k_solve_single_{case}")
+        pmc = db.get(f"{kname}_{case}")
         if pmc and pmc.get("kernel_src_sha256") == khash:
             r["traffic_ratio"] = pmc["traffic_ratio"]
-            r["traffic_source"] = f"profiles/pmc_traffic.json k_solve_single_{case}"
+            r["traffic_source"] = f"profiles/pmc_traffic.json {kname}_{case}"
         else:
             r["traffic_ratio"] = None
             r["traffic_source"] = "no PMC record for this kernel source (scripts/gpu_batch_converge.sh)"
@@ -472,7 +480,8 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
     del pb
     torch.cuda.empty_cache()
     return {"problems": B, "n_dual": N, "m": M, "updates": K, "prepare_ms": prep_ms, **rec,
-            "note": "k_solve_single, one workgroup per problem; ms_per_iteration = (time of a 3K-update call - time "
+            "kernel": kname,
+            "note": f"{kname}, one workgroup per problem; ms_per_iteration = (time of a 3K-update call - time "
                     "of a K-update call) / 2K, the iterations alone; call_ms = one K-update call (K + 1 terminate() "
                     "+ K updates, state init and readback); prepare_ms = pqp_batch_prepare, once per batch"}
 

@@ -47,6 +47,15 @@ extern "C" {
  *                          row (by default it stops after its first 256 rows
  *                          when one is over its bound: terminate() returns 0
  *                          either way)
+ *   pipe_off [0]           batched converge of problems too large for LDS
+ *                          (path 2) on k_solve_single (Gp read twice per
+ *                          iteration) instead of k_solve_pipe (Gp read once;
+ *                          taken when Qp_inv' is prepared and N, M are
+ *                          multiples of 4)
+ *   pipe_variant [0]       k_solve_pipe build: 0 two Gp tiles and 16 update
+ *                          loads per lane in flight, two workgroups per CU;
+ *                          1 four tiles; 2 two tiles, 8 loads, occupancy set
+ *                          by the register count
  *   mid_off [0]            batched solves of mid-size problems through
  *                          k_solve_small / k_solve_single instead of the
  *                          LDS-resident k_solve_mid (path 3)
@@ -82,6 +91,8 @@ int pqp_tune(const char *key, long long value, long long *old_value);
  *   last_path          solver path of the calling thread's last single-problem
  *                      solve (1 persistent fixed, 2 relay fixed, 3 persistent
  *                      converge, 4 converge graph chain, 5 one workgroup)
+ *   last_batch_kernel  1 when the calling thread's last path-2 batched
+ *                      launch ran k_solve_pipe, 0 for k_solve_single
  *   persist_fallbacks  persistent launches that fell back (process total)
  *   converge_grid      in: *value = N << 32 | M; out: workgroups of the
  *                      persistent converge launch for (N, M) (0: not used) */

@@ -1890,6 +1890,8 @@ const KnobRef* find_knob(const char* key) {
         {"batch_opts", &g_tune.batch_opts, nullptr, nullptr},
         {"mid_off", &g_tune.mid_off, nullptr, nullptr},
         {"mid_split", &g_tune.mid_split, nullptr, nullptr},
+        {"pipe_off", &g_tune.pipe_off, nullptr, nullptr},
+        {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},
         {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},
         {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
     };
@@ -1923,6 +1925,10 @@ extern "C" int pqp_tune_get(const char* key, long long* value) {
     if (!key || !value) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_get: null argument");
     if (std::strcmp(key, "last_path") == 0) {
         *value = pqp::g_last_path;
+        return PQP_OK;
+    }
+    if (std::strcmp(key, "last_batch_kernel") == 0) {  // 1: k_solve_pipe, 0: k_solve_single (path 2)
+        *value = pqp::g_last_batch_kernel;
         return PQP_OK;
     }
     if (std::strcmp(key, "persist_fallbacks") == 0) {

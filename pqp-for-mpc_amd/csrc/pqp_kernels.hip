@@ -1408,7 +1408,7 @@ __device__ __forceinline__ float row_dot4(const float* __restrict__ a, const flo
 
 // single_update with four adjacent rows per lane (16-byte loads of QdT)
 constexpr int kSU4 = 8;
-template <int NT, bool FUSE>
+template <int NT, bool FUSE, int SU = kSU4>
 __device__ __forceinline__ void single_update4(const SolveArgs& A, const float* __restrict__ cur,
                                                float* __restrict__ nxt, float* __restrict__ tq) {
     const int N = A.N, ldq = A.ldq;
@@ -1424,16 +1424,16 @@ __device__ __forceinline__ void single_update4(const SolveArgs& A, const float* 
         }
         const float* col = A.QdT + i0;
         int k = 0;
-        for (; k + kSU4 <= N; k += kSU4) {
-            sf4 q[kSU4];
-            float yv[kSU4];
+        for (; k + SU <= N; k += SU) {
+            sf4 q[SU];
+            float yv[SU];
 #pragma unroll
-            for (int j = 0; j < kSU4; ++j) {
+            for (int j = 0; j < SU; ++j) {
                 q[j] = __builtin_nontemporal_load(reinterpret_cast<const sf4*>(col + (size_t)(k + j) * ldq));
                 yv[j] = cur[k + j];
             }
 #pragma unroll
-            for (int j = 0; j < kSU4; ++j)
+            for (int j = 0; j < SU; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const bool d = (k + j == i0 + r);
@@ -1711,6 +1711,287 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
 }
 
 // </solve-single>
+
+// <solve-pipe> (bench.py hashes the text up to </solve-pipe>: k_solve_pipe PMC records are keyed by it)
+// ---------------------------------------------------------------------------
+// k_solve_pipe: converge mode of solveQuadraticDual (PQP_CPU.c:694-750), one
+// workgroup per problem from global memory, like k_solve_single, but with Gp
+// read ONCE per iteration instead of twice.  terminate(Y_h) needs Gp'Y_h
+// (computeUfromY :355) and Gp U_h (checkFeas :636); the update to Y_{h+1}
+// needs only Y_h (updateY2 :603-618), so it runs first, speculatively, and
+// one pass over Gp then gives checkFeas(h)'s rows AND Gp'Y_{h+1}, i.e. the
+// next iterate's computeUfromY:
+//   phase X  Y_{h+1} = updateY2(Y_h) (+ Y_h'Qd fused when Qd is bit-symmetric
+//            and the previous iterate was feasible), U_h = -Qp_inv tM_h
+//   phase Y  Gp in 64 x 64 tiles, each staged once through LDS: lane r of
+//            wave 0 sums row r's terms Gp[i][j] U_h[j] (j in order, the
+//            partial carried across the tiles of a row block), lane c of
+//            wave 1 column c's terms Gp[i][j] Y_{h+1}[i] (i in order, the
+//            partial carried in LDS across row blocks); the loads of the
+//            tiles two ahead are in flight meanwhile
+//   then     checkFeas(h) from the row sums; computeCost on a feasible iterate
+//            as k_solve_single does; Y_{h+1}, tM_{h+1} dropped when h stops.
+// Every sum has the reference's operands and order, so every value is the
+// reference's.  Per iteration Qd + Qp_inv + Gp (+ Qp when feasible) are read
+// once each: 4N^2 + 4M^2 + 4NM (+ 4M^2) bytes, against k_solve_single's two
+// passes over Gp.  Needs the wide-load conditions and Qp_inv' (QinvT).
+// ---------------------------------------------------------------------------
+constexpr int kPipeTR = 64, kPipeTC = 64, kPipeTS = kPipeTC + 1;  // tile rows, columns, LDS row stride
+__host__ __device__ inline size_t pipe_tile_floats() { return (size_t)2 * kPipeTR * kPipeTS; }
+
+template <int NT, int PD, int SU, int MINB>
+__global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveState* __restrict__ st0) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;  // finished in an earlier launch
+    const int N = A.N, M = A.M, ldq = A.ldq, ldm = A.ldm;
+    float* ya = lds;            // ldq   Y_h / Y_{h+1}
+    float* yb = ya + ldq;       // ldq
+    float* tq = yb + ldq;       // ldq   Y_h'Qd (Jd)
+    float* tMa = tq + ldq;      // ldm   tM_h = Gp'Y_h + Fp / tM_{h+1}
+    float* tMb = tMa + ldm;     // ldm
+    float* Us = tMb + ldm;      // ldm   U_h
+    float* tile = Us + ldm;     // 2 x TR x TS (phase Y), then fy, tu, fu (costs)
+    float* fy = tile;           // ldq   Fd.Y terms
+    float* tu = fy + ldq;       // ldm   U'Qp row, then its terms
+    float* fu = tu + ldm;       // ldm   Fp.U terms
+    __shared__ float s_J[2];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool fuse_ok = A.sym && A.sym[blockIdx.x];
+    bool was_feasible = false;
+    const int nI = (N + kPipeTR - 1) / kPipeTR, nJ = (M + kPipeTC - 1) / kPipeTC, nT = nI * nJ;
+
+    long long h = st->h;
+    for (int i = tid; i < ldq; i += NT) {
+        ya[i] = (i < N) ? (st->resume ? A.Y[i] : 1000.0f) : 0.0f;
+        yb[i] = 0.0f;
+    }
+    __syncthreads();
+    float* cur = ya;
+    float* nxt = yb;
+    // tM_h for the launch's first iterate (computeUfromY :355-356)
+    for (int j = 2 * tid; j < M; j += 2 * NT) {
+        float t[2];
+        col_dotv<2, kSU>(A.Gp + j, M, cur, N, t);
+        tMa[j] = t[0] + 1.0f * A.Fp[j];
+        tMa[j + 1] = t[1] + 1.0f * A.Fp[j + 1];
+    }
+    __syncthreads();
+    float* tMc = tMa;  // tM of the current iterate
+    float* tMn = tMb;  // tM of the next
+    int status = kStatusContinue;
+    long long done_here = 0;
+    // timing trace (pqp_tune_trace "mid"): thread 0's phase totals in shader
+    // cycles -- X (update, U), Y (the pass over Gp), the costs and decision
+    const bool tr = A0.trace && (int)blockIdx.x < A0.trace_n;  // uniform: the totals stay in SGPRs
+    unsigned long long t0 = 0, acc_ph[3] = {0, 0, 0}, n_it = 0;
+    // tile t = (I, J), I = t / nJ: lane l loads rows (l >> 4) + 16 s, s < 4,
+    // columns 4 (l & 15) .. +3 (16 lanes per 256-byte row segment)
+    auto load_tile = [&](int t, sf4 (&r)[4]) {
+        const int I = t / nJ, J = t - I * nJ;
+        const int col = J * kPipeTC + 4 * (tid & 15);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int row = I * kPipeTR + (tid >> 4) + 16 * s;
+            r[s] = (row < N && col < M)
+                       ? __builtin_nontemporal_load(reinterpret_cast<const sf4*>(A.Gp + (size_t)row * M + col))
+                       : sf4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    for (;;) {
+        // this iterate breaks before its update whatever terminate() says:
+        // no speculative update or next tM
+        const bool last = done_here >= A.chunk || (A.max_updates > 0 && h - 1 >= A.max_updates);
+        const bool fuse = fuse_ok && was_feasible && !last;
+        if (tr) t0 = __builtin_amdgcn_s_memtime();
+        // ---- phase X ----
+        if (!last) {
+            if (fuse) single_update4<NT, true, SU>(A, cur, nxt, tq);
+            else single_update4<NT, false, SU>(A, cur, nxt, nullptr);
+        }
+        for (int i0 = 2 * tid; i0 < M; i0 += 2 * NT) {  // computeUfromY :357-359
+            float t[2];
+            col_dotv<2, kSU>(A.QinvT + i0, M, tMc, M, t);
+            Us[i0] = -t[0];
+            Us[i0 + 1] = -t[1];
+        }
+        // ---- phase Y: one pass over Gp ----
+        sf4 rq[PD][4];  // the next PD tiles' loads in flight
+#pragma unroll
+        for (int d = 0; d < PD; ++d)
+            if (d < nT) load_tile(d, rq[d]);
+        __syncthreads();  // Y_{h+1}, U_h complete; the tile area is free
+        if (tr) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc_ph[0] += t - t0;
+            t0 = t;
+        }
+        float racc = 0.0f;  // wave 0: row sum of the current row block
+        int bad = 0;
+        for (int t = 0; t < nT; ++t) {
+            float* tl = tile + (t & 1) * (kPipeTR * kPipeTS);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                float* d = tl + ((tid >> 4) + 16 * s) * kPipeTS + 4 * (tid & 15);
+                d[0] = rq[0][s].x;
+                d[1] = rq[0][s].y;
+                d[2] = rq[0][s].z;
+                d[3] = rq[0][s].w;
+            }
+#pragma unroll
+            for (int d = 0; d + 1 < PD; ++d)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) rq[d][s] = rq[d + 1][s];
+            if (t + PD < nT) load_tile(t + PD, rq[PD - 1]);
+            __syncthreads();  // tile t staged (tile t - 2's readers are past the previous barrier)
+            const int I = t / nJ, J = t - I * nJ;
+            const int nr = min(kPipeTR, N - I * kPipeTR), nc = min(kPipeTC, M - J * kPipeTC);
+            if (wave == 0) {
+                // checkFeas :636: gu[i] = sum_j Gp[i][j] U[j], j in order
+                if (J == 0) racc = 0.0f;
+                if (lane < nr) {
+                    const float* tr = tl + lane * kPipeTS;
+                    const float* u = Us + J * kPipeTC;
+                    float s = racc;
+                    int c = 0;
+                    for (; c + 8 <= nc; c += 8) {
+                        float g[8], uv[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            g[e] = tr[c + e];
+                            uv[e] = u[c + e];
+                        }
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) s += g[e] * uv[e];
+                    }
+                    for (; c < nc; ++c) s += tr[c] * u[c];
+                    racc = s;
+                    if (J == nJ - 1) {  // compare :338-341
+                        const float kp = A.Kp[I * kPipeTR + lane];
+                        if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                    }
+                }
+            } else if (wave == 1 && !last) {
+                // Gp'Y_{h+1} :355: tmp[j] = sum_i Gp[i][j] Y[i], i in order
+                if (lane < nc) {
+                    const int col = J * kPipeTC + lane;
+                    const float* y = nxt + I * kPipeTR;
+                    float s = (I == 0) ? 0.0f : tMn[col];
+                    int r = 0;
+                    for (; r + 8 <= nr; r += 8) {
+                        float g[8], yv[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            g[e] = tl[(r + e) * kPipeTS + lane];
+                            yv[e] = y[r + e];
+                        }
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) s += g[e] * yv[e];
+                    }
+                    for (; r < nr; ++r) s += tl[r * kPipeTS + lane] * y[r];
+                    tMn[col] = (I == nI - 1) ? s + 1.0f * A.Fp[col] : s;  // matrixAdd :356
+                }
+            }
+        }
+        const int infeasible = __syncthreads_or(bad);
+        was_feasible = !infeasible;
+        if (tr) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc_ph[1] += t - t0;
+            t0 = t;
+            ++n_it;
+        }
+        int stop = 0;
+        if (!infeasible) {
+            // computeCost(Y, Qd, Fd, Md) and computeCost(U, Qp, Fp, Mp) :648-666
+            if (!fuse)
+                for (int j = 4 * tid; j < N; j += 4 * NT) {
+                    float t[4];
+                    col_dotv<4, kSU4>(A.Qd + j, N, cur, N, t);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) tq[j + c] = t[c];
+                }
+            for (int j = 2 * tid; j < M; j += 2 * NT) {
+                float t[2];
+                col_dotv<2, kSU>(A.Qp + j, M, Us, M, t);
+                tu[j] = t[0];
+                tu[j + 1] = t[1];
+            }
+            __syncthreads();
+            for (int j = tid; j < N; j += NT) {
+                tq[j] = tq[j] * cur[j];
+                fy[j] = A.Fd[j] * cur[j];
+            }
+            for (int j = tid; j < M; j += NT) {
+                tu[j] = tu[j] * Us[j];
+                fu[j] = A.Fp[j] * Us[j];
+            }
+            __syncthreads();
+            if (tid == 0 || tid == 64) {
+                const bool dual = (tid == 0);
+                const float* qv = dual ? tq : tu;
+                const float* lv = dual ? fy : fu;
+                const int n = dual ? N : M;
+                float quad = 0.0f, lin = 0.0f;
+                for (int k = 0; k < n; ++k) quad += qv[k];  // (Z'Q).Z :652-655
+                for (int k = 0; k < n; ++k) lin += lv[k];   // F'Z :656-657
+                float J = 0.0f;
+                J = (float)((double)J + 0.5 * (double)quad);
+                J += lin;
+                J += (dual ? A.Md[0] : A.Mp[0]) / 2;
+                s_J[dual ? 1 : 0] = J;
+            }
+            __syncthreads();
+            const float Jp = s_J[0], Jd = s_J[1];
+            stop = 1;
+            if (Jp > -Jd) stop = 0;
+            if ((double)(Jp + Jd) > kTol) stop = 0;
+            if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+            if (tid == 0) {
+                st->Jp = Jp;
+                st->Jd = Jd;
+                st->have_costs = 1;
+            }
+        }
+        if (tr) acc_ph[2] += __builtin_amdgcn_s_memtime() - t0;
+        if (stop) {
+            status = kStatusDone;
+            break;
+        }
+        if (A.max_updates > 0 && h - 1 >= A.max_updates) {
+            status = kStatusCapped;
+            break;
+        }
+        if (done_here >= A.chunk) {
+            status = kStatusContinue;
+            break;
+        }
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
+        t = tMc;
+        tMc = tMn;
+        tMn = t;
+        ++h;
+        ++done_here;
+        __syncthreads();  // the cost phase's reads of the tile area before the next phase Y's writes
+    }
+    for (int i = tid; i < N; i += NT) A.Y[i] = cur[i];
+    for (int i = tid; i < M; i += NT) A.U[i] = Us[i];
+    if (tr && tid == 0) {  // totals over the launches of a solve
+        unsigned long long* T = A0.trace + 16 * (size_t)blockIdx.x;
+        for (int p = 0; p < 3; ++p) T[p] += acc_ph[p];
+        T[4] += n_it;
+    }
+    if (tid == 0) {
+        st->h = h;
+        st->status = status;
+        st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
+    }
+}
+// </solve-pipe>
 
 // ---------------------------------------------------------------------------
 // k_solve_small: solveQuadraticDual for problems that fit in LDS (the bundled
@@ -3730,6 +4011,12 @@ size_t solve_single_lds_bytes(int ldq, int ldm, bool fused) {
     return sizeof(float) * ((size_t)(fused ? 4 : 3) * ldq + (size_t)3 * ldm);
 }
 
+thread_local int g_last_batch_kernel = 0;
+size_t solve_pipe_lds_bytes(int ldq, int ldm) {
+    const size_t cost = (size_t)ldq + 2 * (size_t)ldm;
+    return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm + (pipe_tile_floats() > cost ? pipe_tile_floats() : cost));
+}
+
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
@@ -3738,6 +4025,22 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
     const bool vec = !g_tune.single_scalar && a.N % 4 == 0 && a.M % 4 == 0 && aligned16(a.QdT) && aligned16(a.Qd) &&
                      aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && aligned16(a.GpT) &&
                      aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
+    // converge mode with Qp_inv': one pass over Gp per iteration (k_solve_pipe)
+    if (vec && !g_tune.pipe_off && a.mode == kModeConverge && a.QinvT && a.N > 64 &&
+        solve_pipe_lds_bytes(a.ldq, a.ldm) <= kPipeLdsMax) {
+        const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm);
+        // Gp tiles in flight, update loads in flight per lane, workgroups per
+        // CU: two per CU with 16 loads per lane beat three with 8 (4096
+        // problems are then 8 whole rounds of 512 resident workgroups)
+        switch (g_tune.pipe_variant) {
+        case 1: hipLaunchKernelGGL((k_solve_pipe<256, 4, 16, 2>), dim3(B), dim3(256), lds, s, a, st); break;
+        case 2: hipLaunchKernelGGL((k_solve_pipe<256, 2, 8, 1>), dim3(B), dim3(256), lds, s, a, st); break;
+        default: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), lds, s, a, st);
+        }
+        g_last_batch_kernel = 1;
+        return hipGetLastError();
+    }
+    g_last_batch_kernel = 0;
     if (a.N <= 64) {
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);

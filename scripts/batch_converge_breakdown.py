@@ -8,7 +8,8 @@ tuning options.  Prints one JSON line.
 Usage: python scripts/batch_converge_breakdown.py [N B K [variant,...]]
 (variants: fused_T unfused_T fused unfused fused_T_occ4 unfused_T_occ4 -- the
 fused Y'Qd pass on / off, with / without the prepared transposes of Gp and
-Qp_inv, k_solve_single built for 4 workgroups per CU)"""
+Qp_inv, k_solve_single built for 4 workgroups per CU; single_T: k_solve_single
+instead of k_solve_pipe, which the *_T variants take by default)"""
 from __future__ import annotations
 
 import json
@@ -47,10 +48,11 @@ def main(N=1024, B=4096, K=4):
     out = {"n_dual": N, "m": M, "problems": B, "K": K}
     GB = B * 1e-9
     variants = {"fused_T": (0, True), "unfused_T": (1, True), "fused": (0, False), "unfused": (1, False),
-                "fused_T_occ4": (8, True), "unfused_T_occ4": (9, True), "fused_T_fullfeas": (16, True)}
+                "fused_T_occ4": (8, True), "unfused_T_occ4": (9, True), "fused_T_fullfeas": (16, True),
+                "single_T": (0, True, 1)}
     names = sys.argv[4].split(",") if len(sys.argv) > 4 else list(variants)
     for name in names:
-        opts, tr = variants[name]
+        opts, tr, pipe_off = (variants[name] + (0,))[:3]
         pb.transposes = tr
         pb.invalidate()
         t0 = time.perf_counter()
@@ -58,6 +60,7 @@ def main(N=1024, B=4096, K=4):
         torch.cuda.synchronize()
         prep_ms = (time.perf_counter() - t0) * 1e3
         prev = L.pqp_tune_batch_converge(opts)
+        prev_pipe = pqp_amd.tune("pipe_off", pipe_off)
         try:
             r = {"fixed": per_iter(mode=1)}
             pb.Kp.copy_(kp)
@@ -65,11 +68,14 @@ def main(N=1024, B=4096, K=4):
             pb.Kp.fill_(1e30)
             r["feasible"] = per_iter()
             pb.Kp.copy_(kp)
+            r["kernel"] = "k_solve_pipe" if pqp_amd.tune_get("last_batch_kernel") else "k_solve_single"
         finally:
             L.pqp_tune_batch_converge(prev)
+            pqp_amd.tune("pipe_off", prev_pipe)
         r["fixed"]["TBps"] = 4.0 * N * N * GB / r["fixed"]["per_iter_ms"]
-        r["infeasible"]["TBps"] = (4.0 * N * N + 8.0 * N * M + 4.0 * M * M) * GB / r["infeasible"]["per_iter_ms"]
-        r["feasible"]["TBps_min_bytes"] = (4.0 * N * N + 8.0 * N * M + 8.0 * M * M) * GB / r["feasible"]["per_iter_ms"]
+        # each matrix once per iterate (what k_solve_pipe moves)
+        r["infeasible"]["TBps_min_bytes"] = (4.0 * N * N + 4.0 * N * M + 4.0 * M * M) * GB / r["infeasible"]["per_iter_ms"]
+        r["feasible"]["TBps_min_bytes"] = (4.0 * N * N + 4.0 * N * M + 8.0 * M * M) * GB / r["feasible"]["per_iter_ms"]
         r["prepare_ms"] = prep_ms
         out[name] = r
     print(json.dumps(out), flush=True)

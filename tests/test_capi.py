@@ -88,8 +88,8 @@ def _gfx950_asm(name: str) -> str:
 @pytest.mark.parametrize("src,pattern,min_kernels", [
     ("pqp_kernels.hip",
      r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|14k_split_update|12k_fixed_tiny"
-     r"|12k_solve_wave|12k_lean_relay)",
-     34),
+     r"|12k_solve_wave|12k_lean_relay|12k_solve_pipe)",
+     35),
     ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 3),
     ("pqp_persist.hip", r"_ZN3pqp15k_split_persist", 1),
     ("pqp_converge.hip", r"_ZN3pqp12_GLOBAL__N_118k_converge_persist", 1),
@@ -116,12 +116,15 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
 @pytest.mark.parametrize("src,name", [
     ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_ii"),
     ("pqp_converge.hip", "_ZN3pqp12_GLOBAL__N_118k_converge_persistILb0EEEvNS_6CvArgsE"),
+    ("pqp_kernels.hip", "_ZN3pqp12k_solve_pipeILi256ELi2ELi16ELi2EEEvNS_9SolveArgsEPNS_10SolveStateE"),
 ])
 def test_persistent_kernels_do_not_spill(src, name):
     """The persistent launches hold a whole slice of products in registers
     (up to 196 VGPRs) at 6 waves per workgroup, i.e. 256 VGPRs per lane: a
     spill to scratch costs 0.3 us per update (measured on k_converge_persist),
-    so the default instantiations must have no scratch."""
+    so the default instantiations must have no scratch.  k_solve_pipe's
+    default build (two workgroups per CU, 256 VGPRs) holds two Gp tiles and 16
+    update loads per lane in flight; it must not spill either."""
     asm = _gfx950_asm(src)
     i = asm.index("\n" + name + ":")
     m = re.search(r"; ScratchSize: (\d+)", asm[i:])
