@@ -256,8 +256,10 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
  * workgroup per problem (N, M <= 32), 3 one workgroup per problem with each
  * matrix held in LDS once (k_solve_mid: mid-size, about N <= 165 at M = N/4),
  * 1 the problem staged in LDS with its split copies (k_solve_small; only with
- * the mid_off knob), 2 one workgroup per problem from HBM (k_solve_single;
- * uses pqp_batch_prepare's data), or PQP_ERR_ARG when (N, M) exceeds every
+ * the mid_off knob), 2 one workgroup per problem from HBM (uses
+ * pqp_batch_prepare's data: k_solve_pipe, which reads every matrix once per
+ * iteration, in converge mode when d_QinvT is given and N, M are multiples of
+ * 4; k_solve_single otherwise), or PQP_ERR_ARG when (N, M) exceeds every
  * solver's LDS budget. */
 int pqp_batch_solve_path(int N, int M);
 
@@ -271,7 +273,9 @@ int pqp_batch_solve_path(int N, int M);
  *     call returns PQP_ERR_ARG with *all_sym_out = 0 (d_sym filled) -- call
  *     again with it.  Optional d_GpT [B][M][N] and d_QinvT [B][M][M] (with
  *     d_Gp / d_Qp_inv) receive transposed copies: terminate()'s row walks of
- *     Gp and Qp_inv (PQP_CPU.c:357, :635) then read coalesced.
+ *     Gp and Qp_inv (PQP_CPU.c:357, :635) then read coalesced.  k_solve_pipe
+ *     needs d_QinvT only (it walks Gp's rows from LDS tiles); d_GpT serves
+ *     k_solve_single.
  *   pqp_batch_solve_prepared: pqp_batch_solve on those (d_QdT NULL when
  *     *all_sym_out was 1; d_GpT / d_QinvT NULL when not prepared).  The
  *     prepared data stay valid until Qd (or Gp, Qp_inv) change.
