@@ -464,11 +464,22 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         dt3 = call(3 * K)  # the same call with 3K updates: the difference is 2K iterations, no per-call cost
         ok = ok and bool((pb.h == 3 * K + 1).all().item())
         per_iter = (dt3 - dt) / (2 * K)
+        single = None
+        if pipe:  # the same iterations on k_solve_single (Gp read twice), same process and box
+            prev = pqp_amd.tune("pipe_off", 1)
+            try:
+                call(1)
+                single = (call(3 * K) - call(K)) / (2 * K)
+            finally:
+                pqp_amd.tune("pipe_off", prev)
         gbs = alg * B / per_iter / 1e9
         r = {"ms_per_iteration": per_iter * 1e3, "instance_iter_per_s": B / per_iter,
              "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
              "design_bytes_per_iter": design, "design_GBps": design * B / per_iter / 1e9,
              "call_ms": dt * 1e3, "call_instance_iter_per_s": B * K / dt, "all_capped": ok}
+        if single is not None:
+            r["k_solve_single_ms_per_iteration"] = single * 1e3
+            r["speedup_vs_k_solve_single"] = single / per_iter
         pmc = db.get(f"{kname}_{case}")
         if pmc and pmc.get("kernel_src_sha256") == khash:
             r["traffic_ratio"] = pmc["traffic_ratio"]

@@ -1856,14 +1856,12 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
                     float s = racc;
                     int c = 0;
                     for (; c + 8 <= nc; c += 8) {
-                        float g[8], uv[8];
+                        float g[8];
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) {
-                            g[e] = tr[c + e];
-                            uv[e] = u[c + e];
-                        }
+                        for (int e = 0; e < 8; ++e) g[e] = tr[c + e];
+                        const sf4 u0 = *reinterpret_cast<const sf4*>(u + c), u1 = *reinterpret_cast<const sf4*>(u + c + 4);
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) s += g[e] * uv[e];
+                        for (int e = 0; e < 8; ++e) s += g[e] * (e < 4 ? u0[e] : u1[e - 4]);
                     }
                     for (; c < nc; ++c) s += tr[c] * u[c];
                     racc = s;
@@ -1880,14 +1878,12 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
                     float s = (I == 0) ? 0.0f : tMn[col];
                     int r = 0;
                     for (; r + 8 <= nr; r += 8) {
-                        float g[8], yv[8];
+                        float g[8];
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) {
-                            g[e] = tl[(r + e) * kPipeTS + lane];
-                            yv[e] = y[r + e];
-                        }
+                        for (int e = 0; e < 8; ++e) g[e] = tl[(r + e) * kPipeTS + lane];
+                        const sf4 y0 = *reinterpret_cast<const sf4*>(y + r), y1 = *reinterpret_cast<const sf4*>(y + r + 4);
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) s += g[e] * yv[e];
+                        for (int e = 0; e < 8; ++e) s += g[e] * (e < 4 ? y0[e] : y1[e - 4]);
                     }
                     for (; r < nr; ++r) s += tl[r * kPipeTS + lane] * y[r];
                     tMn[col] = (I == nI - 1) ? s + 1.0f * A.Fp[col] : s;  // matrixAdd :356
