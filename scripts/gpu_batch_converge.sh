@@ -8,8 +8,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 TAG=${TAG:-bc}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 300 python -u scripts/batch_converge_breakdown.py 1024 4096 4 ${VARIANTS:-fused_T,single_T,unfused_T,fused} > $OUT/breakdown.json 2> $OUT/breakdown.err || { tail -20 $OUT/breakdown.err; exit 1; }
-cat $OUT/breakdown.json
+[ -z "$NO_BREAKDOWN" ] && { timeout -k 10 300 python -u scripts/batch_converge_breakdown.py 1024 4096 4 ${VARIANTS:-fused_T,single_T,unfused_T,fused} > $OUT/breakdown.json 2> $OUT/breakdown.err || { tail -20 $OUT/breakdown.err; exit 1; }; cat $OUT/breakdown.json; }
 [ -n "$NO_PMC" ] && exit 0
 for F in "" 1; do
   sfx=${F:+_feasible}
