@@ -219,7 +219,8 @@ def test_tuning_knobs_roundtrip():
     import pqp_amd
 
     L = pqp_amd.lib()
-    for key in ("persist_off", "lean_min_n", "batch_opts", "split_kind", "converge_chunk", "wide_min_n"):
+    for key in ("persist_off", "lean_min_n", "batch_opts", "split_kind", "converge_chunk", "wide_min_n", "pipe_off",
+                "pipe_variant"):
         old = pqp_amd.tune_get(key)
         assert pqp_amd.tune(key, old + 3) == old
         assert pqp_amd.tune_get(key) == old + 3
@@ -238,3 +239,4 @@ def test_tuning_knobs_roundtrip():
     fb = C.c_longlong(-1)
     assert L.pqp_tune_last_path(C.byref(fb)) == 0 and fb.value == 0
     assert L.pqp_tune_converge_grid(1024, 512) > 0 and L.pqp_tune_converge_grid(28, 7) > 0
+    assert pqp_amd.tune_get("last_batch_kernel") == 0  # no path-2 launch on this thread yet
