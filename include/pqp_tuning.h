@@ -52,10 +52,11 @@ extern "C" {
  *                          iteration) instead of k_solve_pipe (Gp read once;
  *                          taken when Qp_inv' is prepared and N, M are
  *                          multiples of 4)
- *   pipe_variant [0]       k_solve_pipe build: 0 two Gp tiles and 16 update
- *                          loads per lane in flight, two workgroups per CU;
- *                          1 four tiles; 2 two tiles, 8 loads, occupancy set
- *                          by the register count
+ *   pipe_variant [0]       k_solve_pipe build: 0 one 128 x 96 Gp tile per
+ *                          step (every wave sums a chain) and 16 update loads
+ *                          per lane in flight, two workgroups per CU; 3 two
+ *                          64 x 64 tiles in flight; 1 four; 2 two, 8 loads,
+ *                          occupancy set by the register count
  *   mid_off [0]            batched solves of mid-size problems through
  *                          k_solve_small / k_solve_single instead of the
  *                          LDS-resident k_solve_mid (path 3)

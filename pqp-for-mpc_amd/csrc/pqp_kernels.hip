@@ -1723,12 +1723,13 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
 // next iterate's computeUfromY:
 //   phase X  Y_{h+1} = updateY2(Y_h) (+ Y_h'Qd fused when Qd is bit-symmetric
 //            and the previous iterate was feasible), U_h = -Qp_inv tM_h
-//   phase Y  Gp in 64 x 64 tiles, each staged once through LDS: lane r of
-//            wave 0 sums row r's terms Gp[i][j] U_h[j] (j in order, the
-//            partial carried across the tiles of a row block), lane c of
-//            wave 1 column c's terms Gp[i][j] Y_{h+1}[i] (i in order, the
-//            partial carried in LDS across row blocks); the loads of the
-//            tiles two ahead are in flight meanwhile
+//   phase Y  Gp in 128 x 96 tiles, each staged once through LDS: lane r of
+//            waves 0 and 2 sums row r's terms Gp[i][j] U_h[j] (j in order,
+//            the partial carried across the tiles of a row block), lane c of
+//            waves 1 and 3 column c's terms Gp[i][j] Y_{h+1}[i] (i in order,
+//            the partial carried in LDS across row blocks); the next tile's
+//            loads are in flight meanwhile (variants: 64 x 64 tiles on waves
+//            0 and 1, two or four tiles ahead)
 //   then     checkFeas(h) from the row sums; computeCost on a feasible iterate
 //            as k_solve_single does; Y_{h+1}, tM_{h+1} dropped when h stops.
 // Every sum has the reference's operands and order, so every value is the
@@ -1737,9 +1738,16 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
 // passes over Gp.  Needs the wide-load conditions and Qp_inv' (QinvT).
 // ---------------------------------------------------------------------------
 constexpr int kPipeTR = 64, kPipeTC = 64, kPipeTS = kPipeTC + 1;  // tile rows, columns, LDS row stride
-__host__ __device__ inline size_t pipe_tile_floats() { return (size_t)2 * kPipeTR * kPipeTS; }
+// BIG: one 128 x 96 tile at a time (single LDS slot, the next tile's loads in
+// registers): rows summed on waves 0 and 2, columns on waves 1 and 3, so every
+// wave runs a chain and a step holds 3x the terms of a 64 x 64 tile for 2x the
+// chain length
+constexpr int kPipeBR = 128, kPipeBC = 96, kPipeBS = kPipeBC + 1, kPipeBQ = kPipeBR * kPipeBC / 4 / 256;
+__host__ __device__ inline size_t pipe_tile_floats(bool big = false) {
+    return big ? (size_t)kPipeBR * kPipeBS : (size_t)2 * kPipeTR * kPipeTS;
+}
 
-template <int NT, int PD, int SU, int MINB>
+template <int NT, int PD, int SU, int MINB, bool BIG = false>
 __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
@@ -1760,7 +1768,8 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const bool fuse_ok = A.sym && A.sym[blockIdx.x];
     bool was_feasible = false;
-    const int nI = (N + kPipeTR - 1) / kPipeTR, nJ = (M + kPipeTC - 1) / kPipeTC, nT = nI * nJ;
+    constexpr int TR = BIG ? kPipeBR : kPipeTR, TC = BIG ? kPipeBC : kPipeTC;
+    const int nI = (N + TR - 1) / TR, nJ = (M + TC - 1) / TC, nT = nI * nJ;
 
     long long h = st->h;
     for (int i = tid; i < ldq; i += NT) {
@@ -1817,6 +1826,91 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
             Us[i0 + 1] = -t[1];
         }
         // ---- phase Y: one pass over Gp ----
+        int bad = 0;
+        if constexpr (BIG) {
+            // tile t = (I, J): lane l loads chunk e = l + 256 s of the tile's
+            // 128 rows x 24 16-byte chunks (a row's 384 bytes by 24 lanes)
+            auto load_big = [&](int t, sf4 (&r)[kPipeBQ]) {
+                const int I = t / nJ, J = t - I * nJ;
+#pragma unroll
+                for (int s = 0; s < kPipeBQ; ++s) {
+                    const int e = tid + 256 * s, rr = e / 24, c4 = e - rr * 24;
+                    const int row = I * kPipeBR + rr, col = J * kPipeBC + 4 * c4;
+                    r[s] = (row < N && col < M)
+                               ? __builtin_nontemporal_load(reinterpret_cast<const sf4*>(A.Gp + (size_t)row * M + col))
+                               : sf4{0.0f, 0.0f, 0.0f, 0.0f};
+                }
+            };
+            sf4 rb[kPipeBQ];
+            load_big(0, rb);
+            __syncthreads();  // Y_{h+1}, U_h complete; the tile area is free
+            if (tr) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                acc_ph[0] += t - t0;
+                t0 = t;
+            }
+            float racc = 0.0f;  // waves 0 and 2: row sum of the current row block
+            for (int t = 0; t < nT; ++t) {
+#pragma unroll
+                for (int s = 0; s < kPipeBQ; ++s) {
+                    const int e = tid + 256 * s, rr = e / 24, c4 = e - rr * 24;
+                    float* d = tile + rr * kPipeBS + 4 * c4;
+                    d[0] = rb[s].x;
+                    d[1] = rb[s].y;
+                    d[2] = rb[s].z;
+                    d[3] = rb[s].w;
+                }
+                if (t + 1 < nT) load_big(t + 1, rb);
+                __syncthreads();  // tile t staged
+                const int I = t / nJ, J = t - I * nJ;
+                const int nr = min(kPipeBR, N - I * kPipeBR), nc = min(kPipeBC, M - J * kPipeBC);
+                if ((wave & 1) == 0) {
+                    // checkFeas :636: gu[i] = sum_j Gp[i][j] U[j], j in order
+                    const int rl = (wave >> 1) * 64 + lane;
+                    if (J == 0) racc = 0.0f;
+                    if (rl < nr) {
+                        const float* tr = tile + rl * kPipeBS;
+                        const float* u = Us + J * kPipeBC;
+                        float s = racc;
+                        int c = 0;
+                        for (; c + 8 <= nc; c += 8) {
+                            float g[8];
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) g[e] = tr[c + e];
+                            const sf4 u0 = *reinterpret_cast<const sf4*>(u + c), u1 = *reinterpret_cast<const sf4*>(u + c + 4);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) s += g[e] * (e < 4 ? u0[e] : u1[e - 4]);
+                        }
+                        for (; c < nc; ++c) s += tr[c] * u[c];
+                        racc = s;
+                        if (J == nJ - 1) {  // compare :338-341
+                            const float kp = A.Kp[I * kPipeBR + rl];
+                            if (s > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;
+                        }
+                    }
+                } else if (!last) {
+                    // Gp'Y_{h+1} :355: tmp[j] = sum_i Gp[i][j] Y[i], i in order
+                    const int cl = (wave >> 1) * 64 + lane;
+                    if (cl < nc) {
+                        const int col = J * kPipeBC + cl;
+                        const float* y = nxt + I * kPipeBR;
+                        float s = (I == 0) ? 0.0f : tMn[col];
+                        int r = 0;
+                        for (; r + 8 <= nr; r += 8) {
+                            float g[8];
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) g[e] = tile[(r + e) * kPipeBS + cl];
+                            const sf4 y0 = *reinterpret_cast<const sf4*>(y + r), y1 = *reinterpret_cast<const sf4*>(y + r + 4);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) s += g[e] * (e < 4 ? y0[e] : y1[e - 4]);
+                        }
+                        for (; r < nr; ++r) s += tile[r * kPipeBS + cl] * y[r];
+                        tMn[col] = (I == nI - 1) ? s + 1.0f * A.Fp[col] : s;  // matrixAdd :356
+                    }
+                }
+                __syncthreads();  // the slot is free for tile t + 1
+            }
+        } else {
         sf4 rq[PD][4];  // the next PD tiles' loads in flight
 #pragma unroll
         for (int d = 0; d < PD; ++d)
@@ -1828,7 +1922,6 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
             t0 = t;
         }
         float racc = 0.0f;  // wave 0: row sum of the current row block
-        int bad = 0;
         for (int t = 0; t < nT; ++t) {
             float* tl = tile + (t & 1) * (kPipeTR * kPipeTS);
 #pragma unroll
@@ -1889,6 +1982,7 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
                     tMn[col] = (I == nI - 1) ? s + 1.0f * A.Fp[col] : s;  // matrixAdd :356
                 }
             }
+        }
         }
         const int infeasible = __syncthreads_or(bad);
         was_feasible = !infeasible;
@@ -4008,9 +4102,9 @@ size_t solve_single_lds_bytes(int ldq, int ldm, bool fused) {
 }
 
 thread_local int g_last_batch_kernel = 0;
-size_t solve_pipe_lds_bytes(int ldq, int ldm) {
-    const size_t cost = (size_t)ldq + 2 * (size_t)ldm;
-    return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm + (pipe_tile_floats() > cost ? pipe_tile_floats() : cost));
+size_t solve_pipe_lds_bytes(int ldq, int ldm, bool big) {
+    const size_t cost = (size_t)ldq + 2 * (size_t)ldm, tile = pipe_tile_floats(big);
+    return sizeof(float) * ((size_t)3 * ldq + (size_t)3 * ldm + (tile > cost ? tile : cost));
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -4023,15 +4117,18 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
                      aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
     // converge mode with Qp_inv': one pass over Gp per iteration (k_solve_pipe)
     if (vec && !g_tune.pipe_off && a.mode == kModeConverge && a.QinvT && a.N > 64 &&
-        solve_pipe_lds_bytes(a.ldq, a.ldm) <= kPipeLdsMax) {
-        const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm);
+        solve_pipe_lds_bytes(a.ldq, a.ldm, g_tune.pipe_variant == 0) <= kPipeLdsMax) {
+        const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm, g_tune.pipe_variant == 0);
         // Gp tiles in flight, update loads in flight per lane, workgroups per
         // CU: two per CU with 16 loads per lane beat three with 8 (4096
         // problems are then 8 whole rounds of 512 resident workgroups)
+        // 128 x 96 tiles (every wave sums a chain) beat 64 x 64 ones by 2-3 %
+        // on infeasible iterates and tie on feasible ones
         switch (g_tune.pipe_variant) {
         case 1: hipLaunchKernelGGL((k_solve_pipe<256, 4, 16, 2>), dim3(B), dim3(256), lds, s, a, st); break;
         case 2: hipLaunchKernelGGL((k_solve_pipe<256, 2, 8, 1>), dim3(B), dim3(256), lds, s, a, st); break;
-        default: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), lds, s, a, st);
+        case 3: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), lds, s, a, st); break;
+        default: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), lds, s, a, st);
         }
         g_last_batch_kernel = 1;
         return hipGetLastError();

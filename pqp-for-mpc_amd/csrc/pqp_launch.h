@@ -64,7 +64,7 @@ hipError_t launch_cost_finish(const float* quad, const float* lin, const float* 
 hipError_t launch_mp_finish(const float* t, const float* Mp6, float* Mp, hipStream_t s);
 hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* res, int n, hipStream_t s);
 size_t solve_single_lds_bytes(int ldq, int ldm, bool fused = false);
-size_t solve_pipe_lds_bytes(int ldq, int ldm);
+size_t solve_pipe_lds_bytes(int ldq, int ldm, bool big = false);
 constexpr size_t kPipeLdsMax = 150 * 1024;
 extern thread_local int g_last_batch_kernel;  // 1 when the calling thread's last path-2 launch was k_solve_pipe
 size_t solve_small_lds_bytes(int N, int M);
@@ -114,7 +114,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     long long batch_chunk = 0;  // iterates per problem per batched-solve launch (0: sized from N, M)
     int mid_off = 0;
     int mid_split = 0;  // 1: k_solve_mid's stored-split form where its LDS fits  // batched solves of mid-size N through k_solve_small / k_solve_single instead of k_solve_mid
-    int pipe_variant = 0;  // k_solve_pipe build: 0 (2 Gp tiles and 16 loads per lane in flight, 2 WGs/CU), 1 (4 tiles), 2 (2 tiles, 8 loads, VGPR-bound occupancy)
+    int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 1 (64 x 64 tiles, 4 in flight), 2 (64 x 64, 2 in flight, 8 loads, VGPR-bound occupancy), 3 (64 x 64, 2 in flight)
     int pipe_off = 0;  // batched converge of large problems on k_solve_single (two passes over Gp) instead of k_solve_pipe
     int batch_opts = 0;  // pqp_batch_solve: bit 0 no fused Y'Qd, bit 1 per-call transposes, bit 4 checkFeas over every row
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch

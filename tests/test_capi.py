@@ -116,15 +116,16 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
 @pytest.mark.parametrize("src,name", [
     ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_ii"),
     ("pqp_converge.hip", "_ZN3pqp12_GLOBAL__N_118k_converge_persistILb0EEEvNS_6CvArgsE"),
-    ("pqp_kernels.hip", "_ZN3pqp12k_solve_pipeILi256ELi2ELi16ELi2EEEvNS_9SolveArgsEPNS_10SolveStateE"),
+    ("pqp_kernels.hip", "_ZN3pqp12k_solve_pipeILi256ELi2ELi16ELi2ELb1EEEvNS_9SolveArgsEPNS_10SolveStateE"),
+    ("pqp_kernels.hip", "_ZN3pqp12k_solve_pipeILi256ELi2ELi16ELi2ELb0EEEvNS_9SolveArgsEPNS_10SolveStateE"),
 ])
 def test_persistent_kernels_do_not_spill(src, name):
     """The persistent launches hold a whole slice of products in registers
     (up to 196 VGPRs) at 6 waves per workgroup, i.e. 256 VGPRs per lane: a
     spill to scratch costs 0.3 us per update (measured on k_converge_persist),
     so the default instantiations must have no scratch.  k_solve_pipe's
-    default build (two workgroups per CU, 256 VGPRs) holds two Gp tiles and 16
-    update loads per lane in flight; it must not spill either."""
+    builds at two workgroups per CU (up to 256 VGPRs: a 128 x 96 Gp tile, or two
+    64 x 64 ones, and 16 update loads per lane in flight) must not spill either."""
     asm = _gfx950_asm(src)
     i = asm.index("\n" + name + ":")
     m = re.search(r"; ScratchSize: (\d+)", asm[i:])

@@ -25,9 +25,10 @@ def _check(pb, b, h, Y, U, what):
     assert_bitwise(pb.U[b].cpu().numpy(), U, f"{what} U")
 
 
-def _solve(gpu_lib, N, M, B, cap, feasible, pipe_off=0, chunk=0, seed=9, inst0=4):
+def _solve(gpu_lib, N, M, B, cap, feasible, pipe_off=0, chunk=0, seed=9, inst0=4, variant=0):
     prev = pqp_amd.tune("pipe_off", pipe_off)
     prev_chunk = pqp_amd.tune("batch_chunk", chunk)
+    prev_variant = pqp_amd.tune("pipe_variant", variant)
     try:
         pb = gpu_lib.ProblemBatch.synthetic(seed, inst0, B, N, M)
         if feasible:
@@ -37,18 +38,20 @@ def _solve(gpu_lib, N, M, B, cap, feasible, pipe_off=0, chunk=0, seed=9, inst0=4
     finally:
         pqp_amd.tune("pipe_off", prev)
         pqp_amd.tune("batch_chunk", prev_chunk)
+        pqp_amd.tune("pipe_variant", prev_variant)
     return pb, kernel
 
 
+@pytest.mark.parametrize("variant", [0, 3], ids=["tiles128x96", "tiles64"])
 @pytest.mark.parametrize("N,M", [(256, 128), (260, 132), (128, 200), (320, 64), (512, 256)])
 @pytest.mark.parametrize("feasible", [False, True])
-def test_pipe_capped_vs_oracle(gpu_lib, orc, N, M, feasible):
+def test_pipe_capped_vs_oracle(gpu_lib, orc, N, M, feasible, variant):
     """Capped solves through k_solve_pipe: 64-aligned and ragged tiles (N 260,
     M 132: partial row and column tiles), M > N, one column tile (M 64);
     `feasible`: Kp = 1e30 seen by checkFeas only, so every iterate runs all of
     computeCost and the fused Y'Qd rides in the speculative update."""
     B, cap = 3, 6
-    pb, kernel = _solve(gpu_lib, N, M, B, cap, feasible)
+    pb, kernel = _solve(gpu_lib, N, M, B, cap, feasible, variant=variant)
     assert kernel == 1, "k_solve_pipe not taken"
     for b in range(B):
         P = orc.synth_problem(9, 4 + b, N, M)
@@ -58,14 +61,15 @@ def test_pipe_capped_vs_oracle(gpu_lib, orc, N, M, feasible):
         _check(pb, b, h, Y, U, f"pipe N={N} M={M} feasible={feasible} b={b}")
 
 
+@pytest.mark.parametrize("variant", [0, 3], ids=["tiles128x96", "tiles64"])
 @pytest.mark.parametrize("chunk", [1, 2, 5])
 @pytest.mark.parametrize("feasible", [False, True])
-def test_pipe_chunked_launches_vs_oracle(gpu_lib, orc, chunk, feasible):
+def test_pipe_chunked_launches_vs_oracle(gpu_lib, orc, chunk, feasible, variant):
     """A solve split over launches of `chunk` iterates: each launch re-forms
     tM_h from the Y it resumes from, and the last iterate of a launch skips the
     speculative update (it breaks before its update whatever terminate() says)."""
     N, M, B, cap = 256, 128, 2, 7
-    pb, kernel = _solve(gpu_lib, N, M, B, cap, feasible, chunk=chunk)
+    pb, kernel = _solve(gpu_lib, N, M, B, cap, feasible, chunk=chunk, variant=variant)
     assert kernel == 1
     for b in range(B):
         P = orc.synth_problem(9, 4 + b, N, M)
@@ -82,7 +86,10 @@ def test_pipe_same_bits_as_single_at_bench_size(gpu_lib, feasible):
     N, M, B, cap = 1024, 512, 8, 5
     a, ka = _solve(gpu_lib, N, M, B, cap, feasible)
     b, kb = _solve(gpu_lib, N, M, B, cap, feasible, pipe_off=1)
-    assert (ka, kb) == (1, 0)
+    c, kc = _solve(gpu_lib, N, M, B, cap, feasible, variant=3)
+    assert (ka, kb, kc) == (1, 0, 1)
+    assert_bitwise(c.Y.cpu().numpy(), b.Y.cpu().numpy(), "Y pipe 64x64 tiles vs single")
+    assert_bitwise(c.U.cpu().numpy(), b.U.cpu().numpy(), "U pipe 64x64 tiles vs single")
     assert np.array_equal(a.h.cpu().numpy(), b.h.cpu().numpy())
     assert np.array_equal(a.status.cpu().numpy(), b.status.cpu().numpy())
     assert_bitwise(a.Y.cpu().numpy(), b.Y.cpu().numpy(), "Y pipe vs single")
