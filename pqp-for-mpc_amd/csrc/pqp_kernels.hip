@@ -4116,9 +4116,10 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
                      aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && aligned16(a.GpT) &&
                      aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
     // converge mode with Qp_inv': one pass over Gp per iteration (k_solve_pipe)
+    const bool pipe_big = g_tune.pipe_variant < 1 || g_tune.pipe_variant > 3;  // the default build's 128 x 96 tile
     if (vec && !g_tune.pipe_off && a.mode == kModeConverge && a.QinvT && a.N > 64 &&
-        solve_pipe_lds_bytes(a.ldq, a.ldm, g_tune.pipe_variant == 0) <= kPipeLdsMax) {
-        const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm, g_tune.pipe_variant == 0);
+        solve_pipe_lds_bytes(a.ldq, a.ldm, pipe_big) <= kPipeLdsMax) {
+        const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm, pipe_big);
         // Gp tiles in flight, update loads in flight per lane, workgroups per
         // CU: two per CU with 16 loads per lane beat three with 8 (4096
         // problems are then 8 whole rounds of 512 resident workgroups)
