@@ -105,7 +105,8 @@ int pqp_tune_get(const char *key, long long *value);
  * n iterates of k_converge_persist; "mid": 16 words per problem for the first
  * n problems of a batched k_solve_mid solve -- phase A/B/C/D+E clock totals,
  * iterations, then each wave's phase-A busy clocks, added to what the buffer
- * holds).  n = 0 turns it off.  Timing only. */
+ * holds; a k_solve_pipe solve writes phase X / Y / cost clock totals to words
+ * 0-2 and iterations to word 4).  n = 0 turns it off.  Timing only. */
 int pqp_tune_trace(const char *what, void *d_buf, int n);
 
 /* The first n values of glibc's unseeded rand() sequence (the testing/
