@@ -1767,7 +1767,11 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
     __shared__ float s_J[2];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const bool fuse_ok = A.sym && A.sym[blockIdx.x];
-    bool was_feasible = false;
+    // a launch's first iterate fuses Y'Qd as if the previous one was feasible:
+    // resumed converge solves (chunks of a long solve) then need no separate
+    // pass over Qd for Jd, and an infeasible first iterate costs only the
+    // fused sum's VALU work
+    bool was_feasible = true;
     constexpr int TR = BIG ? kPipeBR : kPipeTR, TC = BIG ? kPipeBC : kPipeTC;
     const int nI = (N + TR - 1) / TR, nJ = (M + TC - 1) / TC, nT = nI * nJ;
 

@@ -36,10 +36,10 @@ def design_bytes(case: str, which: str) -> float:
         # Gp, and an update before every iterate but the capped one
         if case == "infeasible":
             return g + K * q + (K + 1) * (qi + g)
-        # feasible: iterate 1 unfused (update, then a pass over Qd for Y'Qd),
-        # iterates 2..K fused, the capped iterate K+1 no update but Y'Qd's
-        # pass; Qp for U'Qp every iterate
-        return g + (K + 2) * q + (K + 1) * (qi + g + qp)
+        # feasible: iterates 1..K fused (a launch's first iterate fuses too),
+        # the capped iterate K+1 no update but Y'Qd's pass; Qp for U'Qp every
+        # iterate
+        return g + (K + 1) * q + (K + 1) * (qi + g + qp)
     if case == "infeasible":  # 8 updates; 9 terminates stopping at checkFeas (Gp'Y, Qp_inv, and Gp U
         # over its first 256 rows, where a row over its bound decides the iterate)
         return K * q + (K + 1) * (g + 4.0 * min(N, 256) * M + qi)
