@@ -50,8 +50,9 @@ extern "C" {
  *   pipe_off [0]           batched converge of problems too large for LDS
  *                          (path 2) on k_solve_single (Gp read twice per
  *                          iteration) instead of k_solve_pipe (Gp read once;
- *                          taken when Qp_inv' is prepared and N, M are
- *                          multiples of 4)
+ *                          taken when Qp_inv' is prepared, N, M are multiples
+ *                          of 4 and M >= N / 3)
+ *   pipe_force [0]         k_solve_pipe also where M < N / 3
  *   pipe_variant [0]       k_solve_pipe build: 0 one 128 x 96 Gp tile per
  *                          step (every wave sums a chain) and 16 update loads
  *                          per lane in flight, two workgroups per CU; 3 two

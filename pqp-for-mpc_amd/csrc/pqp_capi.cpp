@@ -1892,6 +1892,7 @@ const KnobRef* find_knob(const char* key) {
         {"mid_split", &g_tune.mid_split, nullptr, nullptr},
         {"pipe_off", &g_tune.pipe_off, nullptr, nullptr},
         {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},
+        {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},
         {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},
         {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
     };

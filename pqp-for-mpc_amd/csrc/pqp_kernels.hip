@@ -4121,7 +4121,13 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
                      aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
     // converge mode with Qp_inv': one pass over Gp per iteration (k_solve_pipe)
     const bool pipe_big = g_tune.pipe_variant < 1 || g_tune.pipe_variant > 3;  // the default build's 128 x 96 tile
-    if (vec && !g_tune.pipe_off && a.mode == kModeConverge && a.QinvT && a.N > 64 &&
+    // the pipe saves one of the two passes over Gp (4NM bytes per iteration)
+    // but holds two workgroups per CU against k_solve_single's three: where
+    // Gp is a small part of the bytes (M < N / 3, e.g. the MPC plant over
+    // 6..32 horizon steps, M = N / 4) k_solve_single measured faster
+    // (profiles/r03/pipe/horizon_pipe_vs_single.jsonl)
+    const bool pipe_pays = g_tune.pipe_force || 3 * a.M >= a.N;
+    if (vec && !g_tune.pipe_off && pipe_pays && a.mode == kModeConverge && a.QinvT && a.N > 64 &&
         solve_pipe_lds_bytes(a.ldq, a.ldm, pipe_big) <= kPipeLdsMax) {
         const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm, pipe_big);
         // Gp tiles in flight, update loads in flight per lane, workgroups per

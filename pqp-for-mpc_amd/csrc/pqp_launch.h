@@ -115,6 +115,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int mid_off = 0;
     int mid_split = 0;  // 1: k_solve_mid's stored-split form where its LDS fits  // batched solves of mid-size N through k_solve_small / k_solve_single instead of k_solve_mid
     int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 1 (64 x 64 tiles, 4 in flight), 2 (64 x 64, 2 in flight, 8 loads, VGPR-bound occupancy), 3 (64 x 64, 2 in flight)
+    int pipe_force = 0;  // k_solve_pipe also where M < N / 3 (where k_solve_single measured faster)
     int pipe_off = 0;  // batched converge of large problems on k_solve_single (two passes over Gp) instead of k_solve_pipe
     int batch_opts = 0;  // pqp_batch_solve: bit 0 no fused Y'Qd, bit 1 per-call transposes, bit 4 checkFeas over every row
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch

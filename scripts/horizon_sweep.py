@@ -61,6 +61,21 @@ def main(Hs):
                       "mid_off_same_bits": bool(torch.equal(pb.Y.view(torch.int32), Y3.view(torch.int32)))}
             finally:
                 pqp_amd.tune("mid_off", old)
+        if path == 2:  # the same batch on k_solve_single (Gp read twice): time and bits
+            Y2 = pb.Y.clone()
+            kern = pqp_amd.tune_get("last_batch_kernel")
+            old = pqp_amd.tune("pipe_off", 1)
+            try:
+                pb.solve(max_updates=200000)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                pb.solve(max_updates=200000)
+                torch.cuda.synchronize()
+                ab = {"batch_kernel": "k_solve_pipe" if kern else "k_solve_single",
+                      "pipe_off_batch_ms": (time.perf_counter() - t0) * 1e3,
+                      "pipe_off_same_bits": bool(torch.equal(pb.Y.view(torch.int32), Y2.view(torch.int32)))}
+            finally:
+                pqp_amd.tune("pipe_off", old)
         with pqp_amd.Problem(P) as prob:
             prob.solve(max_updates=200000)
             ts = []

@@ -221,7 +221,7 @@ def test_tuning_knobs_roundtrip():
 
     L = pqp_amd.lib()
     for key in ("persist_off", "lean_min_n", "batch_opts", "split_kind", "converge_chunk", "wide_min_n", "pipe_off",
-                "pipe_variant"):
+                "pipe_variant", "pipe_force"):
         old = pqp_amd.tune_get(key)
         assert pqp_amd.tune(key, old + 3) == old
         assert pqp_amd.tune_get(key) == old + 3

@@ -6,7 +6,8 @@ order) and the next iterate's Gp'Y_{h+1} (:355, i in order).  Bar: the
 reference's h, Y, U (and, through h, Jp / Jd) bit for bit against the oracle,
 and the same bits as k_solve_single (pipe_off), on infeasible and all-feasible
 iterates, tile-ragged N and M, M > N, chunked launches and a problem that
-stops inside a launch."""
+stops inside a launch.  Shapes with M < N / 3, which the library sends to
+k_solve_single by default, run here with pqp_tune("pipe_force", 1)."""
 from __future__ import annotations
 
 import numpy as np
@@ -29,6 +30,7 @@ def _solve(gpu_lib, N, M, B, cap, feasible, pipe_off=0, chunk=0, seed=9, inst0=4
     prev = pqp_amd.tune("pipe_off", pipe_off)
     prev_chunk = pqp_amd.tune("batch_chunk", chunk)
     prev_variant = pqp_amd.tune("pipe_variant", variant)
+    prev_force = pqp_amd.tune("pipe_force", 1)  # also the M < N / 3 shapes
     try:
         pb = gpu_lib.ProblemBatch.synthetic(seed, inst0, B, N, M)
         if feasible:
@@ -39,6 +41,7 @@ def _solve(gpu_lib, N, M, B, cap, feasible, pipe_off=0, chunk=0, seed=9, inst0=4
         pqp_amd.tune("pipe_off", prev)
         pqp_amd.tune("batch_chunk", prev_chunk)
         pqp_amd.tune("pipe_variant", prev_variant)
+        pqp_amd.tune("pipe_force", prev_force)
     return pb, kernel
 
 
@@ -119,12 +122,14 @@ def test_pipe_testfile_stops_like_reference(gpu_lib, orc, tmp_path, chunk):
     h, Y, U = orc.solve(P, max_updates=CAP)
     assert h > 0
     prev = pqp_amd.tune("batch_chunk", chunk)
+    prev_force = pqp_amd.tune("pipe_force", 1)  # M = N / 4
     try:
         pb = gpu_lib.ProblemBatch.replicate(P, 3)
         pb.solve(max_updates=CAP)
         kernel = pqp_amd.tune_get("last_batch_kernel")
     finally:
         pqp_amd.tune("batch_chunk", prev)
+        pqp_amd.tune("pipe_force", prev_force)
     assert kernel == 1
     for b in range(3):
         _check(pb, b, h, Y, U, f"test2 copy {b} chunk={chunk}")
@@ -148,8 +153,27 @@ def test_pipe_mixed_symmetric_and_not(gpu_lib, orc):
     pb = gpu_lib.ProblemBatch(2, N, M)
     for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
         pb.set(k, np.stack([np.asarray(P[k], np.float32).reshape(-1) for P in (P0, P1)]))
-    pb.solve(max_updates=cap)
-    assert pqp_amd.tune_get("last_batch_kernel") == 1
+    prev_force = pqp_amd.tune("pipe_force", 1)  # M = N / 4
+    try:
+        pb.solve(max_updates=cap)
+        assert pqp_amd.tune_get("last_batch_kernel") == 1
+    finally:
+        pqp_amd.tune("pipe_force", prev_force)
     for b, P in enumerate((P0, P1)):
         h, Y, U = orc.solve(P, max_updates=cap)
         _check(pb, b, h, Y, U, f"mixed {b}")
+
+
+def test_pipe_routing_by_shape(gpu_lib):
+    """Auto routing of path 2: k_solve_pipe where M >= N / 3 (the second
+    pass over Gp it saves is a large part of the bytes), k_solve_single below
+    (profiles/r03/pipe/horizon_pipe_vs_single.jsonl), whatever the caller
+    leaves in pipe_force."""
+    prev = pqp_amd.tune("pipe_force", 0)
+    try:
+        for N, M, want in ((256, 128, 1), (300, 100, 1), (256, 64, 0), (400, 100, 0)):
+            pb = gpu_lib.ProblemBatch.synthetic(9, 0, 2, N, M)
+            pb.solve(max_updates=2)
+            assert pqp_amd.tune_get("last_batch_kernel") == want, (N, M)
+    finally:
+        pqp_amd.tune("pipe_force", prev)
