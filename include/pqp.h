@@ -258,8 +258,8 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
  * 1 the problem staged in LDS with its split copies (k_solve_small; only with
  * the mid_off knob), 2 one workgroup per problem from HBM (uses
  * pqp_batch_prepare's data: k_solve_pipe, which reads every matrix once per
- * iteration, in converge mode when d_QinvT is given and N, M are multiples of
- * 4; k_solve_single otherwise), or PQP_ERR_ARG when (N, M) exceeds every
+ * iteration, in converge mode when d_QinvT is given, N, M are multiples of 4
+ * and M >= N/3; k_solve_single otherwise), or PQP_ERR_ARG when (N, M) exceeds every
  * solver's LDS budget. */
 int pqp_batch_solve_path(int N, int M);
 
