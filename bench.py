@@ -297,8 +297,7 @@ def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
     import torch
 
     ex = pqp_amd.read_example(ROOT / "tests" / "golden" / "example")
-    rng = np.random.default_rng(5)
-    xs = (ex["x"][None, :] * (1.0 + 0.05 * rng.standard_normal((B, ex["ns"])))).astype(np.float32)
+    xs = pqp_amd.perturbed_states(ex["x"], B, seed=5)
     pb = pqp_amd.mpc_batch(ROOT / "tests" / "golden" / "example", xs)
     pb.solve(max_updates=200000)  # warm
     torch.cuda.synchronize()

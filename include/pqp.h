@@ -37,6 +37,7 @@ extern "C" {
 #define PQP_ERR_IO (-4)            /* input file missing or short                 */
 #define PQP_ERR_NOT_CONVERGED (-5) /* converge mode hit its update cap            */
 #define PQP_ERR_NO_DEVICE (-6)     /* no gfx950 device visible                    */
+#define PQP_ERR_NEEDS_QDT (-7)     /* pqp_batch_prepare: pass d_QdT (see there)   */
 
 /* Solve modes of pqp_solve_dual. */
 #define PQP_MODE_CONVERGE 0 /* while(!terminate(Y)) update  (PQP_CPU.c:718)            */
@@ -263,6 +264,14 @@ int pqp_batch_solve(int B, int N, int M, const float *d_Qd, const float *d_Fd, c
  * solver's LDS budget. */
 int pqp_batch_solve_path(int N, int M);
 
+/* Path 2's converge-mode kernel for (N, M), from the shape alone: 1 when
+ * pqp_batch_solve_prepared (given d_QinvT and 16-byte-aligned arrays) runs
+ * k_solve_pipe, which never reads d_GpT -- so a caller need not allocate it
+ * (B*N*M floats) -- and 0 when it runs k_solve_single (d_GpT, when given, makes
+ * its walks of Gp coalesced); 0 as well for the other paths.  Tuning knobs
+ * (pipe_off, pipe_force) move the answer. */
+int pqp_batch_solve_kernel(int N, int M);
+
 /* pqp_batch_solve in two steps, so that what depends only on the problems is
  * computed once per batch instead of once per call (path 2 above):
  *   pqp_batch_prepare: per-problem bit-symmetry flags of Qd into d_sym [B]
@@ -270,8 +279,8 @@ int pqp_batch_solve_path(int N, int M);
  *     *all_sym_out = 1 when every Qd is bit-symmetric and N % 4 == 0 (Qd is
  *     then its own column-major copy).  Otherwise the column-major copy goes to
  *     d_QdT [B][N][round4(N)], which must then be given: with d_QdT NULL the
- *     call returns PQP_ERR_ARG with *all_sym_out = 0 (d_sym filled) -- call
- *     again with it.  Optional d_GpT [B][M][N] and d_QinvT [B][M][M] (with
+ *     call returns PQP_ERR_NEEDS_QDT with *all_sym_out = 0 (d_sym filled) --
+ *     call again with it.  Optional d_GpT [B][M][N] and d_QinvT [B][M][M] (with
  *     d_Gp / d_Qp_inv) receive transposed copies: terminate()'s row walks of
  *     Gp and Qp_inv (PQP_CPU.c:357, :635) then read coalesced.  k_solve_pipe
  *     needs d_QinvT only (it walks Gp's rows from LDS tiles); d_GpT serves

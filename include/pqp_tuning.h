@@ -39,6 +39,7 @@ extern "C" {
  *   lean_min_n [4096]      row blocks of rows x N >= lean_min_n^2 use the lean
  *                          relay over Qd (k_lean_relay); 0 turns it off
  *   matmul_tiled_off [0]   every setup product through k_matmul_seq
+ *   matmul_pk_off [0]      setup products on the 64 x 64 k_matmul_tiled instead of the packed 128 x 128 k_matmul_pk
  *   gj_blocked_off [0]     batched Gauss_Jordan through the one-pivot-per-sweep
  *                          kernel instead of the blocked one (n <= 1024)
  *   batch_opts [0]         batched converge (k_solve_single): bit 0 no fused

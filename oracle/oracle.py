@@ -220,6 +220,21 @@ class Oracle:
         P.update(Qp=Qp, Fp=Fp, Mp=Mp, Qd=Qd, Fd=Fd, Md=Md)
         return P
 
+    def example_at_state(self, directory, x) -> dict:
+        """main()'s setup (PQP_CPU.c:988-994) with the plant state x replaced:
+        computeFp (:373), computeMp (:395), Gauss_Jordan (:251), convertToDual
+        (:489) on the example's plant."""
+        E = self.load_example(directory)
+        N, M, nd, ns = E["N"], E["M"], E["nd"], E["ns"]
+        x = f32(x)
+        Fp, Mp = np.zeros(M, np.float32), np.zeros(1, np.float32)
+        self.lib.orc_compute_fp(_p(Fp), _p(E["Fp1"]), _p(E["Fp2"]), _p(E["Fp3"]), _p(E["D"]), _p(x), M, nd, ns)
+        self.lib.orc_compute_mp(_p(Mp), *[_p(E[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "D")], _p(x),
+                                nd, ns)
+        Qd, Fd, Md = self.convert_to_dual(E["Qp_inv"], E["Gp"], E["Kp"], Fp, Mp, N, M)
+        return dict(Qd=Qd, Fd=Fd, Md=Md, Qp=self.gauss_jordan(E["Qp_inv"], M), Qp_inv=E["Qp_inv"], Fp=Fp, Mp=Mp,
+                    Gp=E["Gp"], Kp=E["Kp"], N=N, M=M)
+
     def synth_primal(self, seed, inst, N, M) -> dict:
         P = dict(Qp_inv=np.zeros(M * M, np.float32), Gp=np.zeros(N * M, np.float32),
                  Kp=np.zeros(N, np.float32), Fp=np.zeros(M, np.float32), Mp=np.zeros(1, np.float32))

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -90,14 +91,26 @@ int ensure_device() {
 
 // The stream of the drop-ins and of handles made without one: one per host
 // thread and device, so calls from different threads never share a stream
-// (or a lock); the drop-ins keep no other state between calls.
+// (or a lock); the drop-ins keep no other state between calls.  A thread's
+// streams are destroyed when the thread exits (short-lived caller
+// threads must not leak one stream each); the loading thread's stay until the
+// process ends, where the HIP runtime may already be shutting down.
+static const std::thread::id g_load_thread = std::this_thread::get_id();
+struct ThreadStreams {
+    hipStream_t s[64] = {nullptr};
+    ~ThreadStreams() {
+        if (std::this_thread::get_id() == g_load_thread) return;
+        for (hipStream_t& x : s)
+            if (x) (void)hipStreamDestroy(x);
+    }
+};
 hipStream_t lib_stream() {
-    thread_local hipStream_t streams[64] = {nullptr};
+    thread_local ThreadStreams streams;
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= 64) dev = 0;
-    if (!streams[dev]) (void)hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
-    return streams[dev];
+    if (!streams.s[dev]) (void)hipStreamCreateWithFlags(&streams.s[dev], hipStreamNonBlocking);
+    return streams.s[dev];
 }
 
 // Make `dev` the calling thread's current device for a scope (a handle's calls
@@ -1460,6 +1473,11 @@ int pqp_batch_solve_path(int N, int M) {
     return p < 0 ? set_error(PQP_ERR_ARG, "N=%d, M=%d exceeds the batched solvers' LDS budget", N, M) : p;
 }
 
+int pqp_batch_solve_kernel(int N, int M) {
+    if (N <= 0 || M <= 0) return set_error(PQP_ERR_ARG, "pqp_batch_solve_kernel: N and M must be positive");
+    return batch_path(N, M) == 2 && pipe_route(N, M, g_tune.pipe_variant) ? 1 : 0;
+}
+
 int pqp_batch_prepare(int B, int N, int M, const float* d_Qd, const float* d_Gp, const float* d_Qp_inv, float* d_QdT,
                       float* d_theta, int* d_sym, float* d_GpT, float* d_QinvT, int* all_sym_out, void* stream) {
     if (all_sym_out) *all_sym_out = 0;
@@ -1484,7 +1502,7 @@ int pqp_batch_prepare(int B, int N, int M, const float* d_Qd, const float* d_Gp,
     const float* qdt = d_Qd;
     if (!all_sym) {
         if (!d_QdT)
-            return set_error(PQP_ERR_ARG, "pqp_batch_prepare: some Qd is not bit-symmetric (or N %% 4 != 0): pass "
+            return set_error(PQP_ERR_NEEDS_QDT, "pqp_batch_prepare: some Qd is not bit-symmetric (or N %% 4 != 0): pass "
                                           "d_QdT ([B][N][round4(N)] floats) for its column-major copy");
         PQP_HIP(launch_pack_colmajor(B, d_Qd, N, (long long)N * N, d_QdT, ldq, (long long)N * ldq, s));
         qdt = d_QdT;
@@ -1591,11 +1609,12 @@ int pqp_batch_solve(int B, int N, int M, const float* d_Qd, const float* d_Fd, c
         int* ps = static_cast<int*>(sym.p);
         const int rc = pqp_batch_prepare(B, N, M, d_Qd, d_Gp, d_Qp_inv, nullptr, theta.f(), ps, GpT.f(), QinvT.f(),
                                          &all_sym, stream);
-        if (rc != PQP_OK && (all_sym || !sym.p)) return rc;
-        if (rc != PQP_OK) {  // some Qd not bit-symmetric: the column-major copy
+        if (rc != PQP_OK && rc != PQP_ERR_NEEDS_QDT) return rc;
+        if (rc == PQP_ERR_NEEDS_QDT) {  // some Qd not bit-symmetric: the column-major copy
             PQP_TRY(QdT.floats((size_t)B * N * round4(N)));
             PQP_TRY(pqp_batch_prepare(B, N, M, d_Qd, d_Gp, d_Qp_inv, QdT.f(), theta.f(), ps, GpT.f(), QinvT.f(),
                                       &all_sym, stream));
+            restore_error("");  // the first call's "pass d_QdT" text is not this call's outcome
         }
     }
     return pqp_batch_solve_prepared(B, N, M, d_Qd, QdT.f(), theta.f(), static_cast<const int*>(sym.p), GpT.f(),
@@ -1891,6 +1910,7 @@ const KnobRef* find_knob(const char* key) {
         {"mid_off", &g_tune.mid_off, nullptr, nullptr},
         {"mid_split", &g_tune.mid_split, nullptr, nullptr},
         {"pipe_off", &g_tune.pipe_off, nullptr, nullptr},
+        {"matmul_pk_off", &g_tune.matmul_pk_off, nullptr, nullptr},
         {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},
         {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},
         {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},

@@ -1033,6 +1033,8 @@ __global__ void k_zero_pad(float* __restrict__ QdT, int N, int ldq, long long qs
 }
 
 // ---------------------------------------------------------------------------
+typedef float sf4 __attribute__((ext_vector_type(4)));
+
 // Generic sequential-k product: out[a x c] = op(A)[a x b] op(B)[b x c]
 // (matrixMultiply, PQP_CPU.c:84-147).  One thread per output element; used
 // for setup and for the drop-in helpers, not on the iteration path.
@@ -1132,6 +1134,130 @@ __global__ void __launch_bounds__(256) k_matmul_tiled(float* __restrict__ out, c
         for (int q = 0; q < 4; ++q) {
             const int j = j0 + 4 * ty + q;
             if (j < c) out[(size_t)i * c + j] = acc[r][q];
+        }
+    }
+}
+
+// The setup GEMM at scale, on packed fp32: a 128 x 128 output tile per
+// 256-thread workgroup, 8 x 8 outputs per thread (rows 4tx+r and 64+4tx+r,
+// columns 4ty+q and 64+4ty+q), op(A) and op(B) staged KT8 = 32 k at a time
+// through LDS from 16-byte global loads, the next k-slab's loads issued into
+// registers before the current slab is summed.  Every output still sums
+// k = 0..b-1 in order from +0.0f with the product rounded before the add
+// (matrixMultiply, PQP_CPU.c:88-146): the compiler forms the 64 products and
+// adds of a k step as v_pk_mul_f32 / v_pk_add_f32, each half of which rounds
+// like the scalar op.  The k range is zero-padded to a multiple of KT8: a
+// padded step adds 0*0 = +0.0f to a sum that is never -0.0f (it starts at
+// +0.0f; round-to-nearest gives +0.0f on exact cancellation), so the bits are
+// those of the unpadded sum.  TA / TB: the transpose flags, so every staging
+// load is branch-free; needs the contiguous dimension of each operand a
+// multiple of 4 and 16-byte-aligned bases (launch_matmul_seq_b checks).
+// Workgroups are numbered so that consecutive tiles -- the same problem's --
+// run on one XCD (dispatch is round-robin over the 8 XCDs): each problem's
+// operands are then fetched into one XCD's L2, not all eight.
+constexpr int MM8 = 128, KT8 = 32, MM8P = MM8 + 4;
+template <int TA, int TB>
+__global__ void __launch_bounds__(256) k_matmul_pk(float* __restrict__ out, const float* __restrict__ A,
+                                                   const float* __restrict__ B, int a, int bdim, int c, long long sA,
+                                                   long long sB, long long sO, int tiles_x, int tiles_per_problem,
+                                                   int problems) {
+    __shared__ __attribute__((aligned(16))) float As[KT8][MM8P];  // op(A)(i0 + ii, k0 + kk) at [kk][ii]
+    __shared__ __attribute__((aligned(16))) float Bs[KT8][MM8P];  // op(B)(k0 + kk, j0 + jj) at [kk][jj]
+    // XCD-grouped numbering: logical tile q of the whole grid
+    const int G = tiles_per_problem * problems, L = blockIdx.x;
+    const int q = (G % 8 == 0) ? (L % 8) * (G / 8) + L / 8 : L;
+    const int z = q / tiles_per_problem, t = q % tiles_per_problem;
+    const int j0 = (t % tiles_x) * MM8, i0 = (t / tiles_x) * MM8;
+    A += z * sA;
+    B += z * sB;
+    out += z * sO;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    // staging map: 128 x 32 of each operand = 1024 float4, 4 per thread.
+    // k-contiguous operand (A with TA = 0, B with TB = 1): float4 along k,
+    // 8 lanes per 128-byte row segment; element e: row e >> 3, k group e & 7.
+    // i/j-contiguous operand: float4 along i/j; element e: k row e >> 5,
+    // column group e & 31.
+    sf4 ra[4], rb[4];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int e = tid + 256 * s;
+            if (TA == 0) {
+                const int ii = e >> 3, kk = 4 * (e & 7), i = i0 + ii, k = k0 + kk;
+                ra[s] = (i < a && k < bdim) ? *reinterpret_cast<const sf4*>(A + (size_t)i * bdim + k) : sf4{0, 0, 0, 0};
+            } else {
+                const int kk = e >> 5, ii = 4 * (e & 31), i = i0 + ii, k = k0 + kk;
+                ra[s] = (i < a && k < bdim) ? *reinterpret_cast<const sf4*>(A + (size_t)k * a + i) : sf4{0, 0, 0, 0};
+            }
+            if (TB == 1) {
+                const int jj = e >> 3, kk = 4 * (e & 7), j = j0 + jj, k = k0 + kk;
+                rb[s] = (j < c && k < bdim) ? *reinterpret_cast<const sf4*>(B + (size_t)j * bdim + k) : sf4{0, 0, 0, 0};
+            } else {
+                const int kk = e >> 5, jj = 4 * (e & 31), j = j0 + jj, k = k0 + kk;
+                rb[s] = (j < c && k < bdim) ? *reinterpret_cast<const sf4*>(B + (size_t)k * c + j) : sf4{0, 0, 0, 0};
+            }
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int e = tid + 256 * s;
+            if (TA == 0) {
+                const int ii = e >> 3, kk = 4 * (e & 7);
+#pragma unroll
+                for (int x = 0; x < 4; ++x) As[kk + x][ii] = ra[s][x];
+            } else {
+                *reinterpret_cast<sf4*>(&As[e >> 5][4 * (e & 31)]) = ra[s];
+            }
+            if (TB == 1) {
+                const int jj = e >> 3, kk = 4 * (e & 7);
+#pragma unroll
+                for (int x = 0; x < 4; ++x) Bs[kk + x][jj] = rb[s][x];
+            } else {
+                *reinterpret_cast<sf4*>(&Bs[e >> 5][4 * (e & 31)]) = rb[s];
+            }
+        }
+    };
+    float acc[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) acc[r][x] = 0.0f;
+    load(0);
+    for (int k0 = 0; k0 < bdim; k0 += KT8) {
+        __syncthreads();  // the previous slab's sums are done with LDS
+        store();
+        __syncthreads();
+        if (k0 + KT8 < bdim) load(k0 + KT8);  // in flight while this slab is summed
+#pragma unroll 4
+        for (int kk = 0; kk < KT8; ++kk) {
+            const sf4 a0 = *reinterpret_cast<const sf4*>(&As[kk][4 * tx]);
+            const sf4 a1 = *reinterpret_cast<const sf4*>(&As[kk][64 + 4 * tx]);
+            const sf4 b0 = *reinterpret_cast<const sf4*>(&Bs[kk][4 * ty]);
+            const sf4 b1 = *reinterpret_cast<const sf4*>(&Bs[kk][64 + 4 * ty]);
+            const float ar[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const float br[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int x = 0; x < 8; ++x) acc[r][x] += ar[r] * br[x];  // :88-100, k in order
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int i = i0 + (r < 4 ? 4 * tx + r : 64 + 4 * tx + r - 4);
+        if (i >= a) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = j0 + 64 * h + 4 * ty;
+            float* o = out + (size_t)i * c + j;
+            if (j + 3 < c) {
+                *reinterpret_cast<sf4*>(o) = sf4{acc[r][4 * h], acc[r][4 * h + 1], acc[r][4 * h + 2], acc[r][4 * h + 3]};
+            } else {
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+                    if (j + x < c) o[x] = acc[r][4 * h + x];
+            }
         }
     }
 }
@@ -1347,7 +1473,6 @@ __device__ __forceinline__ void single_update(const SolveArgs& A, const float* _
 // loads are 8 or 16 bytes per lane, so a wave moves 2-4x the bytes per
 // instruction and a pass needs 2-4x fewer dependent load batches.
 typedef float sf2 __attribute__((ext_vector_type(2)));
-typedef float sf4 __attribute__((ext_vector_type(4)));
 template <int V> struct SVec;
 template <> struct SVec<2> { typedef sf2 t; };
 template <> struct SVec<4> { typedef sf4 t; };
@@ -3824,6 +3949,21 @@ hipError_t launch_synth(uint32_t seed, long long inst0, int B, int N, int M, flo
 }
 
 static bool use_tiled(int a, int c) { return !g_tune.matmul_tiled_off && a >= 32 && c >= 32; }
+// the packed 128 x 128 form: large outputs whose operands load as float4
+static bool use_pk(const void* out, const float* A, int tA, const float* B, int tB, int a, int b, int c, long long sA,
+                   long long sB, long long sO) {
+    const auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const int ka = tA ? a : b, kb = tB ? b : c;  // each operand's contiguous dimension
+    return !g_tune.matmul_tiled_off && !g_tune.matmul_pk_off && a >= 64 && c >= 64 && b >= 1 && ka % 4 == 0 &&
+           kb % 4 == 0 && c % 4 == 0 && al(out) && al(A) && al(B) && sA % 4 == 0 && sB % 4 == 0 && sO % 4 == 0;
+}
+template <int TA, int TB>
+static void launch_pk(int nb, float* out, const float* A, const float* B, int a, int b, int c, long long sA,
+                      long long sB, long long sO, hipStream_t s) {
+    const int tx = cdiv(c, MM8), tpp = tx * cdiv(a, MM8);
+    hipLaunchKernelGGL((k_matmul_pk<TA, TB>), dim3(tpp * nb), dim3(256), 0, s, out, A, B, a, b, c, sA, sB, sO, tx,
+                       tpp, nb);
+}
 
 hipError_t launch_matmul_seq(float* out, const float* A, int tA, const float* B, int tB, int a, int b, int c,
                              hipStream_t s) {
@@ -3835,7 +3975,15 @@ hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const 
     if (n == 0 || B == 0) return hipSuccess;
     for (int b0 = 0; b0 < B; b0 += 65535) {  // grid y / z limit
         const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
-        if (use_tiled(a, c))
+        const long long tiles = (long long)cdiv(c, MM8) * cdiv(a, MM8);
+        if (use_pk(out, A, tA, Bm, tB, a, b, c, sA, sB, sO) && tiles * nb < (1LL << 31)) {
+            float* o = out + b0 * sO;
+            const float *pa = A + b0 * sA, *pb = Bm + b0 * sB;
+            if (!tA && !tB) launch_pk<0, 0>(nb, o, pa, pb, a, b, c, sA, sB, sO, s);
+            else if (!tA && tB) launch_pk<0, 1>(nb, o, pa, pb, a, b, c, sA, sB, sO, s);
+            else if (tA && !tB) launch_pk<1, 0>(nb, o, pa, pb, a, b, c, sA, sB, sO, s);
+            else launch_pk<1, 1>(nb, o, pa, pb, a, b, c, sA, sB, sO, s);
+        } else if (use_tiled(a, c))
             hipLaunchKernelGGL(k_matmul_tiled, dim3(cdiv(c, MMT), cdiv(a, MMT), nb), dim3(256), 0, s, out + b0 * sO,
                                A + b0 * sA, tA, Bm + b0 * sB, tB, a, b, c, sA, sB, sO);
         else
@@ -4112,6 +4260,20 @@ size_t solve_pipe_lds_bytes(int ldq, int ldm, bool big) {
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+// Path 2's converge-mode kernel by shape alone (given Qp_inv' and 16-byte
+// aligned arrays): k_solve_pipe reads Gp once per iteration but holds two
+// workgroups per CU against k_solve_single's three, so it pays only where Gp
+// is a large part of the bytes (M >= N / 3; the MPC plant over 6..32 horizon
+// steps, M = N / 4, measured faster on k_solve_single:
+// profiles/r03/pipe/horizon_pipe_vs_single.jsonl).  `variant`: the pipe build
+// (g_tune.pipe_variant read once by the caller, so the LDS size and the kernel
+// launched agree).
+bool pipe_route(int N, int M, int variant) {
+    const auto round4 = [](int n) { return (n + 3) & ~3; };
+    const bool big = variant < 1 || variant > 3;  // the default build's 128 x 96 tile
+    return !g_tune.single_scalar && !g_tune.pipe_off && (g_tune.pipe_force || 3 * M >= N) && N > 64 && N % 4 == 0 &&
+           M % 4 == 0 && solve_pipe_lds_bytes(round4(N), round4(M), big) <= kPipeLdsMax;
+}
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
     // wide loads need every row and column start 16-byte aligned: N, M
@@ -4120,26 +4282,20 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
                      aligned16(a.Gp) && aligned16(a.Qinv) && aligned16(a.Qp) && aligned16(a.GpT) &&
                      aligned16(a.QinvT) && (a.ldq & 3) == 0 && (a.ldm & 3) == 0;
     // converge mode with Qp_inv': one pass over Gp per iteration (k_solve_pipe)
-    const bool pipe_big = g_tune.pipe_variant < 1 || g_tune.pipe_variant > 3;  // the default build's 128 x 96 tile
-    // the pipe saves one of the two passes over Gp (4NM bytes per iteration)
-    // but holds two workgroups per CU against k_solve_single's three: where
-    // Gp is a small part of the bytes (M < N / 3, e.g. the MPC plant over
-    // 6..32 horizon steps, M = N / 4) k_solve_single measured faster
-    // (profiles/r03/pipe/horizon_pipe_vs_single.jsonl)
-    const bool pipe_pays = g_tune.pipe_force || 3 * a.M >= a.N;
-    if (vec && !g_tune.pipe_off && pipe_pays && a.mode == kModeConverge && a.QinvT && a.N > 64 &&
-        solve_pipe_lds_bytes(a.ldq, a.ldm, pipe_big) <= kPipeLdsMax) {
-        const size_t lds = solve_pipe_lds_bytes(a.ldq, a.ldm, pipe_big);
+    const int variant = g_tune.pipe_variant;
+    if (vec && a.mode == kModeConverge && a.QinvT && pipe_route(a.N, a.M, variant)) {
+        const bool big = variant < 1 || variant > 3;
+        const size_t plds = solve_pipe_lds_bytes(a.ldq, a.ldm, big);
         // Gp tiles in flight, update loads in flight per lane, workgroups per
         // CU: two per CU with 16 loads per lane beat three with 8 (4096
         // problems are then 8 whole rounds of 512 resident workgroups)
         // 128 x 96 tiles (every wave sums a chain) beat 64 x 64 ones by 2-3 %
         // on infeasible iterates and tie on feasible ones
-        switch (g_tune.pipe_variant) {
-        case 1: hipLaunchKernelGGL((k_solve_pipe<256, 4, 16, 2>), dim3(B), dim3(256), lds, s, a, st); break;
-        case 2: hipLaunchKernelGGL((k_solve_pipe<256, 2, 8, 1>), dim3(B), dim3(256), lds, s, a, st); break;
-        case 3: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), lds, s, a, st); break;
-        default: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), lds, s, a, st);
+        switch (big ? 0 : variant) {
+        case 1: hipLaunchKernelGGL((k_solve_pipe<256, 4, 16, 2>), dim3(B), dim3(256), plds, s, a, st); break;
+        case 2: hipLaunchKernelGGL((k_solve_pipe<256, 2, 8, 1>), dim3(B), dim3(256), plds, s, a, st); break;
+        case 3: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), plds, s, a, st); break;
+        default: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), plds, s, a, st);
         }
         g_last_batch_kernel = 1;
         return hipGetLastError();

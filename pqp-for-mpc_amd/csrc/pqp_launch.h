@@ -66,6 +66,8 @@ hipError_t launch_gauss_jordan(const float* A, float* aug, float* fac, float* re
 size_t solve_single_lds_bytes(int ldq, int ldm, bool fused = false);
 size_t solve_pipe_lds_bytes(int ldq, int ldm, bool big = false);
 constexpr size_t kPipeLdsMax = 150 * 1024;
+// path 2's converge-mode kernel by shape: true = k_solve_pipe (needs Qp_inv' only)
+bool pipe_route(int N, int M, int variant);
 extern thread_local int g_last_batch_kernel;  // 1 when the calling thread's last path-2 launch was k_solve_pipe
 size_t solve_small_lds_bytes(int N, int M);
 size_t solve_mid_lds_bytes(int N, int M, bool conv, bool split = false);
@@ -116,6 +118,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int mid_split = 0;  // 1: k_solve_mid's stored-split form where its LDS fits  // batched solves of mid-size N through k_solve_small / k_solve_single instead of k_solve_mid
     int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 1 (64 x 64 tiles, 4 in flight), 2 (64 x 64, 2 in flight, 8 loads, VGPR-bound occupancy), 3 (64 x 64, 2 in flight)
     int pipe_force = 0;  // k_solve_pipe also where M < N / 3 (where k_solve_single measured faster)
+    int matmul_pk_off = 0;  // setup GEMMs on the 64 x 64 scalar-staged k_matmul_tiled instead of the packed 128 x 128 k_matmul_pk
     int pipe_off = 0;  // batched converge of large problems on k_solve_single (two passes over Gp) instead of k_solve_pipe
     int batch_opts = 0;  // pqp_batch_solve: bit 0 no fused Y'Qd, bit 1 per-call transposes, bit 4 checkFeas over every row
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch

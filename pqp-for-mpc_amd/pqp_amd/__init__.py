@@ -32,6 +32,7 @@ LIB_PATH = Path(os.environ["PQP_LIB"]) if os.environ.get("PQP_LIB") else PKG / "
 
 PQP_OK = 0
 PQP_ERR_ARG, PQP_ERR_HIP, PQP_ERR_ALLOC, PQP_ERR_IO, PQP_ERR_NOT_CONVERGED, PQP_ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
+PQP_ERR_NEEDS_QDT = -7
 MODE_CONVERGE, MODE_FIXED = 0, 1
 
 # The reference's compile-time problem dimensions (PQP_CPU.c:13-17).
@@ -84,6 +85,7 @@ SIGNATURES = {
     "pqp_batch_solve": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [C.c_int, C.c_longlong, C.c_longlong] + [_vp] * 4
                         + [_vp]),
     "pqp_batch_solve_path": (C.c_int, [C.c_int, C.c_int]),
+    "pqp_batch_solve_kernel": (C.c_int, [C.c_int, C.c_int]),
     "pqp_batch_prepare": (C.c_int, [C.c_int] * 3 + [_vp] * 8 + [C.POINTER(C.c_int), _vp]),
     "pqp_batch_solve_prepared": (C.c_int, [C.c_int] * 3 + [_vp] * 14 + [C.c_int, C.c_longlong, C.c_longlong]
                                  + [_vp] * 4 + [_vp]),
@@ -622,27 +624,39 @@ class ProblemBatch:
         return self
 
     def invalidate(self):
-        """Drop the prepared per-problem data (call after writing Qd, Gp or
-        Qp_inv in place; set() and convert_to_dual() do it themselves)."""
+        """Drop the prepared per-problem data.  solve() also notices in-place
+        writes to Qd, Gp or Qp_inv by itself (torch's version counters), so
+        this is only needed after writes torch cannot see (e.g. from C)."""
         self._prep = None
         return self
 
+    def _source_key(self):
+        """What the prepared data were derived from: the storage and torch's
+        in-place version counter of Qd, Gp and Qp_inv (``pb.Qd[i] = ...`` or
+        ``pb.Gp.copy_(...)`` bump the counter), and the solver the shape takes."""
+        L = lib()
+        return (tuple((t.data_ptr(), t._version) for t in (self.Qd, self.Gp, self.Qp_inv)),
+                L.pqp_batch_solve_path(self.N, self.M), L.pqp_batch_solve_kernel(self.N, self.M))
+
     def prepare(self):
         """pqp_batch_prepare: what the solver derives from the problems alone
-        (symmetry flags, Theta, column-major Qd if needed, Gp' and Qp_inv'),
-        computed once and kept for every later solve()."""
+        (symmetry flags, Theta, column-major Qd if needed, Qp_inv', and Gp'
+        where k_solve_single will read it), computed once and kept for every
+        later solve() until Qd, Gp or Qp_inv change."""
         torch = self.torch
-        path = lib().pqp_batch_solve_path(self.N, self.M)
+        key = self._source_key()
+        path = key[1]
         if path < 0:
             _check(path)
-        prep = {"path": path}
+        prep = {"path": path, "key": key}
         if path == 2:
             B, N, M = self.B, self.N, self.M
             f = dict(dtype=torch.float32, device=self.device)
             prep["theta"] = torch.empty(B, N, **f)
             prep["sym"] = torch.empty(B, dtype=torch.int32, device=self.device)
             prep["QdT"] = None
-            prep["GpT"] = torch.empty(B, M * N, **f) if self.transposes else None
+            # k_solve_pipe (pqp_batch_solve_kernel 1) never reads Gp': no B*N*M copy for it
+            prep["GpT"] = torch.empty(B, M * N, **f) if self.transposes and key[2] == 0 else None
             prep["QinvT"] = torch.empty(B, M * M, **f) if self.transposes else None
             p = lambda t: self._p(t) if t is not None else None  # noqa: E731
             all_sym = C.c_int(0)
@@ -650,7 +664,7 @@ class ProblemBatch:
                                 self._p(prep["theta"]), self._p(prep["sym"]), p(prep["GpT"]), p(prep["QinvT"]),
                                 C.byref(all_sym), self._s())
             rc = lib().pqp_batch_prepare(*args(None))
-            if rc != PQP_OK and not all_sym.value and rc == PQP_ERR_ARG and "d_QdT" in last_error():
+            if rc == PQP_ERR_NEEDS_QDT:  # some Qd is not bit-symmetric: its column-major copy
                 prep["QdT"] = torch.empty(B, N * round_up(N, 4), **f)
                 rc = lib().pqp_batch_prepare(*args(self._p(prep["QdT"])))
             _check(rc)
@@ -680,8 +694,8 @@ class ProblemBatch:
                                          mode, num_iter, max_updates, self._p(self.Y), self._p(self.U),
                                          self._p(self.h), self._p(self.status), self._s()))
             return self
-        if self._prep is None or self._prep["path"] != lib().pqp_batch_solve_path(self.N, self.M):
-            self.prepare()  # first solve, new data, or a tuning knob moved the size to another solver
+        if self._prep is None or self._prep["key"] != self._source_key():
+            self.prepare()  # first solve, Qd / Gp / Qp_inv written, or a knob moved the size to another solver
         P = self._prep
         p = lambda k: self._p(P[k]) if P.get(k) is not None else None  # noqa: E731
         _check(lib().pqp_batch_solve_prepared(self.B, self.N, self.M, self._p(self.Qd), p("QdT"), p("theta"), p("sym"),
@@ -691,6 +705,16 @@ class ProblemBatch:
                                               mode, num_iter, max_updates, self._p(self.Y), self._p(self.U),
                                               self._p(self.h), self._p(self.status), self._s()))
         return self
+
+
+def perturbed_states(x, B: int, seed: int = 5, rel: float = 0.05) -> np.ndarray:
+    """B plant states around x ([B, nState] float32): x * (1 + rel * N(0, 1))
+    per entry from numpy's seeded generator -- the MPC workload of the bench's
+    mpc_batch leg (seed 5), whose every solve is pinned to the reference by
+    tests/golden/mpc_states.npz.  Numpy only; no GPU work."""
+    x = np.asarray(x, np.float32).reshape(1, -1)
+    rng = np.random.default_rng(seed)
+    return (x * (1.0 + rel * rng.standard_normal((int(B), x.shape[1])))).astype(np.float32)
 
 
 def mpc_batch(directory, states, device=None) -> ProblemBatch:

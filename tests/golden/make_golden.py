@@ -19,12 +19,16 @@ Outputs (all small):
   blocks.npz            the bundled example as k diagonal blocks (oracle.block_diag_problem,
                         k = 9, 36: n_dual 252, 1008): the reference's h (313), Y*, U*, Jp, Jd --
                         large problems that stop under the exact-float test, every iterate feasible
+  mpc_states.npz        the bench's mpc_batch population: the bundled plant at 16384
+                        perturbed states (pqp_amd.perturbed_states, seed 5), each set up
+                        (computeFp / computeMp / convertToDual) and solved by the reference:
+                        h per state and a 64-bit digest of (Y*, U*) per state
   dense_dual.npz        convertToDual with a DENSE Qp_inv (numpy-seeded,
                         pqp_amd.dense_qinv) at N=1024/M=512 and N=300/M=77: digests of
                         Qd, and Fd / Md (the general setup GEMM's parity case)
 
 Usage: python tests/golden/make_golden.py [part ...]   (parts: bundled converge
-       large testing dense blocks; default all)
+       large testing dense blocks mpc; default all)
 """
 from __future__ import annotations
 
@@ -40,7 +44,7 @@ sys.path.insert(0, str(ROOT / "oracle"))
 from oracle import Oracle, Reference, ReferenceTesting, REF_BIN, block_diag_problem, build  # noqa: E402
 
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-from pqp_amd import dense_qinv  # noqa: E402  (numpy only; the library is not loaded)
+from pqp_amd import dense_qinv, perturbed_states  # noqa: E402  (numpy only; the library is not loaded)
 
 OUT = Path(__file__).resolve().parent
 REFERENCE_DIR = Path("/root/reference")
@@ -203,10 +207,61 @@ def blocks(ref: Reference):
     np.savez(OUT / "blocks.npz", **out)
 
 
+MPC_STATES, MPC_SEED = 16384, 5
+
+
+def state_digest(Y: np.ndarray, U: np.ndarray) -> np.uint64:
+    """64 bits of SHA-256 over one solve's Y* then U* (float32 bytes)."""
+    h = hashlib.sha256(np.ascontiguousarray(Y, np.float32).tobytes() + np.ascontiguousarray(U, np.float32).tobytes())
+    return np.frombuffer(h.digest()[:8], np.uint64)[0]
+
+
+def mpc_states(ref: Reference):
+    """The bench's mpc_batch leg problem by problem on the reference: its own
+    input() (PQP_CPU.c:757-930) for the plant, then per state x_b computeFp
+    (:373), computeMp (:395), convertToDual (:489) and solveQuadraticDual
+    (:694) -- h parsed from its printf, Y* and U* from its output buffers."""
+    import time
+
+    P = ref.bundled_problem(REFERENCE_DIR)
+    N, M = P["N"], P["M"]
+    xs = perturbed_states(P["x"], MPC_STATES, seed=MPC_SEED)
+    hs = np.zeros(MPC_STATES, np.int64)
+    dig = np.zeros(MPC_STATES, np.uint64)
+    keep = {}
+    t0 = time.perf_counter()
+    for b in range(MPC_STATES):
+        Fp, Mp = np.zeros(M, np.float32), np.zeros(1, np.float32)
+        x = np.ascontiguousarray(xs[b])
+        ref.lib.computeFp(_p(Fp), _p(P["Fp1"]), _p(P["Fp2"]), _p(P["Fp3"]), _p(P["D"]), _p(x))
+        ref.lib.computeMp(_p(Mp), *[_p(P[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "D")], _p(x))
+        Qd, Fd, Md = ref.convert_to_dual(P["Qp_inv"], P["Gp"], P["Kp"], Fp, Mp, N, M)
+        Q = dict(P, Fp=Fp, Mp=Mp, Qd=Qd, Fd=Fd, Md=Md)
+        h, Y, U = ref.solve(Q)
+        hs[b], dig[b] = h, state_digest(Y, U)
+        if h != 313 or b < 4:
+            keep[b] = (Y, U)
+    order = sorted(keep)
+    np.savez_compressed(OUT / "mpc_states.npz", h=hs.astype(np.int16), digest=dig,
+                        xs_sha256=np.frombuffer(bytes.fromhex(digest(xs)), np.uint8),
+                        kept=np.asarray(order, np.int64), kept_Y=np.stack([keep[b][0] for b in order]),
+                        kept_U=np.stack([keep[b][1] for b in order]))
+    u, c = np.unique(hs, return_counts=True)
+    print(f"mpc states: {MPC_STATES} solves in {time.perf_counter() - t0:.1f} s; h counts",
+          dict(zip(u.tolist(), c.tolist())))
+
+
+def _p(a):
+    import ctypes as C
+
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
 def main(parts=None):
     build()
     ref, orc = Reference(), Oracle()
-    parts = set(parts or ("bundled", "converge", "large", "testing", "dense", "blocks"))
+    parts = set(parts or ("bundled", "converge", "large", "testing", "dense", "blocks", "mpc"))
     if "bundled" in parts:
         bundled(ref)
     if "converge" in parts:
@@ -219,6 +274,8 @@ def main(parts=None):
         dense_dual(ref, orc)
     if "blocks" in parts:
         blocks(ref)
+    if "mpc" in parts:
+        mpc_states(ref)
 
 
 if __name__ == "__main__":

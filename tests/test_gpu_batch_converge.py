@@ -137,3 +137,73 @@ def test_prepared_data_follow_new_qd(gpu_lib, orc):
     for b, P in enumerate(other):
         h, Y, U = orc.solve(P, max_updates=cap)
         _check(pb, b, h, Y, U, f"reloaded {b}")
+
+
+@pytest.mark.parametrize("how", ["index", "copy_"])
+def test_prepared_data_follow_in_place_writes(gpu_lib, orc, how):
+    """Qd, Gp and Qp_inv written IN PLACE (no set(), no
+    invalidate()) after a prepared solve: solve() sees torch's version counter
+    move and prepares again, so the second solve has the new problems' bits
+    (a stale symmetry flag or Qp_inv' would give silently wrong ones)."""
+    from pqp_amd import dense_qinv
+
+    N, M, cap = 256, 128, 5
+    pb = gpu_lib.ProblemBatch.synthetic(14, 0, 2, N, M)
+    pb.solve(max_updates=cap)
+    # problem 1 becomes a dense-Qp_inv problem: its Qd is not bit-symmetric
+    P = orc.synth_primal(14, 9, N, M)
+    P["Qp_inv"] = dense_qinv(14, M)
+    P["Qd"], P["Fd"], P["Md"] = orc.convert_to_dual(P["Qp_inv"], P["Gp"], P["Kp"], P["Fp"], P["Mp"], N, M)
+    P["Qp"] = orc.gauss_jordan(P["Qp_inv"], M)
+    T = lambda a: pb.torch.as_tensor(np.asarray(a, np.float32).reshape(-1), device=pb.device)  # noqa: E731
+    for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
+        t = getattr(pb, k)
+        if how == "index":
+            t[1] = T(P[k]) if t.dim() == 2 else T(P[k])[0]
+        else:
+            t[1:2].copy_(T(P[k]).reshape(t[1:2].shape))
+    pb.solve(max_updates=cap)
+    assert pb._prep["QdT"] is not None and not pb._prep["all_sym"]
+    h, Y, U = orc.solve(P, max_updates=cap)
+    _check(pb, 1, h, Y, U, f"in-place ({how}) problem 1")
+    P0 = orc.synth_problem(14, 0, N, M)
+    h, Y, U = orc.solve(P0, max_updates=cap)
+    _check(pb, 0, h, Y, U, "untouched problem 0")
+
+
+def test_prepare_needs_qdt_status_and_gpt_only_for_single(gpu_lib):
+    """pqp_batch_prepare asks for the column-major copy with its own
+    status (PQP_ERR_NEEDS_QDT), the retried pqp_batch_solve leaves no error
+    text behind, and Gp' (B*N*M floats) is allocated only where path 2 runs
+    k_solve_single (pqp_batch_solve_kernel 0), never for k_solve_pipe."""
+    import ctypes as C
+
+    import pqp_amd
+    from pqp_amd import dense_qinv
+
+    L = gpu_lib.lib()
+    N, M = 256, 128
+    assert L.pqp_batch_solve_kernel(N, M) == 1 and L.pqp_batch_solve_kernel(256, 64) == 0
+    pb = gpu_lib.ProblemBatch.synthetic(15, 0, 2, N, M)
+    pb.Qp_inv[1] = pb.torch.as_tensor(dense_qinv(15, M), device=pb.device)
+    pb.convert_to_dual()
+    f = dict(dtype=pb.torch.float32, device=pb.device)
+    theta, sym = pb.torch.empty(2, N, **f), pb.torch.empty(2, dtype=pb.torch.int32, device=pb.device)
+    all_sym = C.c_int(7)
+    rc = L.pqp_batch_prepare(2, N, M, pb._p(pb.Qd), pb._p(pb.Gp), pb._p(pb.Qp_inv), None, pb._p(theta), pb._p(sym),
+                             None, None, C.byref(all_sym), pb._s())
+    assert rc == pqp_amd.PQP_ERR_NEEDS_QDT and all_sym.value == 0
+    assert sym.cpu().tolist()[0] != 0 and sym.cpu().tolist()[1] == 0
+    rc = L.pqp_batch_solve(2, N, M, *[pb._p(getattr(pb, k)) for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp",
+                                                                       "Gp", "Kp")],
+                           0, 1000, 3, pb._p(pb.Y), pb._p(pb.U), pb._p(pb.h), pb._p(pb.status), pb._s())
+    assert rc == pqp_amd.PQP_OK and pqp_amd.last_error() == ""
+    pb.solve(max_updates=3)
+    assert pb._prep["GpT"] is None and pb._prep["QinvT"] is not None  # the pipe: no Gp'
+    prev = pqp_amd.tune("pipe_off", 1)
+    try:
+        assert L.pqp_batch_solve_kernel(N, M) == 0
+        pb.solve(max_updates=3)  # the route moved: prepared again, now with Gp'
+        assert pb._prep["GpT"] is not None
+    finally:
+        pqp_amd.tune("pipe_off", prev)

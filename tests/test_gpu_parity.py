@@ -405,19 +405,7 @@ def test_batched_setup_from_primal(gpu_lib, golden_bundled):
 
 def _oracle_example_at_state(orc, x):
     """main()'s setup (PQP_CPU.c:988-994) with the state x replaced."""
-    import ctypes as C
-
-    from oracle import _p, f32
-
-    E = orc.load_example(EXAMPLE_DIR)
-    N, M, nd, ns = E["N"], E["M"], E["nd"], E["ns"]
-    x = f32(x)
-    Fp, Mp = np.zeros(M, np.float32), np.zeros(1, np.float32)
-    orc.lib.orc_compute_fp(_p(Fp), _p(E["Fp1"]), _p(E["Fp2"]), _p(E["Fp3"]), _p(E["D"]), _p(x), M, nd, ns)
-    orc.lib.orc_compute_mp(_p(Mp), *[_p(E[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "D")], _p(x), nd, ns)
-    Qd, Fd, Md = orc.convert_to_dual(E["Qp_inv"], E["Gp"], E["Kp"], Fp, Mp, N, M)
-    return dict(Qd=Qd, Fd=Fd, Md=Md, Qp=orc.gauss_jordan(E["Qp_inv"], M), Qp_inv=E["Qp_inv"], Fp=Fp, Mp=Mp,
-                Gp=E["Gp"], Kp=E["Kp"], N=N, M=M)
+    return orc.example_at_state(EXAMPLE_DIR, x)
 
 
 def test_mpc_batch_of_states_vs_oracle(gpu_lib, orc):
@@ -437,6 +425,37 @@ def test_mpc_batch_of_states_vs_oracle(gpu_lib, orc):
         hr, Yr, _ = orc.solve(P, max_updates=CAP)
         assert st[b] == (1 if hr > 0 else 2) and h[b] == abs(hr), (b, h[b], hr)
         assert_bitwise(Y[b], Yr, f"Y {b}")
+
+
+def test_mpc_population_vs_reference(gpu_lib):
+    """the bench's whole mpc_batch population -- the bundled plant
+    at 16384 perturbed states (pqp_amd.perturbed_states, seed 5) -- solved on
+    the GPU (setup and converge mode on device, as the bench leg runs it)
+    against the REFERENCE's own solve of every state (tests/golden/
+    mpc_states.npz, made by make_golden.py from oracle/_ref): every h
+    (16381 x 313 and 3 x 314) and a digest of every (Y*, U*)
+    (PQP_CPU.c:694-750; the stop test at :718, :683-684)."""
+    import hashlib
+
+    G = np.load(GOLDEN / "mpc_states.npz")
+    E = gpu_lib.read_example(EXAMPLE_DIR)
+    xs = gpu_lib.perturbed_states(E["x"], len(G["h"]), seed=5)
+    assert hashlib.sha256(xs.tobytes()).digest() == G["xs_sha256"].tobytes(), "the state generator moved"
+    pb = gpu_lib.mpc_batch(EXAMPLE_DIR, xs)
+    pb.solve(max_updates=CAP)
+    h, st = pb.h.cpu().numpy(), pb.status.cpu().numpy()
+    Y, U = pb.Y.cpu().numpy(), pb.U.cpu().numpy()
+    for j, b in enumerate(G["kept"]):  # readable first failures: the h = 314 states and a few more, in full
+        assert h[b] == G["h"][b], (b, h[b], G["h"][b])
+        assert_bitwise(Y[b], G["kept_Y"][j], f"Y* of state {b}")
+        assert_bitwise(U[b], G["kept_U"][j], f"U* of state {b}")
+    bad_h = np.nonzero(h != G["h"].astype(np.int64))[0]
+    assert bad_h.size == 0, f"{bad_h.size} states stop at another h than the reference; first {bad_h[:8]}"
+    assert (st == 1).all()
+    dig = np.array([np.frombuffer(hashlib.sha256(Y[b].tobytes() + U[b].tobytes()).digest()[:8], np.uint64)[0]
+                    for b in range(len(h))], np.uint64)
+    bad = np.nonzero(dig != G["digest"])[0]
+    assert bad.size == 0, f"{bad.size} of {len(h)} states differ from the reference in Y* or U*; first {bad[:8]}"
 
 
 def test_batched_synthetic_converge_groups(gpu_lib, golden_converge, orc):

@@ -111,6 +111,24 @@ def test_pipe_bench_size_vs_oracle(gpu_lib, orc):
     _check(pb, 0, h, Y, U, "pipe n_dual 1024 feasible")
 
 
+def test_pipe_bench_size_infeasible_vs_oracle(gpu_lib, orc):
+    """the batch_converge leg's timed case -- n_dual 1024, M 512,
+    the generator's problems, whose every iterate fails checkFeas (terminate()
+    returns at PQP_CPU.c:677 with no computeCost) -- through k_solve_pipe,
+    two problems of the bench's own batch (seed 1, problems 0 and 1) against
+    the oracle, capped at 3 updates."""
+    N, M, cap = 1024, 512, 3
+    pb, kernel = _solve(gpu_lib, N, M, 2, cap, False, seed=1, inst0=0)
+    assert kernel == 1
+    for b in range(2):
+        P = orc.synth_problem(1, b, N, M)
+        assert not orc.feasible(orc.u_from_y(np.full(N, 1000.0, np.float32), P["Fp"], P["Gp"], P["Qp_inv"], N, M),
+                                P["Gp"], P["Kp"], N, M), "want the infeasible case"
+        h, Y, U = orc.solve(P, max_updates=cap)
+        assert h == -(cap + 1) or h == cap + 1, h
+        _check(pb, b, h, Y, U, f"pipe n_dual 1024 infeasible b={b}")
+
+
 @pytest.mark.parametrize("chunk", [0, 1, 2])
 def test_pipe_testfile_stops_like_reference(gpu_lib, orc, tmp_path, chunk):
     """testing/ test2 (n_dual 400, M 100) converges at the reference's h = 3:

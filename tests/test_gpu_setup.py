@@ -75,3 +75,33 @@ def test_tiled_matmul_vs_oracle_and_seq(gpu_lib, orc, a, b, c):
             finally:
                 L.pqp_tune_matmul_tiled(prev)
             assert_bitwise(out, seq, f"tiled vs seq {a}x{b}x{c} t{tA}{tB}")
+
+
+@pytest.mark.parametrize("a,b,c", [(64, 4, 64), (128, 32, 128), (132, 100, 260), (260, 36, 68), (200, 516, 72),
+                                   (1024, 512, 128)])
+def test_packed_matmul_vs_oracle_and_tiled(gpu_lib, orc, a, b, c):
+    """k_matmul_pk (128 x 128 tiles, 8 x 8 outputs per thread on packed fp32,
+    the k range zero-padded to the 32-deep slab) in all four transpose modes:
+    bit-identical to the oracle and to the 64 x 64 k_matmul_tiled
+    (pqp_tune("matmul_pk_off", 1)); ragged tiles in i, j and k, exact +-0,
+    and inf / NaN operands (matrixMultiply, PQP_CPU.c:84-147)."""
+    import pqp_amd
+
+    rng = np.random.default_rng(a * 7 + b * 3 + c)
+    for tA in (0, 1):
+        for tB in (0, 1):
+            A = rng.standard_normal(a * b).astype(np.float32)
+            Bm = rng.standard_normal(b * c).astype(np.float32)
+            A[::7] = 0.0
+            Bm[::11] = -0.0
+            A[5], Bm[9] = np.inf, np.nan
+            out = np.zeros(a * c, np.float32)
+            gpu_lib.matrixMultiply(out, A, tA, Bm, tB, a, b, c)
+            assert_bitwise(out, orc.matmul(A, tA, Bm, tB, a, b, c), f"pk {a}x{b}x{c} t{tA}{tB}")
+            prev = pqp_amd.tune("matmul_pk_off", 1)
+            try:
+                ref = np.zeros(a * c, np.float32)
+                gpu_lib.matrixMultiply(ref, A, tA, Bm, tB, a, b, c)
+            finally:
+                pqp_amd.tune("matmul_pk_off", prev)
+            assert_bitwise(out, ref, f"pk vs tiled {a}x{b}x{c} t{tA}{tB}")

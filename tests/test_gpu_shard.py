@@ -111,3 +111,70 @@ def test_rccl_scatter_gather_one_rank(gpu_lib, orc, tmp_path):
     for j in range(B):
         P = orc.synth_problem(11, j, 300, 150, with_qp=False)
         assert_bitwise(full[j], orc.iterate(P["Qd"], P["Fd"], 300, 4), f"problem {j}")
+
+
+CFG4_N, CFG4_PER_RANK, CFG4_WORLD, CFG4_SEED, CFG4_UPDATES = 1024, 4096, 8, 1, 10
+
+
+def _configs4_rank_main(rank, world, port, out):
+    """One rank of configs[4]'s layout: the bench's shard plan (8 ranks x
+    4096 problems of n_dual 1024, seed 1) scattered from rank 0; the rank runs
+    the first two and the last problem of ITS shard (inst0 = r * 4096) through
+    the fused kernel for one bench launch (10 updates); rank 0 gathers."""
+    import sys
+
+    for p in (ROOT / "pqp-for-mpc_amd", ROOT / "oracle"):
+        sys.path.insert(0, str(p))
+    import torch
+    import torch.distributed as dist
+
+    import pqp_amd
+    from pqp_amd.shard import gather_rows, scatter_plan
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    seed, inst0, count = scatter_plan(dist, rank, world, CFG4_PER_RANK, CFG4_SEED, dev)
+    assert (seed, inst0, count) == (CFG4_SEED, rank * CFG4_PER_RANK, CFG4_PER_RANK)
+    N = CFG4_N
+    ys = []
+    for first, n in ((inst0, 2), (inst0 + count - 1, 1)):
+        b = pqp_amd.Batch(n, N, device=dev).generate(seed, inst0=first, M=N // 2)
+        b.iterate(CFG4_UPDATES)
+        ys.append(b.Y[:, :N].clone())
+    torch.cuda.synchronize(dev)
+    full = gather_rows(dist, rank, world, torch.cat(ys, 0).contiguous())
+    if rank == 0:
+        np.save(out, full.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_configs4_shards_pinned_to_oracle(gpu_lib, orc, tmp_path):
+    """configs[4]'s own problem ids on 8 ranks (gloo, all on this
+    box's one GPU): the shard plan gives rank r problems [r * 4096, (r+1) *
+    4096); each rank's first two and last problem are iterated on the GPU and
+    gathered on rank 0 in rank order.  Every shard's first problem (and the
+    job's last, 32767) bit-exact against the oracle's updates
+    (PQP_CPU.c:603-618, the testing/ loop of PQP_GPU_optimized.cu:799); all 24
+    equal a one-process batch of the same ids."""
+    import torch
+    import torch.multiprocessing as mp
+
+    out = str(tmp_path / "y.npy")
+    mp.spawn(_configs4_rank_main, args=(CFG4_WORLD, _free_port(), out), nprocs=CFG4_WORLD, join=True)
+    got = np.load(out)
+    N = CFG4_N
+    assert got.shape == (CFG4_WORLD * 3, N)
+    ids = [i for r in range(CFG4_WORLD) for i in (r * CFG4_PER_RANK, r * CFG4_PER_RANK + 1,
+                                                   (r + 1) * CFG4_PER_RANK - 1)]
+    for row, inst in enumerate(ids):
+        b = gpu_lib.Batch(1, N, device="cuda:0").generate(CFG4_SEED, inst0=inst, M=N // 2)
+        b.iterate(CFG4_UPDATES)
+        assert_bitwise(got[row], b.result()[0], f"gathered problem {inst}")
+    torch.cuda.empty_cache()
+    for row, inst in enumerate(ids):
+        if inst % CFG4_PER_RANK == 0 or inst == CFG4_WORLD * CFG4_PER_RANK - 1:
+            P = orc.synth_problem(CFG4_SEED, inst, N, N // 2, with_qp=False)
+            assert_bitwise(got[row], orc.iterate(P["Qd"], P["Fd"], N, CFG4_UPDATES), f"problem {inst} vs oracle")

@@ -240,3 +240,28 @@ def test_block_problems_match_reference_golden(orc, golden_bundled, k):
     flag, _, Jp, Jd = orc.terminate(Y, Q["Qd"], Q["Fd"], Q["Md"], Q["Qp"], Q["Qp_inv"], Q["Fp"], Q["Mp"], Q["Gp"],
                                     Q["Kp"], Q["N"], Q["M"])
     assert flag == 1 and np.float32(Jp) == g[f"Jp{k}"] and np.float32(Jd) == g[f"Jd{k}"]
+
+
+def test_mpc_population_sample_matches_reference_golden(orc):
+    """The restatement pinned on the bench's mpc_batch population
+    (tests/golden/mpc_states.npz, made by the reference itself): the states
+    kept in full (every h = 314 one among them) and every 64th state give the
+    reference's h and the same (Y*, U*) digest."""
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+    from pqp_amd import perturbed_states
+
+    G = np.load(GOLDEN / "mpc_states.npz")
+    E = orc.load_example(EXAMPLE_DIR)
+    xs = perturbed_states(E["x"], len(G["h"]), seed=5)
+    assert hashlib.sha256(xs.tobytes()).digest() == G["xs_sha256"].tobytes()
+    assert sorted(set(G["h"].tolist())) == [313, 314] and int((G["h"] == 314).sum()) == 3
+    for b in sorted(set(G["kept"].tolist()) | set(range(0, len(xs), 64))):
+        P = orc.example_at_state(EXAMPLE_DIR, xs[b])
+        h, Y, U = orc.solve(P)
+        assert h == G["h"][b], (b, h, G["h"][b])
+        d = np.frombuffer(hashlib.sha256(Y.tobytes() + U.tobytes()).digest()[:8], np.uint64)[0]
+        assert d == G["digest"][b], f"state {b}: (Y*, U*) differ from the reference"
