@@ -318,23 +318,27 @@ def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
 
 
 def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
-    """The bundled plant over H horizon blocks (oracle.block_diag_problem:
-    n_dual 28 H, M 7 H; every iterate feasible, the reference stops at h =
-    313), B copies solved at once (ProblemBatch; k_solve_mid, one workgroup per
-    problem, each matrix once in LDS), and beside it the reference's own
-    solveQuadraticDual on one copy, one host thread (oracle/_ref, median of
-    3).  Timed: the batched solve only."""
+    """MPC over H horizon stages: B problems of the bundled plant stacked H
+    times (pqp_amd.horizon_batch -- block-diagonal primal, each stage at its
+    own perturbed state (seed 7), per-stage computeFp / computeMp, Gauss_Jordan
+    and convertToDual on the GPU; n_dual 28 H, M 7 H), solved at once in
+    converge mode (path 3: k_solve_mid2, one workgroup per problem, every
+    matrix once in LDS, terminate() beside the update).  Beside it the
+    reference's own solveQuadraticDual on problem 0 (copied back from the GPU
+    batch), one host thread (oracle/_ref, median of 3).  Timed: the batched
+    solve only."""
     import torch
 
     sys.path.insert(0, str(ROOT / "oracle"))
-    from oracle import REF_SO, Oracle, Reference, block_diag_problem
+    from oracle import REF_SO, Reference
 
-    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    ex = ROOT / "tests" / "golden" / "example"
+    E = pqp_amd.read_example(ex)
     ref = Reference() if REF_SO.exists() else None
     out = {}
     for H in Hs:
-        P = block_diag_problem(base, H)
-        pb = pqp_amd.ProblemBatch.replicate(P, B)
+        xs = pqp_amd.perturbed_states(E["x"], B * H, seed=7).reshape(B, H, -1)
+        pb = pqp_amd.horizon_batch(ex, H, xs)
         pb.solve(max_updates=200000)  # warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -342,19 +346,23 @@ def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         h = pb.h.cpu().numpy()
-        row = {"n_dual": int(P["N"]), "m": int(P["M"]), "problems": B,
-               "path": int(pqp_amd.lib().pqp_batch_solve_path(P["N"], P["M"])), "converge_ms": dt * 1e3,
-               "qp_solves_per_s": B / dt, "iterations_per_s": float(h.sum()) / dt,
-               "all_h_313": bool((h == 313).all())}
+        N, M = pb.N, pb.M
+        row = {"n_dual": N, "m": M, "problems": B, "path": int(pqp_amd.lib().pqp_batch_solve_path(N, M)),
+               "kernel": {3: "k_solve_mid2", 2: "k_solve_mid"}.get(pqp_amd.tune_get("last_batch_kernel"), "other"),
+               "converge_ms": dt * 1e3, "qp_solves_per_s": B / dt, "iterations_per_s": float(h.sum()) / dt,
+               "h_min": int(h.min()), "h_max": int(h.max()), "h_mean": float(h.mean()),
+               "converged_frac": float((pb.status.cpu().numpy() == 1).mean())}
         if ref is not None:
+            P0 = pb.problem(0)
             ts = []
             for _ in range(3):
                 tb = time.perf_counter()
-                hr, _, _ = ref.solve(P)
+                hr, _, _ = ref.solve(P0)
                 ts.append(time.perf_counter() - tb)
             tr = sorted(ts)[1]
-            row["ref_cpu"] = {"h": hr, "ms": tr * 1e3, "qp_solves_per_s": 1.0 / tr, "cores": 1,
-                              "what": "PQP_CPU.c solveQuadraticDual (oracle/_ref), one copy, 1 thread, median of 3"}
+            row["ref_cpu"] = {"h": hr, "same_h_as_gpu": bool(hr == int(h[0])), "ms": tr * 1e3,
+                              "qp_solves_per_s": 1.0 / tr, "cores": 1,
+                              "what": "PQP_CPU.c solveQuadraticDual (oracle/_ref) on problem 0, 1 thread, median of 3"}
         out[f"H{H}"] = row
         del pb
         torch.cuda.empty_cache()

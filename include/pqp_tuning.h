@@ -23,17 +23,10 @@ extern "C" {
  *                          k_solve_small instead of k_solve_tiny / k_solve_wave
  *   force_single [0]       fixed mode of large single problems on one
  *                          workgroup (k_solve_single)
- *   fixed_tiny_old [0]     fixed mode of N <= 32 on k_solve_tiny instead of the
- *                          one-wave k_fixed_tiny
  *   fixed_rl_max_b [1024]  largest batch whose k_fixed_tiny keeps y in registers
  *   wave_min_b [1]         converge mode of N, M <= 32 on k_solve_wave from this
  *                          many problems on
  *   wave_pipe_max_b [4096] largest batch of the software-pipelined k_solve_wave
- *   split_u [0]            k_split_update load stage depth (0: 16, 1: 8, 2: 24)
- *   split_kind [0]         kernel behind pqp_rowblock_update and large
- *                          fixed-mode solves (0: k_split_relay 8 waves x 16-packet
- *                          segments, 1: streaming k_split_update, 2: relay 4 x 64,
- *                          3: 8 x 32, 4: 16 x 16, 5: 8 x 16)
  *   split_lw [0]           row sides per workgroup of blocks built afterwards
  *                          (0: auto; 8, 16, 32 or 64)
  *   lean_min_n [4096]      row blocks of rows x N >= lean_min_n^2 use the lean
@@ -57,20 +50,17 @@ extern "C" {
  *   pipe_variant [0]       k_solve_pipe build: 0 one 128 x 96 Gp tile per
  *                          step (every wave sums a chain) and 16 update loads
  *                          per lane in flight, two workgroups per CU; 3 two
- *                          64 x 64 tiles in flight; 1 four; 2 two, 8 loads,
- *                          occupancy set by the register count
+ *                          64 x 64 tiles in flight
  *   mid_off [0]            batched solves of mid-size problems through
  *                          k_solve_small / k_solve_single instead of the
  *                          LDS-resident k_solve_mid (path 3)
- *   mid_split [0]          1: k_solve_mid holds the stored split matrices
- *                          (Qdp_theta, Qdn_theta) instead of Qd where they fit
+ *   mid_v1 [0]             1: path 3 on k_solve_mid (terminate() after each
+ *                          update) instead of k_solve_mid2 (terminate(Y_h)
+ *                          on other waves beside the update to Y_{h+1})
  *   batch_chunk [0]        iterates per problem per batched-solve launch
  *                          (0: sized from N and M)
  *   single_scalar [0]      k_solve_single with 4-byte loads only
- *   single_occ4 [0]        k_solve_single built for 4 workgroups per CU
  *   wide_min_n [384]       converge mode: smallest N solved over many workgroups
- *   wide_flags [0]         converge graph chain: bit 0 the update on a forked
- *                          graph branch, bit 1 gemv segments of 64
  *   converge_chunk [65536] iterates decided per persistent converge launch
  *                          (<= 0 restores the default)
  *  Paths and failure tests:
@@ -94,8 +84,9 @@ int pqp_tune(const char *key, long long value, long long *old_value);
  *   last_path          solver path of the calling thread's last single-problem
  *                      solve (1 persistent fixed, 2 relay fixed, 3 persistent
  *                      converge, 4 converge graph chain, 5 one workgroup)
- *   last_batch_kernel  1 when the calling thread's last path-2 batched
- *                      launch ran k_solve_pipe, 0 for k_solve_single
+ *   last_batch_kernel  the calling thread's last path-2 / path-3 batched
+ *                      launch: 0 k_solve_single, 1 k_solve_pipe, 2 k_solve_mid,
+ *                      3 k_solve_mid2
  *   persist_fallbacks  persistent launches that fell back (process total)
  *   converge_grid      in: *value = N << 32 | M; out: workgroups of the
  *                      persistent converge launch for (N, M) (0: not used) */

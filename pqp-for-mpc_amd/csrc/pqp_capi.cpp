@@ -288,8 +288,6 @@ struct pqp_problem {
     hipGraphExec_t wgraph = nullptr;                 // captured chunk of converge iterations
     hipGraphExec_t wgraph_first = nullptr;           // the short first chunk
     hipGraphExec_t wgraph4 = nullptr, wgraph8 = nullptr;  // the chunks that escalate to kWideChunk
-    hipStream_t side = nullptr;                      // capture-time fork for the speculative update
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     long long wgraph_key = -1;
     long long graph_variant = -1;                    // the settings the fixed-mode graphs were captured with
     pqp::DevBuf Y, U, state;
@@ -306,9 +304,6 @@ struct pqp_problem {
         if (wgraph_first) (void)hipGraphExecDestroy(wgraph_first);
         if (wgraph4) (void)hipGraphExecDestroy(wgraph4);
         if (wgraph8) (void)hipGraphExecDestroy(wgraph8);
-        if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
-        if (side) (void)hipStreamDestroy(side);
         if (hst) (void)hipHostFree(hst);
         if (hio) (void)hipHostFree(hio);
         if (hin) (void)hipHostFree(hin);
@@ -633,8 +628,8 @@ int problem_run_fixed_split(pqp_problem& P, long long num_iter, SolveOut& out, h
     PQP_TRY(ensure_split(P, lw, s));
     // every setting the captured launches bake in as an argument, the relay
     // wait budget's value included
-    const long long variant = (long long)g_tune.split_u | ((long long)g_tune.split_kind << 4) | ((long long)lw << 8) |
-                              ((long long)use_lean(N, N) << 16) | ((long long)(unsigned)g_tune.relay_spin_max << 24);
+    const long long variant = ((long long)lw << 8) | ((long long)use_lean(N, N) << 16) |
+                              ((long long)(unsigned)g_tune.relay_spin_max << 24);
     if (P.graph_variant != variant) {  // kernel selection changed: recapture both
         P.graph_updates = -1;
         P.chunk_ready = false;
@@ -791,35 +786,19 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     long long* cap = static_cast<long long*>(P.wcap.p);
     // every launch argument the capture bakes in (cap: a device word)
     const long long key = (long long)(((unsigned long long)(unsigned)g_tune.relay_spin_max << 32) |
-                                      ((unsigned long long)use_lean(N, N) << 24) |
-                                      ((unsigned long long)(g_tune.wide_flags & 0xff) << 16) |
-                                      ((unsigned long long)(g_tune.split_kind & 0xff) << 8) | (unsigned long long)(lw & 0xff));
+                                      ((unsigned long long)use_lean(N, N) << 24) | (unsigned long long)(lw & 0xff));
     int* rerr = static_cast<int*>(P.rerr.p);
     if (!P.wgraph || P.wgraph_key != key) {
         if (P.wgraph) {
             (void)hipGraphExecDestroy(P.wgraph);
             P.wgraph = nullptr;
         }
-        if (!P.side) {
-            PQP_HIP(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
-            PQP_HIP(hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming));
-            PQP_HIP(hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming));
-        }
-        // One iteration.  The update depends only on the current iterate, so
-        // it may also run speculatively on a forked branch beside terminate()
-        // (tuning bit; measured slower as a graph branch): if the iteration
-        // stops or hits the cap, its result in `nxt` is not used, and the next
-        // iteration's launches, gated on the status, do nothing.
-        const bool fork = (g_tune.wide_flags & 1) != 0;
+        // One iteration: terminate()'s launches, then the update, each gated on
+        // the status word (once an iteration stops or hits the cap, the rest do
+        // nothing).  The update on a forked graph branch beside terminate()
+        // measured slower and was removed in round 4.
         auto iteration = [&](const float* cur, float* nxt) -> hipError_t {
             hipError_t e = hipSuccess;
-            if (fork) {
-                e = hipEventRecord(P.ev_fork, s);
-                if (e == hipSuccess) e = hipStreamWaitEvent(P.side, P.ev_fork, 0);
-                if (e == hipSuccess) e = problem_update(P, lw, cur, nxt, P.side, &dst->status);
-                if (e == hipSuccess) e = hipEventRecord(P.ev_join, P.side);
-                if (e != hipSuccess) return e;
-            }
             GemvJobs j1{};  // tmp = Gp'Y + Fp (computeUfromY :354-356) and Y'Qd (computeCost :652, Jd)
             j1.job[0] = GemvJob{P.Gp.f(), cur, P.tM.f(), P.Fp.f(), M, N, M, kEpiAdd};
             j1.job[1] = GemvJob{P.Qd.f(), cur, P.tq.f(), nullptr, N, N, N, kEpiPlain};
@@ -841,7 +820,6 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
             const WideArgs w{dst, flag, P.tq.f(), P.tu.f(), cur, P.U.f(), P.Fd.f(), P.Fp.f(), P.Md.f(), P.Mp.f(),
                              N, M, cap};
             if ((e = launch_wide_decide(w, s)) != hipSuccess) return e;
-            if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join the update branch
             return problem_update(P, lw, cur, nxt, s, &dst->status);
         };
         // replays of 2, 2, 4, 8, then kWideChunk iterations: a solve that stops
@@ -1887,29 +1865,24 @@ const KnobRef* find_knob(const char* key) {
     static const KnobRef knobs[] = {
         {"relay_spin_max", &g_tune.relay_spin_max, nullptr, nullptr},
         {"lean_min_n", &g_tune.lean_min_n, nullptr, nullptr},
-        {"split_u", &g_tune.split_u, nullptr, nullptr},
         {"split_lw", &g_tune.split_lw, nullptr, nullptr},
-        {"split_kind", &g_tune.split_kind, nullptr, nullptr},
         {"wave_pipe_max_b", &g_tune.wave_pipe_max_b, nullptr, nullptr},
-        {"fixed_tiny_old", &g_tune.fixed_tiny_old, nullptr, nullptr},
         {"fixed_rl_max_b", &g_tune.fixed_rl_max_b, nullptr, nullptr},
         {"wave_min_b", &g_tune.wave_min_b, nullptr, nullptr},
         {"matmul_tiled_off", &g_tune.matmul_tiled_off, nullptr, nullptr},
         {"gj_blocked_off", &g_tune.gj_blocked_off, nullptr, nullptr},
         {"single_scalar", &g_tune.single_scalar, nullptr, nullptr},
-        {"single_occ4", &g_tune.single_occ4, nullptr, nullptr},
         {"persist_off", &g_tune.persist_off, nullptr, nullptr},
         {"persist_stall_wg", &g_tune.persist_stall_wg, nullptr, nullptr},
         {"persist_fit_cus", &g_tune.persist_fit_cus, nullptr, nullptr},
-        {"wide_flags", &g_tune.wide_flags, nullptr, nullptr},
         {"converge_persist_off", &g_tune.converge_persist_off, nullptr, nullptr},
         {"force_small", nullptr, &g_tune.force_small, nullptr},
         {"force_single", nullptr, &g_tune.force_single, nullptr},
         {"wide_min_n", &g_tune.wide_min_n, nullptr, nullptr},
         {"batch_opts", &g_tune.batch_opts, nullptr, nullptr},
         {"mid_off", &g_tune.mid_off, nullptr, nullptr},
-        {"mid_split", &g_tune.mid_split, nullptr, nullptr},
         {"pipe_off", &g_tune.pipe_off, nullptr, nullptr},
+        {"mid_v1", &g_tune.mid_v1, nullptr, nullptr},
         {"matmul_pk_off", &g_tune.matmul_pk_off, nullptr, nullptr},
         {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},
         {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},

@@ -339,83 +339,20 @@ __device__ inline void stage_y_lds(const float* __restrict__ Y, int N, int n_lds
     __syncthreads();
 }
 
-template <int U>
-__global__ void __launch_bounds__(64, 1) k_split_update(const float* __restrict__ SP, const float* __restrict__ fdpn,
-                                                     int N, int rows, int row0, int lw, const float* __restrict__ Yin,
-                                                     float* __restrict__ Yout, const int* __restrict__ gate) {
-    if (gate && *gate != kStatusContinue) return;  // converge-mode solve already finished
-    extern __shared__ __attribute__((aligned(16))) float ys[];
-    const int KB = split_kblocks(N);
-    // lanes >= lw repeat lane % lw's loads (same cache lines) and are discarded
-    const int lane = threadIdx.x, ll = lane % lw;
-    const int p = blockIdx.x * lw + ll;
-    const bool live = lane < lw && p < 2 * rows;
-    const float fd = live ? fdpn[p] : 0.0f;  // this lane's Fdn / Fdp, fetched early
-    float acc = 0.0f;
-    {
-        // buffer loads over this workgroup's region: wave-uniform descriptor,
-        // lane offset in voffset, the k-block offset in an SGPR; two register
-        // stages of U packets in flight
-        const float* region = SP + (size_t)blockIdx.x * KB * lw * 4;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(region), (short)0, KB * lw * 16, 0x00020000);
-        const int vo = ll * 16, kstride = lw * 16;
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        auto ld = [&](int kb) -> f4v { return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, kb * kstride, 0); };
-        auto use = [&](f4v q, int kb) {
-            const float4 y = *reinterpret_cast<const float4*>(ys + 4 * kb);
-            acc += q.x * y.x;  // :608-609, k in order
-            acc += q.y * y.y;
-            acc += q.z * y.z;
-            acc += q.w * y.w;
-        };
-        f4v qa[U], qb[U];
-        int kb = 0;
-        // the first stage does not depend on y: issue it before staging y
-        if (KB >= U) {
-#pragma unroll
-            for (int j = 0; j < U; ++j) qa[j] = ld(j);
-        }
-        stage_y_lds(Yin, N, 4 * KB, ys);
-        for (; kb + 2 * U <= KB; kb += 2 * U) {
-#pragma unroll
-            for (int j = 0; j < U; ++j) qb[j] = ld(kb + U + j);
-#pragma unroll
-            for (int j = 0; j < U; ++j) use(qa[j], kb + j);
-            if (kb + 3 * U <= KB) {
-#pragma unroll
-                for (int j = 0; j < U; ++j) qa[j] = ld(kb + 2 * U + j);
-            }
-#pragma unroll
-            for (int j = 0; j < U; ++j) use(qb[j], kb + U + j);
-        }
-        if (kb + U <= KB) {  // one staged block left
-#pragma unroll
-            for (int j = 0; j < U; ++j) use(qa[j], kb + j);
-            kb += U;
-        }
-        for (; kb < KB; ++kb) use(ld(kb), kb);
-    }
-    const float v = acc + 1.0f * fd;       // even lane: num (:611), odd lane: den (:612)
-    const float den = __shfl_xor(v, 1);  // full wave active
-    if (!(p & 1) && live) {
-        const int i = p >> 1;
-        Yout[i] = v / den * ys[row0 + i];  // :594
-    }
-}
-
-// Relay form of the same update: W waves per workgroup share the workgroup's
-// 32 rows (same layout and lanes as k_split_update) and split the k range
+// One update of a row block over its stored split matrices: W waves per
+// workgroup share the workgroup's 32 rows (lanes 2i + side: one side of row
+// i each, the SP layout of k_build_split) and split the k range
 // into segments of S packets (4S values of k).  Segment g belongs to wave
 // g % W.  A wave loads its segment into registers as early as it can and
 // multiplies it by y while earlier segments are being summed; only the
 // additions form the sequential chain, and they run segment after segment,
 // the running sums handed from wave to wave through LDS (a turn counter
 // orders the hand-off).  Each row's sum therefore still runs over k = 0..N-1
-// in order from +0.0f, bit-identical to the reference and to
-// k_split_update, while a workgroup keeps W*S KiB of packets in flight
-// instead of one wave's pipeline, and the chain issues 4 cycles per k
-// (an add) instead of 8 (a multiply and an add).
+// in order from +0.0f, bit-identical to the reference, while a workgroup
+// keeps W*S KiB of packets in flight, and the chain issues 4 cycles per k (an
+// add) instead of 8 (a multiply and an add).  (A streaming one-wave form and
+// relay shapes W x S = 4 x 64, 8 x 32, 16 x 16 were measured slower and
+// removed in round 4: profiles/r01/split_sweep.txt.)
 template <int W, int S>
 __global__ void __launch_bounds__(64 * W) k_split_relay(const float* __restrict__ SP, const float* __restrict__ fdpn,
                                                         int N, int rows, int row0, int lw,
@@ -800,22 +737,7 @@ static void launch_relay(const float* SP, const float* fdpn, int N, int rows, in
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
                                const float* Yin, float* Yout, hipStream_t s, const int* gate, int* err) {
     if (rows <= 0) return hipSuccess;
-    switch (g_tune.split_kind) {
-        case 1: break;
-        case 2: launch_relay<4, 64>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
-        case 3: launch_relay<8, 32>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
-        case 4: launch_relay<16, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
-        default: launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err); return hipGetLastError();
-    }
-    const size_t lds = split_lds_bytes(N);
-    // one wave per CU with most of the register file as a 2-stage load buffer:
-    // a lane's packet stream is latency-bound (Little's law) with few in flight
-    const dim3 grid(split_wgs(rows, lw));
-    switch (g_tune.split_u) {
-        case 1: hipLaunchKernelGGL((k_split_update<8>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
-        case 2: hipLaunchKernelGGL((k_split_update<24>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
-        default: hipLaunchKernelGGL((k_split_update<16>), grid, dim3(64), lds, s, SP, fdpn, N, rows, row0, lw, Yin, Yout, gate); break;
-    }
+    launch_relay<8, 16>(SP, fdpn, N, rows, row0, lw, Yin, Yout, s, gate, err);
     return hipGetLastError();
 }
 
@@ -3090,7 +3012,7 @@ static void launch_fixed_tiny(int B, const SolveArgs& a, SolveState* st, hipStre
 static hipError_t launch_tiny_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     // the unrolled sums run to the next instantiated width >= N (>= M): the
     // sequential chain is the critical path, so keep the padding small
-    if (a.mode == kModeFixed && !g_tune.fixed_tiny_old) {
+    if (a.mode == kModeFixed) {
         if (B <= g_tune.fixed_rl_max_b) launch_fixed_tiny<true>(B, a, st, s);
         else launch_fixed_tiny<false>(B, a, st, s);
         return hipGetLastError();
@@ -3151,18 +3073,15 @@ hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) 
 __host__ __device__ inline int round8(int n) { return (n + 7) & ~7; }
 struct MidLayout {
     int nk, mk;    // N, M rounded up to 8
-    int ldn, ldm;  // row strides of Qd (nk + 4; split: 2 nk + 4) and of Qp (mk + 1)
+    int ldn, ldm;  // row strides of Qd (nk + 4) and of Qp (mk + 1)
     int ldg, ldi;  // row strides of Gp' (nk + 4; rows 0..mk-1 the columns of Gp, row mk Fd) and Qp_inv (mk + 4)
-    int ya, yb, tq, dP, dN, Fdp, Fdn, Fd, Kp, tM, Us, tu, fu, Fp, sc, qg, Qd, Gp, Qi, Qp, total;
+    int ya, yb, tq, dP, dN, Fdp, Fdn, Fd, Kp, tM, Us, tu, fu, Fp, sc, Qd, Gp, Qi, Qp, total;
 };
-// split: the Qd region holds the reference's stored split matrices instead,
-// row i = {Qdp_theta[i][k], Qdn_theta[i][k]} pairs (computeQdp_theta /
-// computeQdn_theta, PQP_CPU.c:524-537), and qg the diagonal of Qd
-__host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv, bool split = false) {
+__host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv) {
     MidLayout L;
     L.nk = round8(N);
     L.mk = round8(M);
-    L.ldn = split ? 2 * L.nk + 4 : L.nk + 4;
+    L.ldn = L.nk + 4;
     L.ldm = L.mk + 1;
     L.ldg = L.nk + 4;
     L.ldi = L.mk + 4;
@@ -3176,7 +3095,6 @@ __host__ __device__ inline MidLayout mid_layout(int N, int M, bool conv, bool sp
     L.Fdn = o; o += L.nk;
     L.Fd = o;  o += L.nk;
     L.sc = o;  o += 8;
-    L.qg = o;  o += split ? L.nk : 0;
     if (conv) {
         L.Kp = o;  o += L.nk;
         L.tM = o;  o += L.mk;
@@ -3401,92 +3319,7 @@ __device__ __forceinline__ void mid_update(const float* Qd, int ldn, int nk, con
     nxt[i] = num / den * y;                   // :594
 }
 
-// ---- the stored-split form (SPLIT): per k one packed multiply and one
-// packed add on the {Qdp_theta, Qdn_theta} pair, the diagonal literal stored
-// (scripts/microbench/chain_mb.hip: 24 clocks per k against 34 for the max
-// form and 50 in its diagonal blocks); twice the LDS of Qd
-struct SplitBlk {
-    sf4 s[4];  // {p, n} pairs of k .. k+7
-    sf4 y0, y1;
-};
-__device__ __forceinline__ void split_load(SplitBlk& B, const float* r, const float* y, int k) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) B.s[m] = *reinterpret_cast<const sf4*>(r + 2 * k + 4 * m);
-    B.y0 = *reinterpret_cast<const sf4*>(y + k);
-    B.y1 = *reinterpret_cast<const sf4*>(y + k + 4);
-}
-// FUSE: aq += y_k Qd[i][k], with Qd[i][k] = p - n off the diagonal (exact:
-// one of them is +0, and a zero's sign cannot change a sum that is never -0)
-// and qii on it (DIAG: the block holds the diagonal of some lanes' rows)
-template <bool FUSE, bool DIAG>
-__device__ __forceinline__ void split_block(const SplitBlk& B, int k, int i, float qii, sf2& acc, float& aq) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const sf4 v = B.s[j >> 1];
-        const float p = (j & 1) ? v.z : v.x, n = (j & 1) ? v.w : v.y;
-        const float yk = j < 4 ? B.y0[j] : B.y1[j - 4];
-        acc += sf2{p, n} * sf2{yk, yk};
-        if constexpr (FUSE) {
-            float q = p - n;
-            if constexpr (DIAG) q = (k + j == i) ? qii : q;
-            aq += yk * q;
-        }
-    }
-}
-template <bool FUSE>
-__device__ __forceinline__ void split_step(const SplitBlk& B, int k, int w0, int i, float qii, sf2& acc, float& aq) {
-    if (FUSE && k >= w0 && k < w0 + 64) split_block<FUSE, true>(B, k, i, qii, acc, aq);
-    else split_block<FUSE, false>(B, k, i, qii, acc, aq);
-}
-template <bool FUSE>
-__device__ __forceinline__ void mid_update_split(const float* S, int ld2, int nk, const float* cur, float* nxt,
-                                                 float* tq, const float* qg, const float* Fdn, const float* Fdp,
-                                                 int i) {
-    const float* r = S + i * ld2;
-    const float qii = FUSE ? qg[i] : 0.0f;
-    const int w0 = __builtin_amdgcn_readfirstlane(i & ~63);
-    sf2 acc = {0.0f, 0.0f};
-    float aq = 0.0f;
-    SplitBlk c, x;
-    split_load(c, r, cur, 0);
-    int k = 0;
-    for (; k + 16 < nk; k += 16) {
-        split_load(x, r, cur, k + 8);
-        split_step<FUSE>(c, k, w0, i, qii, acc, aq);
-        split_load(c, r, cur, k + 16);
-        split_step<FUSE>(x, k + 8, w0, i, qii, acc, aq);
-    }
-    if (k + 8 < nk) {
-        split_load(x, r, cur, k + 8);
-        split_step<FUSE>(c, k, w0, i, qii, acc, aq);
-        split_step<FUSE>(x, k + 8, w0, i, qii, acc, aq);
-    } else {
-        split_step<FUSE>(c, k, w0, i, qii, acc, aq);
-    }
-    const float y = cur[i];
-    if constexpr (FUSE) tq[i] = aq * y;       // (Y'Qd)_i * Y_i, computeCost :652-655
-    const float num = acc.y + 1.0f * Fdn[i];  // :611
-    const float den = acc.x + 1.0f * Fdp[i];  // :612
-    nxt[i] = num / den * y;                   // :594
-}
-// sum_k y_k Qd[k][j] from the pairs of column j (k in order), Qd[j][j] = qjj
-__device__ __forceinline__ float mid_col_split(const float* S, int ld2, int j, float qjj, const float* y, int nk) {
-    float s = 0.0f;
-    for (int k = 0; k < nk; k += 8) {
-        sf2 v[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) v[m] = *reinterpret_cast<const sf2*>(S + (k + m) * ld2 + 2 * j);
-        const sf4 y0 = *reinterpret_cast<const sf4*>(y + k), y1 = *reinterpret_cast<const sf4*>(y + k + 4);
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const float q = (k + m == j) ? qjj : v[m].x - v[m].y;
-            s += (m < 4 ? y0[m] : y1[m - 4]) * q;
-        }
-    }
-    return s;
-}
-
-template <int NT, bool SPLIT>
+template <int NT>
 __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
@@ -3494,10 +3327,9 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     if (st->status == kStatusDone || st->status == kStatusCapped) return;
     const int N = A.N, M = A.M;
     const bool conv = (A.mode != kModeFixed);
-    const MidLayout L = mid_layout(N, M, conv, SPLIT);
+    const MidLayout L = mid_layout(N, M, conv);
     const int ldn = L.ldn, ldm = L.ldm, ldg = L.ldg, ldi = L.ldi, nk = L.nk, mk = L.mk;
-    float* Qd = lds + L.Qd;  // SPLIT: the {Qdp_theta, Qdn_theta} pairs
-    float* qg = lds + L.qg;
+    float* Qd = lds + L.Qd;
     float* Gp = lds + L.Gp;
     float* Qi = lds + L.Qi;
     float* Qp = lds + L.Qp;
@@ -3521,17 +3353,7 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     __syncthreads();
     for (int e = tid; e < N * N; e += NT) {
         const int i = e / N, k = e - i * N;
-        const float q = A.Qd[e];
-        if constexpr (SPLIT) {  // off the diagonal max(0,+-q) + 1.0f*0.0f (:524-537); the diagonal below
-            if (i != k) {
-                Qd[i * ldn + 2 * k] = max_ref(0.0f, q) + 1.0f * 0.0f;
-                Qd[i * ldn + 2 * k + 1] = max_ref(0.0f, -q) + 1.0f * 0.0f;
-            } else {
-                qg[i] = q;
-            }
-        } else {
-            Qd[i * ldn + k] = q;
-        }
+        Qd[i * ldn + k] = A.Qd[e];
     }
     for (int i = tid; i < N; i += NT) {
         const float f = A.Fd[i];
@@ -3563,30 +3385,14 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     for (int i = tid; i < N; i += NT) {
         const float* row = Qd + i * ldn;
         float s = 0.0f;
-        if constexpr (SPLIT) {
-            // the stored max(0,-q)+0.0f is max(0,-q)*1.0f but for a zero's
-            // sign, which cannot change this sum; symmetry compares the pairs
-            // (equal pairs give equal p - n, the value the fused Y'Qd uses)
-            const float qii = qg[i];
-            for (int k = 0; k < N; ++k) {
-                s += (k == i) ? max_ref(0.0f, -qii) * 1.0f : row[2 * k + 1];
-                if (k > i && (__float_as_uint(row[2 * k]) != __float_as_uint(Qd[k * ldn + 2 * i]) ||
-                              __float_as_uint(row[2 * k + 1]) != __float_as_uint(Qd[k * ldn + 2 * i + 1])))
-                    asym = 1;
-            }
-            const float th = max_ref(s, 5.0f);
-            Qd[i * ldn + 2 * i] = max_ref(0.0f, qii) + 1.0f * th;
-            Qd[i * ldn + 2 * i + 1] = max_ref(0.0f, -qii) + 1.0f * th;
-        } else {
-            for (int k = 0; k < N; ++k) {
-                s += max_ref(0.0f, -row[k]) * 1.0f;
-                if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
-                if (row[k] != row[k]) nan = 1;
-            }
-            const float th = max_ref(s, 5.0f), qii = row[i];
-            dP[i] = max_ref(0.0f, qii) + 1.0f * th;
-            dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
+        for (int k = 0; k < N; ++k) {
+            s += max_ref(0.0f, -row[k]) * 1.0f;
+            if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
+            if (row[k] != row[k]) nan = 1;
         }
+        const float th = max_ref(s, 5.0f), qii = row[i];
+        dP[i] = max_ref(0.0f, qii) + 1.0f * th;
+        dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
     }
     const bool sym = !__syncthreads_or(asym);
     const bool fast = !__syncthreads_or(nan);
@@ -3622,10 +3428,7 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
             if (it < nR) {
                 const int i = it;
                 if (i < N) {
-                    if constexpr (SPLIT) {
-                        if (fuse) mid_update_split<true>(Qd, ldn, nk, cur, nxt, tq, qg, Fdn, Fdp, i);
-                        else mid_update_split<false>(Qd, ldn, nk, cur, nxt, tq, qg, Fdn, Fdp, i);
-                    } else if (fast) {
+                    if (fast) {
                         if (fuse) mid_update<true, true>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
                         else mid_update<false, true>(Qd, ldn, nk, cur, nxt, tq, dP, dN, Fdn, Fdp, i);
                     } else {
@@ -3643,8 +3446,7 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
             } else {
                 const int j = it - nR - nT;
                 if (j < N)  // Y'Qd, column access :110
-                    tq[j] = (SPLIT ? mid_col_split(Qd, ldn, j, qg[j], cur, nk) : mid_dot(Qd + j, ldn, cur, nk)) *
-                            cur[j];
+                    tq[j] = mid_dot(Qd + j, ldn, cur, nk) * cur[j];
             }
         }
         if (uInA && tid >= nR && tid < nR + 64) {
@@ -3704,9 +3506,7 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
                     } else {
                         const int j = it - nU;
                         if (j < N)  // (Y'Qd).Y
-                            tq[j] = (SPLIT ? mid_col_split(Qd, ldn, j, qg[j], cur, nk)
-                                           : mid_dot(Qd + j, ldn, cur, nk)) *
-                                    cur[j];
+                            tq[j] = mid_dot(Qd + j, ldn, cur, nk) * cur[j];
                     }
                 }
                 __syncthreads();
@@ -3796,33 +3596,374 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
     }
 }
 
-size_t solve_mid_lds_bytes(int N, int M, bool conv, bool split) {
-    return sizeof(float) * (size_t)mid_layout(N, M, conv, split).total;
+// ---------------------------------------------------------------------------
+// k_solve_mid2: path 3 with terminate() pipelined beside the update (round 4).
+// updateY2 needs only Y_h (PQP_CPU.c:603-618), so phase s of the loop runs,
+// on disjoint waves of one workgroup per problem, everything that needs only
+// what earlier phases produced:
+//   UW (waves 0 .. nUW-1, nUW = ceil(N / 32)): Y_{s+1} = updateY2(Y_s).  Lanes
+//       2r + side hold one side of row 32w + r: side 1 sums den's terms
+//       max(0,q)*y (:609), side 0 sums min(q,0)*y = -(max(0,-q)*y) (exact:
+//       negation is exact and rounding is sign-symmetric), so num = 0 - sum
+//       (:608; the 0 - turns the all-zero sum's -0 back into the reference's
+//       +0).  One v_med3_f32(q, 0, +-inf) per k gives either side's split
+//       entry: three instructions per k instead of the one-lane-per-row form's
+//       two v_max_f32 and a packed multiply and add.  The literal
+//       (max(0,+-q_ii) + Theta_i) * y on the diagonal (:524-537).  The lanes of
+//       a pair meet once per row: num / den * y (:594).  Where Qd holds a NaN,
+//       or Y_s a NaN or inf (whose sign the negated form could flip), the
+//       phase takes the selects of the reference's max instead.
+//   T  (wave nUW): tM = Gp'Y_s + Fp (computeUfromY :355-356) on lanes j < M,
+//       Fd.Y_s (computeCost :656) on lane M, then U_s = -Qp_inv tM (:357-358).
+//   C  (the other waves): terminate(Y_{s-1}) -- checkFeas's rows Gp U_{s-1}
+//       (:632-641, one lane per row), the (U'Qp).U and Fp.U terms and the
+//       three cost sums (:648-666) on the last C wave -- and, on the row
+//       waves, (Y_s'Qd)_j Y_s,j (:652-655, Qd column j) for the next phase.
+// After the phase barrier every thread reads the C waves' flags and sums and
+// takes terminate(s-1)'s decision (:673-687) itself.  Y_s and Y_{s+1} are
+// dropped when it stops (or a launch ends); each launch starts its pipeline
+// from the saved Y_h.  Every sum keeps the reference's operands and order:
+// the same bits as k_solve_mid.  N <= 160, M < 64 (nUW + 1 + 2 <= 8 waves);
+// other mid sizes, and terminate() alone, stay on k_solve_mid.
+// ---------------------------------------------------------------------------
+struct Mid2Layout {
+    int nk, mk, ldn, ldm, ldg, ldi;
+    int y, tq, dP, dN, Fdp, Fdn, Kp, tM, Us, tu, fu, Fp, fdy, flag, sums, Qd, Gp, Qi, Qp, total;
+};
+__host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
+    Mid2Layout L;
+    L.nk = round8(N);
+    L.mk = round8(M);
+    L.ldn = L.nk + 4;
+    L.ldm = L.mk + 1;
+    L.ldg = L.nk + 4;
+    L.ldi = L.mk + 4;
+    int o = 0;
+    L.y = o;    o += 3 * L.nk;      // Y_{s-1}, Y_s, Y_{s+1}: ring by s mod 3
+    L.tq = o;   o += 2 * L.nk;      // (Y_s'Qd)_j Y_s,j: ring by s & 1
+    L.dP = L.tq;                    // the diagonal literals: read into registers before the first
+    L.dN = L.tq + L.nk;             // phase, then their space is the tq ring's
+    L.Fdp = o;  o += L.nk;
+    L.Fdn = o;  o += L.nk;
+    L.flag = o; o += 8;             // [0..3] checkFeas flags per C row wave; [4 + s&1] Y non-finite
+    if (conv) {
+        L.Kp = o;   o += L.nk;
+        L.tM = o;   o += L.mk;
+        L.Us = o;   o += 2 * L.mk;  // U_s: ring by s & 1
+        L.tu = o;   o += L.mk;
+        L.fu = o;   o += L.mk;
+        L.Fp = o;   o += L.mk;
+        L.fdy = o;  o += 4;         // Fd.Y_s: ring by s & 1
+        L.sums = o; o += 4;         // (Y'Qd).Y, (U'Qp).U, Fp.U of iterate s-1
+    } else {
+        L.Kp = L.tM = L.Us = L.tu = L.fu = L.Fp = L.fdy = L.sums = 0;
+    }
+    L.Qd = o;  o += L.nk * L.ldn;
+    if (conv) {
+        L.Gp = o;  o += (L.mk + 1) * L.ldg;  // Gp' with Fd as row mk
+        L.Qi = o;  o += L.mk * L.ldi;
+        L.Qp = o;  o += L.mk * L.ldm;
+    } else {
+        L.Gp = L.Qi = L.Qp = 0;
+    }
+    L.total = o;
+    return L;
 }
-constexpr size_t kMidLdsBudget = 150 * 1024;
-// the stored-split form (pqp_tune "mid_split" 1, where its LDS fits): half
-// the update's instructions per k, but twice Qd's LDS, so half the resident
-// problems per CU, and no gain on feasible iterates (the fused Y'Qd term needs
-// q = p - n and the diagonal select again).  On the horizon sweep (every
-// iterate feasible) it lost at every H (profiles/r03/horizon_split_vs_qd.txt),
-// so it is off by default.
-bool mid_use_split(int N, int M, bool conv) {
-    return g_tune.mid_split == 1 && solve_mid_lds_bytes(N, M, conv, true) <= kMidLdsBudget;
+__host__ __device__ inline int mid2_uw(int N) { return (N + 31) / 32; }
+// mid2 takes (N, M) in converge or fixed mode when its waves fit 8
+__host__ __device__ inline bool mid2_fits(int N, int M, bool conv) {
+    return N <= 160 && (!conv || M < 64) && mid2_uw(N) + (conv ? 3 : 0) <= 8;
 }
 
-template <bool SPLIT>
-static void launch_mid_t(int B, const SolveArgs& a, SolveState* st, hipStream_t s, size_t lds, int nt) {
-    if (nt == 128) hipLaunchKernelGGL((k_solve_mid<128, SPLIT>), dim3(B), dim3(128), lds, s, a, st);
-    else if (nt == 256) hipLaunchKernelGGL((k_solve_mid<256, SPLIT>), dim3(B), dim3(256), lds, s, a, st);
-    else hipLaunchKernelGGL((k_solve_mid<512, SPLIT>), dim3(B), dim3(512), lds, s, a, st);
+// 8 terms of one side of update row i (k .. k+7).  FAST: the v_med3_f32
+// split (no NaN in Qd, Y finite); else the reference's selects on +y.  DIAG:
+// the block holds the diagonal of some rows of this wave.
+template <bool FAST, bool DIAG>
+__device__ __forceinline__ void mid2_block(float& acc, sf4 q0, sf4 q1, sf4 y0, sf4 y1, int k, int i, int side,
+                                           float lim, float dv) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float qk = j < 4 ? q0[j] : q1[j - 4];
+        const float yk = j < 4 ? y0[j] : y1[j - 4];
+        float t;
+        if constexpr (FAST) {
+            asm("v_med3_f32 %0, %1, 0, %2" : "=v"(t) : "v"(qk), "v"(lim));
+        } else {
+            t = side ? ((qk < 0.0f) ? 0.0f : qk) : ((qk > 0.0f) ? 0.0f : -qk);
+        }
+        if constexpr (DIAG) t = (k + j == i) ? dv : t;
+        acc += t * yk;
+    }
 }
+// one side of update row i, k = 0..nk-1 in order, the next block's LDS reads
+// in flight while a block is summed
+template <bool FAST>
+__device__ __forceinline__ float mid2_side(const float* q, const float* y, int nk, int i, int side, float lim,
+                                           float dv, int w0) {
+    float acc = 0.0f;
+    sf4 q0 = *reinterpret_cast<const sf4*>(q), q1 = *reinterpret_cast<const sf4*>(q + 4);
+    sf4 y0 = *reinterpret_cast<const sf4*>(y), y1 = *reinterpret_cast<const sf4*>(y + 4);
+    for (int k = 0; k < nk; k += 8) {
+        const int kn = (k + 8 < nk) ? k + 8 : k;  // next block (the last one re-read at the end)
+        const sf4 nq0 = *reinterpret_cast<const sf4*>(q + kn), nq1 = *reinterpret_cast<const sf4*>(q + kn + 4);
+        const sf4 ny0 = *reinterpret_cast<const sf4*>(y + kn), ny1 = *reinterpret_cast<const sf4*>(y + kn + 4);
+        if (k >= w0 && k < w0 + 32) mid2_block<FAST, true>(acc, q0, q1, y0, y1, k, i, side, lim, dv);
+        else mid2_block<FAST, false>(acc, q0, q1, y0, y1, k, i, side, lim, dv);
+        q0 = nq0; q1 = nq1; y0 = ny0; y1 = ny1;
+    }
+    return acc;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT, 4) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SolveArgs A = problem_at(A0, blockIdx.x);
+    SolveState* st = st0 + blockIdx.x;
+    if (st->status == kStatusDone || st->status == kStatusCapped) return;
+    const int N = A.N, M = A.M;
+    const bool conv = (A.mode == kModeConverge);
+    const Mid2Layout L = mid2_layout(N, M, conv);
+    const int ldn = L.ldn, ldm = L.ldm, ldg = L.ldg, ldi = L.ldi, nk = L.nk, mk = L.mk;
+    float* Qd = lds + L.Qd;
+    float* Gp = lds + L.Gp;
+    float* Qi = lds + L.Qi;
+    float* Qp = lds + L.Qp;
+    float* Yr = lds + L.y;
+    float* tq = lds + L.tq;
+    float* dP = lds + L.dP;
+    float* dN = lds + L.dN;
+    float* Fdp = lds + L.Fdp;
+    float* Fdn = lds + L.Fdn;
+    float* Kp = lds + L.Kp;
+    float* tM = lds + L.tM;
+    float* Us = lds + L.Us;
+    float* tu = lds + L.tu;
+    float* fu = lds + L.fu;
+    float* Fp = lds + L.Fp;
+    float* fdy = lds + L.fdy;
+    float* sums = lds + L.sums;
+    int* flag = reinterpret_cast<int*>(lds + L.flag);  // [0..3] checkFeas per C row wave, [4 + p] Y non-finite
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nUW = mid2_uw(N), wT = nUW, wC0 = nUW + 1, nC = NT / 64 - wC0;
+    const int nCR = nC - 1;  // C waves that take checkFeas rows and the Y'Qd columns; the last one the costs
+
+    // ---- stage the problem (once per launch; padding zero) ----
+    for (int e = tid; e < L.total; e += NT) lds[e] = 0.0f;
+    __syncthreads();
+    for (int e = tid; e < N * N; e += NT) {
+        const int i = e / N, k = e - i * N;
+        Qd[i * ldn + k] = A.Qd[e];
+    }
+    for (int i = tid; i < N; i += NT) {
+        const float f = A.Fd[i];
+        Fdp[i] = max_ref(0.0f, f);   // matrixPos(Fdp, Fd) :703
+        Fdn[i] = max_ref(0.0f, -f);  // matrixNeg(Fdn, Fd) :704
+    }
+    if (conv) {
+        for (int e = tid; e < N * M; e += NT) {
+            const int i = e / M, j = e - i * M;
+            Gp[j * ldg + i] = A.Gp[e];
+        }
+        for (int i = tid; i < N; i += NT) Gp[mk * ldg + i] = A.Fd[i];  // Fd.Y rides as row mk
+        for (int e = tid; e < M * M; e += NT) {
+            const int i = e / M, j = e - i * M;
+            Qi[i * ldi + j] = A.Qinv[e];
+            Qp[i * ldm + j] = A.Qp[e];
+        }
+        for (int i = tid; i < N; i += NT) Kp[i] = A.Kp[i];
+        for (int j = tid; j < M; j += NT) Fp[j] = A.Fp[j];
+    }
+    long long h0 = st->h;
+    int ynf = 0;
+    for (int i = tid; i < N; i += NT) {
+        const float y = st->resume ? A.Y[i] : 1000.0f;  // initMat(Y,1000) :710
+        Yr[(int)(h0 % 3) * nk + i] = y;
+        if (!(fabsf(y) <= 3.402823466e38f)) ynf = 1;
+    }
+    __syncthreads();
+    // computeTheta (:503-519), the diagonal literals (:524-537); any NaN in Qd?
+    int nan = 0;
+    for (int i = tid; i < N; i += NT) {
+        const float* row = Qd + i * ldn;
+        float s = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            s += max_ref(0.0f, -row[k]) * 1.0f;
+            if (row[k] != row[k]) nan = 1;
+        }
+        const float th = max_ref(s, 5.0f), qii = row[i];
+        dP[i] = max_ref(0.0f, qii) + 1.0f * th;
+        dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
+    }
+    const bool fast = !__syncthreads_or(nan);
+    bool y_nonfinite = __syncthreads_or(ynf);
+    const float Md = conv ? A.Md[0] : 0.0f, Mp = conv ? A.Mp[0] : 0.0f;
+
+    // per-lane constants of the update role
+    const int side = lane & 1, urow = 32 * wave + (lane >> 1);
+    const bool uw = wave < nUW && urow < N;
+    const float lim = side ? __builtin_inff() : -__builtin_inff();
+    const float dv = uw ? (side ? dP[urow] : -dN[urow]) : 0.0f;  // side 0 sums the negated terms
+    const float fdv = uw ? (side ? Fdp[urow] : Fdn[urow]) : 0.0f;
+    const int w0 = 32 * wave;
+    __syncthreads();  // dP / dN read: the tq ring may be written from here on
+
+    const bool tr = A0.trace && (int)blockIdx.x < A0.trace_n;
+    unsigned long long busy = 0, t_phase = 0, n_ph = 0, t0 = 0;
+
+    float Jp_last = 0.0f, Jd_last = 0.0f;
+    bool costs = false;
+    int status = kStatusContinue;
+    long long s = h0, t_out = h0;
+    for (;;) {
+        const bool pend = conv && s > h0;  // terminate(s-1) is this phase's C work
+        const float* ycur = Yr + (int)(s % 3) * nk;
+        float* ynext = Yr + (int)((s + 1) % 3) * nk;
+        // Y_{s+1}'s non-finite flag goes to slot (s+1)&1; slot s&1 was last read
+        // before the previous phase's second barrier
+        if (tid == 0) flag[4 + (int)(s & 1)] = 0;
+        if (tr) t0 = __builtin_amdgcn_s_memtime();
+        if (wave < nUW) {
+            // ---------------- UW: Y_{s+1} = updateY2(Y_s) ----------------
+            if (uw) {
+                const float* q = Qd + urow * ldn;
+                float acc = (fast && !y_nonfinite) ? mid2_side<true>(q, ycur, nk, urow, side, lim, dv, w0)
+                                                   : mid2_side<false>(q, ycur, nk, urow, side, lim, side ? dv : -dv, w0);
+                if (fast && !y_nonfinite && !side) acc = 0.0f - acc;  // num's terms were summed negated
+                const float v = acc + 1.0f * fdv;                     // num += Fdn :611; den += Fdp :612
+                const float other = __shfl_xor(v, 1);
+                if (side) {
+                    const float y = ycur[urow];
+                    const float yn = other / v * y;  // updY :594
+                    ynext[urow] = yn;
+                    if (!(fabsf(yn) <= 3.402823466e38f)) flag[4 + (int)((s + 1) & 1)] = 1;
+                }
+            }
+        } else if (conv && wave == wT) {
+            // ------------- T: tM = Gp'Y_s + Fp, Fd.Y_s, U_s = -Qp_inv tM -------------
+            if (lane <= M) {
+                const float d = mid_dot_row(Gp + (lane < M ? lane : mk) * ldg, ycur, nk);
+                if (lane < M) tM[lane] = d + 1.0f * Fp[lane];  // :355-356
+                else fdy[s & 1] = d;                            // Fd.Y :656
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < M) Us[(s & 1) * mk + lane] = -mid_dot_row(Qi + lane * ldi, tM, mk);  // :357-358
+        } else if (conv) {
+            // ---------------- C: terminate(Y_{s-1}); Y_s'Qd ----------------
+            const int cw = wave - wC0;
+            const float* Uo = Us + ((s - 1) & 1) * mk;
+            if (cw < nCR) {
+                const int l = cw * 64 + lane;
+                int bad = 0;
+                if (pend)
+                    for (int i = l; i < N; i += 64 * nCR) {
+                        const float g = mid_dot(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
+                        const float kp = Kp[i];
+                        if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
+                    }
+                if (pend && lane == 0) flag[cw] = __any(bad) ? 1 : 0;
+                float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
+                for (int j = l; j < N; j += 64 * nCR) tqs[j] = mid_dot(Qd + j, ldn, ycur, nk) * ycur[j];  // :652-655
+            } else if (pend) {
+                if (lane < M) {
+                    tu[lane] = mid_dot(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
+                    fu[lane] = Fp[lane] * Uo[lane];                         // Fp'U :656-657
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 3) {
+                    const float* v = lane == 0 ? tq + ((s - 1) & 1) * nk : (lane == 1 ? tu : fu);
+                    const float r = mid_sum(v, lane == 0 ? nk : mk);
+                    sums[lane] = r;
+                }
+            }
+        }
+        if (tr) busy += __builtin_amdgcn_s_memtime() - t0;
+        __syncthreads();
+        if (tr && wave == 0) {
+            t_phase += __builtin_amdgcn_s_memtime() - t0;
+            ++n_ph;
+        }
+        if (pend) {
+            // ------- terminate(s-1)'s decision, on every thread -------
+            const long long t = s - 1;
+            int infeasible = 0;
+            for (int c = 0; c < nCR; ++c) infeasible |= flag[c];
+            int stop = 0;
+            if (!infeasible) {
+                float Jd = 0.0f;
+                Jd = (float)((double)Jd + 0.5 * (double)sums[0]);
+                Jd += fdy[t & 1];
+                Jd += Md / 2;
+                float Jp = 0.0f;
+                Jp = (float)((double)Jp + 0.5 * (double)sums[1]);
+                Jp += sums[2];
+                Jp += Mp / 2;
+                stop = 1;
+                if (Jp > -Jd) stop = 0;
+                if ((double)(Jp + Jd) > kTol) stop = 0;
+                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                Jp_last = Jp;
+                Jd_last = Jd;
+                costs = true;
+            }
+            t_out = t;
+            if (stop) { status = kStatusDone; break; }
+            if (A.max_updates > 0 && t - 1 >= A.max_updates) { status = kStatusCapped; break; }
+            if (t - h0 >= A.chunk) { status = kStatusContinue; break; }
+        } else if (!conv) {
+            if (s >= A.num_iter) { t_out = s; status = kStatusDone; break; }  // while(h < NUM_ITER)
+            if (s - h0 >= A.chunk) { t_out = s; status = kStatusContinue; break; }
+        }
+        y_nonfinite = flag[4 + (int)((s + 1) & 1)] != 0;  // Y_{s+1}, the next phase's Y_s
+        __syncthreads();             // everyone has read this phase's flags before the next phase writes
+        ++s;
+    }
+    // the result: Y and U of iterate t_out (converge) or Y_s (fixed)
+    const float* yo = Yr + (int)(t_out % 3) * nk;
+    for (int i = tid; i < N; i += NT) A.Y[i] = yo[i];
+    if (conv)
+        for (int i = tid; i < M; i += NT) A.U[i] = Us[(t_out & 1) * mk + i];
+    if (tr && lane == 0) {
+        unsigned long long* T = A0.trace + 16 * (size_t)blockIdx.x;
+        if (wave < 8) T[8 + wave] += busy;
+        if (wave == 0) {
+            T[0] += t_phase;
+            T[4] += n_ph;
+        }
+    }
+    if (tid == 0) {
+        if (costs) {
+            st->Jp = Jp_last;
+            st->Jd = Jd_last;
+            st->have_costs = 1;
+        }
+        st->h = t_out;
+        st->status = status;
+        st->resume = 1;
+        if (status == kStatusContinue && A.pending) atomicAdd(A.pending, 1);
+    }
+}
+
+size_t solve_mid_lds_bytes(int N, int M, bool conv) {
+    return sizeof(float) * (size_t)mid_layout(N, M, conv).total;
+}
+constexpr size_t kMidLdsBudget = 150 * 1024;
+
 static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+    if (a.mode != kModeTerminate && !g_tune.mid_v1 && mid2_fits(a.N, a.M, a.mode == kModeConverge)) {
+        const size_t lds = sizeof(float) * (size_t)mid2_layout(a.N, a.M, a.mode == kModeConverge).total;
+        if (lds <= kMidLdsBudget) {
+            hipLaunchKernelGGL((k_solve_mid2<512>), dim3(B), dim3(512), lds, s, a, st);
+            g_last_batch_kernel = 3;
+            return hipGetLastError();
+        }
+    }
+    g_last_batch_kernel = 2;
     const bool conv = a.mode != kModeFixed;
-    const bool split = mid_use_split(a.N, a.M, conv);
-    const size_t lds = solve_mid_lds_bytes(a.N, a.M, conv, split);
+    const size_t lds = solve_mid_lds_bytes(a.N, a.M, conv);
     const int nt = mid_threads(a.N, a.M, conv);
-    if (split) launch_mid_t<true>(B, a, st, s, lds, nt);
-    else launch_mid_t<false>(B, a, st, s, lds, nt);
+    if (nt == 128) hipLaunchKernelGGL((k_solve_mid<128>), dim3(B), dim3(128), lds, s, a, st);
+    else if (nt == 256) hipLaunchKernelGGL((k_solve_mid<256>), dim3(B), dim3(256), lds, s, a, st);
+    else hipLaunchKernelGGL((k_solve_mid<512>), dim3(B), dim3(512), lds, s, a, st);
     return hipGetLastError();
 }
 
@@ -4270,7 +4411,7 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // launched agree).
 bool pipe_route(int N, int M, int variant) {
     const auto round4 = [](int n) { return (n + 3) & ~3; };
-    const bool big = variant < 1 || variant > 3;  // the default build's 128 x 96 tile
+    const bool big = variant != 3;  // the default build's 128 x 96 tile (3: two 64 x 64 tiles in flight)
     return !g_tune.single_scalar && !g_tune.pipe_off && (g_tune.pipe_force || 3 * M >= N) && N > 64 && N % 4 == 0 &&
            M % 4 == 0 && solve_pipe_lds_bytes(round4(N), round4(M), big) <= kPipeLdsMax;
 }
@@ -4284,19 +4425,15 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
     // converge mode with Qp_inv': one pass over Gp per iteration (k_solve_pipe)
     const int variant = g_tune.pipe_variant;
     if (vec && a.mode == kModeConverge && a.QinvT && pipe_route(a.N, a.M, variant)) {
-        const bool big = variant < 1 || variant > 3;
+        const bool big = variant != 3;
         const size_t plds = solve_pipe_lds_bytes(a.ldq, a.ldm, big);
         // Gp tiles in flight, update loads in flight per lane, workgroups per
         // CU: two per CU with 16 loads per lane beat three with 8 (4096
         // problems are then 8 whole rounds of 512 resident workgroups)
         // 128 x 96 tiles (every wave sums a chain) beat 64 x 64 ones by 2-3 %
         // on infeasible iterates and tie on feasible ones
-        switch (big ? 0 : variant) {
-        case 1: hipLaunchKernelGGL((k_solve_pipe<256, 4, 16, 2>), dim3(B), dim3(256), plds, s, a, st); break;
-        case 2: hipLaunchKernelGGL((k_solve_pipe<256, 2, 8, 1>), dim3(B), dim3(256), plds, s, a, st); break;
-        case 3: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), plds, s, a, st); break;
-        default: hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), plds, s, a, st);
-        }
+        if (big) hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), plds, s, a, st);
+        else hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), plds, s, a, st);
         g_last_batch_kernel = 1;
         return hipGetLastError();
     }
@@ -4304,8 +4441,6 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
     if (a.N <= 64) {
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
-    } else if (vec && g_tune.single_occ4) {
-        hipLaunchKernelGGL((k_solve_single<256, true, 4>), dim3(B), dim3(256), lds, s, a, st);
     } else {
         if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<256, false>), dim3(B), dim3(256), lds, s, a, st);

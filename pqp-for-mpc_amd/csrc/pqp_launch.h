@@ -68,9 +68,9 @@ size_t solve_pipe_lds_bytes(int ldq, int ldm, bool big = false);
 constexpr size_t kPipeLdsMax = 150 * 1024;
 // path 2's converge-mode kernel by shape: true = k_solve_pipe (needs Qp_inv' only)
 bool pipe_route(int N, int M, int variant);
-extern thread_local int g_last_batch_kernel;  // 1 when the calling thread's last path-2 launch was k_solve_pipe
+extern thread_local int g_last_batch_kernel;  // the calling thread's last path-2/3 launch: 0 k_solve_single, 1 k_solve_pipe, 2 k_solve_mid, 3 k_solve_mid2
 size_t solve_small_lds_bytes(int N, int M);
-size_t solve_mid_lds_bytes(int N, int M, bool conv, bool split = false);
+size_t solve_mid_lds_bytes(int N, int M, bool conv);
 hipError_t launch_solve_small(const SolveArgs& a, SolveState* st, hipStream_t s);
 hipError_t launch_solve_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);  // N, M <= 32
 // row block [row0, row0 + rows) of one large problem, fixed mode,
@@ -80,7 +80,7 @@ hipError_t launch_build_split(const float* Qd, int ld, const float* theta, const
 hipError_t launch_theta_rows(const float* Qd, int ld, int N, int rows, float* theta, hipStream_t s);
 // gate: optional; the launch does nothing unless *gate == kStatusContinue.
 // err: optional sticky device word; a relay hand-off wait that expired ORs 1
-// into it (the relay kernels; the streaming k_split_update has no hand-off)
+// into it
 hipError_t launch_split_update(const float* SP, const float* fdpn, int N, int rows, int row0, int lw,
                                const float* Yin, float* Yout, hipStream_t s, const int* gate = nullptr,
                                int* err = nullptr);
@@ -88,23 +88,18 @@ constexpr int kRelaySpinMax = 1 << 20;  // relay hand-off wait budget in polls (
 struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuning.h); defaults = production
     int relay_spin_max = kRelaySpinMax;  // relay hand-off wait budget in polls (< 0: every wait expires at once)
     int lean_min_n = 4096;  // k_lean_relay for row blocks of rows x N >= lean_min_n^2 entries
-    int split_u = 0;  // k_split_update stage depth (0: 16, 1: 8, 2: 24)
     int split_lw = 0;  // relay lanes per workgroup (0 auto, else 8/16/32/64)
-    int split_kind = 0;  // 0 auto (relay W8 S16), 1 k_split_update, 2 relay W4 S64, 3 W8 S32, 4 W16 S16, 5 W8 S16
     int wave_pipe_max_b = 4096;  // largest batch whose k_solve_wave launch is the software-pipelined form
-    int fixed_tiny_old = 0;  // fixed mode of N <= 32 on k_solve_tiny instead of k_fixed_tiny
     int fixed_rl_max_b = 1024;  // largest batch whose k_fixed_tiny keeps y in registers
     int wave_min_b = 1;  // converge mode of N, M <= 32 on k_solve_wave from this many problems on
     int matmul_tiled_off = 0;  // every product through k_matmul_seq
     int gj_blocked_off = 0;  // Gauss_Jordan through the one-pivot-per-sweep kernel
     int single_scalar = 0;  // k_solve_single with 4-byte loads only
-    int single_occ4 = 0;  // k_solve_single built for 4 workgroups per CU
     int persist_off = 0;  // fixed mode of n_dual <= 1024 through the graph-replayed relay
     int persist_stall_wg = -1;  // workgroup of each persistent launch that never runs (error-path tests; -1: none)
     unsigned long long* persist_trace = nullptr;  // k_split_persist timeline buffer (device)
     int persist_trace_n = 0;  // updates the timeline buffer holds
     int persist_fit_cus = 0;  // CU count the residency checks assume (0: the device's)
-    int wide_flags = 0;  // converge chain: bit 0 update on a forked graph branch, bit 1 gemv segments of 64
     int converge_persist_off = 0;  // converge mode through the graph chain instead of the persistent launch
     unsigned long long* mid_trace = nullptr;  // k_solve_mid phase totals buffer (device)
     int mid_trace_n = 0;  // problems it holds
@@ -114,9 +109,9 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     bool force_single = false;  // fixed mode of a large problem on one workgroup (k_solve_single)
     int wide_min_n = 384;  // converge mode: smallest N solved over many workgroups
     long long batch_chunk = 0;  // iterates per problem per batched-solve launch (0: sized from N, M)
-    int mid_off = 0;
-    int mid_split = 0;  // 1: k_solve_mid's stored-split form where its LDS fits  // batched solves of mid-size N through k_solve_small / k_solve_single instead of k_solve_mid
-    int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 1 (64 x 64 tiles, 4 in flight), 2 (64 x 64, 2 in flight, 8 loads, VGPR-bound occupancy), 3 (64 x 64, 2 in flight)
+    int mid_off = 0;  // batched solves of mid-size N through k_solve_small / k_solve_single instead of path 3
+    int mid_v1 = 0;  // path 3 on k_solve_mid (terminate() after the update) instead of the pipelined k_solve_mid2
+    int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 3 (two 64 x 64 tiles in flight)
     int pipe_force = 0;  // k_solve_pipe also where M < N / 3 (where k_solve_single measured faster)
     int matmul_pk_off = 0;  // setup GEMMs on the 64 x 64 scalar-staged k_matmul_tiled instead of the packed 128 x 128 k_matmul_pk
     int pipe_off = 0;  // batched converge of large problems on k_solve_single (two passes over Gp) instead of k_solve_pipe
@@ -147,7 +142,7 @@ hipError_t launch_build_lean(const float* Qd, int ld, const float* theta, const 
 hipError_t launch_lean_update(const float* LP, const float* aux, int N, int rows, int row0, int lw, const float* Yin,
                               float* Yout, hipStream_t s, const int* gate = nullptr, int* err = nullptr);
 int split_pick_lw(int rows);                   // lanes per workgroup for a block of `rows`
-size_t split_lds_bytes(int N);         // k_split_update's LDS (the full y)
+size_t split_lds_bytes(int N);         // LDS of a row block's update (the full y)
 // rows [row0, row0 + rows) of synthetic problem `inst` (row-major, ld >= N,
 // columns [N, ld) zeroed) and, if Fd, its full Fd (and Md)
 hipError_t launch_synth_rows(uint32_t seed, long long inst, int N, int M, int row0, int rows, float* Qrows, int ld,

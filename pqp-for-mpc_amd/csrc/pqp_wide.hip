@@ -295,7 +295,7 @@ hipError_t launch_gemv_relay(const GemvJobs& jobs, hipStream_t s) {
     J.spin_max = g_tune.relay_spin_max;
     int n_in = J.job[0].n_in;
     if (J.job[1].A && J.job[1].n_in > n_in) n_in = J.job[1].n_in;
-    return (g_tune.wide_flags & 2) ? gemv_launch<8, 64>(J, n_in, s) : gemv_launch<8, 32>(J, n_in, s);
+    return gemv_launch<8, 32>(J, n_in, s);
 }
 
 

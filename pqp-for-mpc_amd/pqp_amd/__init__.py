@@ -13,7 +13,7 @@ Layers
     Gauss_Jordan, computeFp, computeMp
   * status API: solve_dual, update, read_example, run_example
   * batched device API (torch tensors as device memory): :class:`Batch`,
-    :class:`ProblemBatch`, :func:`mpc_batch`
+    :class:`ProblemBatch`, :func:`mpc_batch`, :func:`horizon_batch`
   * row blocks of one large problem (row-sharded solve): :class:`RowBlock`
     (driver in :mod:`pqp_amd.rowshard`)
 """
@@ -163,32 +163,26 @@ _KNOB_NAMES = {"persist": "persist_off", "converge_persist": "converge_persist_o
                "lean_min_n": "lean_min_n", "relay_spin_max": "relay_spin_max", "matmul_tiled": "matmul_tiled_off",
                "gj_blocked": "gj_blocked_off", "persist_fit_cus": "persist_fit_cus",
                "persist_stall": "persist_stall_wg", "converge_chunk": "converge_chunk", "wave_min_b": "wave_min_b",
-               "fixed_rl_max_b": "fixed_rl_max_b", "wave_pipe_max_b": "wave_pipe_max_b", "wide_flags": "wide_flags"}
+               "fixed_rl_max_b": "fixed_rl_max_b", "wave_pipe_max_b": "wave_pipe_max_b"}
 
 
 def _set_variant(variant: int) -> int:
     """The packed kernel-variant word of the round-1 tuning API: 0x100
-    force_small, 0x200 force_single, 0x400 fixed_tiny_old, bits 12-13 split_u,
-    14-16 split_kind, 17-19 split_lw (1: 8 ... 4: 64)."""
+    force_small, 0x200 force_single, bits 17-19 split_lw (1: 8 ... 4: 64)."""
     lw_old = tune_get("split_lw")
     old = ((0x100 if tune_get("force_small") else 0) | (0x200 if tune_get("force_single") else 0)
-           | (0x400 if tune_get("fixed_tiny_old") else 0) | (tune_get("split_u") << 12)
-           | (tune_get("split_kind") << 14) | (((lw_old.bit_length() - 3) if lw_old else 0) << 17))
+           | (((lw_old.bit_length() - 3) if lw_old else 0) << 17))
     sel = (variant >> 17) & 7
-    tune("split_u", (variant >> 12) & 3)
-    tune("split_kind", (variant >> 14) & 7)
     tune("split_lw", 4 << sel if 1 <= sel <= 4 else 0)
     tune("force_small", 1 if variant & 0x100 else 0)
     tune("force_single", 1 if variant & 0x200 else 0)
-    tune("fixed_tiny_old", 1 if variant & 0x400 else 0)
     return old
 
 
 def _batch_converge(opts: int) -> int:
-    """batch_opts plus the k_solve_single build bits (2: 4-byte loads, 3: four
-    workgroups per CU) in one word."""
-    old = tune("batch_opts", opts & 19) | (4 if tune("single_scalar", 1 if opts & 4 else 0) else 0)
-    return old | (8 if tune("single_occ4", 1 if opts & 8 else 0) else 0)
+    """batch_opts plus the k_solve_single build bit (2: 4-byte loads) in one
+    word."""
+    return tune("batch_opts", opts & 19) | (4 if tune("single_scalar", 1 if opts & 4 else 0) else 0)
 
 
 def _last_path(fallbacks=None) -> int:
@@ -743,6 +737,62 @@ def mpc_batch(directory, states, device=None) -> ProblemBatch:
                                       p(D), p(x), p(pb.Fp), s))
     _check(lib().pqp_batch_compute_mp(B, E["nd"], ns, *[p(plant[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5",
                                                                                 "Mp6")], p(D), p(x), p(pb.Mp), s))
+    pb.gauss_jordan().convert_to_dual()
+    return pb
+
+
+def horizon_batch(directory, H: int, states, device=None) -> ProblemBatch:
+    """B MPC problems over H horizon stages of the bundled plant
+    (example/*.txt), each stage at its own state: problem b stacks H copies
+    of the plant's constraint set, stage h of it at state states[b, h]
+    (``states`` is [B, H, nState] or [B, nState] for one state per problem).
+    The primal is block-diagonal -- Qp_inv = diag(Qp_inv, ..., Qp_inv), Gp =
+    diag(Gp, ..., Gp), Kp stacked, Fp = the stages' computeFp (PQP_CPU.c:373)
+    stacked, Mp = the stages' computeMp (:395) summed in stage order -- and
+    the dual is formed on the GPU from it like any other problem: Qp =
+    Gauss_Jordan(Qp_inv) (:251) and convertToDual (:489).  n_dual = 28 H,
+    M = 7 H.  Setup runs on the device through the C ABI (pqp_batch_compute_fp
+    / _mp, pqp_batch_gauss_jordan, pqp_batch_convert_to_dual); torch only
+    places the blocks.  The reference stops these problems at h = 313 for
+    every H it was run at (tests/test_gpu_mid.py)."""
+    import torch
+
+    E = read_example(directory)
+    m, nd, ns, n = E["M"], E["nd"], E["ns"], E["N"]
+    H = int(H)
+    xs = np.asarray(states, np.float32)
+    if xs.ndim == 2:
+        xs = np.repeat(xs[:, None, :], H, axis=1)
+    if xs.ndim != 3 or xs.shape[1] != H or xs.shape[2] != ns:
+        raise ValueError(f"states must be [B, {H}, {ns}] or [B, {ns}]")
+    B = xs.shape[0]
+    pb = ProblemBatch(B, n * H, m * H, device)
+    dev = pb.device
+    T = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=dev).contiguous()  # noqa: E731
+    plant = {k: T(E[k]) for k in ("Fp1", "Fp2", "Fp3", "Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6")}
+    x = T(xs.reshape(B * H, ns))
+    D = T(np.tile(E["D"], (B * H, 1)))
+    Fps = torch.empty(B * H, m, dtype=torch.float32, device=dev)
+    Mps = torch.empty(B * H, dtype=torch.float32, device=dev)
+    p = ProblemBatch._p
+    s = pb._s()
+    _check(lib().pqp_batch_compute_fp(B * H, m, nd, ns, p(plant["Fp1"]), p(plant["Fp2"]), p(plant["Fp3"]), p(D),
+                                      p(x), p(Fps), s))
+    _check(lib().pqp_batch_compute_mp(B * H, nd, ns, *[p(plant[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5",
+                                                                               "Mp6")], p(D), p(x), p(Mps), s))
+    Qinv, Gp = T(E["Qp_inv"]).reshape(m, m), T(E["Gp"]).reshape(n, m)
+    QI = pb.Qp_inv.view(B, H * m, H * m)
+    GP = pb.Gp.view(B, H * n, H * m)
+    for h in range(H):  # the diagonal blocks (the rest stays +0.0)
+        QI[:, h * m:(h + 1) * m, h * m:(h + 1) * m] = Qinv
+        GP[:, h * n:(h + 1) * n, h * m:(h + 1) * m] = Gp
+    pb.Kp.copy_(T(E["Kp"]).repeat(H).expand(B, -1))
+    pb.Fp.copy_(Fps.view(B, H * m))
+    Mv = Mps.view(B, H)
+    pb.Mp.copy_(Mv[:, 0])
+    for h in range(1, H):  # ((Mp_0 + Mp_1) + Mp_2) + ... in fp32, stage order
+        pb.Mp.add_(Mv[:, h])
+    torch.cuda.current_stream(dev).synchronize()  # the staging tensors go out of scope
     pb.gauss_jordan().convert_to_dual()
     return pb
 

@@ -26,7 +26,6 @@ def main(Hs):
     from oracle import Oracle, block_diag_problem
 
     base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
-    pqp_amd.tune("mid_split", int(os.environ.get("MID_SPLIT", "0")))
     for H in Hs:
         P = block_diag_problem(base, H)
         N, M = P["N"], P["M"]

@@ -6,16 +6,22 @@ typedef float sf4 __attribute__((ext_vector_type(4)));
 
 // V: 0 scalar add chain over LDS values; 1 mul+add chain (dot); 2 pk_mul+pk_add chain (pairs);
 //    3 max,max,pk_mul,pk_add (row, no diag); 4 like 3 with diag select; 5 register-only add chain
-//    6: two interleaved rows of V3 per lane
+//    6: two interleaved rows of V3 per lane; 12-15: lane pairs (one side of a row per lane,
+//    v_med3_f32 against +-inf gives max(q,0) / min(q,0), odd lanes multiply by -y): plain,
+//    with the fused Y'Qd term, two rows per lane, with the diagonal select
 template <int V>
 __global__ void __launch_bounds__(256) mb(const float* g, float* out, unsigned long long* cyc, int n, int reps) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
     const int ld = n + 4;
-    for (int e = tid; e < 64 * ld + n; e += blockDim.x) lds[e] = g[e % 1000] * 1e-3f;
+    for (int e = tid; e < 64 * ld + 2 * (n + 8); e += blockDim.x) lds[e] = g[e % 1000] * 1e-3f;
     __syncthreads();
     const float* row = lds + (tid & 63) * ld;
     const float* y = lds + 64 * ld;
+    // V >= 12 (lane pairs): odd lanes read the negated copy of y
+    const float* ys = (V >= 12 && (tid & 1)) ? y + n + 8 : y;
+    const float lim = (tid & 1) ? -__builtin_inff() : __builtin_inff();
+    float s2 = 0.0f;
     float s = 0.0f;
     sf2 acc = {0.0f, 0.0f}, acc2 = {0.f, 0.f};
     const int i = tid & 63;
@@ -23,7 +29,7 @@ __global__ void __launch_bounds__(256) mb(const float* g, float* out, unsigned l
     for (int r = 0; r < reps; ++r) {
         for (int k = 0; k < n; k += 8) {
             const sf4 q0 = *reinterpret_cast<const sf4*>(row + k), q1 = *reinterpret_cast<const sf4*>(row + k + 4);
-            const sf4 y0 = *reinterpret_cast<const sf4*>(y + k), y1 = *reinterpret_cast<const sf4*>(y + k + 4);
+            const sf4 y0 = *reinterpret_cast<const sf4*>(ys + k), y1 = *reinterpret_cast<const sf4*>(ys + k + 4);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float q = j < 4 ? q0[j] : q1[j - 4];
@@ -71,6 +77,18 @@ __global__ void __launch_bounds__(256) mb(const float* g, float* out, unsigned l
                     acc.x += tp;
                     acc.y += tn;
                 }
+                else if constexpr (V >= 12 && V <= 15) {  // lane pairs: one side per lane, med3 split
+                    float t;
+                    asm("v_med3_f32 %0, %1, 0, %2" : "=v"(t) : "v"(q), "v"(lim));
+                    if constexpr (V == 15) t = (k + j == i) ? 3.0f : t;
+                    s += t * yk;
+                    if constexpr (V == 13) s2 += yk * q;
+                    if constexpr (V == 14) {
+                        float t2;
+                        asm("v_med3_f32 %0, %1, 0, %2" : "=v"(t2) : "v"(-q), "v"(lim));
+                        s2 += t2 * yk;
+                    }
+                }
                 else if constexpr (V == 11) {  // row scalar + fused aq chain
                     float qp, qn;
                     asm("v_max_f32 %0, %1, 0" : "=v"(qp) : "v"(q));
@@ -85,14 +103,14 @@ __global__ void __launch_bounds__(256) mb(const float* g, float* out, unsigned l
         }
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    out[blockIdx.x * blockDim.x + tid] = s + acc.x + acc.y + acc2.x + acc2.y;
+    out[blockIdx.x * blockDim.x + tid] = s + s2 + acc.x + acc.y + acc2.x + acc2.y;
     if ((tid & 63) == 0) cyc[blockIdx.x * 4 + (tid >> 6)] = t1 - t0;
 }
 
 template <int V>
 void run(const float* g, float* out, unsigned long long* cyc, int n, int threads, const char* name) {
     const int reps = 50;
-    size_t lds = sizeof(float) * (64 * (n + 4) + n + 8);
+    size_t lds = sizeof(float) * (64 * (n + 4) + 2 * (n + 8));
     hipLaunchKernelGGL(mb<V>, dim3(1), dim3(threads), lds, 0, g, out, cyc, n, reps);
     hipLaunchKernelGGL(mb<V>, dim3(1), dim3(threads), lds, 0, g, out, cyc, n, reps);
     hipDeviceSynchronize();
@@ -124,6 +142,10 @@ int main() {
         run<9>(g, out, cyc, n, t, "split pairs scalar");
         run<10>(g, out, cyc, n, t, "product then max");
         run<11>(g, out, cyc, n, t, "row scalar + fused aq");
+        run<12>(g, out, cyc, n, t, "lane pair med3");
+        run<13>(g, out, cyc, n, t, "lane pair med3 + fused aq");
+        run<14>(g, out, cyc, n, t, "lane pair med3, 2 rows");
+        run<15>(g, out, cyc, n, t, "lane pair med3 + diag");
     }
     return 0;
 }

@@ -35,7 +35,6 @@ def main(Hs):
 
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
-    pqp_amd.tune("mid_split", int(os.environ.get("MID_SPLIT", "0")))
     for H in Hs:
         P = block_diag_problem(base, H)
         N, M = P["N"], P["M"]

@@ -25,7 +25,7 @@ def main(Hs):
     from oracle import Oracle, block_diag_problem
 
     base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
-    pqp_amd.tune("mid_split", int(os.environ.get("MID_SPLIT", "0")))
+    pqp_amd.tune("mid_v1", int(os.environ.get("MID_V1", "0")))
     B = int(os.environ.get("B", "4096"))
     ntr = 256
     buf = torch.zeros(ntr * 16, dtype=torch.int64, device="cuda")

@@ -1,7 +1,7 @@
 """k_solve_pipe build variants (pqp_tune "pipe_variant") on the bench's
 batch_converge workload: steady-state ms per iteration (3K-call minus K-call,
 as bench.py's leg) on infeasible and all-feasible iterates, and each variant's
-phase trace.  Usage: python scripts/pipe_variants.py [variants, e.g. 0,1,2,3]"""
+phase trace.  Usage: python scripts/pipe_variants.py [variants, e.g. 0,3]"""
 from __future__ import annotations
 
 import ctypes as C
@@ -60,4 +60,4 @@ def main(variants):
 
 
 if __name__ == "__main__":
-    main([int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3").split(",")])
+    main([int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,3").split(",")])

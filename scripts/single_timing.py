@@ -29,11 +29,9 @@ def main(N: int = 1024, iters: int = 1000, reps: int = 5):
     out = {"n_dual": N, "iterations": iters}
     with pqp_amd.Problem(P) as prob:
         ys = {}
-        variants = [("split_multi_wg", 0), ("stream_u16_lw64", (1 << 14) | (4 << 17)),
-                    ("stream_u16_lw8", (1 << 14) | (1 << 17))]
-        for kind, kn in ((2, "w4s64"), (3, "w8s32"), (4, "w16s16"), (5, "w8s16")):
-            for lwsel, lw in ((1, 8), (2, 16), (4, 64)):
-                variants.append((f"relay_{kn}_lw{lw}", (kind << 14) | (lwsel << 17)))
+        variants = [("split_multi_wg", 0)]
+        for lwsel, lw in ((1, 8), (2, 16), (4, 64)):
+            variants.append((f"relay_w8s16_lw{lw}", lwsel << 17))
         variants.append(("single_wg", 0x200))
         variants.insert(0, ("persistent", 0))
         for name, var in variants:

@@ -35,11 +35,9 @@ def main():
         out = {"n_dual": N, "m": M}
         ys = {}
         with pqp_amd.Problem(P) as prob:
-            arms = [("wide", 0, 0, 200), ("wide_fork", 0, 1, 200), ("wide_s64", 0, 2, 200),
-                    ("single_wg", 0x200, 0, 20)]
-            for name, var, wf, cap in arms:
+            arms = [("wide", 0, 200), ("single_wg", 0x200, 20)]
+            for name, var, cap in arms:
                 L.pqp_tune_set_variant(var)
-                L.pqp_tune_wide_flags(wf)
                 prob.solve(max_updates=2)
                 t0 = time.perf_counter()
                 r = prob.solve(max_updates=cap)
@@ -47,7 +45,6 @@ def main():
                 out[name] = {"updates": cap, "us_per_iter": dt / (cap + 1) * 1e6}
                 ys[name] = (r, cap)
             L.pqp_tune_set_variant(0)
-            L.pqp_tune_wide_flags(0)
             r = prob.solve(max_updates=20)
         out["bit_identical_at_20"] = bool(np.array_equal(r["Y"].view(np.uint32), ys["single_wg"][0]["Y"].view(np.uint32)))
         out["speedup"] = out["single_wg"]["us_per_iter"] / out["wide"]["us_per_iter"]

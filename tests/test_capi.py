@@ -87,10 +87,10 @@ def _gfx950_asm(name: str) -> str:
 
 @pytest.mark.parametrize("src,pattern,min_kernels", [
     ("pqp_kernels.hip",
-     r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|14k_split_update|12k_fixed_tiny"
-     r"|12k_solve_wave|12k_lean_relay|12k_solve_pipe)",
-     35),
-    ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 3),
+     r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|12k_fixed_tiny"
+     r"|12k_solve_wave|12k_lean_relay|12k_solve_pipe|12k_solve_mid2|11k_matmul_pk)",
+     30),
+    ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 2),
     ("pqp_persist.hip", r"_ZN3pqp15k_split_persist", 1),
     ("pqp_converge.hip", r"_ZN3pqp12_GLOBAL__N_118k_converge_persist", 1),
 ])
@@ -220,8 +220,8 @@ def test_tuning_knobs_roundtrip():
     import pqp_amd
 
     L = pqp_amd.lib()
-    for key in ("persist_off", "lean_min_n", "batch_opts", "split_kind", "converge_chunk", "wide_min_n", "pipe_off",
-                "pipe_variant", "pipe_force"):
+    for key in ("persist_off", "lean_min_n", "batch_opts", "converge_chunk", "wide_min_n", "pipe_off",
+                "pipe_variant", "pipe_force", "mid_v1", "matmul_pk_off"):
         old = pqp_amd.tune_get(key)
         assert pqp_amd.tune(key, old + 3) == old
         assert pqp_amd.tune_get(key) == old + 3
@@ -229,12 +229,13 @@ def test_tuning_knobs_roundtrip():
     assert pqp_amd.tune("relay_spin_max", 2**40) == 1 << 20 and pqp_amd.tune_get("relay_spin_max") == 1 << 30
     pqp_amd.tune("relay_spin_max", 0)
     assert pqp_amd.tune_get("relay_spin_max") == 1 << 20
-    with pytest.raises(pqp_amd.PQPError):
-        pqp_amd.tune("no_such_knob", 1)
-    prev = L.pqp_tune_set_variant((3 << 17) | (2 << 14) | 0x200)
-    assert pqp_amd.tune_get("split_lw") == 32 and pqp_amd.tune_get("split_kind") == 2
+    for gone in ("no_such_knob", "split_kind", "split_u", "fixed_tiny_old", "single_occ4", "wide_flags", "mid_split"):
+        with pytest.raises(pqp_amd.PQPError):  # round 4 removed the measured-slower arms behind these
+            pqp_amd.tune(gone, 1)
+    prev = L.pqp_tune_set_variant((3 << 17) | 0x200)
+    assert pqp_amd.tune_get("split_lw") == 32
     assert pqp_amd.tune_get("force_single") == 1
-    assert L.pqp_tune_set_variant(prev) == (3 << 17) | (2 << 14) | 0x200
+    assert L.pqp_tune_set_variant(prev) == (3 << 17) | 0x200
     assert L.pqp_tune_batch_converge(1 | 4 | 16) == 0 and pqp_amd.tune_get("single_scalar") == 1
     assert L.pqp_tune_batch_converge(0) == 1 | 4 | 16
     fb = C.c_longlong(-1)

@@ -1,7 +1,9 @@
-"""Batched solves of mid-size problems on k_solve_mid: one
-workgroup per problem with Gp, Qp_inv, Qp and either the reference's stored
-split matrices (where they fit, about N <= 100) or Qd held in LDS once, the
-update's split entries then formed on the fly (v_max_f32 form when the
+"""Batched solves of mid-size problems, path 3: one
+workgroup per problem.  Default (round 4) k_solve_mid2: terminate(Y_h) on
+other waves beside the update to Y_{h+1}, each update row summed as two lane
+sides (v_med3_f32 split entries).  Knobs: mid_v1 (k_solve_mid: terminate()
+after the update).  k_solve_mid holds Qd, Gp, Qp_inv and Qp in LDS once,
+the update's split entries formed on the fly (v_max_f32 form when the
 problem's Qd holds no NaN, the reference's selects otherwise).
 Bar: the oracle's h, Y and U bit for bit -- the bundled plant over H horizon
 blocks (stops at the reference's h = 313), synthetic problems capped with
@@ -19,6 +21,8 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 MID = 3
+# mid_v1 -> the kernel path 3 launches (pqp_tune_get last_batch_kernel)
+FORMS = {"mid2": (0, 3), "v1": (1, 2)}
 
 
 def _batch(gpu_lib, Ps):
@@ -56,8 +60,8 @@ def _bundled(golden_bundled):
 
 
 @pytest.mark.parametrize("H", [2, 3, 4, 5])
-@pytest.mark.parametrize("mid_off,split", [(0, 0), (0, 1), (1, 0)])
-def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off, split):
+@pytest.mark.parametrize("mid_off,v1", [(0, 0), (0, 1), (1, 0)])
+def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off, v1):
     """The bundled plant as H diagonal blocks (n_dual 28 H) stops at h = 313
     (the oracle's, itself pinned to oracle/_ref for 9 and 36 blocks): 8 copies
     in one launch, every value bit for bit."""
@@ -65,24 +69,28 @@ def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs,
 
     Q = block_diag_problem(_bundled(golden_bundled), H)
     knobs("mid_off", mid_off)
-    knobs("mid_split", split)
+    knobs("mid_v1", v1)
     if not mid_off:
         assert gpu_lib.lib().pqp_batch_solve_path(Q["N"], Q["M"]) == MID
     pb = _batch(gpu_lib, [Q] * 8).solve(max_updates=CAP)
+    if not mid_off:
+        assert gpu_lib.tune_get("last_batch_kernel") == (2 if v1 else 3)
     h, Y, U = orc.solve(Q, max_updates=CAP)
     assert h == 313
     for b in (0, 7):
         _check(pb, b, h, Y, U, f"H={H} copy {b} mid_off={mid_off}")
 
 
-@pytest.mark.parametrize("chunk", [1, 7, 50])
-def test_horizon_blocks_chunked(gpu_lib, golden_bundled, orc, knobs, chunk):
+@pytest.mark.parametrize("v1", [0, 1])
+@pytest.mark.parametrize("chunk", [1, 2, 7, 50])
+def test_horizon_blocks_chunked(gpu_lib, golden_bundled, orc, knobs, chunk, v1):
     """Launches of `chunk` iterates per problem, resumed from Y in HBM: the
     stop lands inside a later launch, same bits."""
     from oracle import block_diag_problem
 
     Q = block_diag_problem(_bundled(golden_bundled), 3)
     knobs("batch_chunk", chunk)
+    knobs("mid_v1", v1)
     pb = _batch(gpu_lib, [Q] * 3).solve(max_updates=CAP)
     h, Y, U = orc.solve(Q, max_updates=CAP)
     for b in range(3):
@@ -91,13 +99,13 @@ def test_horizon_blocks_chunked(gpu_lib, golden_bundled, orc, knobs, chunk):
 
 @pytest.mark.parametrize("N,M", [(33, 5), (40, 20), (57, 57), (64, 16), (100, 50), (127, 31), (150, 40)])
 @pytest.mark.parametrize("feasible", [False, True])
-@pytest.mark.parametrize("split", [0, 1])
-def test_synthetic_capped_vs_oracle(gpu_lib, orc, knobs, N, M, feasible, split):
+@pytest.mark.parametrize("form", list(FORMS))
+def test_synthetic_capped_vs_oracle(gpu_lib, orc, knobs, N, M, feasible, form):
     """Capped solves of synthetic problems; `feasible`: Kp = 1e30, so every
     iterate runs all of computeCost and, from the second on, the Y'Qd sums
-    ride in the update rows.  split 1: the stored-split form where its LDS
-    fits (N <~ 100), 0: the Qd form (default)."""
-    knobs("mid_split", split)
+    ride in the update rows (k_solve_mid) or run on the C waves (mid2)."""
+    v1, _ = FORMS[form]
+    knobs("mid_v1", v1)
     assert gpu_lib.lib().pqp_batch_solve_path(N, M) == MID
     B, cap = 3, 9
     Ps = [orc.synth_problem(31, b, N, M) for b in range(B)]
@@ -110,10 +118,11 @@ def test_synthetic_capped_vs_oracle(gpu_lib, orc, knobs, N, M, feasible, split):
         _check(pb, b, h, Y, U, f"{N}/{M} problem {b} feasible={feasible}")
 
 
-@pytest.mark.parametrize("N,M", [(48, 24), (101, 25)])
-@pytest.mark.parametrize("split", [0, 1])
-def test_fixed_mode_vs_oracle(gpu_lib, orc, knobs, N, M, split):
-    knobs("mid_split", split)
+@pytest.mark.parametrize("N,M", [(48, 24), (101, 25), (150, 36)])
+@pytest.mark.parametrize("form", list(FORMS))
+def test_fixed_mode_vs_oracle(gpu_lib, orc, knobs, N, M, form):
+    v1, _ = FORMS[form]
+    knobs("mid_v1", v1)
     Ps = [orc.synth_problem(32, b, N, M) for b in range(4)]
     pb = _batch(gpu_lib, Ps).solve(gpu_lib.MODE_FIXED, num_iter=40)
     assert np.all(pb.h.cpu().numpy() == 40)
@@ -123,13 +132,14 @@ def test_fixed_mode_vs_oracle(gpu_lib, orc, knobs, N, M, split):
 
 
 @pytest.mark.parametrize("feasible", [False, True])
-@pytest.mark.parametrize("split", [0, 1])
-def test_non_symmetric_qd_mixed(gpu_lib, orc, knobs, feasible, split):
+@pytest.mark.parametrize("form", list(FORMS))
+def test_non_symmetric_qd_mixed(gpu_lib, orc, knobs, feasible, form):
     """Problem 0's Qd is bit-symmetric, problem 1's is not (dense Qp_inv):
     the Y'Qd columns then run beside the update rows instead of inside them."""
     from pqp_amd import dense_qinv
 
-    knobs("mid_split", split)
+    v1, _ = FORMS[form]
+    knobs("mid_v1", v1)
     N, M, cap = 96, 24, 7
     P0 = orc.synth_problem(33, 0, N, M)
     P1 = orc.synth_primal(33, 1, N, M)
@@ -148,14 +158,14 @@ def test_non_symmetric_qd_mixed(gpu_lib, orc, knobs, feasible, split):
         _check(pb, b, h, Y, U, f"problem {b} feasible={feasible}")
 
 
-@pytest.mark.parametrize("split", [0, 1])
-def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, split):
+@pytest.mark.parametrize("form", list(FORMS))
+def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, form):
     """One NaN off the diagonal of row 5: the reference's selects keep it
     (row 5's sums turn NaN), a v_max_f32 form would drop it.  Fixed mode, one
     and two updates: NaN where the oracle has NaN, every other value bit for
-    bit; problem 1 (no NaN) unaffected.  (The stored-split form keeps the
-    reference's literal entries, NaN included.)"""
-    knobs("mid_split", split)
+    bit; problem 1 (no NaN) unaffected."""
+    v1, _ = FORMS[form]
+    knobs("mid_v1", v1)
     N, M = 48, 12
     P0 = orc.synth_problem(34, 0, N, M)
     P1 = orc.synth_problem(34, 1, N, M)
@@ -171,3 +181,76 @@ def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, split):
             assert np.isnan(Y).any() == (b == 0)
             ok = ~np.isnan(Y)
             assert_bitwise(got[ok], Y[ok], f"num_iter={n} problem {b}")
+
+
+@pytest.mark.parametrize("N,M,cap", [(112, 28, 1), (112, 28, 2), (84, 21, 3), (150, 40, 4)])
+def test_mid2_short_caps_and_costs(gpu_lib, orc, knobs, N, M, cap):
+    """k_solve_mid2 decides terminate(Y_h) one phase after it was formed:
+    caps of 1..4 updates stop on the right iterate with its own Y and U
+    (Y_{h+1}, Y_{h+2} are dropped), every iterate feasible (Kp = 1e30) so the
+    costs of the last terminate() run too; the same bits as k_solve_mid."""
+    Ps = [orc.synth_problem(35, b, N, M) for b in range(2)]
+    for P in Ps:
+        P["Kp"] = np.full(N, 1e30, np.float32)
+    pb = _batch(gpu_lib, Ps).solve(max_updates=cap)
+    assert gpu_lib.tune_get("last_batch_kernel") == 3
+    knobs("mid_v1", 1)
+    pv = _batch(gpu_lib, Ps).solve(max_updates=cap)
+    for b, P in enumerate(Ps):
+        h, Y, U = orc.solve(P, max_updates=cap)
+        _check(pb, b, h, Y, U, f"mid2 {N}/{M} cap={cap} problem {b}")
+        _check(pv, b, h, Y, U, f"mid v1 {N}/{M} cap={cap} problem {b}")
+
+
+def _oracle_horizon_problem(orc, states):
+    """The reference's setup of one stacked-horizon problem (the oracle's
+    computeFp / computeMp per stage state, the block-diagonal primal, Mp summed
+    in stage order, Gauss_Jordan and convertToDual of the whole)."""
+    from conftest import EXAMPLE_DIR
+
+    stages = [orc.example_at_state(EXAMPLE_DIR, x) for x in states]
+    H = len(stages)
+    N, M = stages[0]["N"], stages[0]["M"]
+
+    def bd(k, r, c):
+        out = np.zeros((H * r, H * c), np.float32)
+        for h, S in enumerate(stages):
+            out[h * r:(h + 1) * r, h * c:(h + 1) * c] = np.asarray(S[k], np.float32).reshape(r, c)
+        return out.reshape(-1)
+
+    Mp = np.float32(stages[0]["Mp"][0])
+    for S in stages[1:]:
+        Mp = np.float32(Mp + np.float32(S["Mp"][0]))
+    Q = dict(Qp_inv=bd("Qp_inv", M, M), Gp=bd("Gp", N, M), Kp=np.concatenate([S["Kp"] for S in stages]),
+             Fp=np.concatenate([S["Fp"] for S in stages]), Mp=np.array([Mp], np.float32), N=H * N, M=H * M)
+    Q["Qd"], Q["Fd"], Q["Md"] = orc.convert_to_dual(Q["Qp_inv"], Q["Gp"], Q["Kp"], Q["Fp"], Q["Mp"], H * N, H * M)
+    Q["Qp"] = orc.gauss_jordan(Q["Qp_inv"], H * M)
+    return Q
+
+
+@pytest.mark.parametrize("H", [1, 3, 4])
+def test_horizon_batch_built_by_the_product(gpu_lib, golden_bundled, orc, H):
+    """the horizon workload built by the product (pqp_amd.
+    horizon_batch: per-stage computeFp / computeMp, block-diagonal primal,
+    Gauss_Jordan and convertToDual on the GPU) equals the oracle's setup of the
+    same stacked primal bit for bit, and its solves stop at the oracle's h with
+    its Y and U.  Identical stages give oracle.block_diag_problem's Qd, Fd and
+    Qp (the round-3 bench input); perturbed stage states give a real batch."""
+    from conftest import EXAMPLE_DIR
+    from oracle import block_diag_problem
+
+    E = gpu_lib.read_example(EXAMPLE_DIR)
+    B = 6
+    xs = gpu_lib.perturbed_states(E["x"], B * H, seed=7).reshape(B, H, -1)
+    xs[0] = E["x"]  # problem 0: every stage at the example's own state
+    pb = gpu_lib.horizon_batch(EXAMPLE_DIR, H, xs)
+    ref0 = block_diag_problem(_bundled(golden_bundled), H)
+    for k in ("Qd", "Fd", "Qp"):
+        assert_bitwise(getattr(pb, k)[0].cpu().numpy(), ref0[k], f"identical stages {k}")
+    pb.solve(max_updates=CAP)
+    for b in (0, 1, B - 1):
+        Q = _oracle_horizon_problem(orc, xs[b])
+        for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp"):
+            assert_bitwise(getattr(pb, k)[b].cpu().numpy().reshape(-1), np.asarray(Q[k]).reshape(-1), f"{k} of {b}")
+        h, Y, U = orc.solve(Q, max_updates=CAP)
+        _check(pb, b, h, Y, U, f"H={H} problem {b}")

@@ -54,29 +54,26 @@ def _variant_case(orc, N):
     return _VARIANT_CASES[N]
 
 
-@pytest.mark.parametrize("kind,lwsel", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (0, 1), (0, 2), (0, 3), (0, 4),
-                                        (1, 1), (1, 4)])
+@pytest.mark.parametrize("lwsel", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("N", [28, 1025, 2100])
-def test_split_kernel_variants_vs_oracle(gpu_lib, orc, kind, lwsel, N):
-    """Every update kernel behind pqp_rowblock_update (the streaming
-    k_split_update and the relay k_split_relay at each (waves, segment)
-    shape) and every workgroup width (8..64 row sides per workgroup),
-    selected through pqp_tune_set_variant, on ragged blocks; at N = 2100 a
-    wave sums several segments."""
+def test_split_kernel_variants_vs_oracle(gpu_lib, orc, lwsel, N):
+    """The relay update behind pqp_rowblock_update (k_split_relay) at every
+    workgroup width (8..64 row sides per workgroup, pqp_tune_set_variant), on
+    ragged blocks; at N = 2100 a wave sums several segments."""
     import torch
 
     P, want = _variant_case(orc, N)
     Qd = torch.from_numpy(P["Qd"]).cuda()
     Fd = torch.from_numpy(P["Fd"]).cuda()
     L = gpu_lib.lib()
-    prev = L.pqp_tune_set_variant((kind << 14) | (lwsel << 17))
+    prev = L.pqp_tune_set_variant(lwsel << 17)
     try:
         cuts = [N // 3, N // 3 + min(33, N // 3)]
         blocks = [gpu_lib.RowBlock(Qd[r0 * N:], Fd, N, r0, rows) for r0, rows in _blocks(N, cuts)]
         got = _run_blocks(torch, blocks, N, 3)
     finally:
         L.pqp_tune_set_variant(prev)
-    assert_bitwise(got, want, f"kind={kind} lw={lwsel} N={N}")
+    assert_bitwise(got, want, f"lw={lwsel} N={N}")
 
 
 def test_rowblock_bundled_fixed_999(gpu_lib, golden_bundled):
