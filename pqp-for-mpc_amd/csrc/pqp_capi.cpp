@@ -1883,6 +1883,8 @@ const KnobRef* find_knob(const char* key) {
         {"mid_off", &g_tune.mid_off, nullptr, nullptr},
         {"pipe_off", &g_tune.pipe_off, nullptr, nullptr},
         {"mid_v1", &g_tune.mid_v1, nullptr, nullptr},
+        {"mid2_pair", &g_tune.mid2_pair, nullptr, nullptr},
+        {"mid2_min_n", &g_tune.mid2_min_n, nullptr, nullptr},
         {"matmul_pk_off", &g_tune.matmul_pk_off, nullptr, nullptr},
         {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},
         {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},

@@ -955,7 +955,7 @@ __global__ void k_zero_pad(float* __restrict__ QdT, int N, int ldq, long long qs
 }
 
 // ---------------------------------------------------------------------------
-typedef float sf4 __attribute__((ext_vector_type(4)));
+typedef float sf4 __attribute__((ext_vector_type(4)));  // (repeated, same type, in the solve-single region)
 
 // Generic sequential-k product: out[a x c] = op(A)[a x b] op(B)[b x c]
 // (matrixMultiply, PQP_CPU.c:84-147).  One thread per output element; used
@@ -1058,6 +1058,39 @@ __global__ void __launch_bounds__(256) k_matmul_tiled(float* __restrict__ out, c
             if (j < c) out[(size_t)i * c + j] = acc[r][q];
         }
     }
+}
+
+// The mat-vec form out[i] = sum_k A[i][k] x[k] (row-major A, c = 1; the Fd =
+// (Gp Qp_inv) Fp of convertToDual, PQP_CPU.c:456-460, and computeUfromY's
+// products, :352-360) at scale: 256 rows per workgroup, one lane per row
+// summing k = 0..b-1 in order from +0.0f, the rows staged 32 k at a time
+// through LDS with coalesced loads (32 lanes per 128-byte row segment)
+// instead of each lane walking its own row at a stride of b floats.  k past
+// b adds 0*0 = +0.0f to a sum that is never -0.0f.
+__global__ void __launch_bounds__(256) k_matvec_rows(float* __restrict__ out, const float* __restrict__ A,
+                                                     const float* __restrict__ x, int a, int bdim, long long sA,
+                                                     long long sB, long long sO) {
+    __shared__ float T[256][33];
+    __shared__ float xs[32];
+    const int z = blockIdx.y;
+    A += z * sA;
+    x += z * sB;
+    out += z * sO;
+    const int tid = threadIdx.x, row0 = blockIdx.x * 256, i = row0 + tid;
+    float acc = 0.0f;
+    for (int k0 = 0; k0 < bdim; k0 += 32) {
+#pragma unroll 8
+        for (int q = 0; q < 32; ++q) {
+            const int e = q * 256 + tid, r = e >> 5, kk = e & 31;
+            T[r][kk] = (row0 + r < a && k0 + kk < bdim) ? A[(size_t)(row0 + r) * bdim + k0 + kk] : 0.0f;
+        }
+        if (tid < 32) xs[tid] = (k0 + tid < bdim) ? x[k0 + tid] : 0.0f;
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 32; ++kk) acc += T[tid][kk] * xs[kk];  // :88-100, k in order
+        __syncthreads();
+    }
+    if (i < a) out[i] = acc;
 }
 
 // The setup GEMM at scale, on packed fp32: a 128 x 128 output tile per
@@ -1395,6 +1428,7 @@ __device__ __forceinline__ void single_update(const SolveArgs& A, const float* _
 // loads are 8 or 16 bytes per lane, so a wave moves 2-4x the bytes per
 // instruction and a pass needs 2-4x fewer dependent load batches.
 typedef float sf2 __attribute__((ext_vector_type(2)));
+typedef float sf4 __attribute__((ext_vector_type(4)));
 template <int V> struct SVec;
 template <> struct SVec<2> { typedef sf2 t; };
 template <> struct SVec<4> { typedef sf4 t; };
@@ -2641,7 +2675,10 @@ __global__ void __launch_bounds__(64) k_fixed_tiny(SolveArgs A0, SolveState* __r
                 break;
             }
             if (done_here >= A.chunk) break;
-            const float yi = __shfl(yk, 2 * ic);  // this row's y_i on both of its lanes
+            // this row's y_i (lane 2i) on its den lane 2i+1: DPP quad_perm
+            // [0,0,2,2] within the quad, no LDS round trip (a ds_bpermute here
+            // left its latency after the division, on the loop's critical path)
+            const float yi = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(yk), 0xA0, 0xF, 0xF, true));
             float p[NMAX];
 #pragma unroll
             for (int k = 0; k < NMAX; k += 2) {
@@ -3645,7 +3682,7 @@ __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
     L.dN = L.tq + L.nk;             // phase, then their space is the tq ring's
     L.Fdp = o;  o += L.nk;
     L.Fdn = o;  o += L.nk;
-    L.flag = o; o += 8;             // [0..3] checkFeas flags per C row wave; [4 + s&1] Y non-finite
+    L.flag = o; o += 16;            // [0..11] checkFeas flags per C row wave; [12 + s&1] Y non-finite
     if (conv) {
         L.Kp = o;   o += L.nk;
         L.tM = o;   o += L.mk;
@@ -3669,17 +3706,23 @@ __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
     L.total = o;
     return L;
 }
-__host__ __device__ inline int mid2_uw(int N) { return (N + 31) / 32; }
-// mid2 takes (N, M) in converge or fixed mode when its waves fit 8
-__host__ __device__ inline bool mid2_fits(int N, int M, bool conv) {
-    return N <= 160 && (!conv || M < 64) && mid2_uw(N) + (conv ? 3 : 0) <= 8;
+// waves of each role: UW (PAIR: 32 rows per wave, lane sides; else 64 rows,
+// one lane per row), T (one), C (ceil(N/64) row waves and the cost wave)
+__host__ __device__ inline int mid2_uw(int N, bool pair) { return pair ? (N + 31) / 32 : (N + 63) / 64; }
+__host__ __device__ inline int mid2_waves(int N, bool conv, bool pair) {
+    return mid2_uw(N, pair) + (conv ? 1 + (N + 63) / 64 + 1 : 0);
+}
+// mid2 takes (N, M) in converge or fixed mode when T fits one wave and the
+// workgroup 16
+__host__ __device__ inline bool mid2_fits(int N, int M, bool conv, bool pair) {
+    return (!conv || M < 64) && mid2_waves(N, conv, pair) <= 16;
 }
 
 // 8 terms of one side of update row i (k .. k+7).  FAST: the v_med3_f32
 // split (no NaN in Qd, Y finite); else the reference's selects on +y.  DIAG:
 // the block holds the diagonal of some rows of this wave.
 template <bool FAST, bool DIAG>
-__device__ __forceinline__ void mid2_block(float& acc, sf4 q0, sf4 q1, sf4 y0, sf4 y1, int k, int i, int side,
+__device__ __forceinline__ void mid2_block(float& acc, sf4 q0, sf4 q1, sf4 y0, sf4 y1, int k, int w0, int side,
                                            float lim, float dv) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -3691,7 +3734,13 @@ __device__ __forceinline__ void mid2_block(float& acc, sf4 q0, sf4 q1, sf4 y0, s
         } else {
             t = side ? ((qk < 0.0f) ? 0.0f : qk) : ((qk > 0.0f) ? 0.0f : -qk);
         }
-        if constexpr (DIAG) t = (k + j == i) ? dv : t;
+        if constexpr (DIAG) {
+            // k + j is the diagonal of row w0 + r, r = k + j - w0 (uniform): its
+            // two lanes 2r, 2r + 1 take the literal, by a mask made on the
+            // scalar unit -- one v_cndmask per k instead of a compare and a select
+            const unsigned long long m = 3ull << (2 * (k + j - w0));
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(t) : "v"(t), "v"(dv), "s"(m));
+        }
         acc += t * yk;
     }
 }
@@ -3707,15 +3756,43 @@ __device__ __forceinline__ float mid2_side(const float* q, const float* y, int n
         const int kn = (k + 8 < nk) ? k + 8 : k;  // next block (the last one re-read at the end)
         const sf4 nq0 = *reinterpret_cast<const sf4*>(q + kn), nq1 = *reinterpret_cast<const sf4*>(q + kn + 4);
         const sf4 ny0 = *reinterpret_cast<const sf4*>(y + kn), ny1 = *reinterpret_cast<const sf4*>(y + kn + 4);
-        if (k >= w0 && k < w0 + 32) mid2_block<FAST, true>(acc, q0, q1, y0, y1, k, i, side, lim, dv);
-        else mid2_block<FAST, false>(acc, q0, q1, y0, y1, k, i, side, lim, dv);
+        if (k >= w0 && k < w0 + 32) mid2_block<FAST, true>(acc, q0, q1, y0, y1, k, w0, side, lim, dv);
+        else mid2_block<FAST, false>(acc, q0, q1, y0, y1, k, w0, side, lim, dv);
         q0 = nq0; q1 = nq1; y0 = ny0; y1 = ny1;
     }
     return acc;
 }
 
-template <int NT>
-__global__ void __launch_bounds__(NT, 4) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
+// one update row on one lane, both sides packed (k_solve_mid's form,
+// row_step): Y_next[i] = num / den * y_i (PQP_CPU.c:603-618)
+template <bool FAST>
+__device__ __forceinline__ float mid2_row(const float* q, const float* y, int nk, int i, float dp, float dn,
+                                          float fdn, float fdp, int w0) {
+    sf2 acc = {0.0f, 0.0f};
+    float aq = 0.0f;
+    RowBlk c, x;
+    row_load(c, q, y, 0);
+    int k = 0;
+    for (; k + 16 < nk; k += 16) {
+        row_load(x, q, y, k + 8);
+        row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
+        row_load(c, q, y, k + 16);
+        row_step<false, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
+    }
+    if (k + 8 < nk) {
+        row_load(x, q, y, k + 8);
+        row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
+        row_step<false, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
+    } else {
+        row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
+    }
+    const float num = acc.y + 1.0f * fdn;  // :611
+    const float den = acc.x + 1.0f * fdp;  // :612
+    return num / den * y[i];               // :594
+}
+
+template <int MAXT, bool PAIR>
+__global__ void __launch_bounds__(MAXT) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
     SolveState* st = st0 + blockIdx.x;
@@ -3742,10 +3819,11 @@ __global__ void __launch_bounds__(NT, 4) k_solve_mid2(SolveArgs A0, SolveState* 
     float* Fp = lds + L.Fp;
     float* fdy = lds + L.fdy;
     float* sums = lds + L.sums;
-    int* flag = reinterpret_cast<int*>(lds + L.flag);  // [0..3] checkFeas per C row wave, [4 + p] Y non-finite
+    int* flag = reinterpret_cast<int*>(lds + L.flag);  // [0..11] checkFeas per C row wave, [12 + p] Y non-finite
+    const int NT = blockDim.x;  // 64 * mid2_waves(N, conv, PAIR)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int nUW = mid2_uw(N), wT = nUW, wC0 = nUW + 1, nC = NT / 64 - wC0;
-    const int nCR = nC - 1;  // C waves that take checkFeas rows and the Y'Qd columns; the last one the costs
+    const int nUW = mid2_uw(N, PAIR), wT = nUW, wC0 = nUW + 1;
+    const int nCR = (N + 63) / 64;  // C waves that take checkFeas rows and the Y'Qd terms; wave wC0 + nCR the costs
 
     // ---- stage the problem (once per launch; padding zero) ----
     for (int e = tid; e < L.total; e += NT) lds[e] = 0.0f;
@@ -3781,109 +3859,56 @@ __global__ void __launch_bounds__(NT, 4) k_solve_mid2(SolveArgs A0, SolveState* 
         if (!(fabsf(y) <= 3.402823466e38f)) ynf = 1;
     }
     __syncthreads();
-    // computeTheta (:503-519), the diagonal literals (:524-537); any NaN in Qd?
-    int nan = 0;
+    // computeTheta (:503-519), the diagonal literals (:524-537); any NaN in
+    // Qd?  Qd bit-symmetric (then Y'Qd's column j is row j's dot, read 16 bytes
+    // at a time)?
+    int nan = 0, asym = 0;
     for (int i = tid; i < N; i += NT) {
         const float* row = Qd + i * ldn;
         float s = 0.0f;
         for (int k = 0; k < N; ++k) {
             s += max_ref(0.0f, -row[k]) * 1.0f;
             if (row[k] != row[k]) nan = 1;
+            if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
         }
         const float th = max_ref(s, 5.0f), qii = row[i];
         dP[i] = max_ref(0.0f, qii) + 1.0f * th;
         dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
     }
+    const bool sym = !__syncthreads_or(asym);
     const bool fast = !__syncthreads_or(nan);
     bool y_nonfinite = __syncthreads_or(ynf);
     const float Md = conv ? A.Md[0] : 0.0f, Mp = conv ? A.Mp[0] : 0.0f;
 
-    // per-lane constants of the update role
-    const int side = lane & 1, urow = 32 * wave + (lane >> 1);
+    // per-lane constants of the update role.  PAIR: lane 2r + side holds one
+    // side of row 32 w + r (side 0 sums the negated num terms, so its diagonal
+    // literal is -dN); else lane l holds row 64 w + l, both sides packed.
+    const int side = lane & 1;
+    const int urow = PAIR ? 32 * wave + (lane >> 1) : 64 * wave + lane;
     const bool uw = wave < nUW && urow < N;
     const float lim = side ? __builtin_inff() : -__builtin_inff();
-    const float dv = uw ? (side ? dP[urow] : -dN[urow]) : 0.0f;  // side 0 sums the negated terms
+    const float dpr = uw ? dP[urow] : 0.0f, dnr = uw ? dN[urow] : 0.0f;
+    const float dv = side ? dpr : -dnr;
     const float fdv = uw ? (side ? Fdp[urow] : Fdn[urow]) : 0.0f;
-    const int w0 = 32 * wave;
+    const float fdp = uw ? Fdp[urow] : 0.0f, fdn = uw ? Fdn[urow] : 0.0f;
+    // uniform: the diagonal masks are scalar
+    const int w0 = __builtin_amdgcn_readfirstlane(PAIR ? 32 * wave : 64 * wave);
     __syncthreads();  // dP / dN read: the tq ring may be written from here on
-
     const bool tr = A0.trace && (int)blockIdx.x < A0.trace_n;
     unsigned long long busy = 0, t_phase = 0, n_ph = 0, t0 = 0;
 
     float Jp_last = 0.0f, Jd_last = 0.0f;
     bool costs = false;
     int status = kStatusContinue;
-    long long s = h0, t_out = h0;
-    for (;;) {
-        const bool pend = conv && s > h0;  // terminate(s-1) is this phase's C work
-        const float* ycur = Yr + (int)(s % 3) * nk;
-        float* ynext = Yr + (int)((s + 1) % 3) * nk;
-        // Y_{s+1}'s non-finite flag goes to slot (s+1)&1; slot s&1 was last read
-        // before the previous phase's second barrier
-        if (tid == 0) flag[4 + (int)(s & 1)] = 0;
-        if (tr) t0 = __builtin_amdgcn_s_memtime();
-        if (wave < nUW) {
-            // ---------------- UW: Y_{s+1} = updateY2(Y_s) ----------------
-            if (uw) {
-                const float* q = Qd + urow * ldn;
-                float acc = (fast && !y_nonfinite) ? mid2_side<true>(q, ycur, nk, urow, side, lim, dv, w0)
-                                                   : mid2_side<false>(q, ycur, nk, urow, side, lim, side ? dv : -dv, w0);
-                if (fast && !y_nonfinite && !side) acc = 0.0f - acc;  // num's terms were summed negated
-                const float v = acc + 1.0f * fdv;                     // num += Fdn :611; den += Fdp :612
-                const float other = __shfl_xor(v, 1);
-                if (side) {
-                    const float y = ycur[urow];
-                    const float yn = other / v * y;  // updY :594
-                    ynext[urow] = yn;
-                    if (!(fabsf(yn) <= 3.402823466e38f)) flag[4 + (int)((s + 1) & 1)] = 1;
-                }
-            }
-        } else if (conv && wave == wT) {
-            // ------------- T: tM = Gp'Y_s + Fp, Fd.Y_s, U_s = -Qp_inv tM -------------
-            if (lane <= M) {
-                const float d = mid_dot_row(Gp + (lane < M ? lane : mk) * ldg, ycur, nk);
-                if (lane < M) tM[lane] = d + 1.0f * Fp[lane];  // :355-356
-                else fdy[s & 1] = d;                            // Fd.Y :656
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (lane < M) Us[(s & 1) * mk + lane] = -mid_dot_row(Qi + lane * ldi, tM, mk);  // :357-358
-        } else if (conv) {
-            // ---------------- C: terminate(Y_{s-1}); Y_s'Qd ----------------
-            const int cw = wave - wC0;
-            const float* Uo = Us + ((s - 1) & 1) * mk;
-            if (cw < nCR) {
-                const int l = cw * 64 + lane;
-                int bad = 0;
-                if (pend)
-                    for (int i = l; i < N; i += 64 * nCR) {
-                        const float g = mid_dot(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
-                        const float kp = Kp[i];
-                        if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
-                    }
-                if (pend && lane == 0) flag[cw] = __any(bad) ? 1 : 0;
-                float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
-                for (int j = l; j < N; j += 64 * nCR) tqs[j] = mid_dot(Qd + j, ldn, ycur, nk) * ycur[j];  // :652-655
-            } else if (pend) {
-                if (lane < M) {
-                    tu[lane] = mid_dot(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
-                    fu[lane] = Fp[lane] * Uo[lane];                         // Fp'U :656-657
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (lane < 3) {
-                    const float* v = lane == 0 ? tq + ((s - 1) & 1) * nk : (lane == 1 ? tu : fu);
-                    const float r = mid_sum(v, lane == 0 ? nk : mk);
-                    sums[lane] = r;
-                }
-            }
-        }
-        if (tr) busy += __builtin_amdgcn_s_memtime() - t0;
-        __syncthreads();
-        if (tr && wave == 0) {
-            t_phase += __builtin_amdgcn_s_memtime() - t0;
-            ++n_ph;
-        }
-        if (pend) {
-            // ------- terminate(s-1)'s decision, on every thread -------
+    long long t_out = h0;
+    // After phase s's barrier, on every thread: terminate(s-1)'s decision
+    // (converge mode) or the fixed-mode loop test.  Returns true to leave the
+    // loop (status and t_out set).  Every wave runs its role in a loop of its
+    // own (so each role's registers are allocated apart), each iteration with
+    // the same two barriers and this same uniform decision.
+    auto decide = [&](long long s) -> bool {
+        if (conv) {
+            if (s == h0) return false;  // nothing pending in the launch's first phase
             const long long t = s - 1;
             int infeasible = 0;
             for (int c = 0; c < nCR; ++c) infeasible |= flag[c];
@@ -3906,16 +3931,121 @@ __global__ void __launch_bounds__(NT, 4) k_solve_mid2(SolveArgs A0, SolveState* 
                 costs = true;
             }
             t_out = t;
-            if (stop) { status = kStatusDone; break; }
-            if (A.max_updates > 0 && t - 1 >= A.max_updates) { status = kStatusCapped; break; }
-            if (t - h0 >= A.chunk) { status = kStatusContinue; break; }
-        } else if (!conv) {
-            if (s >= A.num_iter) { t_out = s; status = kStatusDone; break; }  // while(h < NUM_ITER)
-            if (s - h0 >= A.chunk) { t_out = s; status = kStatusContinue; break; }
+            if (stop) { status = kStatusDone; return true; }
+            if (A.max_updates > 0 && t - 1 >= A.max_updates) { status = kStatusCapped; return true; }
+            if (t - h0 >= A.chunk) { status = kStatusContinue; return true; }
+            return false;
         }
-        y_nonfinite = flag[4 + (int)((s + 1) & 1)] != 0;  // Y_{s+1}, the next phase's Y_s
-        __syncthreads();             // everyone has read this phase's flags before the next phase writes
-        ++s;
+        t_out = s;
+        if (s >= A.num_iter) { status = kStatusDone; return true; }  // while(h < NUM_ITER)
+        if (s - h0 >= A.chunk) { status = kStatusContinue; return true; }
+        return false;
+    };
+    auto phase_end = [&](long long s) -> bool {
+        if (tr) busy += __builtin_amdgcn_s_memtime() - t0;
+        __syncthreads();
+        if (tr && wave == 0) {
+            t_phase += __builtin_amdgcn_s_memtime() - t0;
+            ++n_ph;
+        }
+        return decide(s);
+    };
+
+    if (wave < nUW) {
+        // ---------------- UW: Y_{s+1} = updateY2(Y_s) ----------------
+        const float* q = Qd + (uw ? urow : 0) * ldn;
+        for (long long s = h0;; ++s) {
+            const float* ycur = Yr + (int)(s % 3) * nk;
+            float* ynext = Yr + (int)((s + 1) % 3) * nk;
+            // Y_{s+1}'s non-finite flag goes to slot (s+1)&1; slot s&1 was last
+            // read before the previous phase's second barrier
+            if (tid == 0) flag[12 + (int)(s & 1)] = 0;
+            if (tr) t0 = __builtin_amdgcn_s_memtime();
+            if (uw) {
+                if constexpr (PAIR) {
+                    float acc = (fast && !y_nonfinite) ? mid2_side<true>(q, ycur, nk, urow, side, lim, dv, w0)
+                                                       : mid2_side<false>(q, ycur, nk, urow, side, lim, side ? dv : -dv, w0);
+                    if (fast && !y_nonfinite && !side) acc = 0.0f - acc;  // num's terms were summed negated
+                    const float v = acc + 1.0f * fdv;                     // num += Fdn :611; den += Fdp :612
+                    const float other = __shfl_xor(v, 1);
+                    if (side) {
+                        const float y = ycur[urow];
+                        const float yn = other / v * y;  // updY :594
+                        ynext[urow] = yn;
+                        if (!(fabsf(yn) <= 3.402823466e38f)) flag[12 + (int)((s + 1) & 1)] = 1;
+                    }
+                } else {
+                    // k_solve_mid's row (max form, or the selects where Qd holds a NaN)
+                    const float yn = fast ? mid2_row<true>(q, ycur, nk, urow, dpr, dnr, fdn, fdp, w0)
+                                          : mid2_row<false>(q, ycur, nk, urow, dpr, dnr, fdn, fdp, w0);
+                    ynext[urow] = yn;
+                }
+            }
+            if (phase_end(s)) break;
+            y_nonfinite = flag[12 + (int)((s + 1) & 1)] != 0;  // Y_{s+1}, the next phase's Y_s
+            __syncthreads();  // everyone has read this phase's flags before the next phase writes
+        }
+    } else if (conv && wave == wT) {
+        // ------------- T: tM = Gp'Y_s + Fp, Fd.Y_s, U_s = -Qp_inv tM -------------
+        const float* grow = Gp + (lane < M ? lane : mk) * ldg;
+        const float* qirow = Qi + (lane < M ? lane : 0) * ldi;
+        const float fpl = lane < M ? Fp[lane] : 0.0f;
+        for (long long s = h0;; ++s) {
+            const float* ycur = Yr + (int)(s % 3) * nk;
+            if (tr) t0 = __builtin_amdgcn_s_memtime();
+            if (lane <= M) {
+                const float d = mid_dot_row(grow, ycur, nk);
+                if (lane < M) tM[lane] = d + 1.0f * fpl;  // :355-356
+                else fdy[s & 1] = d;                      // Fd.Y :656
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < M) Us[(s & 1) * mk + lane] = -mid_dot_row(qirow, tM, mk);  // :357-358
+            if (phase_end(s)) break;
+            __syncthreads();
+        }
+    } else if (conv) {
+        // ---------------- C: terminate(Y_{s-1}); Y_s'Qd ----------------
+        const int cw = wave - wC0;
+        for (long long s = h0;; ++s) {
+            const float* ycur = Yr + (int)(s % 3) * nk;
+            const bool pend = s > h0;
+            const float* Uo = Us + ((s - 1) & 1) * mk;
+            if (tr) t0 = __builtin_amdgcn_s_memtime();
+            if (cw < nCR) {
+                const int l = cw * 64 + lane;
+                int bad = 0;
+                if (pend)
+                    for (int i = l; i < N; i += 64 * nCR) {
+                        const float g = mid_dot(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
+                        const float kp = Kp[i];
+                        if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
+                    }
+                if (pend && lane == 0) flag[cw] = __any(bad) ? 1 : 0;
+                float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
+                for (int j = l; j < N; j += 64 * nCR)  // (Y'Qd)_j Y_j :652-655; column j = row j when Qd is symmetric
+                    tqs[j] = (sym ? mid_dot_row(Qd + j * ldn, ycur, nk) : mid_dot(Qd + j, ldn, ycur, nk)) * ycur[j];
+            } else if (pend && cw == nCR) {
+                if (lane < M) {
+                    tu[lane] = mid_dot(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
+                    fu[lane] = Fp[lane] * Uo[lane];                         // Fp'U :656-657
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 3) {
+                    const float* v = lane == 0 ? tq + ((s - 1) & 1) * nk : (lane == 1 ? tu : fu);
+                    const float r = mid_sum(v, lane == 0 ? nk : mk);
+                    sums[lane] = r;
+                }
+            }
+            if (phase_end(s)) break;
+            __syncthreads();
+        }
+    } else {
+        // fixed mode: the waves beside the update keep the barrier count
+        for (long long s = h0;; ++s) {
+            if (tr) t0 = __builtin_amdgcn_s_memtime();
+            if (phase_end(s)) break;
+            __syncthreads();
+        }
     }
     // the result: Y and U of iterate t_out (converge) or Y_s (fixed)
     const float* yo = Yr + (int)(t_out % 3) * nk;
@@ -3949,10 +4079,14 @@ size_t solve_mid_lds_bytes(int N, int M, bool conv) {
 constexpr size_t kMidLdsBudget = 150 * 1024;
 
 static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
-    if (a.mode != kModeTerminate && !g_tune.mid_v1 && mid2_fits(a.N, a.M, a.mode == kModeConverge)) {
-        const size_t lds = sizeof(float) * (size_t)mid2_layout(a.N, a.M, a.mode == kModeConverge).total;
+    const bool conv2 = a.mode == kModeConverge;
+    const bool pair = g_tune.mid2_pair != 0;
+    if (a.mode != kModeTerminate && !g_tune.mid_v1 && a.N >= g_tune.mid2_min_n && mid2_fits(a.N, a.M, conv2, pair)) {
+        const size_t lds = sizeof(float) * (size_t)mid2_layout(a.N, a.M, conv2).total;
         if (lds <= kMidLdsBudget) {
-            hipLaunchKernelGGL((k_solve_mid2<512>), dim3(B), dim3(512), lds, s, a, st);
+            const int nt = 64 * mid2_waves(a.N, conv2, pair);
+            if (pair) hipLaunchKernelGGL((k_solve_mid2<1024, true>), dim3(B), dim3(nt), lds, s, a, st);
+            else hipLaunchKernelGGL((k_solve_mid2<1024, false>), dim3(B), dim3(nt), lds, s, a, st);
             g_last_batch_kernel = 3;
             return hipGetLastError();
         }
@@ -4116,6 +4250,11 @@ hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const 
     if (n == 0 || B == 0) return hipSuccess;
     for (int b0 = 0; b0 < B; b0 += 65535) {  // grid y / z limit
         const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        if (c == 1 && !tA && a >= 64 && b >= 32 && !g_tune.matmul_tiled_off) {
+            hipLaunchKernelGGL(k_matvec_rows, dim3(cdiv(a, 256), nb), dim3(256), 0, s, out + b0 * sO, A + b0 * sA,
+                               Bm + b0 * sB, a, b, sA, sB, sO);
+            continue;
+        }
         const long long tiles = (long long)cdiv(c, MM8) * cdiv(a, MM8);
         if (use_pk(out, A, tA, Bm, tB, a, b, c, sA, sB, sO) && tiles * nb < (1LL << 31)) {
             float* o = out + b0 * sO;
@@ -4212,11 +4351,20 @@ __device__ __forceinline__ void gj_steps(float (&v)[4 * C], const float* __restr
             }
             const float t = mji / Pd[s];  // temp (:298)
             const float* prow = P + (size_t)s * W;
+            typedef float f2v __attribute__((ext_vector_type(2)));
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const sf4 q = *reinterpret_cast<const sf4*>(prow + 256 * c + 4 * lane);
+                // m_jk - m_ik * temp (:301), two elements per packed multiply
+                // and packed add of the negated product (each half rounds as
+                // the scalar op; a - b == a + (-b) exactly)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[4 * c + e] -= q[e] * t;  // (:301)
+                for (int e = 0; e < 4; e += 2) {
+                    const f2v pr = f2v{q[e], q[e + 1]} * f2v{t, t};
+                    const f2v r = f2v{v[4 * c + e], v[4 * c + e + 1]} + (-pr);
+                    v[4 * c + e] = r.x;
+                    v[4 * c + e + 1] = r.y;
+                }
             }
         }
     }

@@ -26,6 +26,8 @@ def main(Hs):
 
     base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
     pqp_amd.tune("mid_v1", int(os.environ.get("MID_V1", "0")))
+    pqp_amd.tune("mid2_pair", int(os.environ.get("MID2_PAIR", "0")))
+    pqp_amd.tune("mid2_min_n", 0)
     B = int(os.environ.get("B", "4096"))
     ntr = 256
     buf = torch.zeros(ntr * 16, dtype=torch.int64, device="cuda")

@@ -21,8 +21,9 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 MID = 3
-# mid_v1 -> the kernel path 3 launches (pqp_tune_get last_batch_kernel)
-FORMS = {"mid2": (0, 3), "v1": (1, 2)}
+# form -> (mid_v1, mid2_pair, kernel path 3 launches: pqp_tune_get last_batch_kernel);
+# the mid2 forms run on every size here (mid2_min_n 0)
+FORMS = {"mid2": (0, 0, 3), "pair": (0, 1, 3), "v1": (1, 0, 2)}
 
 
 def _batch(gpu_lib, Ps):
@@ -38,6 +39,13 @@ def _check(pb, b, h, Y, U, what):
     assert int(pb.status[b]) == (1 if h > 0 else 2), (what, int(pb.status[b]))
     assert_bitwise(pb.Y[b].cpu().numpy(), Y, f"{what} Y")
     assert_bitwise(pb.U[b].cpu().numpy(), U, f"{what} U")
+
+
+def _form(knobs, form):
+    v1, pair, _ = FORMS[form]
+    knobs("mid_v1", v1)
+    knobs("mid2_pair", pair)
+    knobs("mid2_min_n", 0)
 
 
 @pytest.fixture
@@ -60,8 +68,8 @@ def _bundled(golden_bundled):
 
 
 @pytest.mark.parametrize("H", [2, 3, 4, 5])
-@pytest.mark.parametrize("mid_off,v1", [(0, 0), (0, 1), (1, 0)])
-def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off, v1):
+@pytest.mark.parametrize("mid_off,form", [(0, "mid2"), (0, "pair"), (0, "v1"), (1, "mid2")])
+def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off, form):
     """The bundled plant as H diagonal blocks (n_dual 28 H) stops at h = 313
     (the oracle's, itself pinned to oracle/_ref for 9 and 36 blocks): 8 copies
     in one launch, every value bit for bit."""
@@ -69,28 +77,28 @@ def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs,
 
     Q = block_diag_problem(_bundled(golden_bundled), H)
     knobs("mid_off", mid_off)
-    knobs("mid_v1", v1)
+    _form(knobs, form)
     if not mid_off:
         assert gpu_lib.lib().pqp_batch_solve_path(Q["N"], Q["M"]) == MID
     pb = _batch(gpu_lib, [Q] * 8).solve(max_updates=CAP)
     if not mid_off:
-        assert gpu_lib.tune_get("last_batch_kernel") == (2 if v1 else 3)
+        assert gpu_lib.tune_get("last_batch_kernel") == FORMS[form][2]
     h, Y, U = orc.solve(Q, max_updates=CAP)
     assert h == 313
     for b in (0, 7):
         _check(pb, b, h, Y, U, f"H={H} copy {b} mid_off={mid_off}")
 
 
-@pytest.mark.parametrize("v1", [0, 1])
+@pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("chunk", [1, 2, 7, 50])
-def test_horizon_blocks_chunked(gpu_lib, golden_bundled, orc, knobs, chunk, v1):
+def test_horizon_blocks_chunked(gpu_lib, golden_bundled, orc, knobs, chunk, form):
     """Launches of `chunk` iterates per problem, resumed from Y in HBM: the
     stop lands inside a later launch, same bits."""
     from oracle import block_diag_problem
 
     Q = block_diag_problem(_bundled(golden_bundled), 3)
     knobs("batch_chunk", chunk)
-    knobs("mid_v1", v1)
+    _form(knobs, form)
     pb = _batch(gpu_lib, [Q] * 3).solve(max_updates=CAP)
     h, Y, U = orc.solve(Q, max_updates=CAP)
     for b in range(3):
@@ -104,8 +112,7 @@ def test_synthetic_capped_vs_oracle(gpu_lib, orc, knobs, N, M, feasible, form):
     """Capped solves of synthetic problems; `feasible`: Kp = 1e30, so every
     iterate runs all of computeCost and, from the second on, the Y'Qd sums
     ride in the update rows (k_solve_mid) or run on the C waves (mid2)."""
-    v1, _ = FORMS[form]
-    knobs("mid_v1", v1)
+    _form(knobs, form)
     assert gpu_lib.lib().pqp_batch_solve_path(N, M) == MID
     B, cap = 3, 9
     Ps = [orc.synth_problem(31, b, N, M) for b in range(B)]
@@ -121,8 +128,7 @@ def test_synthetic_capped_vs_oracle(gpu_lib, orc, knobs, N, M, feasible, form):
 @pytest.mark.parametrize("N,M", [(48, 24), (101, 25), (150, 36)])
 @pytest.mark.parametrize("form", list(FORMS))
 def test_fixed_mode_vs_oracle(gpu_lib, orc, knobs, N, M, form):
-    v1, _ = FORMS[form]
-    knobs("mid_v1", v1)
+    _form(knobs, form)
     Ps = [orc.synth_problem(32, b, N, M) for b in range(4)]
     pb = _batch(gpu_lib, Ps).solve(gpu_lib.MODE_FIXED, num_iter=40)
     assert np.all(pb.h.cpu().numpy() == 40)
@@ -138,8 +144,7 @@ def test_non_symmetric_qd_mixed(gpu_lib, orc, knobs, feasible, form):
     the Y'Qd columns then run beside the update rows instead of inside them."""
     from pqp_amd import dense_qinv
 
-    v1, _ = FORMS[form]
-    knobs("mid_v1", v1)
+    _form(knobs, form)
     N, M, cap = 96, 24, 7
     P0 = orc.synth_problem(33, 0, N, M)
     P1 = orc.synth_primal(33, 1, N, M)
@@ -164,8 +169,7 @@ def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, form):
     (row 5's sums turn NaN), a v_max_f32 form would drop it.  Fixed mode, one
     and two updates: NaN where the oracle has NaN, every other value bit for
     bit; problem 1 (no NaN) unaffected."""
-    v1, _ = FORMS[form]
-    knobs("mid_v1", v1)
+    _form(knobs, form)
     N, M = 48, 12
     P0 = orc.synth_problem(34, 0, N, M)
     P1 = orc.synth_problem(34, 1, N, M)
@@ -183,8 +187,9 @@ def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, form):
             assert_bitwise(got[ok], Y[ok], f"num_iter={n} problem {b}")
 
 
+@pytest.mark.parametrize("pair", [0, 1])
 @pytest.mark.parametrize("N,M,cap", [(112, 28, 1), (112, 28, 2), (84, 21, 3), (150, 40, 4)])
-def test_mid2_short_caps_and_costs(gpu_lib, orc, knobs, N, M, cap):
+def test_mid2_short_caps_and_costs(gpu_lib, orc, knobs, N, M, cap, pair):
     """k_solve_mid2 decides terminate(Y_h) one phase after it was formed:
     caps of 1..4 updates stop on the right iterate with its own Y and U
     (Y_{h+1}, Y_{h+2} are dropped), every iterate feasible (Kp = 1e30) so the
@@ -192,6 +197,8 @@ def test_mid2_short_caps_and_costs(gpu_lib, orc, knobs, N, M, cap):
     Ps = [orc.synth_problem(35, b, N, M) for b in range(2)]
     for P in Ps:
         P["Kp"] = np.full(N, 1e30, np.float32)
+    knobs("mid2_pair", pair)
+    knobs("mid2_min_n", 0)
     pb = _batch(gpu_lib, Ps).solve(max_updates=cap)
     assert gpu_lib.tune_get("last_batch_kernel") == 3
     knobs("mid_v1", 1)
