@@ -57,6 +57,10 @@ extern "C" {
  *   mid_v1 [0]             1: path 3 on k_solve_mid (terminate() after each
  *                          update) instead of k_solve_mid2 (terminate(Y_h)
  *                          on other waves beside the update to Y_{h+1})
+ *   mid2_pair [0]          k_solve_mid2's update rows: 0 by shape (lane sides
+ *                          for 96 <= N <= 128), 1 lane sides (v_med3_f32), 2
+ *                          one lane per row (max form)
+ *   mid2_min_n [48]        smallest N path 3 runs on k_solve_mid2
  *   batch_chunk [0]        iterates per problem per batched-solve launch
  *                          (0: sized from N and M)
  *   single_scalar [0]      k_solve_single with 4-byte loads only

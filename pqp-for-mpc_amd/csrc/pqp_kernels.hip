@@ -1093,6 +1093,38 @@ __global__ void __launch_bounds__(256) k_matvec_rows(float* __restrict__ out, co
     if (i < a) out[i] = acc;
 }
 
+// The row-vector form out[j] = sum_k x[k] B(k, j) (a = 1: convertToDual's
+// Fp'Qp_inv and (Fp'Qp_inv) Fp, PQP_CPU.c:472-479, and computeCost-style
+// dots): one lane per output j, k = 0..b-1 in order from +0.0f; x[k] is
+// wave-uniform (scalar loads) and the k loop issues 8 loads of B ahead of its
+// adds, so a lane's chain is not one memory round trip per k.  k past b adds
+// 0*0 = +0.0f to a sum that is never -0.0f.
+__global__ void __launch_bounds__(256) k_vecmat(float* __restrict__ out, const float* __restrict__ x,
+                                                const float* __restrict__ B, int tB, int bdim, int c, long long sA,
+                                                long long sB, long long sO) {
+    const int z = blockIdx.y;
+    x += z * sA;
+    B += z * sB;
+    out += z * sO;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= c) return;
+    const float* col = tB ? B + (size_t)j * bdim : B + j;  // B(k, j) = col[k * step]
+    const size_t step = tB ? 1 : (size_t)c;
+    float s = 0.0f;
+    for (int k0 = 0; k0 < bdim; k0 += 8) {
+        float v[8], xv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = k0 + e;
+            v[e] = k < bdim ? col[(size_t)k * step] : 0.0f;
+            xv[e] = k < bdim ? x[k] : 0.0f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += xv[e] * v[e];  // :88-146, k in order
+    }
+    out[j] = s;
+}
+
 // The setup GEMM at scale, on packed fp32: a 128 x 128 output tile per
 // 256-thread workgroup, 8 x 8 outputs per thread (rows 4tx+r and 64+4tx+r,
 // columns 4ty+q and 64+4ty+q), op(A) and op(B) staged KT8 = 32 k at a time
@@ -3709,13 +3741,15 @@ __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
 // waves of each role: UW (PAIR: 32 rows per wave, lane sides; else 64 rows,
 // one lane per row), T (one), C (ceil(N/64) row waves and the cost wave)
 __host__ __device__ inline int mid2_uw(int N, bool pair) { return pair ? (N + 31) / 32 : (N + 63) / 64; }
-__host__ __device__ inline int mid2_waves(int N, bool conv, bool pair) {
-    return mid2_uw(N, pair) + (conv ? 1 + (N + 63) / 64 + 1 : 0);
+// C row waves: `crows` checkFeas rows (and Y'Qd terms) per wave, 64 or 32
+__host__ __device__ inline int mid2_cr(int N, int crows) { return (N + crows - 1) / crows; }
+__host__ __device__ inline int mid2_waves(int N, bool conv, bool pair, int crows) {
+    return mid2_uw(N, pair) + (conv ? 1 + mid2_cr(N, crows) + 1 : 0);
 }
 // mid2 takes (N, M) in converge or fixed mode when T fits one wave and the
 // workgroup 16
-__host__ __device__ inline bool mid2_fits(int N, int M, bool conv, bool pair) {
-    return (!conv || M < 64) && mid2_waves(N, conv, pair) <= 16;
+__host__ __device__ inline bool mid2_fits(int N, int M, bool conv, bool pair, int crows) {
+    return (!conv || M < 64) && mid2_waves(N, conv, pair, crows) <= 16;
 }
 
 // 8 terms of one side of update row i (k .. k+7).  FAST: the v_med3_f32
@@ -3820,10 +3854,13 @@ __global__ void __launch_bounds__(MAXT) k_solve_mid2(SolveArgs A0, SolveState* _
     float* fdy = lds + L.fdy;
     float* sums = lds + L.sums;
     int* flag = reinterpret_cast<int*>(lds + L.flag);  // [0..11] checkFeas per C row wave, [12 + p] Y non-finite
-    const int NT = blockDim.x;  // 64 * mid2_waves(N, conv, PAIR)
+    const int NT = blockDim.x;  // 64 * mid2_waves(N, conv, PAIR, crows)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nUW = mid2_uw(N, PAIR), wT = nUW, wC0 = nUW + 1;
-    const int nCR = (N + 63) / 64;  // C waves that take checkFeas rows and the Y'Qd terms; wave wC0 + nCR the costs
+    // C waves that take checkFeas rows and the Y'Qd terms (crows each); wave
+    // wC0 + nCR the costs
+    const int crows = (NT / 64 - nUW - 2 >= (N + 31) / 32) ? 32 : 64;
+    const int nCR = mid2_cr(N, crows);
 
     // ---- stage the problem (once per launch; padding zero) ----
     for (int e = tid; e < L.total; e += NT) lds[e] = 0.0f;
@@ -4012,17 +4049,18 @@ __global__ void __launch_bounds__(MAXT) k_solve_mid2(SolveArgs A0, SolveState* _
             const float* Uo = Us + ((s - 1) & 1) * mk;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
             if (cw < nCR) {
-                const int l = cw * 64 + lane;
+                const int l = cw * crows + lane;  // rows [cw * crows, +crows): lanes < crows
+                const int lend = lane < crows ? N : 0;
                 int bad = 0;
                 if (pend)
-                    for (int i = l; i < N; i += 64 * nCR) {
+                    for (int i = l; i < lend; i += crows * nCR) {
                         const float g = mid_dot(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
                         const float kp = Kp[i];
                         if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
                     }
                 if (pend && lane == 0) flag[cw] = __any(bad) ? 1 : 0;
                 float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
-                for (int j = l; j < N; j += 64 * nCR)  // (Y'Qd)_j Y_j :652-655; column j = row j when Qd is symmetric
+                for (int j = l; j < lend; j += crows * nCR)  // (Y'Qd)_j Y_j :652-655; column j = row j when Qd is symmetric
                     tqs[j] = (sym ? mid_dot_row(Qd + j * ldn, ycur, nk) : mid_dot(Qd + j, ldn, ycur, nk)) * ycur[j];
             } else if (pend && cw == nCR) {
                 if (lane < M) {
@@ -4080,11 +4118,17 @@ constexpr size_t kMidLdsBudget = 150 * 1024;
 
 static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const bool conv2 = a.mode == kModeConverge;
-    const bool pair = g_tune.mid2_pair != 0;
-    if (a.mode != kModeTerminate && !g_tune.mid_v1 && a.N >= g_tune.mid2_min_n && mid2_fits(a.N, a.M, conv2, pair)) {
+    // the update rows as lane sides where that measured faster: the horizon
+    // sweep (profiles/r04/mid2_arms.jsonl) at n_dual 112 (H = 4) 40.4 vs 43.4
+    // ms, and slower at 56, 84 and 140 (more waves per workgroup, fewer
+    // workgroups per CU); mid2_pair 1 / 2 force either form
+    const bool pair = g_tune.mid2_pair == 1 || (g_tune.mid2_pair == 0 && a.N >= 96 && a.N <= 128);
+    const int crows = 64;  // 32 rows per C wave measured slower at every H (more waves per workgroup)
+    if (a.mode != kModeTerminate && !g_tune.mid_v1 && a.N >= g_tune.mid2_min_n &&
+        mid2_fits(a.N, a.M, conv2, pair, crows)) {
         const size_t lds = sizeof(float) * (size_t)mid2_layout(a.N, a.M, conv2).total;
         if (lds <= kMidLdsBudget) {
-            const int nt = 64 * mid2_waves(a.N, conv2, pair);
+            const int nt = 64 * mid2_waves(a.N, conv2, pair, crows);
             if (pair) hipLaunchKernelGGL((k_solve_mid2<1024, true>), dim3(B), dim3(nt), lds, s, a, st);
             else hipLaunchKernelGGL((k_solve_mid2<1024, false>), dim3(B), dim3(nt), lds, s, a, st);
             g_last_batch_kernel = 3;
@@ -4250,6 +4294,11 @@ hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const 
     if (n == 0 || B == 0) return hipSuccess;
     for (int b0 = 0; b0 < B; b0 += 65535) {  // grid y / z limit
         const int nb = (B - b0) < 65535 ? (B - b0) : 65535;
+        if (a == 1 && b >= 32 && !g_tune.matmul_tiled_off) {  // x' B (tA is moot for a one-row A)
+            hipLaunchKernelGGL(k_vecmat, dim3(cdiv(c, 256), nb), dim3(256), 0, s, out + b0 * sO, A + b0 * sA,
+                               Bm + b0 * sB, tB, b, c, sA, sB, sO);
+            continue;
+        }
         if (c == 1 && !tA && a >= 64 && b >= 32 && !g_tune.matmul_tiled_off) {
             hipLaunchKernelGGL(k_matvec_rows, dim3(cdiv(a, 256), nb), dim3(256), 0, s, out + b0 * sO, A + b0 * sA,
                                Bm + b0 * sB, a, b, sA, sB, sO);

@@ -32,7 +32,7 @@ def main(Hs):
         out = {"H": H, "n_dual": P["N"], "m": P["M"], "problems": B}
         res = {}
         for mode in ("converge", "fixed"):
-            arms = (("mid2", 0, 0), ("pair", 0, 1), ("v1", 1, 0))
+            arms = (("mid2", 0, 2), ("pair", 0, 1), ("v1", 1, 0))
             ts = {a[0]: [] for a in arms}
             for rep in range(2):
                 for name, v1, pair in arms:

@@ -26,7 +26,7 @@ def main(Hs):
 
     base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
     pqp_amd.tune("mid_v1", int(os.environ.get("MID_V1", "0")))
-    pqp_amd.tune("mid2_pair", int(os.environ.get("MID2_PAIR", "0")))
+    pqp_amd.tune("mid2_pair", int(os.environ.get("MID2_PAIR", "0")))  # 0 by shape, 1 lane sides, 2 one lane per row
     pqp_amd.tune("mid2_min_n", 0)
     B = int(os.environ.get("B", "4096"))
     ntr = 256

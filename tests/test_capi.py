@@ -89,7 +89,7 @@ def _gfx950_asm(name: str) -> str:
     ("pqp_kernels.hip",
      r"_ZN3pqp(15k_batch_iterate|14k_batch_update|14k_solve_single|13k_split_relay|12k_fixed_tiny"
      r"|12k_solve_wave|12k_lean_relay|12k_solve_pipe|12k_solve_mid2|11k_matmul_pk|14k_matmul_tiled"
-     r"|12k_gj_blocked|13k_matvec_rows)",
+     r"|12k_gj_blocked|13k_matvec_rows|8k_vecmat)",
      40),
     ("pqp_wide.hip", r"_ZN3pqp12_GLOBAL__N_1(12k_gemv_relay|13k_wide_decide)", 2),
     ("pqp_persist.hip", r"_ZN3pqp15k_split_persist", 1),

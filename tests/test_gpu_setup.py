@@ -139,3 +139,26 @@ def test_matvec_rows_vs_oracle_and_seq(gpu_lib, orc, a, b):
         finally:
             gpu_lib.tune("matmul_tiled_off", prev)
         assert_bitwise(out, seq, f"matvec vs seq {a}x{b}")
+
+
+@pytest.mark.parametrize("b,c", [(32, 1), (512, 512), (77, 300), (1000, 1), (513, 65)])
+def test_vecmat_vs_oracle_and_seq(gpu_lib, orc, b, c):
+    """k_vecmat (a = 1: out[j] = sum_k x[k] B(k, j), one lane per j, eight
+    loads ahead of the adds): bit-identical to the oracle and to k_matmul_seq
+    for either transpose flag of B (and of the one-row A)."""
+    rng = np.random.default_rng(b * 31 + c)
+    x = rng.standard_normal(b).astype(np.float32)
+    Bm = rng.standard_normal(b * c).astype(np.float32)
+    Bm[::9] = -0.0
+    for tA in (0, 1):
+        for tB in (0, 1):
+            out = np.zeros(c, np.float32)
+            gpu_lib.matrixMultiply(out, x, tA, Bm, tB, 1, b, c)
+            assert_bitwise(out, orc.matmul(x, tA, Bm, tB, 1, b, c), f"vecmat {b}x{c} t{tA}{tB}")
+            prev = gpu_lib.tune("matmul_tiled_off", 1)
+            try:
+                seq = np.zeros(c, np.float32)
+                gpu_lib.matrixMultiply(seq, x, tA, Bm, tB, 1, b, c)
+            finally:
+                gpu_lib.tune("matmul_tiled_off", prev)
+            assert_bitwise(out, seq, f"vecmat vs seq {b}x{c}")
