@@ -339,10 +339,15 @@ def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
     for H in Hs:
         xs = pqp_amd.perturbed_states(E["x"], B * H, seed=7).reshape(B, H, -1)
         pb = pqp_amd.horizon_batch(ex, H, xs)
-        pb.solve(max_updates=200000)  # warm
+        # capped at the testing/ harness's 1000 iterations: a problem the
+        # reference's exact-float gap test never stops (one of the 16384 at H =
+        # 2, seed 7 -- the oracle runs it past 3000 updates too) costs 999
+        # updates, not the whole timing
+        cap = 999
+        pb.solve(max_updates=cap)  # warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        pb.solve(max_updates=200000)
+        pb.solve(max_updates=cap)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         h = pb.h.cpu().numpy()
@@ -350,8 +355,9 @@ def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
         row = {"n_dual": N, "m": M, "problems": B, "path": int(pqp_amd.lib().pqp_batch_solve_path(N, M)),
                "kernel": {3: "k_solve_mid2", 2: "k_solve_mid"}.get(pqp_amd.tune_get("last_batch_kernel"), "other"),
                "converge_ms": dt * 1e3, "qp_solves_per_s": B / dt, "iterations_per_s": float(h.sum()) / dt,
-               "h_min": int(h.min()), "h_max": int(h.max()), "h_mean": float(h.mean()),
-               "converged_frac": float((pb.status.cpu().numpy() == 1).mean())}
+               "h_min": int(h.min()), "h_max": int(h.max()), "h_mean": float(h.mean()), "max_updates": cap,
+               "converged_frac": float((pb.status.cpu().numpy() == 1).mean()),
+               "capped": int((pb.status.cpu().numpy() == 2).sum())}
         if ref is not None:
             P0 = pb.problem(0)
             ts = []
