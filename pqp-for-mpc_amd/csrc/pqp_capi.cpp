@@ -1890,7 +1890,6 @@ const KnobRef* find_knob(const char* key) {
         {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},
         {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},
         {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
-        {"pipe_stagger", nullptr, nullptr, &g_tune.pipe_stagger},
     };
     for (const KnobRef& k : knobs)
         if (std::strcmp(k.key, key) == 0) return &k;

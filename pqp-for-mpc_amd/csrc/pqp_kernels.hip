@@ -1867,11 +1867,6 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
     SolveState* st = st0 + blockIdx.x;
     if (st->status == kStatusDone || st->status == kStatusCapped) return;  // finished in an earlier launch
     const int N = A.N, M = A.M, ldq = A.ldq, ldm = A.ldm;
-    if (A0.stagger_cyc > 0 && !st->resume && (int)blockIdx.x >= A0.stagger_lo &&
-        (int)blockIdx.x < A0.stagger_lo + A0.stagger_n) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)A0.stagger_cyc) __builtin_amdgcn_s_sleep(127);
-    }
     float* ya = lds;            // ldq   Y_h / Y_{h+1}
     float* yb = ya + ldq;       // ldq
     float* tq = yb + ldq;       // ldq   Y_h'Qd (Jd)
@@ -4629,29 +4624,6 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
     if (vec && a.mode == kModeConverge && a.QinvT && pipe_route(a.N, a.M, variant)) {
         const bool big = variant != 3;
         const size_t plds = solve_pipe_lds_bytes(a.ldq, a.ldm, big);
-        if (g_tune.pipe_stagger > 0) {
-            // the first round's second workgroup of each CU (dispatch fills one
-            // slot per CU first) starts late, offsetting the CU's two problems
-            static int cus = 0;
-            if (!cus) {
-                int dev = 0;
-                (void)hipGetDevice(&dev);
-                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            }
-            SolveArgs b = a;
-            b.stagger_lo = cus;
-            b.stagger_n = cus;
-            b.stagger_cyc = g_tune.pipe_stagger;
-            if (big) hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), plds, s, b, st);
-            else hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), plds, s, b, st);
-            g_last_batch_kernel = 1;
-            return hipGetLastError();
-        }
-        // Gp tiles in flight, update loads in flight per lane, workgroups per
-        // CU: two per CU with 16 loads per lane beat three with 8 (4096
-        // problems are then 8 whole rounds of 512 resident workgroups)
-        // 128 x 96 tiles (every wave sums a chain) beat 64 x 64 ones by 2-3 %
-        // on infeasible iterates and tie on feasible ones
         if (big) hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2, true>), dim3(B), dim3(256), plds, s, a, st);
         else hipLaunchKernelGGL((k_solve_pipe<256, 2, 16, 2>), dim3(B), dim3(256), plds, s, a, st);
         g_last_batch_kernel = 1;

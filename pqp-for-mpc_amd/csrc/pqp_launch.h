@@ -35,11 +35,6 @@ struct SolveArgs {
     int feas_split;  // k_solve_single with GpT: checkFeas decides on its first rows when one is over its bound
     unsigned long long* trace;  // optional (k_solve_mid): 16 words of phase cycle totals per traced problem
     int trace_n;                // problems traced (workgroups 0..trace_n-1)
-    // k_solve_pipe: workgroups [stagger_lo, stagger_lo + stagger_n) of a fresh
-    // solve start stagger_cyc shader cycles late (their CU neighbours are then
-    // in the other phase of the iteration)
-    int stagger_lo, stagger_n;
-    long long stagger_cyc;
 };
 hipError_t launch_transpose_b(int B, const float* src, int rows, int cols, float* dst, hipStream_t s);
 // sym[b] = nonzero iff problem b's row-major Qd equals its transpose bit for bit
@@ -119,7 +114,6 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int mid2_min_n = 48;  // smallest N path 3 runs on k_solve_mid2 (below it k_solve_mid)
     int mid_v1 = 0;  // path 3 on k_solve_mid (terminate() after the update) instead of the pipelined k_solve_mid2
     int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 3 (two 64 x 64 tiles in flight)
-    long long pipe_stagger = 0;  // k_solve_pipe: the second resident workgroup of each CU starts this many cycles late
     int pipe_force = 0;  // k_solve_pipe also where M < N / 3 (where k_solve_single measured faster)
     int matmul_pk_off = 0;  // setup GEMMs on the 64 x 64 scalar-staged k_matmul_tiled instead of the packed 128 x 128 k_matmul_pk
     int pipe_off = 0;  // batched converge of large problems on k_solve_single (two passes over Gp) instead of k_solve_pipe

@@ -261,3 +261,19 @@ def test_horizon_batch_built_by_the_product(gpu_lib, golden_bundled, orc, H):
             assert_bitwise(getattr(pb, k)[b].cpu().numpy().reshape(-1), np.asarray(Q[k]).reshape(-1), f"{k} of {b}")
         h, Y, U = orc.solve(Q, max_updates=CAP)
         _check(pb, b, h, Y, U, f"H={H} problem {b}")
+
+
+def test_horizon_problem_the_reference_never_stops(gpu_lib, orc):
+    """Problem 4160 of the bench's H = 2 horizon batch (stage states
+    pqp_amd.perturbed_states(seed 7)) never meets the reference's exact-float
+    gap test (the oracle runs it past 3000 updates): the GPU hits the bench
+    leg's cap of 999 updates on the same iterate, with the oracle's Y and U."""
+    from conftest import EXAMPLE_DIR
+
+    E = gpu_lib.read_example(EXAMPLE_DIR)
+    xs = gpu_lib.perturbed_states(E["x"], 2 * 4161, seed=7).reshape(4161, 2, -1)
+    pb = gpu_lib.horizon_batch(EXAMPLE_DIR, 2, xs[4160:4161]).solve(max_updates=999)
+    Q = _oracle_horizon_problem(orc, xs[4160])
+    h, Y, U = orc.solve(Q, max_updates=999)
+    assert h == -1000
+    _check(pb, 0, h, Y, U, "horizon H=2 problem 4160, capped")
