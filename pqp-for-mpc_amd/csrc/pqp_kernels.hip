@@ -4400,20 +4400,14 @@ __device__ __forceinline__ void gj_steps(float (&v)[4 * C], const float* __restr
             }
             const float t = mji / Pd[s];  // temp (:298)
             const float* prow = P + (size_t)s * W;
-            typedef float f2v __attribute__((ext_vector_type(2)));
+            // (a packed form -- v_pk_mul_f32 and v_pk_add_f32 of the negated
+            // product -- measured 0.140 vs 0.129 s for 4096 n = 512 inverses:
+            // profiles/r04/gj_timing_packed_dropped.json)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const sf4 q = *reinterpret_cast<const sf4*>(prow + 256 * c + 4 * lane);
-                // m_jk - m_ik * temp (:301), two elements per packed multiply
-                // and packed add of the negated product (each half rounds as
-                // the scalar op; a - b == a + (-b) exactly)
 #pragma unroll
-                for (int e = 0; e < 4; e += 2) {
-                    const f2v pr = f2v{q[e], q[e + 1]} * f2v{t, t};
-                    const f2v r = f2v{v[4 * c + e], v[4 * c + e + 1]} + (-pr);
-                    v[4 * c + e] = r.x;
-                    v[4 * c + e + 1] = r.y;
-                }
+                for (int e = 0; e < 4; ++e) v[4 * c + e] -= q[e] * t;  // (:301)
             }
         }
     }

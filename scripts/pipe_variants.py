@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import ctypes as C
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -32,6 +33,8 @@ def main(variants):
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    if os.environ.get("PIPE_OFF"):  # k_solve_single (pipe_variant 5: its round-3 form)
+        pqp_amd.tune("pipe_off", 1)
     for v in variants:
         pqp_amd.tune("pipe_variant", v)
         for case in ("infeasible", "feasible"):
