@@ -28,6 +28,7 @@ REF_SO = HERE / "_ref" / "libpqp_ref.so"
 REF_BIN = HERE / "_ref" / "pqp_cpu_ref"
 REF_TEST_SO = HERE / "_ref" / "libpqp_ref_test.so"
 REF_FIXED_SO = HERE / "_ref" / "libref_fixed.so"
+REF_CONVERGE_SO = HERE / "_ref" / "libref_converge.so"
 
 # Bundled-example dimensions: PQP_CPU.c:13-17 (pHorizon=1, nState=29, nInput=7,
 # nOutput=7, nDis=1) -> M = 7 primal, N = 28 dual (PQP_CPU.c:940-941).
@@ -235,6 +236,31 @@ class Oracle:
         return dict(Qd=Qd, Fd=Fd, Md=Md, Qp=self.gauss_jordan(E["Qp_inv"], M), Qp_inv=E["Qp_inv"], Fp=Fp, Mp=Mp,
                     Gp=E["Gp"], Kp=E["Kp"], N=N, M=M)
 
+    def horizon_problem(self, directory, states) -> dict:
+        """One stacked-horizon problem (bench.py's horizon leg, pqp_amd.
+        horizon_batch): the example's plant once per stage, stage h at state
+        states[h] -- computeFp / computeMp per stage (:373, :395), the
+        block-diagonal primal, Mp summed in stage order, then Gauss_Jordan
+        (:251) and convertToDual (:489) of the whole."""
+        stages = [self.example_at_state(directory, x) for x in states]
+        H = len(stages)
+        N, M = stages[0]["N"], stages[0]["M"]
+
+        def bd(k, r, c):
+            out = np.zeros((H * r, H * c), np.float32)
+            for h, S in enumerate(stages):
+                out[h * r:(h + 1) * r, h * c:(h + 1) * c] = np.asarray(S[k], np.float32).reshape(r, c)
+            return out.reshape(-1)
+
+        Mp = np.float32(stages[0]["Mp"][0])
+        for S in stages[1:]:
+            Mp = np.float32(Mp + np.float32(S["Mp"][0]))
+        Q = dict(Qp_inv=bd("Qp_inv", M, M), Gp=bd("Gp", N, M), Kp=np.concatenate([S["Kp"] for S in stages]),
+                 Fp=np.concatenate([S["Fp"] for S in stages]), Mp=np.array([Mp], np.float32), N=H * N, M=H * M)
+        Q["Qd"], Q["Fd"], Q["Md"] = self.convert_to_dual(Q["Qp_inv"], Q["Gp"], Q["Kp"], Q["Fp"], Q["Mp"], H * N, H * M)
+        Q["Qp"] = self.gauss_jordan(Q["Qp_inv"], H * M)
+        return Q
+
     def synth_primal(self, seed, inst, N, M) -> dict:
         P = dict(Qp_inv=np.zeros(M * M, np.float32), Gp=np.zeros(N * M, np.float32),
                  Kp=np.zeros(N, np.float32), Fp=np.zeros(M, np.float32), Mp=np.zeros(1, np.float32))
@@ -385,6 +411,25 @@ class Reference:
         total = self._fixed.ref_fixed_solve(_p(Y), _p(f32(P["Qd"]).copy()), _p(f32(P["Fd"]).copy()), N, num_iter,
                                             C.byref(loop))
         return Y, float(total), float(loop.value)
+
+    def converge_solve(self, P, cap: int):
+        """The reference's converge-mode solve stopped after `cap` updates
+        (oracle/ref_converge.c over this library's own setup, terminate and
+        updateY2: PQP_CPU.c:696-740 plus the cap test).  Returns (h, Y, U), h < 0
+        when capped -- the Oracle.solve(max_updates=cap) convention."""
+        if not hasattr(self, "_conv"):
+            if not REF_CONVERGE_SO.exists():
+                raise FileNotFoundError(f"{REF_CONVERGE_SO} not built (needs /root/reference; run make -C oracle)")
+            self._conv = C.CDLL(str(REF_CONVERGE_SO))
+            self._conv.ref_converge_solve.argtypes = [_fp] * 11 + [C.c_int, C.c_int, C.c_long]
+            self._conv.ref_converge_solve.restype = C.c_long
+        N, M = P["N"], P["M"]
+        Y, U = np.zeros(N, np.float32), np.zeros(M, np.float32)
+        a = {k: f32(P[k]).copy() for k in ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")}
+        h = self._conv.ref_converge_solve(_p(Y), _p(a["Qd"]), _p(a["Fd"]), _p(a["Md"]), _p(U), _p(a["Qp"]),
+                                          _p(a["Qp_inv"]), _p(a["Fp"]), _p(a["Mp"]), _p(a["Gp"]), _p(a["Kp"]),
+                                          N, M, cap)
+        return int(h), Y, U
 
     def solve(self, P):
         """The reference solveQuadraticDual; returns (h, Y, U) with h parsed from

@@ -23,12 +23,20 @@ Outputs (all small):
                         perturbed states (pqp_amd.perturbed_states, seed 5), each set up
                         (computeFp / computeMp / convertToDual) and solved by the reference:
                         h per state and a 64-bit digest of (Y*, U*) per state
+  horizon_states.npz    the bench's horizon leg population: the bundled plant stacked over
+                        H = 2 and 4 stages, each stage at its own perturbed state
+                        (pqp_amd.perturbed_states(seed 7), B x H states), set up by the
+                        reference (computeFp / computeMp per stage, block-diagonal primal,
+                        Mp summed in stage order, Gauss_Jordan, convertToDual) and solved by
+                        it in converge mode capped at 999 updates (oracle/ref_converge.c
+                        over the reference's own terminate / updateY2): h per problem
+                        (negative: capped) and a 64-bit digest of (Y*, U*) per problem
   dense_dual.npz        convertToDual with a DENSE Qp_inv (numpy-seeded,
                         pqp_amd.dense_qinv) at N=1024/M=512 and N=300/M=77: digests of
                         Qd, and Fd / Md (the general setup GEMM's parity case)
 
 Usage: python tests/golden/make_golden.py [part ...]   (parts: bundled converge
-       large testing dense blocks mpc; default all)
+       large testing dense blocks mpc horizon; default all)
 """
 from __future__ import annotations
 
@@ -251,6 +259,84 @@ def mpc_states(ref: Reference):
           dict(zip(u.tolist(), c.tolist())))
 
 
+HORIZON_HS, HORIZON_STATES, HORIZON_SEED, HORIZON_CAP = (2, 4), 16384, 7, 999
+_H_REF = {}
+
+
+def _horizon_one(args):
+    """(b, h, digest, Y, U) of horizon problem b: the reference's setup of the
+    stacked primal from the stage states xs[b] and its capped converge solve."""
+    H, b, xs_b = args
+    if "P" not in _H_REF:
+        _H_REF["ref"] = Reference()
+        _H_REF["P"] = _H_REF["ref"].bundled_problem(REFERENCE_DIR)
+    ref, P = _H_REF["ref"], _H_REF["P"]
+    N, M = P["N"], P["M"]
+    Fps, Mps = [], []
+    for x in xs_b:
+        Fp, Mp = np.zeros(M, np.float32), np.zeros(1, np.float32)
+        x = np.ascontiguousarray(x, np.float32)
+        ref.lib.computeFp(_p(Fp), _p(P["Fp1"]), _p(P["Fp2"]), _p(P["Fp3"]), _p(P["D"]), _p(x))
+        ref.lib.computeMp(_p(Mp), *[_p(P[k]) for k in ("Mp1", "Mp2", "Mp3", "Mp4", "Mp5", "Mp6", "D")], _p(x))
+        Fps.append(Fp)
+        Mps.append(Mp)
+
+    def bd(k, r, c):
+        out = np.zeros((H * r, H * c), np.float32)
+        for h in range(H):
+            out[h * r:(h + 1) * r, h * c:(h + 1) * c] = P[k].reshape(r, c)
+        return np.ascontiguousarray(out.reshape(-1))
+
+    Mp = np.float32(Mps[0][0])
+    for m in Mps[1:]:
+        Mp = np.float32(Mp + np.float32(m[0]))  # stage order
+    Q = dict(Qp_inv=bd("Qp_inv", M, M), Gp=bd("Gp", N, M), Kp=np.concatenate([P["Kp"]] * H),
+             Fp=np.concatenate(Fps), Mp=np.array([Mp], np.float32), N=H * N, M=H * M)
+    Q["Qd"], Q["Fd"], Q["Md"] = ref.convert_to_dual(Q["Qp_inv"], Q["Gp"], Q["Kp"], Q["Fp"], Q["Mp"], H * N, H * M)
+    Q["Qp"] = ref.gauss_jordan(Q["Qp_inv"], H * M)
+    h, Y, U = ref.converge_solve(Q, HORIZON_CAP)
+    return b, h, state_digest(Y, U), Y, U
+
+
+def horizon_states():
+    """The bench's horizon leg (bench.horizon_bench) problem by problem on the
+    reference, over 8 processes."""
+    import multiprocessing as mp
+    import time
+
+    E = Reference().bundled_problem(REFERENCE_DIR)
+    out = {"H": np.asarray(HORIZON_HS, np.int64), "cap": np.int64(HORIZON_CAP)}
+    for H in HORIZON_HS:
+        t0 = time.perf_counter()
+        xs = perturbed_states(E["x"], HORIZON_STATES * H, seed=HORIZON_SEED).reshape(HORIZON_STATES, H, -1)
+        hs = np.zeros(HORIZON_STATES, np.int64)
+        dig = np.zeros(HORIZON_STATES, np.uint64)
+        keep = {}
+        with mp.get_context("fork").Pool(8) as pool:
+            for b, h, d, Y, U in pool.imap_unordered(_horizon_one, [(H, b, xs[b]) for b in range(HORIZON_STATES)],
+                                                     chunksize=64):
+                hs[b], dig[b] = h, d
+                if b < 4 or h < 0:
+                    keep[b] = (Y, U)
+        u, c = np.unique(hs, return_counts=True)
+        mode = u[np.argmax(c)]
+        order = sorted(keep) + [int(b) for b in np.nonzero(hs != mode)[0][:16] if int(b) not in keep]
+        order = sorted(set(order))
+        for b in order:
+            if b not in keep:
+                _, _, _, Y, U = _horizon_one((H, b, xs[b]))
+                keep[b] = (Y, U)
+        out[f"h{H}"] = hs.astype(np.int16)
+        out[f"digest{H}"] = dig
+        out[f"xs_sha256_{H}"] = np.frombuffer(bytes.fromhex(digest(xs)), np.uint8)
+        out[f"kept{H}"] = np.asarray(order, np.int64)
+        out[f"kept_Y{H}"] = np.stack([keep[b][0] for b in order])
+        out[f"kept_U{H}"] = np.stack([keep[b][1] for b in order])
+        print(f"horizon H={H}: {HORIZON_STATES} solves in {time.perf_counter() - t0:.1f} s; h counts",
+              dict(zip(u.tolist(), c.tolist())))
+    np.savez_compressed(OUT / "horizon_states.npz", **out)
+
+
 def _p(a):
     import ctypes as C
 
@@ -261,7 +347,7 @@ def _p(a):
 def main(parts=None):
     build()
     ref, orc = Reference(), Oracle()
-    parts = set(parts or ("bundled", "converge", "large", "testing", "dense", "blocks", "mpc"))
+    parts = set(parts or ("bundled", "converge", "large", "testing", "dense", "blocks", "mpc", "horizon"))
     if "bundled" in parts:
         bundled(ref)
     if "converge" in parts:
@@ -276,6 +362,8 @@ def main(parts=None):
         blocks(ref)
     if "mpc" in parts:
         mpc_states(ref)
+    if "horizon" in parts:
+        horizon_states()
 
 
 if __name__ == "__main__":

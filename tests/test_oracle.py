@@ -265,3 +265,30 @@ def test_mpc_population_sample_matches_reference_golden(orc):
         assert h == G["h"][b], (b, h, G["h"][b])
         d = np.frombuffer(hashlib.sha256(Y.tobytes() + U.tobytes()).digest()[:8], np.uint64)[0]
         assert d == G["digest"][b], f"state {b}: (Y*, U*) differ from the reference"
+
+
+def test_horizon_population_sample_matches_reference_golden(orc):
+    """The restatement pinned on the bench's horizon leg population
+    (tests/golden/horizon_states.npz, made by the reference itself: its setup
+    of each stacked problem and its converge solve capped at 999 updates): the
+    problems kept in full (the capped H = 2 one and every h = 314 among them)
+    and every 512th give the reference's h and (Y*, U*) digest."""
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
+    from pqp_amd import perturbed_states
+
+    G = np.load(GOLDEN / "horizon_states.npz")
+    E = orc.load_example(EXAMPLE_DIR)
+    cap = int(G["cap"])
+    for H in G["H"].tolist():
+        hg = G[f"h{H}"].astype(np.int64)
+        xs = perturbed_states(E["x"], len(hg) * H, seed=7).reshape(len(hg), H, -1)
+        assert hashlib.sha256(xs.tobytes()).digest() == G[f"xs_sha256_{H}"].tobytes()
+        for b in sorted(set(G[f"kept{H}"].tolist()) | set(range(0, len(hg), 512))):
+            h, Y, U = orc.solve(orc.horizon_problem(EXAMPLE_DIR, xs[b]), max_updates=cap)
+            assert h == hg[b], (H, b, h, hg[b])
+            d = np.frombuffer(hashlib.sha256(Y.tobytes() + U.tobytes()).digest()[:8], np.uint64)[0]
+            assert d == G[f"digest{H}"][b], f"H={H} problem {b}: (Y*, U*) differ from the reference"
