@@ -6,6 +6,8 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --
 tail -3 gpurun_out/pytest_gpu_r04j.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r04j.log 2>&1 || { tail -20 gpurun_out/smoke_r04j.log; exit 1; }
 tail -1 gpurun_out/smoke_r04j.log
+ARMS=def,rot timeout -k 10 300 python -u scripts/mid2_arms.py 2 3 4 5 > gpurun_out/mid2_rot_r04j.jsonl 2>gpurun_out/mid2_rot_r04j.err || { tail -20 gpurun_out/mid2_rot_r04j.err; exit 1; }
+cat gpurun_out/mid2_rot_r04j.jsonl
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_r04j.json 2> gpurun_out/bench_r04j.err || { tail -30 gpurun_out/bench_r04j.err; exit 1; }
 cat gpurun_out/bench_r04j.json
 bash scripts/gpu_profile.sh r04

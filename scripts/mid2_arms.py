@@ -16,6 +16,7 @@ sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
 ARMS = {
+    "def": {},
     "v1": {"mid_v1": 1},
     "mid2": {"mid2_min_n": 0},
     "packed": {"mid2_min_n": 0, "mid2_pair": 2},
