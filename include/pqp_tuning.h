@@ -61,6 +61,9 @@ extern "C" {
  *                          for 96 <= N <= 128), 1 lane sides (v_med3_f32), 2
  *                          one lane per row (max form)
  *   mid2_min_n [48]        smallest N path 3 runs on k_solve_mid2
+ *   mid2_fat [0]           k_solve_mid2 workgroups of <= 6 waves on the
+ *                          128-VGPR build (default: the 80-VGPR build, 6 waves
+ *                          per SIMD, as many problems per CU as LDS allows)
  *   batch_chunk [0]        iterates per problem per batched-solve launch
  *                          (0: sized from N and M)
  *   single_scalar [0]      k_solve_single with 4-byte loads only

@@ -1885,6 +1885,7 @@ const KnobRef* find_knob(const char* key) {
         {"mid_v1", &g_tune.mid_v1, nullptr, nullptr},
         {"mid2_pair", &g_tune.mid2_pair, nullptr, nullptr},
         {"mid2_min_n", &g_tune.mid2_min_n, nullptr, nullptr},
+        {"mid2_fat", &g_tune.mid2_fat, nullptr, nullptr},
         {"matmul_pk_off", &g_tune.matmul_pk_off, nullptr, nullptr},
         {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},
         {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},

@@ -3825,8 +3825,8 @@ __device__ __forceinline__ float mid2_row(const float* q, const float* y, int nk
     return num / den * y[i];               // :594
 }
 
-template <int MAXT, bool PAIR>
-__global__ void __launch_bounds__(MAXT) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
+template <int MAXT, bool PAIR, int MINW = 1>
+__global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
     SolveState* st = st0 + blockIdx.x;
@@ -4129,7 +4129,13 @@ static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hip
         const size_t lds = sizeof(float) * (size_t)mid2_layout(a.N, a.M, conv2).total;
         if (lds <= kMidLdsBudget) {
             const int nt = 64 * mid2_waves(a.N, conv2, pair, crows);
-            if (pair) hipLaunchKernelGGL((k_solve_mid2<1024, true>), dim3(B), dim3(nt), lds, s, a, st);
+            // workgroups of <= 6 waves: the build held to 80 VGPRs (6 waves per
+            // SIMD), so as many problems share a CU as LDS allows (n_dual 56: 6
+            // instead of 4, 84: 4 instead of 2)
+            const bool lean = nt <= 384 && !g_tune.mid2_fat;
+            if (lean && pair) hipLaunchKernelGGL((k_solve_mid2<384, true, 6>), dim3(B), dim3(nt), lds, s, a, st);
+            else if (lean) hipLaunchKernelGGL((k_solve_mid2<384, false, 6>), dim3(B), dim3(nt), lds, s, a, st);
+            else if (pair) hipLaunchKernelGGL((k_solve_mid2<1024, true>), dim3(B), dim3(nt), lds, s, a, st);
             else hipLaunchKernelGGL((k_solve_mid2<1024, false>), dim3(B), dim3(nt), lds, s, a, st);
             g_last_batch_kernel = 3;
             return hipGetLastError();

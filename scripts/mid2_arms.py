@@ -17,6 +17,9 @@ sys.path.insert(0, str(ROOT / "oracle"))
 
 ARMS = {
     "def": {},
+    "fat": {"mid2_fat": 1},
+    "pair_lean": {"mid2_pair": 1},
+    "row_lean": {"mid2_pair": 2},
     "v1": {"mid_v1": 1},
     "mid2": {"mid2_min_n": 0},
     "packed": {"mid2_min_n": 0, "mid2_pair": 2},
