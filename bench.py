@@ -472,6 +472,12 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         if case == "feasible":
             pb.Kp.fill_(1e30)
             pb.solve(max_updates=1)
+        # warm-up: >= 0.5 s of these very iterations first.  Run after the
+        # compute-heavy legs, the first few hundred ms of the pass ran up to 8 %
+        # slower than the same process later (profiles/r04/pipe/bench_vs_standalone.json)
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < 0.5:
+            call(3 * K)
         # the same call with K and with 3K updates: the difference is 2K
         # iterations, no per-call cost; the median of 3 such pairs
         samples, ok, dts = [], True, []
@@ -488,7 +494,9 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         if pipe:  # the same iterations on k_solve_single (Gp read twice), same process and box
             prev = pqp_amd.tune("pipe_off", 1)
             try:
-                call(1)
+                tw = time.perf_counter()
+                while time.perf_counter() - tw < 0.5:
+                    call(3 * K)
                 single = sorted((call(3 * K) - call(K)) / (2 * K) for _ in range(3))[1]
             finally:
                 pqp_amd.tune("pipe_off", prev)
@@ -917,6 +925,11 @@ def main():
         g = em.leg("gather", gather_leg)
         if result is not None:
             result["gather_ms"], result["gather_ok"] = g.get("ms"), g.get("ok")
+    if world == 1 and not args.no_bundled:
+        # first of the legs: run after the others (their allocations and
+        # frees, compute-heavy kernels) the same pass measured 5-9 % slower
+        # than in a fresh process (profiles/r04/pipe/bench_vs_standalone.json)
+        em.leg("batch_converge", lambda: batch_converge_bench(pqp_amd))
     sizes = [int(v) for v in str(args.rowshard_n).split(",") if v.strip() and int(v) > 0]
     for i, n_rs in enumerate(sizes):  # every rank takes part
         em.leg("rowshard" if i == 0 else f"rowshard_{n_rs}",
@@ -929,7 +942,6 @@ def main():
         em.leg("single_n1024", lambda: single_bench(pqp_amd))
         em.leg("single_converge", lambda: single_converge_bench(pqp_amd))
         em.leg("setup_convert", lambda: setup_bench(pqp_amd))
-        em.leg("batch_converge", lambda: batch_converge_bench(pqp_amd))
     tol_cases = None
     if world == 1 and not args.no_bundled:
         import tempfile

@@ -753,8 +753,10 @@ def horizon_batch(directory, H: int, states, device=None) -> ProblemBatch:
     Gauss_Jordan(Qp_inv) (:251) and convertToDual (:489).  n_dual = 28 H,
     M = 7 H.  Setup runs on the device through the C ABI (pqp_batch_compute_fp
     / _mp, pqp_batch_gauss_jordan, pqp_batch_convert_to_dual); torch only
-    places the blocks.  The reference stops these problems at h = 313 for
-    every H it was run at (tests/test_gpu_mid.py)."""
+    places the blocks.  Every problem's setup and solve equal the reference's
+    (tests/test_gpu_mid.py; the bench's 16384-problem populations at H = 2 and
+    4 against tests/golden/horizon_states.npz: at H = 2 16377 stop at h = 313,
+    6 at 314, and one never meets the reference's exact-float gap test)."""
     import torch
 
     E = read_example(directory)
