@@ -925,6 +925,15 @@ def main():
         g = em.leg("gather", gather_leg)
         if result is not None:
             result["gather_ms"], result["gather_ok"] = g.get("ms"), g.get("ok")
+    # the CPU baseline's sample: distinct problems of this very workload, from
+    # the GPU batch (host copies, 4 MiB of Qd each)
+    inst = None
+    if world == 1 and not args.no_cpu_baseline:
+        inst = [(batch.qd_rowmajor(j), batch.Fd[j, :N].cpu().numpy()) for j in range(min(args.cpu_instances, B))]
+    # the headline's 4096 problems (Qd alone 16 GiB per GPU) are no longer
+    # needed: free them before the legs allocate their own
+    batch = Yh = None
+    torch.cuda.empty_cache()
     if world == 1 and not args.no_bundled:
         # first of the legs: run after the others (their allocations and
         # frees, compute-heavy kernels) the same pass measured 5-9 % slower
@@ -950,8 +959,6 @@ def main():
             tol_cases = tol_problems(pqp_amd, Path(td))
         em.leg("iters_to_tol", lambda: iters_to_tol_bench(pqp_amd, tol_cases))
     if world == 1 and not args.no_cpu_baseline:
-        # distinct problems of this very workload, from the GPU batch
-        inst = [(batch.qd_rowmajor(j), batch.Fd[j, :N].cpu().numpy()) for j in range(min(args.cpu_instances, B))]
         cb = em.leg("cpu_baseline", lambda: cpu_baseline(N, args.cpu_seconds, inst, tol_cases))
         ref_tol = cb.get("bundled", {}).get("iters_to_tol")
         if ref_tol and "iters_to_tol" in result and "error" not in result["iters_to_tol"]:
