@@ -425,7 +425,7 @@ def setup_bench(pqp_amd, N: int = 1024, M: int = 512, B: int = 64) -> dict:
                     "the reference's one-problem setup time is cpu_baseline.setup_convert_s"}
 
 
-def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> dict:
+def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 4) -> dict:
     """converge mode of B synthetic problems at once
     (ProblemBatch over pqp_batch_prepare + pqp_batch_solve_prepared,
     terminate() before every update), capped at K updates (the synthetic
@@ -453,6 +453,9 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         return time.perf_counter() - t0
 
     pipe = pqp_amd.tune_get("last_batch_kernel") == 1
+    # iterates per launch of pqp_batch_solve_prepared (pqp_capi.cpp: 2^26 / the
+    # update's and terminate()'s element count)
+    chunk = max(1, int((1 << 28) / (3.0 * N * N + 2.0 * N * M + 2.0 * M * M + 1.0)))
     kname = "k_solve_pipe" if pipe else "k_solve_single"
     rec = {}
     tf = ROOT / "profiles" / "pmc_traffic.json"
@@ -478,8 +481,10 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         tw = time.perf_counter()
         while time.perf_counter() - tw < 0.5:
             call(3 * K)
-        # the same call with K and with 3K updates: the difference is 2K
-        # iterations, no per-call cost; the median of 3 such pairs
+        # the same call with K and with 3K updates, both within one launch (a
+        # launch runs `chunk` iterates, pqp_capi.cpp): the difference is 2K
+        # iterations, no per-call or per-launch cost; the median of 3 such pairs
+        assert 3 * K <= chunk, (K, chunk)
         samples, ok, dts = [], True, []
         for _ in range(3):
             dt = call(K)
@@ -490,6 +495,10 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
             dts.append(dt)
         per_iter = sorted(samples)[1]
         dt = sorted(dts)[1]
+        # a long solve also pays each launch's start (state, the first Gp'Y
+        # pass, the host's check of the pending count): chunk vs 2 chunk
+        # updates, one launch more per chunk iterations
+        per_iter_solve = (call(2 * chunk) - call(chunk)) / chunk
         single = None
         if pipe:  # the same iterations on k_solve_single (Gp read twice), same process and box
             prev = pqp_amd.tune("pipe_off", 1)
@@ -505,7 +514,9 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
              "instance_iter_per_s": B / per_iter,
              "alg_bytes_per_iter": alg, "alg_GBps": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
              "design_bytes_per_iter": design, "design_GBps": design * B / per_iter / 1e9,
-             "call_ms": dt * 1e3, "call_instance_iter_per_s": B * K / dt, "all_capped": ok}
+             "call_ms": dt * 1e3, "call_instance_iter_per_s": B * K / dt, "all_capped": ok,
+             "ms_per_iteration_incl_launches": per_iter_solve * 1e3,
+             "frac_of_hbm_peak_incl_launches": alg * B / per_iter_solve / 1e9 / HBM_PEAK_GBS}
         if single is not None:
             r["k_solve_single_ms_per_iteration"] = single * 1e3
             r["speedup_vs_k_solve_single"] = single / per_iter
@@ -519,12 +530,14 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 8) -> d
         rec[case] = r
     del pb
     torch.cuda.empty_cache()
-    return {"problems": B, "n_dual": N, "m": M, "updates": K, "prepare_ms": prep_ms, **rec,
-            "kernel": kname,
+    return {"problems": B, "n_dual": N, "m": M, "updates": K, "iterates_per_launch": chunk, "prepare_ms": prep_ms,
+            **rec, "kernel": kname,
             "note": f"{kname}, one workgroup per problem; ms_per_iteration = (time of a 3K-update call - time "
-                    "of a K-update call) / 2K, the iterations alone, median of 3 pairs; call_ms = one K-update call "
-                    "(K + 1 terminate() "
-                    "+ K updates, state init and readback); prepare_ms = pqp_batch_prepare, once per batch"}
+                    "of a K-update call) / 2K, both within one launch: the iterations alone, median of 3 pairs; "
+                    "ms_per_iteration_incl_launches = the same over calls of 1 and 2 launches (each launch's "
+                    "start amortized over its iterates, as in a long solve); call_ms = one K-update call "
+                    "(K + 1 terminate() + K updates, state init and readback); prepare_ms = pqp_batch_prepare, "
+                    "once per batch"}
 
 
 def _testing_file(name: str, tmpdir: Path) -> Path:

@@ -1549,7 +1549,11 @@ int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float
     a.num_iter = num_iter;
     a.max_updates = max_updates;
     const double per_update = (double)N * N * 3.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
-    const long long chunk = (long long)((double)(1 << 26) / per_update);
+    // iterates per launch: about 2^28 element updates per problem (56 at n_dual
+    // 1024, M 512: each launch's start -- its first Gp'Y pass, the state, the
+    // host's check of the pending count -- cost about a quarter (infeasible) to
+    // 1.4 (feasible) iterates at 2^26: profiles/r04/pipe/launch_amortization.json)
+    const long long chunk = (long long)((double)(1 << 28) / per_update);
     a.chunk = g_tune.batch_chunk > 0 ? g_tune.batch_chunk : (chunk < 1 ? 1 : chunk);
     a.pending = static_cast<int*>(pending.p);
     SolveState* st = static_cast<SolveState*>(state.p);
