@@ -475,11 +475,11 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 4) -> d
         if case == "feasible":
             pb.Kp.fill_(1e30)
             pb.solve(max_updates=1)
-        # warm-up: >= 0.5 s of these very iterations first.  Run after the
-        # compute-heavy legs, the first few hundred ms of the pass ran up to 8 %
-        # slower than the same process later (profiles/r04/pipe/bench_vs_standalone.json)
+        # warm-up: >= 2 s of these very iterations first (after 0.5 s the
+        # pass still ran up to 5 % slower than a second later:
+        # profiles/r04/bench_r04q.json, profiles/r04/pipe/bench_vs_standalone.json)
         tw = time.perf_counter()
-        while time.perf_counter() - tw < 0.5:
+        while time.perf_counter() - tw < 2.0:
             call(3 * K)
         # the same call with K and with 3K updates, both within one launch (a
         # launch runs `chunk` iterates, pqp_capi.cpp): the difference is 2K

@@ -2139,10 +2139,22 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_pipe(SolveArgs A0, SolveStat
                 const bool dual = (tid == 0);
                 const float* qv = dual ? tq : tu;
                 const float* lv = dual ? fy : fu;
-                const int n = dual ? N : M;
+                const int n = dual ? N : M;  // multiples of 4 here, the vectors 16-byte aligned
+                // (Z'Q).Z :652-655 and F'Z :656-657, each in k order; the two
+                // chains interleaved and read 16 bytes at a time (one after the
+                // other, term by term, they took most of the cost phase)
                 float quad = 0.0f, lin = 0.0f;
-                for (int k = 0; k < n; ++k) quad += qv[k];  // (Z'Q).Z :652-655
-                for (int k = 0; k < n; ++k) lin += lv[k];   // F'Z :656-657
+                for (int k = 0; k < n; k += 4) {
+                    const sf4 a = *reinterpret_cast<const sf4*>(qv + k), b = *reinterpret_cast<const sf4*>(lv + k);
+                    quad += a.x;
+                    lin += b.x;
+                    quad += a.y;
+                    lin += b.y;
+                    quad += a.z;
+                    lin += b.z;
+                    quad += a.w;
+                    lin += b.w;
+                }
                 float J = 0.0f;
                 J = (float)((double)J + 0.5 * (double)quad);
                 J += lin;
