@@ -1756,9 +1756,27 @@ __global__ void __launch_bounds__(NT, MINB) k_solve_single(SolveArgs A0, SolveSt
                     const float* qv = dual ? tq : tu;
                     const float* lv = dual ? fy : tM;
                     const int n = dual ? N : M;
+                    // (Z'Q).Z :652-655 and F'Z :656-657, each in k order; the two
+                    // chains interleaved (read 16 bytes at a time where N, M are
+                    // multiples of 4 and the vectors 16-byte aligned)
                     float quad = 0.0f, lin = 0.0f;
-                    for (int k = 0; k < n; ++k) quad += qv[k];  // (Z'Q).Z :652-655
-                    for (int k = 0; k < n; ++k) lin += lv[k];   // F'Z :656-657
+                    int k = 0;
+                    if constexpr (VEC)
+                        for (; k + 4 <= n; k += 4) {
+                            const sf4 a = *reinterpret_cast<const sf4*>(qv + k), b = *reinterpret_cast<const sf4*>(lv + k);
+                            quad += a.x;
+                            lin += b.x;
+                            quad += a.y;
+                            lin += b.y;
+                            quad += a.z;
+                            lin += b.z;
+                            quad += a.w;
+                            lin += b.w;
+                        }
+                    for (; k < n; ++k) {
+                        quad += qv[k];
+                        lin += lv[k];
+                    }
                     float J = 0.0f;
                     J = (float)((double)J + 0.5 * (double)quad);
                     J += lin;
