@@ -4664,7 +4664,15 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
     } else {
-        if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);
+        // workgroups per CU by the register cap: where the passes are short
+        // (n_dual <= 512) more problems in flight beat deeper loads per lane --
+        // the MPC plant over 8 / 16 horizon stages (n_dual 224 / 448) 334.6 ->
+        // 244.4 ms at 5 and 199.1 -> 169.4 ms at 4; n_dual 1024 the same at 3,
+        // 4, 5 (profiles/r04/single_occ_ab.jsonl); single_occ 3 / 4 / 5 forces one
+        const int occ = g_tune.single_occ ? g_tune.single_occ : (a.N <= 256 ? 5 : (a.N <= 512 ? 4 : 3));
+        if (vec && occ == 5) hipLaunchKernelGGL((k_solve_single<256, true, 5>), dim3(B), dim3(256), lds, s, a, st);
+        else if (vec && occ == 4) hipLaunchKernelGGL((k_solve_single<256, true, 4>), dim3(B), dim3(256), lds, s, a, st);
+        else if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<256, false>), dim3(B), dim3(256), lds, s, a, st);
     }
     return hipGetLastError();
