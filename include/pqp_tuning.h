@@ -62,8 +62,10 @@ extern "C" {
  *                          one lane per row (max form)
  *   mid2_min_n [48]        smallest N path 3 runs on k_solve_mid2
  *   single_occ [0]         k_solve_single (16-byte loads) workgroups per CU, by
- *                          its register cap: 0 by n_dual (5 up to 256, 4 up to
- *                          512, else 3); 3, 4 or 5 forces one
+ *                          its register cap: 0 by shape and batch size (3
+ *                          above n_dual 768; below, the fewest rounds of
+ *                          resident problems, weighted +10 % per step); 3, 4
+ *                          or 5 forces one
  *   mid2_fat [0]           k_solve_mid2 workgroups of <= 6 waves on the
  *                          128-VGPR build (default: the 80-VGPR build, 6 waves
  *                          per SIMD, as many problems per CU as LDS allows)

@@ -4664,12 +4664,29 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
         if (vec) hipLaunchKernelGGL((k_solve_single<64, true>), dim3(B), dim3(64), lds, s, a, st);
         else hipLaunchKernelGGL((k_solve_single<64, false>), dim3(B), dim3(64), lds, s, a, st);
     } else {
-        // workgroups per CU by the register cap: where the passes are short
-        // (n_dual <= 512) more problems in flight beat deeper loads per lane --
-        // the MPC plant over 8 / 16 horizon stages (n_dual 224 / 448) 334.6 ->
-        // 244.4 ms at 5 and 199.1 -> 169.4 ms at 4; n_dual 1024 the same at 3,
-        // 4, 5 (profiles/r04/single_occ_ab.jsonl); single_occ 3 / 4 / 5 forces one
-        const int occ = g_tune.single_occ ? g_tune.single_occ : (a.N <= 256 ? 5 : (a.N <= 512 ? 4 : 3));
+        // workgroups per CU by the register cap (3, 4 or 5).  Up to n_dual 768
+        // the passes are latency-bound: more problems in flight pay, but each
+        // step up costs 5-13 % per round of resident problems, so the choice
+        // minimises rounds x (1 + 0.1 (occ - 3)) -- the MPC plant over 8 / 12 /
+        // 16 / 24 horizon stages measured best at 5 / 5 / 4 / 5, as predicted
+        // (profiles/r04/single_occ_ab*.jsonl); n_dual 896 and 1024 the same at
+        // 3, 4 and 5.  single_occ 3 / 4 / 5 forces one.
+        int occ = g_tune.single_occ;
+        if (!occ) {
+            occ = 3;
+            int dev = 0, cus = 0;
+            if (a.N <= 768 && hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+                double best = 1e300;
+                for (int o = 3; o <= 5; ++o) {
+                    const double cost = (double)((B + (long long)cus * o - 1) / ((long long)cus * o)) * (1.0 + 0.1 * (o - 3));
+                    if (cost < best - 1e-9) {
+                        best = cost;
+                        occ = o;
+                    }
+                }
+            }
+        }
         if (vec && occ == 5) hipLaunchKernelGGL((k_solve_single<256, true, 5>), dim3(B), dim3(256), lds, s, a, st);
         else if (vec && occ == 4) hipLaunchKernelGGL((k_solve_single<256, true, 4>), dim3(B), dim3(256), lds, s, a, st);
         else if (vec) hipLaunchKernelGGL((k_solve_single<256, true>), dim3(B), dim3(256), lds, s, a, st);

@@ -111,7 +111,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     long long batch_chunk = 0;  // iterates per problem per batched-solve launch (0: sized from N, M)
     int mid_off = 0;  // batched solves of mid-size N through k_solve_small / k_solve_single instead of path 3
     int mid2_pair = 0;  // k_solve_mid2's update rows: 0 by shape, 1 lane sides (v_med3_f32), 2 one lane per row
-    int single_occ = 0;  // k_solve_single (wide loads) workgroups per CU by register cap: 0 by n_dual (5 to 256, 4 to 512, else 3), 3 / 4 / 5 forced
+    int single_occ = 0;  // k_solve_single (wide loads) workgroups per CU by register cap: 0 by shape and batch (3 above n_dual 768), 3 / 4 / 5 forced
     int mid2_fat = 0;  // k_solve_mid2 workgroups of <= 6 waves on the 128-VGPR build (default: 80 VGPRs, 6 waves per SIMD)
     int mid2_min_n = 48;  // smallest N path 3 runs on k_solve_mid2 (below it k_solve_mid)
     int mid_v1 = 0;  // path 3 on k_solve_mid (terminate() after the update) instead of the pipelined k_solve_mid2
