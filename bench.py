@@ -654,12 +654,12 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
         blk = _FaultyBlock(blk)
     solver = RowShardedSolver(blk, N, dev, dist=dist)
 
-    def timed(n):
+    def timed(n, fn=None):
         _sync(dev)
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
-        solver.advance(n)
+        (fn or solver.advance)(n)
         _sync(dev)
         if dist is not None:
             dist.barrier()
@@ -678,6 +678,10 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     solver.advance(5)
     dt_eager = timed(updates)
     y_eager = solver.Y[:N].clone()
+    # the same eager updates without the collective (each rank's block alone,
+    # max over ranks): the difference is what the all-gather costs per update
+    # (DESIGN §6 assumed 10-25 us for it; this measures it on the first N > 1 run)
+    dt_block = timed(updates, solver.block_steps)
     # the same updates as hipGraph replays (block update + RCCL all-gather per
     # step, 16 steps per graph); not on gloo (rehearsal), see RowShardedSolver.capture
     G = 16
@@ -697,6 +701,8 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
            "iter_per_s": 1.0 / dt,
            "finite_nonneg": bool(torch.isfinite(y).all().item()) and bool((y >= 0).all().item()),
            "us_per_update_eager": dt_eager * 1e6,
+           "us_per_update_block_only": dt_block * 1e6,
+           "allgather_us_per_update": (dt_eager - dt_block) * 1e6 if dist is not None else None,
            "us_per_update_graph": dt_graph * 1e6 if dt_graph else None,
            "graph_same_bits_as_eager": same,
            "graph_note": (f"{G} updates ({'block update + all-gather' if dist is not None else 'block update'}) "

@@ -67,6 +67,14 @@ class RowShardedSolver:
             self.dist.all_gather_into_tensor(self.Y2, self.local, group=self.group)
         self.Y, self.Y2 = self.Y2, self.Y
 
+    def block_steps(self, updates: int):
+        """`updates` block updates with NO collective (Y is left as it is):
+        what each update costs this rank without the all-gather, for the
+        bench's `allgather_us_per_update` (the eager step minus this)."""
+        out = self.local if self.dist is not None else self.Y2
+        for _ in range(int(updates)):
+            self.block.update(self.Y, out)
+
     def capture(self, steps: int = 16) -> bool:
         """Record `steps` (even) updates -- each rank's block update and the
         RCCL all-gather -- as ONE hipGraph, replayed by :meth:`run`.  This

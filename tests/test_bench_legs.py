@@ -76,6 +76,9 @@ def test_rowshard_leg_failure_keeps_headline(tmp_path, fault):
     leg = r0["result"]["rowshard"]
     if not fault:
         assert "error" not in leg and leg["ranks"] == 2 and leg["finite_nonneg"] and leg["us_per_update"] > 0
+        # the block update timed alone beside update + all-gather
+        assert leg["us_per_update_block_only"] > 0
+        assert leg["allgather_us_per_update"] == pytest.approx(leg["us_per_update_eager"] - leg["us_per_update_block_only"])
     else:
         assert "error" in leg, leg
         r1 = json.loads((tmp_path / "r1.json").read_text())
