@@ -70,7 +70,11 @@ int terminate(float *Y, float *Qd, float *Fd, float *Md, float *U, float *Qp, fl
               float *Mp, float *Gp, float *Kp, int N, int M);
 
 /* PQP_CPU.c:489-498: Qd = (Gp Qp_inv) Gp', Fd = (Gp Qp_inv) Fp + Kp,
- * Md = (Fp' Qp_inv) Fp - Mp. */
+ * Md = (Fp' Qp_inv) Fp - Mp.
+ * NaN operands: where an operand is NaN, the output is NaN wherever the
+ * reference's is, but the NaN's sign and payload may differ (the host's and the
+ * GPU's multiply carry a NaN operand's bits differently); every non-NaN output
+ * is bit-identical.  DESIGN.md section 2. */
 void convertToDual(float *Qd, float *Fd, float *Md, float *Qp_inv, float *Gp, float *Kp, float *Fp,
                    float *Mp, int N, int M);
 
@@ -88,7 +92,11 @@ int checkFeas(float *U, float *Gp, float *Kp, int N, int M);
 void computeTheta(float *theta, float *Qd, int N);
 
 /* PQP_CPU.c:84-147: output[a x c] = op(mat1)[a x b] * op(mat2)[b x c];
- * output may alias an input. */
+ * output may alias an input.
+ * NaN operands: where an operand is NaN, the output is NaN wherever the
+ * reference's is, but the NaN's sign and payload may differ (the host's and the
+ * GPU's multiply carry a NaN operand's bits differently); every non-NaN output
+ * is bit-identical.  DESIGN.md section 2. */
 void matrixMultiply(float *output, float *mat1, int transpose1, float *mat2, int transpose2, int a, int b,
                     int c);
 
@@ -229,7 +237,8 @@ int pqp_batch_iterate(int B, int N, const float *d_QdT, int ldq, long long qstri
 /* Gauss_Jordan (PQP_CPU.c:251-326) on B n x n matrices. */
 int pqp_batch_gauss_jordan(int B, int n, const float *d_A, float *d_res, void *stream);
 
-/* convertToDual (PQP_CPU.c:489-498) on B primal problems. */
+/* convertToDual (PQP_CPU.c:489-498) on B primal problems (NaN operands: as
+ * convertToDual above). */
 int pqp_batch_convert_to_dual(int B, int N, int M, const float *d_Qp_inv, const float *d_Gp, const float *d_Kp,
                               const float *d_Fp, const float *d_Mp, float *d_Qd, float *d_Fd, float *d_Md,
                               void *stream);

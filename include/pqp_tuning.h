@@ -8,6 +8,12 @@
  * All knobs live in one process-wide struct (pqp::Tuning in the library) and
  * are reached through one keyed setter/getter, so the exported surface is four
  * functions whatever the number of knobs.
+ *
+ * Threading: pqp_tune and pqp_tune_trace serialize their writers, but the
+ * launches read the knobs without a lock.  Call them only while no other
+ * thread is inside a libpqp solve or launch (set up, then solve); a knob
+ * changed during a concurrent solve may be seen by some of its launches and
+ * not by others.
  */
 #ifndef PQP_TUNING_H
 #define PQP_TUNING_H

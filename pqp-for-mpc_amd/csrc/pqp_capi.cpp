@@ -974,7 +974,7 @@ using namespace pqp;
 
 extern "C" {
 
-int pqp_version(void) { return 100; }
+int pqp_version(void) { return 105; }  // ABI revision: INTEGRATION.md section 6
 
 // ---------------------------------------------------------------------------
 // 2a. status-returning host API
@@ -1904,7 +1904,13 @@ const KnobRef* find_knob(const char* key) {
 long long knob_value(const KnobRef& k) { return k.i ? *k.i : (k.b ? (long long)*k.b : *k.ll); }
 }  // namespace
 
+static std::mutex g_tune_mu;  // pqp_tune / pqp_tune_trace writers
+
 extern "C" int pqp_tune(const char* key, long long value, long long* old_value) {
+    // writers are serialized; readers (the launches) take no lock: the knobs
+    // are test and tuning hooks that must not change while another thread is
+    // inside a solve (include/pqp_tuning.h)
+    std::lock_guard<std::mutex> lk(g_tune_mu);
     const KnobRef* k = key ? find_knob(key) : nullptr;
     if (!k) return pqp::set_error(PQP_ERR_ARG, "pqp_tune: unknown key '%s'", key ? key : "(null)");
     if (old_value) *old_value = knob_value(*k);
@@ -1951,6 +1957,7 @@ extern "C" int pqp_tune_get(const char* key, long long* value) {
 extern "C" int pqp_tune_trace(const char* what, void* d_buf, int n) {
     if (!what || n < 0 || (n > 0 && !d_buf)) return pqp::set_error(PQP_ERR_ARG, "pqp_tune_trace: bad arguments");
     auto* buf = n > 0 ? static_cast<unsigned long long*>(d_buf) : nullptr;
+    std::lock_guard<std::mutex> lk(g_tune_mu);
     if (std::strcmp(what, "persist") == 0) {
         pqp::g_tune.persist_trace = buf;
         pqp::g_tune.persist_trace_n = n;

@@ -46,7 +46,7 @@ def test_python_mirror_binds_every_symbol():
     L = pqp_amd.lib()
     for n in declared_functions():
         assert getattr(L, n) is not None
-    assert L.pqp_version() >= 100
+    assert L.pqp_version() >= 105
 
 
 def declared_arity() -> dict[str, int]:
