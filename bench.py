@@ -453,9 +453,9 @@ def batch_converge_bench(pqp_amd, N: int = 1024, B: int = 4096, K: int = 4) -> d
         return time.perf_counter() - t0
 
     pipe = pqp_amd.tune_get("last_batch_kernel") == 1
-    # iterates per launch of pqp_batch_solve_prepared (pqp_capi.cpp: 2^26 / the
-    # update's and terminate()'s element count)
-    chunk = max(1, int((1 << 28) / (3.0 * N * N + 2.0 * N * M + 2.0 * M * M + 1.0)))
+    # iterates per launch of pqp_batch_solve_prepared, as the library sizes it
+    # (2^28 / the update's and terminate()'s element count, or the batch_chunk knob)
+    chunk = pqp_amd.batch_chunk_for(N, M)
     kname = "k_solve_pipe" if pipe else "k_solve_single"
     rec = {}
     tf = ROOT / "profiles" / "pmc_traffic.json"

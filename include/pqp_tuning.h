@@ -107,7 +107,9 @@ int pqp_tune(const char *key, long long value, long long *old_value);
  *                      3 k_solve_mid2
  *   persist_fallbacks  persistent launches that fell back (process total)
  *   converge_grid      in: *value = N << 32 | M; out: workgroups of the
- *                      persistent converge launch for (N, M) (0: not used) */
+ *                      persistent converge launch for (N, M) (0: not used)
+ *   batch_chunk_for    in: *value = N << 32 | M; out: iterates per problem per
+ *                      pqp_batch_solve launch (the batch_chunk knob if set) */
 int pqp_tune_get(const char *key, long long *value);
 
 /* Record an on-device timeline (s_memrealtime / s_memtime marks) of the

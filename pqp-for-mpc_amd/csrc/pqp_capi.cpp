@@ -1548,13 +1548,7 @@ int pqp_batch_solve_prepared(int B, int N, int M, const float* d_Qd, const float
     a.mode = (mode == PQP_MODE_CONVERGE) ? kModeConverge : kModeFixed;
     a.num_iter = num_iter;
     a.max_updates = max_updates;
-    const double per_update = (double)N * N * 3.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
-    // iterates per launch: about 2^28 element updates per problem (56 at n_dual
-    // 1024, M 512: each launch's start -- its first Gp'Y pass, the state, the
-    // host's check of the pending count -- cost about a quarter (infeasible) to
-    // 1.4 (feasible) iterates at 2^26: profiles/r04/pipe/launch_amortization.json)
-    const long long chunk = (long long)((double)(1 << 28) / per_update);
-    a.chunk = g_tune.batch_chunk > 0 ? g_tune.batch_chunk : (chunk < 1 ? 1 : chunk);
+    a.chunk = pqp::batch_chunk_for(N, M);
     a.pending = static_cast<int*>(pending.p);
     SolveState* st = static_cast<SolveState*>(state.p);
     for (;;) {
@@ -1904,6 +1898,20 @@ const KnobRef* find_knob(const char* key) {
 long long knob_value(const KnobRef& k) { return k.i ? *k.i : (k.b ? (long long)*k.b : *k.ll); }
 }  // namespace
 
+namespace pqp {
+// iterates per problem per batched-solve launch: about 2^28 element updates per
+// problem (56 at n_dual 1024, M 512: each launch's start -- its first Gp'Y
+// pass, the state, the host's check of the pending count -- cost about a
+// quarter (infeasible) to 1.4 (feasible) iterates at 2^26:
+// profiles/r04/pipe/launch_amortization.json), or the batch_chunk knob
+long long batch_chunk_for(int N, int M) {
+    if (g_tune.batch_chunk > 0) return g_tune.batch_chunk;
+    const double per_update = (double)N * N * 3.0 + 2.0 * N * M + 2.0 * M * M + 1.0;
+    const long long chunk = (long long)((double)(1 << 28) / per_update);
+    return chunk < 1 ? 1 : chunk;
+}
+}  // namespace pqp
+
 static std::mutex g_tune_mu;  // pqp_tune / pqp_tune_trace writers
 
 extern "C" int pqp_tune(const char* key, long long value, long long* old_value) {
@@ -1941,6 +1949,11 @@ extern "C" int pqp_tune_get(const char* key, long long* value) {
     }
     if (std::strcmp(key, "persist_fallbacks") == 0) {
         *value = pqp::g_persist_fallbacks;
+        return PQP_OK;
+    }
+    if (std::strcmp(key, "batch_chunk_for") == 0) {  // in: N << 32 | M; out: iterates per batched launch
+        const long long v = *value;
+        *value = pqp::batch_chunk_for((int)(v >> 32), (int)(v & 0xffffffff));
         return PQP_OK;
     }
     if (std::strcmp(key, "converge_grid") == 0) {  // in: N << 32 | M

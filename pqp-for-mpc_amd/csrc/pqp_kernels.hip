@@ -20,6 +20,7 @@
 // k*ldq + i) so that at a fixed k a wave's 64 lanes x 4 rows read 1 KiB of
 // contiguous HBM with one global_load_dwordx4 each (fully coalesced), while
 // y[k] is a wave-uniform LDS broadcast.
+#include <atomic>
 #include <type_traits>
 
 #include "pqp_device.h"
@@ -4642,6 +4643,21 @@ bool pipe_route(int N, int M, int variant) {
     return !g_tune.single_scalar && !g_tune.pipe_off && (g_tune.pipe_force || 3 * M >= N) && N > 64 && N % 4 == 0 &&
            M % 4 == 0 && solve_pipe_lds_bytes(round4(N), round4(M), big) <= kPipeLdsMax;
 }
+// CU count of the current device, queried once per device (the
+// occupancy choice below ran the attribute query on every launch)
+static int current_device_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    if (dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
+    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
+    return cus;
+}
 static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
     const size_t lds = solve_single_lds_bytes(a.ldq, a.ldm, a.sym != nullptr);
     // wide loads need every row and column start 16-byte aligned: N, M
@@ -4674,9 +4690,8 @@ static hipError_t launch_single_grid(int B, const SolveArgs& a, SolveState* st, 
         int occ = g_tune.single_occ;
         if (!occ) {
             occ = 3;
-            int dev = 0, cus = 0;
-            if (a.N <= 768 && hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+            const int cus = a.N <= 768 ? current_device_cus() : 0;
+            if (cus > 0) {
                 double best = 1e300;
                 for (int o = 3; o <= 5; ++o) {
                     const double cost = (double)((B + (long long)cus * o - 1) / ((long long)cus * o)) * (1.0 + 0.1 * (o - 3));

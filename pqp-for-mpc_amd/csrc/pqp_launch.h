@@ -123,6 +123,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
 };
 extern Tuning g_tune;
+long long batch_chunk_for(int N, int M);  // iterates per problem per batched-solve launch (pqp_capi.cpp)
 hipError_t launch_fill(float* a, float v, int n, hipStream_t s);
 // packets of 4 k per row side in the split layout (k padded to a multiple of 4)
 __host__ __device__ inline int split_kblocks(int N) { return (N + 3) / 4; }

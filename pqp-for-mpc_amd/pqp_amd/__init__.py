@@ -157,6 +157,12 @@ def tune_get(key: str, arg: int = 0) -> int:
     return int(v.value)
 
 
+def batch_chunk_for(N: int, M: int) -> int:
+    """Iterates per problem that one pqp_batch_solve launch runs for (N, M):
+    the library's own sizing (or the batch_chunk knob when set)."""
+    return tune_get("batch_chunk_for", (int(N) << 32) | int(M))
+
+
 # L.pqp_tune_<name>(value) -> previous value, for the knobs the tests and
 # scripts set (one C entry point behind them all)
 _KNOB_NAMES = {"persist": "persist_off", "converge_persist": "converge_persist_off", "wide_min_n": "wide_min_n",
@@ -169,6 +175,9 @@ _KNOB_NAMES = {"persist": "persist_off", "converge_persist": "converge_persist_o
 def _set_variant(variant: int) -> int:
     """The packed kernel-variant word of the round-1 tuning API: 0x100
     force_small, 0x200 force_single, bits 17-19 split_lw (1: 8 ... 4: 64)."""
+    known = 0x100 | 0x200 | (7 << 17)
+    if variant & ~known:  # the retired arms' bits (split_kind, split_u, ...): refused, not dropped
+        raise PQPError(PQP_ERR_ARG, f"pqp_tune_set_variant: retired variant bits {variant & ~known:#x}")
     lw_old = tune_get("split_lw")
     old = ((0x100 if tune_get("force_small") else 0) | (0x200 if tune_get("force_single") else 0)
            | (((lw_old.bit_length() - 3) if lw_old else 0) << 17))

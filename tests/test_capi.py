@@ -237,6 +237,15 @@ def test_tuning_knobs_roundtrip():
     assert pqp_amd.tune_get("split_lw") == 32
     assert pqp_amd.tune_get("force_single") == 1
     assert L.pqp_tune_set_variant(prev) == (3 << 17) | 0x200
+    with pytest.raises(pqp_amd.PQPError):  # a retired arm's bit is refused, not dropped
+        L.pqp_tune_set_variant(0x1000)
+    # the batched launch's chunk as the library sizes it (bench.py reads it)
+    assert pqp_amd.batch_chunk_for(1024, 512) == int((1 << 28) / (3.0 * 1024 * 1024 + 2.0 * 1024 * 512 + 2.0 * 512 * 512 + 1))
+    old_bc = pqp_amd.tune("batch_chunk", 7)
+    try:
+        assert pqp_amd.batch_chunk_for(1024, 512) == 7
+    finally:
+        pqp_amd.tune("batch_chunk", old_bc)
     assert L.pqp_tune_batch_converge(1 | 4 | 16) == 0 and pqp_amd.tune_get("single_scalar") == 1
     assert L.pqp_tune_batch_converge(0) == 1 | 4 | 16
     fb = C.c_longlong(-1)
