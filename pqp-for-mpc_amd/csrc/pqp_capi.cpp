@@ -296,6 +296,8 @@ struct pqp_problem {
     size_t hio_floats = 0;
     float* hin = nullptr;                            // pinned staging of small problems' inputs
     size_t hin_floats = 0;
+    float* hout = nullptr;                           // pinned output of the one-launch tiny solves (kTinyOut* layout)
+    void* hout_dev = nullptr;                        // its device address
     ~pqp_problem() {
         if (own_stream && stream) (void)hipStreamDestroy(stream);
         if (graph) (void)hipGraphExecDestroy(graph);
@@ -307,6 +309,7 @@ struct pqp_problem {
         if (hst) (void)hipHostFree(hst);
         if (hio) (void)hipHostFree(hio);
         if (hin) (void)hipHostFree(hin);
+        if (hout) (void)hipHostFree(hout);
     }
 };
 
@@ -879,6 +882,66 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     return PQP_OK;
 }
 
+// One small problem (N, M <= 32) from Y = 1000 in ONE launch (pqp_tiny.hip:
+// k_fixed_one / k_solve_trio): the kernel starts from h = 1 itself (no state
+// upload) and writes Y, U, the state and its error word to pinned host memory,
+// so a solve is one launch and one synchronisation, no copy kernels.
+int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max_updates, SolveOut& out,
+                     hipStream_t s) {
+    const int N = P.N, M = P.M;
+    if (!P.hout) {
+        PQP_HIP(hipHostMalloc((void**)&P.hout, sizeof(float) * kTinyOutFloats, hipHostMallocDefault));
+        PQP_HIP(hipHostGetDevicePointer(&P.hout_dev, P.hout, 0));
+    }
+    SolveArgs a{};
+    a.Qd = P.Qd.f();
+    a.Fd = P.Fd.f();
+    a.Md = P.Md.f();
+    a.Qp = P.Qp.f();
+    a.Qinv = P.Qinv.f();
+    a.Fp = P.Fp.f();
+    a.Mp = P.Mp.f();
+    a.Gp = P.Gp.f();
+    a.Kp = P.Kp.f();
+    a.Y = P.Y.f();
+    a.U = P.U.f();
+    a.N = N;
+    a.M = M;
+    a.ldq = round4(N);
+    a.ldm = round4(M);
+    a.mode = mode;
+    a.num_iter = num_iter;
+    a.max_updates = max_updates;
+    a.chunk = 1LL << 30;  // one launch: the kernel runs to the stop, the cap or num_iter
+    a.fresh = 1;
+    a.hout = P.hout_dev;
+    a.tiny_flags = (g_tune.tiny_dense ? kTinyDense : 0) | (g_tune.tiny_stall ? kTinyStall : 0);
+    a.trace = g_tune.tiny_trace;  // k_solve_trio timing (bundled size only): 4 words per wave
+    SolveState* dst = static_cast<SolveState*>(P.state.p);
+    const SolveState* hs = reinterpret_cast<const SolveState*>(P.hout + kTinyOutStateOffset);
+    const int* herr = reinterpret_cast<const int*>(P.hout) + kTinyOutErrOffset;
+    for (;;) {
+        PQP_HIP(launch_one_tiny(a, dst, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (*herr) return set_error(PQP_ERR_HIP, "k_solve_quintet: a wave's hand-off wait expired (N=%d, M=%d)", N, M);
+        if (hs->status != kStatusContinue) break;
+        a.fresh = 0;  // (a 2^30-iterate chunk ran out) resume from the device state
+    }
+    std::memcpy(P.hio, P.hout, sizeof(float) * N);
+    if (mode == kModeConverge) std::memcpy(P.hio + N, P.hout + kTinyOutUOffset, sizeof(float) * M);
+    out.staged = true;
+    out.h = hs->h;
+    out.status = hs->status;
+    out.have_costs = hs->have_costs;
+    out.last_stop = hs->last_stop;
+    if (hs->have_costs) {
+        out.Jp = hs->Jp;
+        out.Jd = hs->Jd;
+    }
+    g_last_path = kPathOneWorkgroup;
+    return PQP_OK;
+}
+
 int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_updates, bool resume, SolveOut& out,
                 hipStream_t s) {
     const int N = P.N, M = P.M;
@@ -898,6 +961,9 @@ int problem_run(pqp_problem& P, int mode, long long num_iter, long long max_upda
             return problem_run_wide(P, max_updates, out, s);
         }
     }
+    if (!resume && !g_tune.tiny_old && N <= 32 && M <= 32 && !g_tune.force_small && !g_tune.force_single &&
+        (mode == kModeFixed || (mode == kModeConverge && N + M < 64)))
+        return problem_run_tiny(P, mode, num_iter, max_updates, out, s);
     if (!P.small) PQP_TRY(ensure_single(P, s));
     SolveState& st = *P.hst;
     st = SolveState{};
@@ -1890,6 +1956,10 @@ const KnobRef* find_knob(const char* key) {
         {"pipe_force", &g_tune.pipe_force, nullptr, nullptr},
         {"batch_chunk", nullptr, nullptr, &g_tune.batch_chunk},
         {"converge_chunk", nullptr, nullptr, &g_tune.converge_chunk},
+        {"tiny_old", &g_tune.tiny_old, nullptr, nullptr},
+        {"tiny_dense", &g_tune.tiny_dense, nullptr, nullptr},
+        {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
+        {"iterate_stream", &g_tune.iterate_stream, nullptr, nullptr},
     };
     for (const KnobRef& k : knobs)
         if (std::strcmp(k.key, key) == 0) return &k;
@@ -1977,6 +2047,8 @@ extern "C" int pqp_tune_trace(const char* what, void* d_buf, int n) {
     } else if (std::strcmp(what, "mid") == 0) {
         pqp::g_tune.mid_trace = buf;
         pqp::g_tune.mid_trace_n = n;
+    } else if (std::strcmp(what, "tiny") == 0) {
+        pqp::g_tune.tiny_trace = buf;
     } else if (std::strcmp(what, "converge") == 0) {
         pqp::g_tune.converge_trace = buf;
         pqp::g_tune.converge_trace_n = n;

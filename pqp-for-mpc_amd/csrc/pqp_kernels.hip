@@ -197,6 +197,104 @@ __global__ void __launch_bounds__(NT) k_batch_iterate(const float* __restrict__ 
     const float* fin = (updates & 1) ? yb : ya;
     for (int i = tid; i < N; i += NT) Y[(size_t)b * ldv + i] = fin[i];
 }
+
+// ---------------------------------------------------------------------------
+// k_batch_stream: k_batch_iterate's arithmetic (the same lean / literal terms
+// in the same k order per row) with Qd's loads kept in flight continuously:
+// two register buffers of U float4 per lane, the block b + 1 loaded while
+// block b is summed, and the next row pass's (or the next iteration's) first
+// block loaded before the pass ends -- Qd does not depend on y, so only the
+// sums wait at the iteration's barrier.  N % 1024 == 0 (256 lanes x 4 rows
+// per pass, whole blocks of U k, block-aligned diagonal windows).
+// ---------------------------------------------------------------------------
+template <int U, bool NTL>
+__device__ __forceinline__ void stream_load(float4 (&q)[U], const float* __restrict__ src, int ldq) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) q[j] = ldq4<NTL>(src + (size_t)j * ldq);
+}
+template <int U>
+__device__ __forceinline__ void stream_block(Acc4& a, const float4 (&q)[U], int k0, bool literal,
+                                             const float* __restrict__ y, int row, const float th[4]) {
+    if (literal) {
+#pragma unroll
+        for (int j = 0; j < U; j += 4) {
+            const float4 yv = *reinterpret_cast<const float4*>(y + k0 + j);
+            literal4(a, q[j + 0], yv.x, k0 + j + 0, row, th);
+            literal4(a, q[j + 1], yv.y, k0 + j + 1, row, th);
+            literal4(a, q[j + 2], yv.z, k0 + j + 2, row, th);
+            literal4(a, q[j + 3], yv.w, k0 + j + 3, row, th);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < U; j += 4) {
+            const float4 yv = *reinterpret_cast<const float4*>(y + k0 + j);
+            lean4(a, q[j + 0], yv.x);
+            lean4(a, q[j + 1], yv.y);
+            lean4(a, q[j + 2], yv.z);
+            lean4(a, q[j + 3], yv.w);
+        }
+    }
+}
+template <int U, bool NTL>
+__global__ void __launch_bounds__(256) k_batch_stream(const float* __restrict__ QdT, long long qstride, int ldq,
+                                                      int N, const float* __restrict__ theta,
+                                                      const float* __restrict__ Fd, int ldv,
+                                                      const float* Y0, float* Y, int updates) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* ya = lds;
+    float* yb = lds + ldq;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const float* Q = QdT + (size_t)b * (size_t)qstride;
+    const float* th_g = theta + (size_t)b * ldv;
+    const float* fd_g = Fd + (size_t)b * ldv;
+    for (int i = tid; i < ldq; i += 256) {
+        ya[i] = (i < N) ? (Y0 ? Y0[(size_t)b * ldv + i] : 1000.0f) : 0.0f;  // initMat(Y,1000) :710
+        yb[i] = 0.0f;
+    }
+    const int nb = N / U, npass = N / 1024;
+    float4 qa[U], qb[U];
+    if (updates > 0) stream_load<U, NTL>(qa, Q + 4 * tid, ldq);
+    __syncthreads();
+    for (int u = 0; u < updates; ++u) {
+        const float* cur = (u & 1) ? yb : ya;
+        float* nxt = (u & 1) ? ya : yb;
+        for (int pass = 0; pass < npass; ++pass) {
+            const int row = pass * 1024 + 4 * tid;
+            const int wa = pass * 1024 + 256 * wave, wbd = wa + 256;  // this wave's diagonal window
+            Acc4 a;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a.p[r] = a.n[r] = 0.0f;
+            float th[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) th[r] = th_g[row + r];
+            const float* col = Q + row;
+            for (int kb = 0; kb < nb; kb += 2) {
+                stream_load<U, NTL>(qb, col + (size_t)(kb + 1) * U * ldq, ldq);
+                int k0 = kb * U;
+                stream_block<U>(a, qa, k0, k0 >= wa && k0 < wbd, cur, row, th);
+                // one block ahead: this pass's next, else the next pass's (or
+                // the next iteration's) first
+                if (kb + 2 < nb) stream_load<U, NTL>(qa, col + (size_t)(kb + 2) * U * ldq, ldq);
+                else if (pass + 1 < npass) stream_load<U, NTL>(qa, Q + (pass + 1) * 1024 + 4 * tid, ldq);
+                else if (u + 1 < updates) stream_load<U, NTL>(qa, Q + 4 * tid, ldq);
+                k0 += U;
+                stream_block<U>(a, qb, k0, k0 >= wa && k0 < wbd, cur, row, th);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = row + r;
+                const float f = fd_g[i];
+                const float num = a.n[r] + 1.0f * max_ref(0.0f, -f);  // matrixAdd(num, Fdn, 1) :611
+                const float den = a.p[r] + 1.0f * max_ref(0.0f, f);   // matrixAdd(den, Fdp, 1) :612
+                nxt[i] = num / den * cur[i];                           // updY :594
+            }
+        }
+        __syncthreads();
+    }
+    const float* fin = (updates & 1) ? yb : ya;
+    for (int i = tid; i < N; i += 256) Y[(size_t)b * ldv + i] = fin[i];
+}
 // </hot-kernel>
 
 // ---------------------------------------------------------------------------
@@ -4232,6 +4330,22 @@ static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qs
     // B = 4096, chunk 10.  The other unroll depths (4, 8, 32), default-policy
     // loads and max-based terms were measured and removed (DESIGN.md section 4,
     // profiles/r01/ab_4096*.txt).
+    if (g_tune.iterate_stream && N % 1024 == 0) {
+        const size_t lds = (size_t)2 * ldq * sizeof(float);
+        if (g_tune.iterate_stream == 2)
+            hipLaunchKernelGGL((k_batch_stream<8, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd,
+                               ldv, Y0, Y, updates);
+        else if (g_tune.iterate_stream == 3)
+            hipLaunchKernelGGL((k_batch_stream<32, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
+                               Fd, ldv, Y0, Y, updates);
+        else if (g_tune.iterate_stream == 4)
+            hipLaunchKernelGGL((k_batch_stream<16, false>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
+                               Fd, ldv, Y0, Y, updates);
+        else
+            hipLaunchKernelGGL((k_batch_stream<16, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
+                               Fd, ldv, Y0, Y, updates);
+        return hipGetLastError();
+    }
     launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s);
     return hipGetLastError();
 }

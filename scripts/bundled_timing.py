@@ -1,5 +1,11 @@
 """Time the bundled example (BASELINE configs[1]) through the C ABI: the
-problem is uploaded once; each solve is one pqp_problem_solve call.  Run under
+problem is uploaded once; each solve is one pqp_problem_solve call (launch,
+synchronisation, results on the host).  Forms, alternating in one process:
+  new    k_fixed_one (sparse form where the split rows allow) / k_solve_trio,
+         results written by the kernel to pinned host memory
+  dense  k_fixed_one's dense form only (pqp_tune tiny_dense)
+  old    the round-4 k_fixed_tiny / k_solve_wave with state copies (tiny_old)
+Each solve's bits are checked against tests/golden/bundled.npz.  Run under
 rocprofv3 --kernel-trace --stats to split kernel time from launch/readback."""
 from __future__ import annotations
 
@@ -8,25 +14,47 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
+FORMS = {"new": {}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
 
-def main(reps: int = 50):
+
+def main(reps: int = 200, rounds: int = 3):
     import pqp_amd
 
+    g = np.load(ROOT / "tests" / "golden" / "bundled.npz")
     P = pqp_amd.example_problem(ROOT / "tests" / "golden" / "example")
-    out = {}
+    modes = (("fixed1000", dict(mode=pqp_amd.MODE_FIXED, num_iter=1000)), ("converge", dict(max_updates=200000)))
+    out = {f"{m}_{f}": [] for m, _ in modes for f in FORMS}
+    bits = {}
     with pqp_amd.Problem(P) as prob:
-        for name, kw in (("fixed1000", dict(mode=pqp_amd.MODE_FIXED, num_iter=1000)), ("converge", dict(max_updates=200000))):
-            prob.solve(**kw)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                r = prob.solve(**kw)
-            dt = (time.perf_counter() - t0) / reps
-            out[name] = {"ms_per_solve": dt * 1e3, "h": r["h"], "iter_per_s": (r["h"] - 1 if name == "fixed1000" else r["h"]) / dt}
-    print(json.dumps(out))
+        for _ in range(rounds):
+            for form, knobs in FORMS.items():
+                old = {k: pqp_amd.tune(k, v) for k, v in knobs.items()}
+                try:
+                    for name, kw in modes:
+                        r = prob.solve(**kw)
+                        t0 = time.perf_counter()
+                        for _ in range(reps):
+                            r = prob.solve(**kw)
+                        dt = (time.perf_counter() - t0) / reps
+                        out[f"{name}_{form}"].append(dt * 1e3)
+                        if name == "fixed1000":
+                            ok = r["Y"].tobytes() == g["Y_fixed999"].tobytes() and r["h"] == 1000
+                        else:
+                            ok = (r["Y"].tobytes() == g["Ystar"].tobytes() and r["U"].tobytes() == g["Ustar"].tobytes()
+                                  and r["h"] == int(g["h"]) and np.float32(r["Jp"]) == g["Jp"] and np.float32(r["Jd"]) == g["Jd"])
+                        bits[f"{name}_{form}"] = bits.get(f"{name}_{form}", True) and bool(ok)
+                finally:
+                    for k, v in old.items():
+                        pqp_amd.tune(k, v)
+    res = {k: {"ms_per_solve_median": float(np.median(v)), "ms_all": [round(x, 4) for x in v],
+               "bit_exact": bits[k]} for k, v in out.items()}
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
-    main()
+    main(*(int(a) for a in sys.argv[1:]))

@@ -17,6 +17,19 @@ bundled)
   python scripts/probes/bundled_probe_data.py $O/bundled.bin &&
   timeout -k 10 60 ./scripts/probes/bundled_probe $O/bundled.bin 200 > $O/probe.jsonl 2>&1; cat $O/probe.jsonl
   ;;
+tiny)
+  # configs[1] on k_fixed_one / k_solve_trio: parity first, then the A/B timing
+  # and its kernel durations
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_tiny.py tests/test_gpu_parity.py tests/test_gpu_wave.py tests/test_gpu_handles.py tests/test_gpu_converge.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] &&
+  timeout -k 10 180 python -u scripts/bundled_timing.py > $O/ab.json 2>&1 && cat $O/ab.json &&
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 -u scripts/bundled_timing.py 50 1 > $O/prof.log 2>&1 && tail -2 $O/prof.log
+  ;;
+trio)
+  timeout -k 10 120 python -u scripts/trio_trace.py > $O/trio.json 2>&1; cat $O/trio.json
+  ;;
+iterab)
+  timeout -k 10 300 python -u scripts/iterate_ab.py > $O/iterate_ab.json 2>&1; cat $O/iterate_ab.json
+  ;;
 *)
   echo "unknown step $STEP"; exit 2;;
 esac

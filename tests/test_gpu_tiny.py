@@ -1,0 +1,146 @@
+"""One small problem in one launch (pqp_tiny.hip, configs[1]): k_fixed_one
+(fixed mode; the sparse form where every split row has few nonzero entries,
+else or on request the dense form) and k_solve_quintet (converge mode on five
+waves), both writing their results to pinned host memory.  Bar: the
+reference's bits (golden fixtures from PQP_CPU.c, and the oracle), identical
+h, for every form; the sparse form's switch to the dense form at the first
+non-finite y; the bounded waits' error path."""
+from __future__ import annotations
+
+from contextlib import contextmanager
+
+import numpy as np
+import pytest
+
+from conftest import CAP, assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
+FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}}
+
+
+@contextmanager
+def tuned(gpu_lib, knobs):
+    old = {k: gpu_lib.tune(k, v) for k, v in knobs.items()}
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            gpu_lib.tune(k, v)
+
+
+def bundled_problem(g):
+    P = {k: np.ascontiguousarray(g[k], dtype=np.float32) for k in KEYS}
+    P.update(N=int(g["N"]), M=int(g["M"]))
+    return P
+
+
+def _same_bits_or_both_nan(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all(nan | (a.view(np.uint32) == b.view(np.uint32))))
+
+
+@pytest.mark.parametrize("form", list(FORMS))
+def test_bundled_both_modes_every_form(gpu_lib, golden_bundled, form):
+    """configs[1] through one pqp_problem handle: converge (h = 313, Y*, U*,
+    Jp, Jd), fixed 1000 and fixed k updates, repeated solves."""
+    g = golden_bundled
+    with tuned(gpu_lib, FORMS[form]), gpu_lib.Problem(bundled_problem(g)) as prob:
+        for _ in range(2):
+            r = prob.solve(max_updates=CAP)
+            assert r["converged"] and r["h"] == int(g["h"]) == 313
+            assert_bitwise(r["Y"], g["Ystar"], f"{form}: Y*")
+            assert_bitwise(r["U"], g["Ustar"], f"{form}: U*")
+            assert np.float32(r["Jp"]) == g["iter_Jp"][-1] and np.float32(r["Jd"]) == g["iter_Jd"][-1]
+            f = prob.solve(gpu_lib.MODE_FIXED, num_iter=1000)
+            assert f["h"] == 1000
+            assert_bitwise(f["Y"], g["Y_fixed999"], f"{form}: fixed-999 Y")
+        for k in (1, 2, 10, 100, 312):
+            f = prob.solve(gpu_lib.MODE_FIXED, num_iter=k)
+            assert_bitwise(f["Y"], g[f"Y_h{k}"], f"{form}: Y after {k - 1} updates")
+
+
+@pytest.mark.parametrize("form", ["sparse", "dense"])
+@pytest.mark.parametrize("cap", [1, 2, 3, 7, 8, 9, 16, 311])
+def test_bundled_converge_capped(gpu_lib, golden_bundled, orc, form, cap):
+    """A cap inside and at the ring's depth (8 iterates in flight): the solve
+    ends on Y after `cap` updates, U from its terminate(), and the costs of
+    the last feasible iterate, exactly as the one-wave solver."""
+    g = golden_bundled
+    P = bundled_problem(g)
+    with tuned(gpu_lib, FORMS[form]):
+        r = gpu_lib.solve_dual(P, max_updates=cap)
+    assert not r["converged"] and r["h"] == cap + 1
+    assert_bitwise(r["Y"], orc.iterate(P["Qd"], P["Fd"], P["N"], cap), "Y at the cap")
+    flag, U, Jp, Jd = orc.terminate(r["Y"], *[P[k] for k in KEYS], P["N"], P["M"])
+    assert flag == 0
+    assert_bitwise(r["U"], U, "U of the last terminate()")
+    with tuned(gpu_lib, {"tiny_old": 1}):
+        o = gpu_lib.solve_dual(P, max_updates=cap)
+    assert o["h"] == r["h"] and np.float32(o["Jp"]) == np.float32(r["Jp"]) and np.float32(o["Jd"]) == np.float32(r["Jd"])
+
+
+def _growing_problem(N, M, seed):
+    """Rows with three negative off-diagonal entries (a = 3 < 5 = Theta) and
+    q_ii = 1: num / den = 8 / 6 per update, so y overflows to inf within a
+    few hundred updates (then inf / inf = NaN); a few all-zero rows stay at
+    their start.  Most entries are zero: the sparse form is taken."""
+    rng = np.random.default_rng(seed)
+    Q = np.zeros((N, N), np.float32)
+    for i in range(N - 2):
+        Q[i, i] = 1.0
+        for j in rng.choice([k for k in range(N) if k != i], 3, replace=False):
+            Q[i, j] = -1.0
+    Fd = np.zeros(N, np.float32)
+    Fd[: N // 2] = rng.standard_normal(N // 2).astype(np.float32)
+    P = dict(Qd=Q.reshape(-1), Fd=Fd, Md=np.ones(1, np.float32), Qp=np.eye(M, dtype=np.float32).reshape(-1),
+             Qp_inv=np.eye(M, dtype=np.float32).reshape(-1), Fp=rng.standard_normal(M).astype(np.float32),
+             Mp=np.ones(1, np.float32), Gp=rng.integers(-1, 2, (N, M)).astype(np.float32).reshape(-1),
+             Kp=(rng.random(N) * 10).astype(np.float32), N=N, M=M)
+    return P
+
+
+@pytest.mark.parametrize("N,M", [(8, 4), (28, 7), (32, 16)])
+def test_sparse_form_hands_over_at_the_first_nonfinite_y(gpu_lib, orc, N, M):
+    """y grows to inf and then NaN: the sparse form (which skips +-0 entries,
+    exact only for a finite y) must hand over to the dense form in time --
+    the fixed-mode Y equals the reference's update by update, NaN included."""
+    P = _growing_problem(N, M, N)
+    for k in (50, 200, 400, 1000):
+        want = orc.iterate(P["Qd"], P["Fd"], N, k - 1)
+        for form in ("sparse", "dense"):
+            with tuned(gpu_lib, FORMS[form]):
+                r = gpu_lib.solve_dual(P, mode=gpu_lib.MODE_FIXED, num_iter=k)
+            assert _same_bits_or_both_nan(r["Y"], want), f"{form} N={N} after {k - 1} updates"
+    assert not np.all(np.isfinite(orc.iterate(P["Qd"], P["Fd"], N, 999)))  # the case is exercised
+
+
+@pytest.mark.parametrize("N,M", [(8, 4), (28, 7), (32, 16)])
+def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M):
+    """Converge mode capped past the overflow: k_solve_quintet's update wave
+    (sparse form, then dense) against the oracle's solve, Y and U."""
+    P = _growing_problem(N, M, N + 1)
+    for cap in (100, 500):
+        h, Y, U = orc.solve(P, 0, 1000, cap)
+        r = gpu_lib.solve_dual(P, max_updates=cap)
+        # the oracle returns -h when capped; a NaN cost passes every gap test
+        # (NaN comparisons are false), so the reference may also stop there
+        assert r["h"] == abs(h) and r["converged"] == (h > 0), (r["h"], h)
+        assert _same_bits_or_both_nan(r["Y"], Y), f"N={N} cap={cap}"
+        assert _same_bits_or_both_nan(r["U"], U), f"U N={N} cap={cap}"
+
+
+def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled):
+    """Every wait of k_solve_quintet is bounded: with its deciding waves
+    stalled (test knob), the launch ends and the solve returns PQP_ERR_HIP
+    instead of hanging; the next solve on the same handle is exact again."""
+    g = golden_bundled
+    with gpu_lib.Problem(bundled_problem(g)) as prob:
+        with tuned(gpu_lib, {"tiny_stall": 1}):
+            with pytest.raises(gpu_lib.PQPError, match="hand-off wait expired"):
+                prob.solve(max_updates=CAP)
+        r = prob.solve(max_updates=CAP)
+        assert r["h"] == 313
+        assert_bitwise(r["Y"], g["Ystar"], "Y* after the error")
