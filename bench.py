@@ -58,7 +58,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-KERNEL = "k_batch_iterate<256,16,nt>"
+KERNEL = "k_batch_stream<16,nt>"
 
 
 def hot_kernel_hash() -> str:

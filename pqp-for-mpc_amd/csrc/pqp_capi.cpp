@@ -1959,7 +1959,7 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_old", &g_tune.tiny_old, nullptr, nullptr},
         {"tiny_dense", &g_tune.tiny_dense, nullptr, nullptr},
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
-        {"iterate_stream", &g_tune.iterate_stream, nullptr, nullptr},
+        {"iterate_v1", &g_tune.iterate_v1, nullptr, nullptr},
     };
     for (const KnobRef& k : knobs)
         if (std::strcmp(k.key, key) == 0) return &k;

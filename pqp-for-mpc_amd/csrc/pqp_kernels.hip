@@ -4330,20 +4330,16 @@ static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qs
     // B = 4096, chunk 10.  The other unroll depths (4, 8, 32), default-policy
     // loads and max-based terms were measured and removed (DESIGN.md section 4,
     // profiles/r01/ab_4096*.txt).
-    if (g_tune.iterate_stream && N % 1024 == 0) {
+    // n_dual a multiple of 1024 (the bench shape): k_batch_stream, one
+    // workgroup per CU, 16 + 16 float4 loads per lane kept in flight: 7.24-7.26
+    // TB/s against 7.02-7.04 for k_batch_iterate in one process (same bits).
+    // Measured slower and dropped: 8 + 8 (3 workgroups per CU, 7.07-7.09),
+    // 32 + 32 (7.10), 16 + 16 capped to 256 VGPRs (2 per CU, spills: 7.05),
+    // default-policy loads (6.34) -- profiles/r05/iterate_ab_*.json.
+    if (!g_tune.iterate_v1 && N % 1024 == 0) {
         const size_t lds = (size_t)2 * ldq * sizeof(float);
-        if (g_tune.iterate_stream == 2)
-            hipLaunchKernelGGL((k_batch_stream<8, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd,
-                               ldv, Y0, Y, updates);
-        else if (g_tune.iterate_stream == 3)
-            hipLaunchKernelGGL((k_batch_stream<32, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
-                               Fd, ldv, Y0, Y, updates);
-        else if (g_tune.iterate_stream == 4)
-            hipLaunchKernelGGL((k_batch_stream<16, false>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
-                               Fd, ldv, Y0, Y, updates);
-        else
-            hipLaunchKernelGGL((k_batch_stream<16, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta,
-                               Fd, ldv, Y0, Y, updates);
+        hipLaunchKernelGGL((k_batch_stream<16, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd,
+                           ldv, Y0, Y, updates);
         return hipGetLastError();
     }
     launch_iterate_t<16, true>(B, QdT, qstride, ldq, N, theta, Fd, ldv, Y0, Y, updates, s);

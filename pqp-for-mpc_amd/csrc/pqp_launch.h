@@ -134,7 +134,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
     int tiny_old = 0;    // one small problem on k_fixed_tiny / k_solve_wave (state copies) instead of k_fixed_one / k_solve_trio
     int tiny_dense = 0;  // k_fixed_one / k_solve_quintet without the sparse update form
-    int iterate_stream = 0;  // pqp_batch_iterate on k_batch_stream (N % 1024 == 0): 1 two 16-block buffers, 2 two 8-block buffers
+    int iterate_v1 = 0;  // pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate instead of k_batch_stream
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
     unsigned long long* tiny_trace = nullptr;  // k_solve_trio per-wave clocks (12 words; N = 28, M <= 8 only)
 };

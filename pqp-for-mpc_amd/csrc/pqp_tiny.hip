@@ -54,14 +54,18 @@ __device__ __forceinline__ float own_y(float yk) {
 __device__ __forceinline__ float partner(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
+// Progress words between the waves of one workgroup (LDS): a consumer's load
+// is an acquire and a producer's store a release at workgroup scope, so the
+// data a word covers is written before it and read after it (the compiler may
+// neither hoist a ring read above the wait nor sink a ring write below the
+// publish); the value is made wave-uniform (readfirstlane) so every wait is a
+// scalar branch, not an exec-mask loop.
 __device__ __forceinline__ int lds_ld(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// publish a progress word after the data it covers: the compiler keeps the
-// order (memory clobber), the LDS completes one wave's operations in order
+__device__ __forceinline__ void lds_after_wait() { __asm__ volatile("" ::: "memory"); }
 __device__ __forceinline__ void lds_publish(int* p, int v) {
-    __asm__ volatile("" ::: "memory");
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 constexpr int kRing = 8;             // iterates in flight between wave A and the decision
@@ -335,6 +339,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
                 if (d == kStopWord || d >= r - kRing || spin > spin_max) break;
             }
             QT_WAIT_END()
+            lds_after_wait();
             if (d == kStopWord) break;
             if (spin > spin_max) {
                 S.err = 1;
@@ -389,6 +394,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
                 QT_WAIT_END()
                 if (over) break;
             }
+            lds_after_wait();
             QT_MARK(0)
             const int slot = r & (kRing - 1);
             f4v y4[NMAX / 4];
@@ -463,6 +469,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
                 }
             }
             QT_WAIT_END()
+            lds_after_wait();
             if (over) break;
             const int slot = r & (kRing - 1);
             f4v t4[MMAX / 4];
@@ -517,6 +524,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
                 d = lds_ld(&S.decided);
                 if (d == r - 1 || d == kStopWord || spin > spin_max) break;
             }
+            lds_after_wait();
             if (d != r - 1) {
                 if (spin > spin_max) S.err = 1;
                 break;

@@ -30,6 +30,13 @@ trio)
 iterab)
   timeout -k 10 300 python -u scripts/iterate_ab.py > $O/iterate_ab.json 2>&1; cat $O/iterate_ab.json
   ;;
+headline)
+  # the batched iterate's parity, then its rocprofv3 kernel trace and the
+  # FETCH_SIZE / WRITE_SIZE passes behind profiles/pmc_traffic.json
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shard.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] &&
+  bash scripts/gpu_profile.sh $TAG && cat gpurun_out/prof_$TAG/kt_bench.json
+  # (then, here: python scripts/pmc_traffic.py gpurun_out/prof_TAG/pmc_fetch/..csv ..pmc_write/..csv 1024 4096 10)
+  ;;
 *)
   echo "unknown step $STEP"; exit 2;;
 esac

@@ -144,3 +144,21 @@ def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled):
         r = prob.solve(max_updates=CAP)
         assert r["h"] == 313
         assert_bitwise(r["Y"], g["Ystar"], "Y* after the error")
+
+
+def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled):
+    """A race between the waves (a ring slot read before it is written) shows
+    up as a wrong h or wrong bits in some solves: 400 one-shot solves in a
+    row, alternating modes, every one exact (k_solve_quintet's progress words
+    are acquire / release at workgroup scope)."""
+    g = golden_bundled
+    P = bundled_problem(g)
+    bad = []
+    for n in range(200):
+        r = gpu_lib.solve_dual(P, max_updates=CAP)
+        if r["h"] != 313 or r["Y"].tobytes() != g["Ystar"].tobytes() or r["U"].tobytes() != g["Ustar"].tobytes():
+            bad.append(("converge", n, r["h"]))
+        f = gpu_lib.solve_dual(P, mode=gpu_lib.MODE_FIXED, num_iter=1000)
+        if f["Y"].tobytes() != g["Y_fixed999"].tobytes():
+            bad.append(("fixed", n, f["h"]))
+    assert not bad, bad[:10]
