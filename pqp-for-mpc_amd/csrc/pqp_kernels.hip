@@ -4187,7 +4187,10 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                         const float kp = Kp[i];
                         if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
                     }
-                if (pend && lane == 0) flag[cw] = __any(bad) ? 1 : 0;
+                // the vote over every lane's rows, taken with the whole wave
+                // active (inside `lane == 0` it would see lane 0's rows only)
+                const bool any_bad = __any(bad);
+                if (pend && lane == 0) flag[cw] = any_bad ? 1 : 0;
                 float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
                 for (int j = l; j < lend; j += crows * nCR)  // (Y'Qd)_j Y_j :652-655; column j = row j when Qd is symmetric
                     tqs[j] = (sym ? mid_dot_row(Qd + j * ldn, ycur, nk) : mid_dot(Qd + j, ldn, ycur, nk)) * ycur[j];

@@ -37,6 +37,20 @@ headline)
   bash scripts/gpu_profile.sh $TAG && cat gpurun_out/prof_$TAG/kt_bench.json
   # (then, here: python scripts/pmc_traffic.py gpurun_out/prof_TAG/pmc_fetch/..csv ..pmc_write/..csv 1024 4096 10)
   ;;
+pytest)
+  # bash scripts/gpu_r05.sh pytest TAG <pytest args...>
+  shift 2
+  timeout -k 10 900 python -u -m pytest "$@" -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -15 $O/pytest.log; exit $rc
+  ;;
+hpmc)
+  # k_solve_mid2's VALU counters on the bench's horizon workload, H = 2, 4, 5:
+  # one rocprofv3 pass per H (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_BUSY_CYCLES,
+  # GRBM_GUI_ACTIVE) beside a kernel trace of the same command
+  for H in 2 4 5; do
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/h$H -o pmc -- python3 scripts/horizon_pmc.py $H > $O/h$H.json 2> $O/h$H.err || { tail -5 $O/h$H.err; exit 1; }
+    cat $O/h$H.json
+  done
+  ;;
 *)
   echo "unknown step $STEP"; exit 2;;
 esac

@@ -207,3 +207,29 @@ def test_prepare_needs_qdt_status_and_gpt_only_for_single(gpu_lib):
         assert pb._prep["GpT"] is not None
     finally:
         pqp_amd.tune("pipe_off", prev)
+
+
+@pytest.mark.parametrize("occ", [3, 4, 5])
+@pytest.mark.parametrize("feasible", [False, True])
+def test_single_register_capped_builds_vs_oracle(gpu_lib, orc, occ, feasible):
+    """k_solve_single's builds capped to 4 and 5 workgroups per CU
+    (taken by the launch only for batches above ~3 x the CU count at n_dual <=
+    768) forced on a small batch: n_dual 256, M 64 (M < N / 3, so path 2 runs
+    k_solve_single, not the pipe), infeasible and all-feasible iterates, the
+    oracle's h, Y and U bit for bit."""
+    B, N, M, cap = 3, 256, 64, 6
+    prev = gpu_lib.tune("single_occ", occ)
+    try:
+        pb = gpu_lib.ProblemBatch.synthetic(21, 0, B, N, M)
+        if feasible:
+            pb.Kp.fill_(1e30)
+        pb.solve(max_updates=cap)
+        assert gpu_lib.tune_get("last_batch_kernel") == 0
+    finally:
+        gpu_lib.tune("single_occ", prev)
+    for b in range(B):
+        P = orc.synth_problem(21, b, N, M)
+        if feasible:
+            P["Kp"] = np.full(N, 1e30, np.float32)
+        h, Y, U = orc.solve(P, max_updates=cap)
+        _check(pb, b, h, Y, U, f"single_occ={occ} feasible={feasible} problem {b}")

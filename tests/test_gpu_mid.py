@@ -294,3 +294,56 @@ def test_horizon_population_vs_reference(gpu_lib, H):
                     for b in range(B)], np.uint64)
     bad = np.nonzero(dig != G[f"digest{H}"])[0]
     assert bad.size == 0, f"{bad.size} of {B} problems differ from the reference in Y* or U*; first {bad[:8]}"
+
+
+def _growing(N, M, seed):
+    """Rows with three -1 entries off the diagonal and q_ii = 1 (Theta 5):
+    num / den = 8 / 6 per update, so Y overflows to inf after a few hundred
+    updates and then turns NaN (inf / inf); two all-zero rows stay put."""
+    rng = np.random.default_rng(seed)
+    Q = np.zeros((N, N), np.float32)
+    for i in range(N - 2):
+        Q[i, i] = 1.0
+        Q[i, rng.choice([k for k in range(N) if k != i], 3, replace=False)] = -1.0
+    Fd = np.zeros(N, np.float32)
+    Fd[: N // 2] = rng.standard_normal(N // 2).astype(np.float32)
+    return dict(Qd=Q.reshape(-1), Fd=Fd, Md=np.ones(1, np.float32), Qp=np.eye(M, dtype=np.float32).reshape(-1),
+                Qp_inv=np.eye(M, dtype=np.float32).reshape(-1), Fp=rng.standard_normal(M).astype(np.float32),
+                Mp=np.ones(1, np.float32), Gp=rng.integers(-1, 2, (N, M)).astype(np.float32).reshape(-1),
+                Kp=(rng.random(N) * 10).astype(np.float32), N=N, M=M)
+
+
+def _same_or_both_nan(got, want, what):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    assert np.array_equal(np.isnan(got), np.isnan(want)), what
+    ok = ~np.isnan(want)
+    assert_bitwise(got[ok], want[ok], what)
+
+
+@pytest.mark.parametrize("pair", [1, 2])
+def test_mid2_y_turning_nonfinite(gpu_lib, orc, knobs, pair):
+    """ADVICE r4: the lane-pair form sums num's terms negated (v_med3_f32);
+    once Y holds an inf or a NaN the phase must take the reference's selects
+    (whose signs the negated form could flip).  Y grows to inf and then NaN
+    during the solve: fixed mode before, across and after the overflow, and a
+    capped converge solve, against the oracle (NaN positions, every other
+    bit), on both update forms."""
+    knobs("mid2_pair", pair)
+    knobs("mid2_min_n", 0)
+    N, M = 112, 28
+    Ps = [_growing(N, M, s) for s in (1, 2)]
+    seen_inf = False
+    for n in (250, 300, 330, 400):
+        pb = _batch(gpu_lib, Ps).solve(gpu_lib.MODE_FIXED, num_iter=n)
+        assert gpu_lib.tune_get("last_batch_kernel") == 3
+        for b, P in enumerate(Ps):
+            _, Y, _ = orc.solve(P, mode=1, num_iter=n)
+            seen_inf |= bool(np.isinf(Y).any() or np.isnan(Y).any())
+            _same_or_both_nan(pb.Y[b].cpu().numpy(), Y, f"pair={pair} fixed num_iter={n} problem {b}")
+    assert seen_inf  # the non-finite case is exercised
+    pb = _batch(gpu_lib, Ps).solve(max_updates=350)
+    for b, P in enumerate(Ps):
+        h, Y, U = orc.solve(P, max_updates=350)
+        assert int(pb.h[b]) == abs(h)
+        _same_or_both_nan(pb.Y[b].cpu().numpy(), Y, f"pair={pair} converge problem {b} Y")
+        _same_or_both_nan(pb.U[b].cpu().numpy(), U, f"pair={pair} converge problem {b} U")
