@@ -317,7 +317,7 @@ def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
                     "on device, excluded from the timing; each solve bit-exact with PQP_CPU.c (tests)"}
 
 
-def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
+def horizon_bench(pqp_amd, Hs=(2, 4, 5), B: int = 16384) -> dict:
     """MPC over H horizon stages: B problems of the bundled plant stacked H
     times (pqp_amd.horizon_batch -- block-diagonal primal, each stage at its
     own perturbed state (seed 7), per-stage computeFp / computeMp, Gauss_Jordan
@@ -358,6 +358,28 @@ def horizon_bench(pqp_amd, Hs=(2, 4), B: int = 16384) -> dict:
                "h_min": int(h.min()), "h_max": int(h.max()), "h_mean": float(h.mean()), "max_updates": cap,
                "converged_frac": float((pb.status.cpu().numpy() == 1).mean()),
                "capped": int((pb.status.cpu().numpy() == 2).sum())}
+        # VALU-issue roofline (the kernel keeps every matrix in LDS: it is bound
+        # by instruction issue, not HBM): the wave-level VALU instructions of
+        # this exact solve (profiles/pmc_valu.json, rocprofv3 SQ_INSTS_VALU of
+        # scripts/horizon_pmc.py H, keyed by the kernel's source hash and the
+        # workload's iteration count) over this timed solve, against one VALU
+        # instruction per SIMD every 4 clocks (256 CUs x 4 SIMDs x 2.4 GHz / 4)
+        vf = ROOT / "profiles" / "pmc_valu.json"
+        vrec = json.loads(vf.read_text()).get(f"mid2_H{H}") if vf.exists() else None
+        khash = kernel_src_hash("solve-mid2")
+        if vrec and vrec.get("kernel_src_sha256") == khash and vrec.get("h_sum") == int(h.sum()):
+            peak = 256 * 4 * 2.4e9 / 4 / 1e9
+            ach = vrec["sq_insts_valu"] / dt / 1e9
+            row["roofline"] = {"bound": "valu", "achieved": ach, "peak": peak, "unit": "G wave-instr/s",
+                               "frac": ach / peak, "valu_insts": vrec["sq_insts_valu"],
+                               "source": "profiles/pmc_valu.json " + f"mid2_H{H}"}
+        else:
+            row["roofline"] = {"bound": "valu", "achieved": None,
+                               "source": "stale or missing VALU record for this kernel source / workload "
+                                         f"({khash}); re-run scripts/gpu_r05.sh hpmc + scripts/pmc_valu.py"}
+        row["note"] = ("the H stages are stacked block-diagonally and decoupled (each stage its own copy of "
+                       "the bundled plant at its own state): a size class of the MPC horizon (n_dual 28 H), "
+                       "not a coupled horizon")
         if ref is not None:
             P0 = pb.problem(0)
             ts = []

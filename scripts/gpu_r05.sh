@@ -51,6 +51,13 @@ hpmc)
     cat $O/h$H.json
   done
   ;;
+hab)
+  # horizon A/B: bash scripts/gpu_r05.sh hab TAG "H knob=v ..." "H knob=v ..." ...
+  shift 2
+  for args in "$@"; do
+    timeout -k 10 120 python -u scripts/horizon_pmc.py $args || exit 1
+  done
+  ;;
 *)
   echo "unknown step $STEP"; exit 2;;
 esac

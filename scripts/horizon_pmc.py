@@ -12,10 +12,14 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
 
-def main(H: int, B: int = 16384):
+def main(H: int, knobs=(), B: int = 16384):
     import torch
 
     import pqp_amd
+
+    for kv in knobs:  # key=value pqp_tune settings (A/B runs)
+        k, v = kv.split("=")
+        pqp_amd.tune(k, int(v))
 
     ex = ROOT / "tests" / "golden" / "example"
     E = pqp_amd.read_example(ex)
@@ -28,10 +32,10 @@ def main(H: int, B: int = 16384):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     h = pb.h.cpu().numpy()
-    print(json.dumps({"H": H, "n_dual": pb.N, "m": pb.M, "problems": B, "converge_ms": dt * 1e3,
+    print(json.dumps({"H": H, "knobs": list(knobs), "n_dual": pb.N, "m": pb.M, "problems": B, "converge_ms": dt * 1e3,
                       "kernel": pqp_amd.tune_get("last_batch_kernel"), "h_sum": int(h.sum()),
                       "h_mean": float(h.mean())}))
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]))
+    main(int(sys.argv[1]), sys.argv[2:])
