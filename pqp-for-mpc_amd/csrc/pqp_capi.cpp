@@ -1431,6 +1431,32 @@ int pqp_batch_gauss_jordan(int B, int n, const float* d_A, float* d_res, void* s
     return PQP_OK;
 }
 
+// A grow-only device workspace per (thread, device) for the batched setup
+// calls; never freed (a thread's buffer lives until the process ends: freeing
+// it at thread exit could run after the HIP runtime is gone).  Calls on one
+// thread are serialised (each synchronises its stream before returning).
+static int setup_workspace(size_t floats, float** out) {
+    thread_local void* buf[64] = {};
+    thread_local size_t cap[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return set_error(PQP_ERR_NO_DEVICE, "libpqp: cannot query the current device");
+    const size_t bytes = floats * sizeof(float);
+    if (cap[dev] < bytes) {
+        if (buf[dev]) (void)hipFree(buf[dev]);
+        buf[dev] = nullptr;
+        cap[dev] = 0;
+        const hipError_t e = hipMalloc(&buf[dev], bytes);
+        if (e != hipSuccess) {
+            buf[dev] = nullptr;
+            return set_error(PQP_ERR_ALLOC, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+        }
+        cap[dev] = bytes;
+    }
+    *out = static_cast<float*>(buf[dev]);
+    return PQP_OK;
+}
+
 int pqp_batch_convert_to_dual(int B, int N, int M, const float* d_Qp_inv, const float* d_Gp, const float* d_Kp,
                               const float* d_Fp, const float* d_Mp, float* d_Qd, float* d_Fd, float* d_Md,
                               void* stream) {
@@ -1439,16 +1465,19 @@ int pqp_batch_convert_to_dual(int B, int N, int M, const float* d_Qp_inv, const 
     PQP_TRY(ensure_device());
     hipStream_t s = static_cast<hipStream_t>(stream);
     const long long nm = (long long)N * M, mm = (long long)M * M, nn = (long long)N * N;
-    DevBuf GQ, fq;
-    PQP_TRY(GQ.floats((size_t)B * nm));
-    PQP_TRY(fq.floats((size_t)B * M));
+    // Gp Qp_inv (and Fp'Qp_inv) in this thread's grow-only workspace: no
+    // hipMalloc / hipFree (which synchronises the device) per call
+    float* ws = nullptr;
+    PQP_TRY(setup_workspace((size_t)B * nm + (size_t)B * M + 64, &ws));
+    float* GQ = ws;
+    float* fq = ws + (((size_t)B * nm + 63) & ~(size_t)63);
     // same sequence as dev_convert_to_dual (PQP_CPU.c:489-498), problem-strided
-    PQP_HIP(launch_matmul_seq_b(B, GQ.f(), d_Gp, 0, d_Qp_inv, 0, N, M, M, nm, mm, nm, s));
-    PQP_HIP(launch_matmul_seq_b(B, d_Qd, GQ.f(), 0, d_Gp, 1, N, M, N, nm, nm, nn, s));
-    PQP_HIP(launch_matmul_seq_b(B, d_Fd, GQ.f(), 0, d_Fp, 0, N, M, 1, nm, M, N, s));
+    PQP_HIP(launch_matmul_seq_b(B, GQ, d_Gp, 0, d_Qp_inv, 0, N, M, M, nm, mm, nm, s));
+    PQP_HIP(launch_matmul_seq_b(B, d_Qd, GQ, 0, d_Gp, 1, N, M, N, nm, nm, nn, s));
+    PQP_HIP(launch_matmul_seq_b(B, d_Fd, GQ, 0, d_Fp, 0, N, M, 1, nm, M, N, s));
     PQP_HIP(launch_axpy_b(B, d_Fd, d_Kp, 1.0f, N, N, N, s));
-    PQP_HIP(launch_matmul_seq_b(B, fq.f(), d_Fp, 1, d_Qp_inv, 0, 1, M, M, M, mm, M, s));
-    PQP_HIP(launch_matmul_seq_b(B, d_Md, fq.f(), 0, d_Fp, 0, 1, M, 1, M, M, 1, s));
+    PQP_HIP(launch_matmul_seq_b(B, fq, d_Fp, 1, d_Qp_inv, 0, 1, M, M, M, mm, M, s));
+    PQP_HIP(launch_matmul_seq_b(B, d_Md, fq, 0, d_Fp, 0, 1, M, 1, M, M, 1, s));
     PQP_HIP(launch_axpy_b(B, d_Md, d_Mp, -1.0f, 1, 1, 1, s));
     PQP_HIP(hipStreamSynchronize(s));
     return PQP_OK;
@@ -1960,6 +1989,7 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_dense", &g_tune.tiny_dense, nullptr, nullptr},
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
         {"iterate_v1", &g_tune.iterate_v1, nullptr, nullptr},
+        {"matvec_lds", &g_tune.matvec_lds, nullptr, nullptr},
     };
     for (const KnobRef& k : knobs)
         if (std::strcmp(k.key, key) == 0) return &k;

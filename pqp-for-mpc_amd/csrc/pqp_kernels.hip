@@ -29,6 +29,7 @@
 namespace pqp {
 
 static inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+static bool aligned16(const void* p);
 
 // <hot-kernel> (bench.py hashes the text up to </hot-kernel>: PMC traffic records are keyed by it)
 // ---------------------------------------------------------------------------
@@ -1190,6 +1191,47 @@ __global__ void __launch_bounds__(256) k_matvec_rows(float* __restrict__ out, co
         __syncthreads();
     }
     if (i < a) out[i] = acc;
+}
+
+// The same mat-vec with one lane per row and no LDS: each lane walks its own
+// row 16 bytes at a time, 16 loads in flight (a row's 128-byte lines are
+// fetched once and re-read from the vector cache), x[k] wave-uniform
+// (scalar loads).  One wave per 64 rows, so a batch of problems fills the
+// chip (convertToDual's Fd = (Gp Qp_inv) Fp of 64 problems of n_dual 1024:
+// 16 x 64 waves).  Needs bdim % 4 == 0 and 16-byte-aligned rows.
+__global__ void __launch_bounds__(64) k_matvec_lane(float* __restrict__ out, const float* __restrict__ A,
+                                                    const float* __restrict__ x, int a, int bdim, long long sA,
+                                                    long long sB, long long sO) {
+    const int z = blockIdx.y;
+    A += z * sA;
+    x += z * sB;
+    out += z * sO;
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a) return;
+    const float* row = A + (size_t)i * bdim;
+    float acc = 0.0f;
+    int k0 = 0;
+    for (; k0 + 64 <= bdim; k0 += 64) {
+        float4 v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = *reinterpret_cast<const float4*>(row + k0 + 4 * e);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {  // :88-100, k in order
+            const int k = k0 + 4 * e;
+            acc += v[e].x * x[k];
+            acc += v[e].y * x[k + 1];
+            acc += v[e].z * x[k + 2];
+            acc += v[e].w * x[k + 3];
+        }
+    }
+    for (; k0 < bdim; k0 += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(row + k0);
+        acc += v.x * x[k0];
+        acc += v.y * x[k0 + 1];
+        acc += v.z * x[k0 + 2];
+        acc += v.w * x[k0 + 3];
+    }
+    out[i] = acc;
 }
 
 // The row-vector form out[j] = sum_k x[k] B(k, j) (a = 1: convertToDual's
@@ -4458,8 +4500,12 @@ hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const 
             continue;
         }
         if (c == 1 && !tA && a >= 64 && b >= 32 && !g_tune.matmul_tiled_off) {
-            hipLaunchKernelGGL(k_matvec_rows, dim3(cdiv(a, 256), nb), dim3(256), 0, s, out + b0 * sO, A + b0 * sA,
-                               Bm + b0 * sB, a, b, sA, sB, sO);
+            if (b % 4 == 0 && sA % 4 == 0 && aligned16(A) && !g_tune.matvec_lds)
+                hipLaunchKernelGGL(k_matvec_lane, dim3(cdiv(a, 64), nb), dim3(64), 0, s, out + b0 * sO,
+                                   A + b0 * sA, Bm + b0 * sB, a, b, sA, sB, sO);
+            else
+                hipLaunchKernelGGL(k_matvec_rows, dim3(cdiv(a, 256), nb), dim3(256), 0, s, out + b0 * sO,
+                                   A + b0 * sA, Bm + b0 * sB, a, b, sA, sB, sO);
             continue;
         }
         const long long tiles = (long long)cdiv(c, MM8) * cdiv(a, MM8);
