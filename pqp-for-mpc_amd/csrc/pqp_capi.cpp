@@ -1990,6 +1990,7 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
         {"iterate_v1", &g_tune.iterate_v1, nullptr, nullptr},
         {"matvec_lds", &g_tune.matvec_lds, nullptr, nullptr},
+        {"gj_v1", &g_tune.gj_v1, nullptr, nullptr},
     };
     for (const KnobRef& k : knobs)
         if (std::strcmp(k.key, key) == 0) return &k;
