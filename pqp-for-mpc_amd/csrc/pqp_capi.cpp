@@ -297,6 +297,7 @@ struct pqp_problem {
     float* hin = nullptr;                            // pinned staging of small problems' inputs
     size_t hin_floats = 0;
     float* hout = nullptr;                           // pinned output of the one-launch tiny solves (kTinyOut* layout)
+    int out_tag = 0;                                 // the last tag a tiny launch was given
     void* hout_dev = nullptr;                        // its device address
     ~pqp_problem() {
         if (own_stream && stream) (void)hipStreamDestroy(stream);
@@ -571,6 +572,7 @@ enum SolvePath : int {
 };
 thread_local int g_last_path = 0;               // of the calling thread's last solve
 std::atomic<long long> g_persist_fallbacks{0};
+std::atomic<long long> g_tiny_stale{0};  // tiny solves whose pinned output did not carry their tag
 // problem_run_*_persist: a wait of the persistent launch expired (its
 // workgroups were not all resident); the caller falls back
 constexpr int kPersistStalled = 1;
@@ -890,8 +892,12 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
                      hipStream_t s) {
     const int N = P.N, M = P.M;
     if (!P.hout) {
-        PQP_HIP(hipHostMalloc((void**)&P.hout, sizeof(float) * kTinyOutFloats, hipHostMallocDefault));
+        // fine-grained (coherent) host memory: the kernel's stores reach it
+        // without a cache write-back at the kernel's end
+        PQP_HIP(hipHostMalloc((void**)&P.hout, sizeof(float) * kTinyOutFloats,
+                              hipHostMallocMapped | hipHostMallocCoherent));
         PQP_HIP(hipHostGetDevicePointer(&P.hout_dev, P.hout, 0));
+        reinterpret_cast<int*>(P.hout)[kTinyOutTagOffset] = 0;
     }
     SolveArgs a{};
     a.Qd = P.Qd.f();
@@ -920,9 +926,21 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     const SolveState* hs = reinterpret_cast<const SolveState*>(P.hout + kTinyOutStateOffset);
     const int* herr = reinterpret_cast<const int*>(P.hout) + kTinyOutErrOffset;
+    volatile const int* htag = reinterpret_cast<const int*>(P.hout) + kTinyOutTagOffset;
     for (;;) {
+        a.out_tag = ++P.out_tag;
+        if (a.out_tag == 0) a.out_tag = ++P.out_tag;
         PQP_HIP(launch_one_tiny(a, dst, s));
         PQP_HIP(hipStreamSynchronize(s));
+        if (*htag != a.out_tag) {
+            // not this launch's output (never seen so far): read the device copy instead
+            ++g_tiny_stale;
+            PQP_HIP(hipMemcpyAsync(P.hout, P.Y.p, sizeof(float) * N, hipMemcpyDeviceToHost, s));
+            if (mode == kModeConverge)
+                PQP_HIP(hipMemcpyAsync(P.hout + kTinyOutUOffset, P.U.p, sizeof(float) * M, hipMemcpyDeviceToHost, s));
+            PQP_HIP(hipMemcpyAsync(P.hout + kTinyOutStateOffset, dst, sizeof(SolveState), hipMemcpyDeviceToHost, s));
+            PQP_HIP(hipStreamSynchronize(s));
+        }
         if (*herr) return set_error(PQP_ERR_HIP, "k_solve_quintet: a wave's hand-off wait expired (N=%d, M=%d)", N, M);
         if (hs->status != kStatusContinue) break;
         a.fresh = 0;  // (a 2^30-iterate chunk ran out) resume from the device state
@@ -2046,6 +2064,10 @@ extern "C" int pqp_tune_get(const char* key, long long* value) {
     }
     if (std::strcmp(key, "last_batch_kernel") == 0) {  // 1: k_solve_pipe, 0: k_solve_single (path 2)
         *value = pqp::g_last_batch_kernel;
+        return PQP_OK;
+    }
+    if (std::strcmp(key, "tiny_stale") == 0) {  // tiny solves whose pinned output lacked their tag
+        *value = pqp::g_tiny_stale;
         return PQP_OK;
     }
     if (std::strcmp(key, "persist_fallbacks") == 0) {

@@ -39,10 +39,12 @@ struct SolveArgs {
     int fresh;        // 1: start from SolveState{h = 1}, ignoring the device state (no state upload)
     void* hout;       // optional pinned host buffer (kTinyOut* layout): Y, U, state, error word
     int tiny_flags;   // kTinyDense: the fixed-mode solve sums every entry (no sparse form)
+    int out_tag;      // written last to hout (kTinyOutTagOffset): the host checks it is this launch's
 };
 // k_fixed_one / k_solve_trio host output: Y at 0, U at kTinyOutUOffset, the
 // SolveState at kTinyOutStateOffset (floats), an int error word at kTinyOutErrOffset
-constexpr int kTinyOutUOffset = 32, kTinyOutStateOffset = 64, kTinyOutErrOffset = 72, kTinyOutFloats = 80;
+constexpr int kTinyOutUOffset = 32, kTinyOutStateOffset = 64, kTinyOutErrOffset = 72, kTinyOutTagOffset = 73,
+              kTinyOutFloats = 80;
 constexpr int kTinyDense = 1;
 constexpr int kTinyStall = 2;  // error-path tests: k_solve_quintet's deciding waves never decide
 // one problem with N, M <= 32 (fixed mode; converge mode needs N + M < 64) in one launch

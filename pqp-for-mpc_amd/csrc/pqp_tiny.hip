@@ -180,12 +180,21 @@ __device__ __forceinline__ void write_out(const SolveArgs& A, SolveState* st, in
     for (int k = tid; k < N; k += 64) A.Y[k] = Y[k];
     if (tid == 0) *st = s;
     if (A.hout) {
-        float* hy = static_cast<float*>(A.hout);
-        for (int k = tid; k < N; k += 64) hy[k] = Y[k];
+        // host memory (fine-grained): system-scope write-through stores of the
+        // data, their completion (vmcnt), then the launch's tag -- the host
+        // takes the buffer only with its own tag (a full system fence here, an
+        // L2 write-back, cost 11 us per launch: profiles/r05/bundled_ab_r05x.json)
+        int* hy = static_cast<int*>(A.hout);
+        for (int k = tid; k < N; k += 64)
+            __hip_atomic_store(hy + k, __float_as_int(Y[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (tid == 0) {
-            *reinterpret_cast<SolveState*>(hy + kTinyOutStateOffset) = s;
-            reinterpret_cast<int*>(hy)[kTinyOutErrOffset] = err;
+            const int* sw = reinterpret_cast<const int*>(&s);
+            for (int e = 0; e < (int)(sizeof(SolveState) / 4); ++e)
+                __hip_atomic_store(hy + kTinyOutStateOffset + e, sw[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(hy + kTinyOutErrOffset, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) __hip_atomic_store(hy + kTinyOutTagOffset, A.out_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -542,7 +551,10 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
             if (status >= 0) {
                 // computeUfromY wrote U on every terminate(): this one's stands
                 if (lane < M) A.U[lane] = u;
-                if (A.hout && lane < M) static_cast<float*>(A.hout)[kTinyOutUOffset + lane] = u;
+                if (A.hout && lane < M)
+                    __hip_atomic_store(static_cast<int*>(A.hout) + kTinyOutUOffset + lane, __float_as_int(u),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // U completed before wave A's tag
                 if (lane == 0) {
                     SolveState so = s0;
                     so.h = h;

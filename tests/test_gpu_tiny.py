@@ -154,11 +154,21 @@ def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled):
     g = golden_bundled
     P = bundled_problem(g)
     bad = []
+    stale0 = gpu_lib.tune_get("tiny_stale")
     for n in range(200):
         r = gpu_lib.solve_dual(P, max_updates=CAP)
         if r["h"] != 313 or r["Y"].tobytes() != g["Ystar"].tobytes() or r["U"].tobytes() != g["Ustar"].tobytes():
             bad.append(("converge", n, r["h"]))
+        # a short solve between the long ones: a stale pinned output would
+        # hand the next solve this one's h (1 or 2)
+        k = 1 + n % 2
+        f = gpu_lib.solve_dual(P, mode=gpu_lib.MODE_FIXED, num_iter=k)
+        if f["h"] != k or f["Y"].tobytes() != g[f"Y_h{k}"].tobytes():
+            bad.append(("fixed", k, n, f["h"]))
         f = gpu_lib.solve_dual(P, mode=gpu_lib.MODE_FIXED, num_iter=1000)
         if f["Y"].tobytes() != g["Y_fixed999"].tobytes():
-            bad.append(("fixed", n, f["h"]))
+            bad.append(("fixed", 1000, n, f["h"]))
     assert not bad, bad[:10]
+    # every solve's pinned output carried its own launch's tag (the device-copy
+    # fallback never ran)
+    assert gpu_lib.tune_get("tiny_stale") == stale0
