@@ -122,6 +122,12 @@ int pqp_tune_get(const char *key, long long *value);
  * 0-2 and iterations to word 4).  n = 0 turns it off.  Timing only. */
 int pqp_tune_trace(const char *what, void *d_buf, int n);
 
+/* Test hook: fill the LDS of every CU of the current device with `value`
+ * (64 KB per workgroup, 8 workgroups per CU, on the library stream, then
+ * synchronise).  A later kernel that reads LDS it never wrote -- padding of a
+ * vector -- then reads `value` (e.g. a NaN) instead of whatever was there. */
+int pqp_tune_poison_lds(float value);
+
 /* The first n values of glibc's unseeded rand() sequence (the testing/
  * reader's Kp overwrite), for the tests. */
 int pqp_tune_glibc_rand(int n, int *out);

@@ -885,7 +885,7 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
 }
 
 // One small problem (N, M <= 32) from Y = 1000 in ONE launch (pqp_tiny.hip:
-// k_fixed_one / k_solve_trio): the kernel starts from h = 1 itself (no state
+// k_fixed_one / k_solve_quintet): the kernel starts from h = 1 itself (no state
 // upload) and writes Y, U, the state and its error word to pinned host memory,
 // so a solve is one launch and one synchronisation, no copy kernels.
 int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max_updates, SolveOut& out,
@@ -922,7 +922,7 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
     a.fresh = 1;
     a.hout = P.hout_dev;
     a.tiny_flags = (g_tune.tiny_dense ? kTinyDense : 0) | (g_tune.tiny_stall ? kTinyStall : 0);
-    a.trace = g_tune.tiny_trace;  // k_solve_trio timing (bundled size only): 4 words per wave
+    a.trace = g_tune.tiny_trace;  // k_solve_quintet timing (bundled size only): 4 words per wave
     SolveState* dst = static_cast<SolveState*>(P.state.p);
     const SolveState* hs = reinterpret_cast<const SolveState*>(P.hout + kTinyOutStateOffset);
     const int* herr = reinterpret_cast<const int*>(P.hout) + kTinyOutErrOffset;
@@ -2108,6 +2108,21 @@ extern "C" int pqp_tune_trace(const char* what, void* d_buf, int n) {
     } else {
         return pqp::set_error(PQP_ERR_ARG, "pqp_tune_trace: unknown timeline '%s'", what);
     }
+    return PQP_OK;
+}
+
+extern "C" int pqp_tune_poison_lds(float value) {
+    PQP_TRY(pqp::ensure_device());
+    hipStream_t s = pqp::lib_stream();
+    int dev = 0, cus = 0;
+    PQP_HIP(hipGetDevice(&dev));
+    PQP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    pqp::DevBuf seen;
+    PQP_TRY(seen.alloc(sizeof(int)));
+    int bits;
+    std::memcpy(&bits, &value, sizeof bits);
+    PQP_HIP(pqp::launch_poison_lds(bits, static_cast<int*>(seen.p), cus, s));
+    PQP_HIP(hipStreamSynchronize(s));
     return PQP_OK;
 }
 

@@ -41,7 +41,7 @@ struct SolveArgs {
     int tiny_flags;   // kTinyDense: the fixed-mode solve sums every entry (no sparse form)
     int out_tag;      // written last to hout (kTinyOutTagOffset): the host checks it is this launch's
 };
-// k_fixed_one / k_solve_trio host output: Y at 0, U at kTinyOutUOffset, the
+// k_fixed_one / k_solve_quintet host output: Y at 0, U at kTinyOutUOffset, the
 // SolveState at kTinyOutStateOffset (floats), an int error word at kTinyOutErrOffset
 constexpr int kTinyOutUOffset = 32, kTinyOutStateOffset = 64, kTinyOutErrOffset = 72, kTinyOutTagOffset = 73,
               kTinyOutFloats = 80;
@@ -49,6 +49,8 @@ constexpr int kTinyDense = 1;
 constexpr int kTinyStall = 2;  // error-path tests: k_solve_quintet's deciding waves never decide
 // one problem with N, M <= 32 (fixed mode; converge mode needs N + M < 64) in one launch
 hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);
+// test hook: 8 * cus workgroups each fill 64 KB of LDS with `bits` (pqp_tune_poison_lds)
+hipError_t launch_poison_lds(int bits, int* seen, int cus, hipStream_t s);
 hipError_t launch_transpose_b(int B, const float* src, int rows, int cols, float* dst, hipStream_t s);
 // sym[b] = nonzero iff problem b's row-major Qd equals its transpose bit for bit
 hipError_t launch_check_symmetric(int B, const float* Qd, int N, int* sym, hipStream_t s);
@@ -134,13 +136,13 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int pipe_off = 0;  // batched converge of large problems on k_solve_single (two passes over Gp) instead of k_solve_pipe
     int batch_opts = 0;  // pqp_batch_solve: bit 0 no fused Y'Qd, bit 1 per-call transposes, bit 4 checkFeas over every row
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
-    int tiny_old = 0;    // one small problem on k_fixed_tiny / k_solve_wave (state copies) instead of k_fixed_one / k_solve_trio
+    int tiny_old = 0;    // one small problem on k_fixed_tiny / k_solve_wave (state copies) instead of k_fixed_one / k_solve_quintet
     int tiny_dense = 0;  // k_fixed_one / k_solve_quintet without the sparse update form
     int iterate_v1 = 0;
     int matvec_lds = 0;
     int gj_v1 = 0;  // batched Gauss_Jordan on k_gj_blocked (a division per row and step) instead of k_gj_blocked2  // setup mat-vecs on the LDS-staged k_matvec_rows instead of k_matvec_lane  // pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate instead of k_batch_stream
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
-    unsigned long long* tiny_trace = nullptr;  // k_solve_trio per-wave clocks (12 words; N = 28, M <= 8 only)
+    unsigned long long* tiny_trace = nullptr;  // k_solve_quintet per-wave clocks (24 words; N = 28, M <= 8 only)
 };
 extern Tuning g_tune;
 long long batch_chunk_for(int N, int M);  // iterates per problem per batched-solve launch (pqp_capi.cpp)

@@ -1,24 +1,28 @@
 // pqp_tiny.hip -- ONE small problem (N, M <= 32: the bundled example, configs[1])
 // solved by one launch whose results go straight to pinned host memory.
 //
-//   k_solve_trio  converge mode (solveQuadraticDual, PQP_CPU.c:694-750) on
-//                 three waves of one workgroup, one per SIMD, pipelined over
-//                 iterates:
-//                   wave A  updateY2 (:603-618): Y_{h+1} from Y_h, nothing else
-//                   wave B  terminate()'s N-long sums of Y_h: Gp'Y + Fp
-//                           (computeUfromY :354-355), (Y'Qd).Y and Fd.Y
-//                           (computeCost :652-657 for Jd)
-//                   wave C  the M-side chain of terminate(Y_h): U = -Qp_inv t
-//                           (:356-359), checkFeas (:632-641), U'Qp.U and Fp.U
-//                           (Jp), the gap tests (:680-686) and the decision
+//   k_solve_quintet  converge mode (solveQuadraticDual, PQP_CPU.c:694-750) on
+//                 five waves of one workgroup, pipelined over iterates:
+//                   wave A      updateY2 (:603-618): Y_{h+1} from Y_h, nothing else
+//                   waves B0/B1 terminate()'s N-long sums of the even / odd
+//                               iterates: Gp'Y + Fp (computeUfromY :354-355),
+//                               (Y'Qd).Y and Fd.Y (computeCost :652-657, Jd)
+//                   waves C0/C1 the M-side chain of the even / odd iterates:
+//                               U = -Qp_inv t (:356-359), checkFeas (:632-641),
+//                               U'Qp.U and Fp.U (Jp), the gap tests (:680-686);
+//                               decisions are taken in iterate order
 //                 updateY2 needs only Y_h, not terminate()'s verdict, so A runs
 //                 ahead of the decision (at most kRing iterates) and B, C follow;
 //                 iterates past the stopping one are discarded.  Vectors pass
 //                 through LDS rings indexed by the iterate; each wave publishes
-//                 its progress in one LDS word (data first, then the word: a
-//                 wave's LDS operations complete in order).  Every wait is
-//                 bounded: an expired wait ends the launch with an error word
-//                 instead of a hang.
+//                 its progress in one LDS word, a release store after its data
+//                 (a consumer's load of the word is an acquire: LDS operations
+//                 of one wave may complete out of order, and relaxed words lost
+//                 a race on cold launches).  LDS is never read where this
+//                 launch did not write it (padding of y and t is zeroed first:
+//                 a NaN left by an earlier kernel made 0 * NaN a NaN U).  Every
+//                 wait is bounded: an expired wait ends the launch with an error
+//                 word instead of a hang.
 //   k_fixed_one   fixed mode (while(h < NUM_ITER) updateY2, the testing/
 //                 harness loop) on one wave.  Where every lane's split row
 //                 (lane 2i + side: Qdn_theta / Qdp_theta row i) has at most P
@@ -293,7 +297,11 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
     // roles by hardware wave: 0 / 4 (one SIMD) B0 / B1, 1 A, 2 / 3 C0 / C1
     const int hw = tid >> 6;
     const int role = hw == 1 ? 0 : (hw == 0 ? 1 : (hw == 4 ? 4 : hw));  // 0 A, 1 B0, 4 B1, 2 C0, 3 C1
-    for (int k = tid; k < kRing * NMAX; k += 320) (&S.y[0][0])[k] = 0.0f;  // padding y_k = +0
+    // padding y_k, t_j = +0: C reads all MMAX entries of t (times qinv's zero
+    // padding), and LDS holds whatever the previous kernel left -- a NaN there
+    // made 0 * NaN a NaN U (seen after kernels that ran on non-finite data)
+    for (int k = tid; k < kRing * NMAX; k += 320) (&S.y[0][0])[k] = 0.0f;
+    for (int k = tid; k < kRing * MMAX; k += 320) (&S.t[0][0])[k] = 0.0f;
     if (tid == 0) {
         S.a_h = -1;
         S.b_h[0] = S.b_h[1] = -1;
@@ -590,7 +598,23 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
     }
 }
 
+// Test hook (pqp_tune_poison_lds): every workgroup fills 64 KB of LDS with
+// `bits` and leaves it there, over enough workgroups to pass through every CU:
+// a later kernel that reads LDS it never wrote (padding) then sees the value.
+__global__ void __launch_bounds__(256) k_poison_lds(int bits, int* __restrict__ seen) {
+    __shared__ int pool[16384];
+    for (int k = threadIdx.x; k < 16384; k += 256) pool[k] = bits;
+    __syncthreads();
+    // a read the compiler cannot predict keeps the stores
+    if (pool[(threadIdx.x * 61 + blockIdx.x) & 16383] != bits) seen[0] = 1;
+}
+
 }  // namespace
+
+hipError_t launch_poison_lds(int bits, int* seen, int cus, hipStream_t s) {
+    hipLaunchKernelGGL(k_poison_lds, dim3(8 * (cus > 0 ? cus : 256)), dim3(256), 0, s, bits, seen);
+    return hipGetLastError();
+}
 
 hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
     if (a.N > 32 || a.M > 32) return hipErrorInvalidValue;

@@ -99,6 +99,7 @@ SIGNATURES = {
     "pqp_tune_get": (C.c_int, [C.c_char_p, C.POINTER(C.c_longlong)]),
     "pqp_tune_trace": (C.c_int, [C.c_char_p, _vp, C.c_int]),
     "pqp_tune_glibc_rand": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
+    "pqp_tune_poison_lds": (C.c_int, [C.c_float]),
 }
 
 
@@ -155,6 +156,12 @@ def tune_get(key: str, arg: int = 0) -> int:
     v = C.c_longlong(int(arg))
     _check(lib().pqp_tune_get(key.encode(), C.byref(v)))
     return int(v.value)
+
+
+def poison_lds(value: float = float("nan")) -> None:
+    """pqp_tune_poison_lds (test hook): fill every CU's LDS with `value`, so a
+    kernel that reads LDS it never wrote reads that value."""
+    _check(lib().pqp_tune_poison_lds(float(value)))
 
 
 def batch_chunk_for(N: int, M: int) -> int:

@@ -1,7 +1,7 @@
 """Time the bundled example (BASELINE configs[1]) through the C ABI: the
 problem is uploaded once; each solve is one pqp_problem_solve call (launch,
 synchronisation, results on the host).  Forms, alternating in one process:
-  new    k_fixed_one (sparse form where the split rows allow) / k_solve_trio,
+  new    k_fixed_one (sparse form where the split rows allow) / k_solve_quintet,
          results written by the kernel to pinned host memory
   dense  k_fixed_one's dense form only (pqp_tune tiny_dense)
   old    the round-4 k_fixed_tiny / k_solve_wave with state copies (tiny_old)

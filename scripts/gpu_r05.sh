@@ -18,7 +18,7 @@ bundled)
   timeout -k 10 60 ./scripts/probes/bundled_probe $O/bundled.bin 200 > $O/probe.jsonl 2>&1; cat $O/probe.jsonl
   ;;
 tiny)
-  # configs[1] on k_fixed_one / k_solve_trio: parity first, then the A/B timing
+  # configs[1] on k_fixed_one / k_solve_quintet: parity first, then the A/B timing
   # and its kernel durations
   timeout -k 10 600 python -u -m pytest tests/test_gpu_tiny.py tests/test_gpu_parity.py tests/test_gpu_wave.py tests/test_gpu_handles.py tests/test_gpu_converge.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] &&
   timeout -k 10 180 python -u scripts/bundled_timing.py > $O/ab.json 2>&1 && cat $O/ab.json &&

@@ -22,7 +22,7 @@ ASAN = ROOT / "tests" / "asan"
 def built(tmp_path_factory):
     if not shutil.which("g++"):
         pytest.skip("g++ not available")
-    kobj = ROOT / "pqp-for-mpc_amd" / "build" / "pqp_kernels.o"
+    kobj = ROOT / "pqp-for-mpc_amd" / "build" / "pqp_tiny.o"
     if not kobj.exists():
         subprocess.run(["make", "-s", "-C", str(ROOT / "pqp-for-mpc_amd")], check=True)
     out = tmp_path_factory.mktemp("asan_build")

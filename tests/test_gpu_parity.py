@@ -25,12 +25,14 @@ def bundled_problem(g):
 # ---------------------------------------------------------------------------
 # bundled example (configs 1/2)
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("solver", ["wave_pipelined", "wave_plain", "tiny"])
+@pytest.mark.parametrize("solver", ["quintet", "wave_pipelined", "wave_plain", "tiny"])
 def test_bundled_converge_bit_exact(gpu_lib, golden_bundled, solver):
-    """One problem in converge mode: the one-wave solver (default; pipelined
-    and plain forms) and the four-wave k_solve_tiny."""
+    """One problem in converge mode: k_solve_quintet (default), and with the
+    tiny_old knob the round-4 kernels -- the one-wave solver (pipelined and
+    plain forms) and the four-wave k_solve_tiny."""
     g = golden_bundled
     L = gpu_lib.lib()
+    old_t = gpu_lib.tune("tiny_old", 0 if solver == "quintet" else 1)
     old_b = L.pqp_tune_wave_min_b(1 << 30 if solver == "tiny" else 1)
     old_p = L.pqp_tune_wave_pipe_max_b(0 if solver == "wave_plain" else 1 << 30)
     try:
@@ -38,8 +40,9 @@ def test_bundled_converge_bit_exact(gpu_lib, golden_bundled, solver):
     finally:
         L.pqp_tune_wave_min_b(old_b)
         L.pqp_tune_wave_pipe_max_b(old_p)
+        gpu_lib.tune("tiny_old", old_t)
     assert r["converged"]
-    assert r["h"] == int(g["h"]) == 313
+    assert r["h"] == int(g["h"]) == 313, (r["h"], r["Jp"], r["Jd"], gpu_lib.tune_get("last_path"))
     assert_bitwise(r["Y"], g["Ystar"], "Y*")
     assert_bitwise(r["U"], g["Ustar"], "U from the final terminate()")
     assert np.float32(r["Jp"]) == g["iter_Jp"][-1] and np.float32(r["Jd"]) == g["iter_Jd"][-1]
