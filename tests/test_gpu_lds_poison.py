@@ -127,3 +127,41 @@ def test_horizon_single_after_poison(gpu_lib, golden_bundled, orc, H):
     assert r["h"] == h == 313
     assert_bitwise(r["Y"], Y, "Y")
     assert_bitwise(r["U"], U, "U")
+
+
+def test_converge_fixtures_after_poison(gpu_lib, golden_converge, orc):
+    """The reference's converging synthetic cases (default routes: one
+    workgroup, the persistent converge launch, the graph chain by size)."""
+    cases, Ys, Us = golden_converge["cases"], golden_converge["Y"], golden_converge["U"]
+    yo = uo = 0
+    for (N, M, seed, h_ref) in cases:
+        N, M = int(N), int(M)
+        P = orc.synth_problem(int(seed), 0, N, M)
+        gpu_lib.poison_lds(float("nan"))
+        r = gpu_lib.solve_dual(P, max_updates=CAP)
+        assert r["converged"] and r["h"] == int(h_ref), (N, M, seed, r["h"])
+        assert_bitwise(r["Y"], Ys[yo:yo + N], f"Y {N}/{M}/{seed}")
+        assert_bitwise(r["U"], Us[uo:uo + M], f"U {N}/{M}/{seed}")
+        yo += N
+        uo += M
+
+
+@pytest.mark.parametrize("N,M", [(33, 9), (300, 70), (1024, 512), (2050, 100)])
+def test_fixed_mode_after_poison(gpu_lib, orc, N, M):
+    """Fixed mode of one problem (persistent / relay updates by size)."""
+    P = orc.synth_problem(43, 1, N, M)
+    gpu_lib.poison_lds(float("nan"))
+    f = gpu_lib.solve_dual(P, mode=gpu_lib.MODE_FIXED, num_iter=9)
+    _, Y, _ = orc.solve(P, mode=1, num_iter=9)
+    assert_bitwise(f["Y"], Y, f"{N}/{M} fixed 9")
+
+
+@pytest.mark.parametrize("tag", ["n1024_m512_s1_i0", "n1000_m500_s2_i7"])
+def test_batched_updates_after_poison(gpu_lib, golden_large, tag):
+    """The headline batched update (k_batch_stream / the iterate kernels)."""
+    N, M, seed, inst, ups = (int(v) for v in golden_large[f"{tag}_meta"])
+    b = gpu_lib.Batch(1, N).generate(seed, inst0=inst, M=M)
+    b.reset()
+    gpu_lib.poison_lds(float("nan"))
+    b.iterate(ups)
+    assert_bitwise(b.result()[0], golden_large[f"{tag}_Y"], "Y via batch_iterate")
