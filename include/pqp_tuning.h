@@ -81,6 +81,19 @@ extern "C" {
  *   wide_min_n [384]       converge mode: smallest N solved over many workgroups
  *   converge_chunk [65536] iterates decided per persistent converge launch
  *                          (<= 0 restores the default)
+ *   tiny_old [0]           one problem with N, M <= 32 on the round-4 kernels
+ *                          (k_fixed_tiny / k_solve_wave, state copies) instead
+ *                          of k_fixed_one / k_solve_quintet (one launch, results
+ *                          straight to pinned host memory)
+ *   tiny_dense [0]         k_fixed_one / k_solve_quintet without the sparse
+ *                          update form (every split entry summed)
+ *   iterate_v1 [0]         pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate
+ *                          instead of k_batch_stream
+ *   matvec_lds [0]         convertToDual's mat-vec on the LDS-staged
+ *                          k_matvec_rows instead of k_matvec_lane
+ *   gj_v1 [0]              batched Gauss_Jordan (n <= 1024): 0 k_gj_blocked3
+ *                          (only the columns that can still change an output),
+ *                          1 k_gj_blocked, 2 k_gj_blocked2 (every column)
  *  Paths and failure tests:
  *   persist_off [0]        fixed mode of n_dual <= 1024 through the graph-replayed
  *                          relay instead of the persistent launch
@@ -95,6 +108,8 @@ extern "C" {
  *   relay_spin_max [2^20]  relay hand-off wait budget in polls; 0 restores the
  *                          default, < 0 makes every wait expire (error path),
  *                          clamped to 2^30
+ *   tiny_stall [0]         k_solve_quintet's deciding waves return at once, so
+ *                          every wait of the launch expires (error path)
  * Settings apply to launches and graphs made afterwards. */
 int pqp_tune(const char *key, long long value, long long *old_value);
 

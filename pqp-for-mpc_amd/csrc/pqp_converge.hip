@@ -72,6 +72,15 @@ constexpr int kMaxW = 7;   // waves per workgroup: the chain roles use up to 6 (
 #ifndef PQP_CV_UPD_INPLACE  // upd_wave: later waves read their q while they wait for y
 #define PQP_CV_UPD_INPLACE 1
 #endif
+#ifndef PQP_CV_SLEEP0  // s_sleep units between UPD wave 0's / wave 1's / later waves' y sweeps
+#define PQP_CV_SLEEP0 0  // wave 0 (the chain starts on its slice) polls back to back
+#endif
+#ifndef PQP_CV_SLEEP1
+#define PQP_CV_SLEEP1 1
+#endif
+#ifndef PQP_CV_SLEEPN
+#define PQP_CV_SLEEPN 4  // waves 2+ (their turn comes later) poll a quarter as often
+#endif
 #ifndef PQP_CONVERGE_RING
 #define PQP_CONVERGE_RING 8
 #endif
@@ -261,7 +270,13 @@ __device__ __forceinline__ void upd_wave(const CvArgs& a, int g, int w, const f4
                             return false;
                         }
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    if (w == 0) {
+                        if (PQP_CV_SLEEP0 > 0) __builtin_amdgcn_s_sleep(PQP_CV_SLEEP0);
+                    } else if (w == 1) {
+                        __builtin_amdgcn_s_sleep(PQP_CV_SLEEP1);
+                    } else {
+                        __builtin_amdgcn_s_sleep(PQP_CV_SLEEPN);
+                    }
                 }
             } while (!ok);
 #pragma unroll

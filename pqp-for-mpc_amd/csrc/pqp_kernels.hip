@@ -4847,6 +4847,228 @@ __global__ void __launch_bounds__(256) k_gj_blocked2(const float* __restrict__ A
     }
 }
 
+// k_gj_blocked3's row update: rows j_i = g + r + i (i < RR) take the panel's
+// steps on their own columns (left [llo, n) and the diagonal, right [n, rhi):
+// see the kernel's header), each pivot row's LDS read shared by the RR rows;
+// SKIP: a row leaves out its own step (the panel's pivot rows).  Each element
+// is m -= q * t as the reference (:301): a packed multiply, then a packed add
+// of the negated product, each half rounded as the scalar operation.
+template <int C, int NB, int RR, bool SKIP>
+__device__ __forceinline__ void gj3_rows(float* __restrict__ aug, float* __restrict__ res, const int* perm,
+                                         const float* P, int* full, const float (&t)[NB],
+                                         unsigned long long badmask, bool fullp, bool last, int n, int p0, int ns,
+                                         int rwin, int g, int r, int lane) {
+    constexpr int W = 256 * C;
+    bool on[RR][C];
+    float v[RR][4 * C];
+#pragma unroll
+    for (int i = 0; i < RR; ++i) {
+        const int j = g + r + i;
+        const bool rowfull = fullp || ((badmask >> (r + i)) & 1ull);
+        if (rowfull && !fullp && lane == 0) *full = 1;  // every column from the next panel on
+        const int llo = j >= p0 ? 0 : p0;
+        const int rhi = n + (rowfull ? n : rwin);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int a = 256 * c + 4 * lane, b0 = 256 * c;
+            const bool blk = (b0 + 256 > llo && b0 < n) || (b0 <= j && j < b0 + 256) || (b0 + 256 > n && b0 < rhi);
+            on[i][c] = blk && ((a + 4 > llo && a < n) || (a <= j && j < a + 4) || (a + 4 > n && a < rhi));
+            sf4 q = sf4{0, 0, 0, 0};
+            if (on[i][c]) q = *reinterpret_cast<const sf4*>(aug + (size_t)j * W + 256 * c + 4 * lane);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[i][4 * c + e] = q[e];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+        if (s < ns) {
+            const float* prow = P + (size_t)s * W;
+            sf4 q[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) q[c] = *reinterpret_cast<const sf4*>(prow + 256 * c + 4 * lane);
+#pragma unroll
+            for (int i = 0; i < RR; ++i) {
+                if (SKIP && p0 + s == g + r + i) continue;
+                const float ts = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[s]), r + i));
+                const sf2 tt = sf2{ts, ts};
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    sf2 lo = sf2{v[i][4 * c], v[i][4 * c + 1]}, hi = sf2{v[i][4 * c + 2], v[i][4 * c + 3]};
+                    lo = lo - sf2{q[c].x, q[c].y} * tt;  // (:301)
+                    hi = hi - sf2{q[c].z, q[c].w} * tt;
+                    v[i][4 * c] = lo.x;
+                    v[i][4 * c + 1] = lo.y;
+                    v[i][4 * c + 2] = hi.x;
+                    v[i][4 * c + 3] = hi.y;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < RR; ++i) {
+        const int j = g + r + i;
+        if (!last) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (!on[i][c]) continue;
+                sf4 q;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) q[e] = v[i][4 * c + e];
+                *reinterpret_cast<sf4*>(aug + (size_t)j * W + 256 * c + 4 * lane) = q;
+            }
+        } else {  // temp = m_jj; the row / temp; right column n + q is res's column perm[q]
+            const float d = gj_any_col<C>(v[i], j);
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = 256 * c + 4 * lane + e;
+                    if (k >= n && k < 2 * n) res[(size_t)j * n + perm[k - n]] = v[i][4 * c + e] / d;
+                }
+        }
+    }
+}
+
+// k_gj_blocked3: k_gj_blocked2's panels and per-element operations on only
+// the columns that can still change an output.  Two facts of the reference's
+// loops (PQP_CPU.c:291-305), both exact:
+//  * The right half is kept in the bubble pass's row order (row r's 1 at
+//    column n + r; each column's operations are independent of the others, so
+//    a column permutation changes no value) and res is written through the
+//    permutation.  Right column n + q holds +0 in every row but row q until
+//    pivot q, and while every multiplier is finite, m_jq -= (+-0) * t leaves
+//    +0 and 1 as they are -- so a panel of pivots [p0, p0 + NB) touches right
+//    columns [n, n + p0 + NB) only.  A non-finite multiplier (an inf or NaN t
+//    turns 0 * t into NaN, as in the reference) makes its row take every
+//    column, and every row from the next panel on (a sticky flag); the pivot
+//    rows always take every column.
+//  * Left column c of row j is read again only while row j is still to be a
+//    pivot (j >= p0: its column c feeds the diagonal m_cc through step j) or
+//    as row j's own diagonal (the final scaling, :307-314).  So a row j < p0
+//    touches left columns [p0, n) and its diagonal only.
+// Per row and panel about (n + p0 + NB) - (j < p0 ? p0 : 0) of the 2n
+// columns: the loads and stores are masked per lane chunk (4 columns) and
+// skipped per 256-column block; the arithmetic runs on every block.
+template <int C, int NB>
+__global__ void __launch_bounds__(256) k_gj_blocked3(const float* __restrict__ A, float* __restrict__ aug,
+                                                     float* __restrict__ res, int n) {
+    constexpr int W = 256 * C;  // padded row of the augmented matrix
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* P = lds;                                                // [NB][W] pivot rows at their step
+    float* Pd = lds + NB * W;                                      // [NB] their diagonals
+    int* perm = reinterpret_cast<int*>(lds + NB * W + NB);         // [n] the bubble pass's row order
+    int* full = perm + n;                                          // sticky: every column from now on
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    {
+        const size_t b = blockIdx.x;
+        A += b * n * n;
+        res += b * n * n;
+        aug += b * (size_t)n * W;
+    }
+    // the one bubble pass on column 0 (:280-289) as a row order, then [A | I]
+    // with I in that order (:262-276), zero-padded to W columns
+    float* col0 = P;
+    for (int r = tid; r < n; r += 256) col0[r] = A[(size_t)r * n];
+    __syncthreads();
+    if (tid == 0) {
+        for (int r = 0; r < n; ++r) perm[r] = r;
+        for (int r = n - 1; r > 0; --r)
+            if (col0[perm[r - 1]] < col0[perm[r]]) {
+                const int t = perm[r];
+                perm[r] = perm[r - 1];
+                perm[r - 1] = t;
+            }
+        *full = 0;
+    }
+    __syncthreads();
+    for (int r = wv; r < n; r += 4) {
+        const int src = perm[r];
+        float v[4 * C];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = 256 * c + 4 * lane + e;
+                v[4 * c + e] = k < n ? A[(size_t)src * n + k] : (k == n + r ? 1.0f : 0.0f);
+            }
+        gj_store<C>(aug + (size_t)r * W, lane, v);
+    }
+    __syncthreads();
+    for (int p0 = 0; p0 < n; p0 += NB) {
+        const int ns = n - p0 < NB ? n - p0 : NB;
+        const int rwin = p0 + NB < n ? p0 + NB : n;  // right columns [n, n + rwin) can be nonzero
+        if (wv == 0) {  // 1. the pivot rows at their step, every column
+            for (int s = 0; s < ns; ++s) {
+                float v[4 * C];
+                gj_load<C>(aug + (size_t)(p0 + s) * W, lane, v);
+                gj_steps_any<C, NB>(v, P, Pd, W, p0, s, -1, lane);
+                gj_store<C>(P + (size_t)s * W, lane, v);
+                const float d = gj_any_col<C>(v, p0 + s);
+                if (lane == 0) Pd[s] = d;
+            }
+            // the pivot rows' right columns past the window are +-0 unless a
+            // non-finite multiplier of theirs made them NaN: then every row
+            // takes every column from this panel on
+            bool dirty = false;
+            for (int s = 0; s < ns; ++s)
+                for (int k = n + rwin + lane; k < 2 * n; k += 64) dirty |= P[(size_t)s * W + k] != 0.0f;
+            if (__any(dirty) && lane == 0) *full = 1;
+        }
+        __syncthreads();
+        const bool fullp = *full != 0;
+        const bool last = p0 + NB >= n;
+        for (int g = 64 * wv; g < n; g += 256) {
+            // 2a. row g + lane's multipliers of the panel's steps (k_gj_blocked2)
+            const int jl = g + lane;
+            float t[NB];
+            bool tbad = false;  // a multiplier this row uses is inf or NaN
+            {
+                float m[NB];
+#pragma unroll
+                for (int q = 0; q < NB; q += 4) {
+                    const sf4 x = jl < n ? *reinterpret_cast<const sf4*>(aug + (size_t)jl * W + p0 + q) : sf4{0, 0, 0, 0};
+                    m[q] = x.x;
+                    m[q + 1] = x.y;
+                    m[q + 2] = x.z;
+                    m[q + 3] = x.w;
+                }
+#pragma unroll
+                for (int s = 0; s < NB; ++s) {
+                    float x = m[s];
+#pragma unroll
+                    for (int s2 = 0; s2 < s; ++s2)
+                        if (p0 + s2 != jl) x -= P[(size_t)s2 * W + p0 + s] * t[s2];  // (:301) on column p0 + s
+                    t[s] = x / Pd[s];  // temp (:298)
+                    if (s < ns && p0 + s != jl) tbad |= !__builtin_isfinite(t[s]);
+                }
+            }
+            const unsigned long long badmask = __ballot(tbad);
+            // 2b. each row of the group takes the panel's steps on its columns:
+            // R rows at a time share each LDS read of a pivot row (the LDS
+            // reads, one pivot row per row and step, bounded k_gj_blocked2);
+            // the rows of this panel's own pivots one at a time (their own
+            // step is skipped)
+            constexpr int R = C <= 4 ? 4 : 2;
+            const int rend = n - g < 64 ? n - g : 64;
+            int r = 0;
+            for (; r + R <= rend; r += R) {
+                if (g + r < p0 + ns && g + r + R > p0) {
+#pragma unroll
+                    for (int i = 0; i < R; ++i)
+                        gj3_rows<C, NB, 1, true>(aug, res, perm, P, full, t, badmask, fullp, last, n, p0, ns, rwin, g,
+                                                 r + i, lane);
+                } else {
+                    gj3_rows<C, NB, R, false>(aug, res, perm, P, full, t, badmask, fullp, last, n, p0, ns, rwin, g, r,
+                                              lane);
+                }
+            }
+            for (; r < rend; ++r)
+                gj3_rows<C, NB, 1, true>(aug, res, perm, P, full, t, badmask, fullp, last, n, p0, ns, rwin, g, r, lane);
+        }
+        __syncthreads();
+    }
+}
+
 // padded row width and panel of the blocked kernel for an n x n matrix (0: not handled)
 static int gj_blocked_c(int n) { return n >= 1 && n <= 1024 ? (2 * n + 255) / 256 : 0; }
 size_t gauss_jordan_aug_floats(int n) {
@@ -4859,8 +5081,11 @@ static void launch_gj_blocked_c(int B, const float* A, float* aug, float* res, i
     const size_t lds = sizeof(float) * ((size_t)NB * 256 * C + NB);
     // k_gj_blocked2 (multipliers lane-parallel): 4096 n = 512 inverses 0.127-0.130
     // -> 0.114 s, n = 256 0.018 -> 0.016 s (profiles/r05/gj_timing_*.json)
-    if (g_tune.gj_v1) hipLaunchKernelGGL((k_gj_blocked<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
-    else hipLaunchKernelGGL((k_gj_blocked2<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
+    if (g_tune.gj_v1 == 1) hipLaunchKernelGGL((k_gj_blocked<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
+    else if (g_tune.gj_v1 == 2) hipLaunchKernelGGL((k_gj_blocked2<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
+    else
+        hipLaunchKernelGGL((k_gj_blocked3<C, NB>), dim3(B), dim3(256), lds + sizeof(int) * ((size_t)n + 1), s, A, aug,
+                           res, n);
 }
 static hipError_t launch_gj_blocked(int B, const float* A, float* aug, float* res, int n, hipStream_t s) {
     switch (gj_blocked_c(n)) {

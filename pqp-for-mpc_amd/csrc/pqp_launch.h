@@ -138,9 +138,9 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
     int tiny_old = 0;    // one small problem on k_fixed_tiny / k_solve_wave (state copies) instead of k_fixed_one / k_solve_quintet
     int tiny_dense = 0;  // k_fixed_one / k_solve_quintet without the sparse update form
-    int iterate_v1 = 0;
-    int matvec_lds = 0;
-    int gj_v1 = 0;  // batched Gauss_Jordan on k_gj_blocked (a division per row and step) instead of k_gj_blocked2  // setup mat-vecs on the LDS-staged k_matvec_rows instead of k_matvec_lane  // pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate instead of k_batch_stream
+    int iterate_v1 = 0;  // pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate instead of k_batch_stream
+    int matvec_lds = 0;  // setup mat-vecs on the LDS-staged k_matvec_rows instead of k_matvec_lane
+    int gj_v1 = 0;  // batched Gauss_Jordan: 1 k_gj_blocked (a division per row and step), 2 k_gj_blocked2 (every column of every row per panel), 0 k_gj_blocked3
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
     unsigned long long* tiny_trace = nullptr;  // k_solve_quintet per-wave clocks (24 words; N = 28, M <= 8 only)
 };

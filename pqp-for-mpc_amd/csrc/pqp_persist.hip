@@ -62,6 +62,15 @@ static_assert(kPW0 + kPW1 + 4 * kPW >= 256, "six waves must cover n_dual 1024");
 static_assert(kPW0 <= 64 && kPW1 <= 64 && kPW <= 64, "a slice is at most 4 granules per lane (one sweep)");
 constexpr int kLateGate = 1; // waves 4, 5 form their products once this wave has handed on its sums
 constexpr int kPMaxWaves = 6;
+#ifndef PQP_PS_SLEEP0  // s_sleep units between wave 0's / wave 1's / later waves' y sweeps
+#define PQP_PS_SLEEP0 0  // wave 0 (the chain starts on its slice) polls back to back
+#endif
+#ifndef PQP_PS_SLEEP1
+#define PQP_PS_SLEEP1 1
+#endif
+#ifndef PQP_PS_SLEEPN
+#define PQP_PS_SLEEPN 4  // waves 2+ (their turn comes later) poll a quarter as often
+#endif
 
 
 __device__ __forceinline__ void fail(int* err, int code) {
@@ -225,8 +234,16 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                     if ((++spins & 63) == 0 && dl.expired()) return false;
                     // one sweep at a time, a short pause between them (two sweeps
                     // in flight, issued 256 to 512 clocks apart, measured 5-15 %
-                    // slower: the pollers' own traffic)
-                    __builtin_amdgcn_s_sleep(1);
+                    // slower: the pollers' own traffic); wave 0 without a pause
+                    // and waves 2+ with 4 units: 3.58-3.64 against 3.61-3.69 us
+                    // per update (profiles/r05/persist_sleep_ab*.txt)
+                    if (w == 0) {
+                        if (PQP_PS_SLEEP0 > 0) __builtin_amdgcn_s_sleep(PQP_PS_SLEEP0);
+                    } else if (w == 1) {
+                        __builtin_amdgcn_s_sleep(PQP_PS_SLEEP1);
+                    } else {
+                        __builtin_amdgcn_s_sleep(PQP_PS_SLEEPN);
+                    }
                 }
             } while (!ok);
             // duplicates store the same value to the same word

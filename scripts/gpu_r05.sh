@@ -58,6 +58,12 @@ hab)
     timeout -k 10 120 python -u scripts/horizon_pmc.py $args || exit 1
   done
   ;;
+gj)
+  # Gauss_Jordan: parity of every form (incl. non-finite inputs), then the timing
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_wide.py -k gauss_jordan -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] &&
+  timeout -k 10 300 python -u scripts/gj_timing.py 512 4096 > $O/gj_timing.json 2>&1 && cat $O/gj_timing.json &&
+  timeout -k 10 300 python -u scripts/gj_timing.py 256 4096 > $O/gj_timing_256.json 2>&1 && cat $O/gj_timing_256.json
+  ;;
 *)
   echo "unknown step $STEP"; exit 2;;
 esac

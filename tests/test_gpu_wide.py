@@ -164,15 +164,79 @@ def test_problem_beyond_one_workgroup_budget(gpu_lib, orc):
     assert_bitwise(f["Y"], orc.iterate(P["Qd"], P["Fd"], N, 2), "fixed-mode Y")
 
 
+def _gj_batch(gpu_lib, A, form):
+    """pqp_batch_gauss_jordan of the matrices A (B x n x n) on `form`: 3
+    k_gj_blocked3, 2 k_gj_blocked2, 1 k_gj_blocked, 0 the per-sweep kernel;
+    B > 8 keeps large n off the one-launch-per-pivot path (replicated)."""
+    import torch
+
+    B, n = A.shape[0], A.shape[1]
+    L = gpu_lib.lib()
+    reps = 9 if n >= 64 and B <= 8 else 1
+    dA = torch.from_numpy(np.ascontiguousarray(A).reshape(B, -1)).cuda().repeat(reps, 1)
+    dR = torch.zeros_like(dA)
+    prev = L.pqp_tune_gj_blocked(0 if form else 1)
+    prev_v = gpu_lib.tune("gj_v1", {3: 0, 2: 2, 1: 1, 0: 0}[form])
+    try:
+        gpu_lib._check(L.pqp_batch_gauss_jordan(B * reps, n, gpu_lib.C.c_void_p(dA.data_ptr()),
+                                                gpu_lib.C.c_void_p(dR.data_ptr()),
+                                                gpu_lib.C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    finally:
+        L.pqp_tune_gj_blocked(prev)
+        gpu_lib.tune("gj_v1", prev_v)
+    return dR.cpu().numpy().reshape(reps, B, n * n)
+
+
+def _same_bits_or_nan(got, want, what):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    nan = np.isnan(got) & np.isnan(want)
+    bad = np.nonzero(~nan & (got.view(np.uint32) != want.view(np.uint32)))[0]
+    assert bad.size == 0, f"{what}: {bad.size} values differ; first at {bad[0]}: {got[bad[0]]!r} vs {want[bad[0]]!r}"
+
+
+@pytest.mark.parametrize("kind", ["zero_pivot", "nan_entry", "inf_entry", "neg_zero", "singular_late"])
+@pytest.mark.parametrize("n", [20, 100, 300])
+def test_gauss_jordan_nonfinite_vs_oracle(gpu_lib, orc, n, kind):
+    """Inputs that make a multiplier inf or NaN (a zero pivot, a NaN or inf
+    entry, a row that turns singular late) or carry -0: k_gj_blocked3 skips
+    right columns that are still exactly zero only while every multiplier is
+    finite, so these must match the reference as the full kernels do (NaN
+    positions; every other bit)."""
+    rng = np.random.default_rng(77 + n)
+    A = rng.standard_normal((2, n, n)).astype(np.float32)
+    A += np.eye(n, dtype=np.float32)[None] * n
+    if kind == "zero_pivot":
+        A[:, 3, :] = 0.0  # row 3 all zero: its pivot is 0, t = m / 0
+    elif kind == "nan_entry":
+        A[0, n // 2, n // 3] = np.nan
+        A[1, 5, 7] = np.nan
+    elif kind == "inf_entry":
+        A[0, n - 2, 1] = np.inf
+        A[1, 2, n - 1] = -np.inf
+    elif kind == "neg_zero":
+        A[:, :, n // 2] = -0.0
+        A[:, n // 2, n // 2] = 1.0
+    else:  # row n - 5 a copy of row n - 6: its pivot cancels to zero late
+        A[:, n - 5, :] = A[:, n - 6, :]
+    want = [orc.gauss_jordan(A[b].reshape(-1), n) for b in range(2)]
+    for form in (3, 2):
+        got = _gj_batch(gpu_lib, A, form)
+        for r in range(got.shape[0]):
+            for b in range(2):
+                _same_bits_or_nan(got[r, b], want[b], f"{kind} form {form} inverse {b} copy {r}")
+
+
 @pytest.mark.parametrize("n,B", [(1, 3), (7, 5), (15, 2), (16, 2), (17, 2), (63, 2), (100, 3), (256, 2), (300, 2),
                                  (385, 1), (512, 2), (640, 1), (1024, 1)])
-@pytest.mark.parametrize("blocked", [1, 0])
+@pytest.mark.parametrize("blocked", [3, 2, 1, 0])
 def test_gauss_jordan_blocked_vs_oracle(gpu_lib, orc, n, B, blocked):
     """The blocked batched Gauss_Jordan (pivots 16 or 8 at a time, one pass
-    over the augmented matrix per panel) and the one-pivot-per-sweep kernel:
-    bit-identical to the reference's restatement (PQP_CPU.c:251-326),
-    including the bubble pass (column 0 random, rows swapped), ragged panels
-    and both register layouts (n <= 512: 16-pivot panels, above: 8)."""
+    over the augmented matrix per panel: k_gj_blocked3 over the columns that
+    can still change an output, k_gj_blocked2 / k_gj_blocked over all) and
+    the one-pivot-per-sweep kernel: bit-identical to the reference's
+    restatement (PQP_CPU.c:251-326), including the bubble pass (column 0
+    random, rows swapped), ragged panels and both register layouts (n <= 512:
+    16-pivot panels, above: 8)."""
     import torch
 
     if n >= 640 and not blocked:
@@ -184,6 +248,7 @@ def test_gauss_jordan_blocked_vs_oracle(gpu_lib, orc, n, B, blocked):
     dR = torch.zeros_like(dA)
     L = gpu_lib.lib()
     prev = L.pqp_tune_gj_blocked(0 if blocked else 1)
+    prev_v = gpu_lib.tune("gj_v1", {3: 0, 2: 2, 1: 1, 0: 0}[blocked])
     try:
         # B > 8 keeps large n off the one-launch-per-pivot path: replicate
         reps = 9 if n >= 64 else 1
@@ -194,6 +259,7 @@ def test_gauss_jordan_blocked_vs_oracle(gpu_lib, orc, n, B, blocked):
                                                 gpu_lib.C.c_void_p(torch.cuda.current_stream().cuda_stream)))
     finally:
         L.pqp_tune_gj_blocked(prev)
+        gpu_lib.tune("gj_v1", prev_v)
     got = dR9.cpu().numpy()
     for b in range(B):
         want = orc.gauss_jordan(A[b].reshape(-1), n)
