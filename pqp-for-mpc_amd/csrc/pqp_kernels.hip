@@ -3374,12 +3374,24 @@ __device__ __forceinline__ void mid_load(MidBlk& B, const float* a, int as, cons
     B.b0 = *reinterpret_cast<const sf4*>(b + k);
     B.b1 = *reinterpret_cast<const sf4*>(b + k + 4);
 }
+// PK: the products two at a time (v_pk_mul_f32, each half rounded as the
+// scalar multiply), then the adds in k order -- a quarter fewer instructions
+// (the 80-VGPR mid2 build keeps the scalar form: the packed one spilled there)
+template <bool PK = false>
 __device__ __forceinline__ void mid_acc(float& s, const MidBlk& B) {
+    if constexpr (PK) {
+        const sf2 p0 = sf2{B.a[0], B.a[1]} * sf2{B.b0.x, B.b0.y}, p1 = sf2{B.a[2], B.a[3]} * sf2{B.b0.z, B.b0.w};
+        const sf2 p2 = sf2{B.a[4], B.a[5]} * sf2{B.b1.x, B.b1.y}, p3 = sf2{B.a[6], B.a[7]} * sf2{B.b1.z, B.b1.w};
+        s += p0.x; s += p0.y; s += p1.x; s += p1.y;
+        s += p2.x; s += p2.y; s += p3.x; s += p3.y;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += B.a[j] * (j < 4 ? B.b0[j] : B.b1[j - 4]);
+        for (int j = 0; j < 8; ++j) s += B.a[j] * (j < 4 ? B.b0[j] : B.b1[j - 4]);
+    }
 }
 // s = sum_k a[k * as] * b[k], k = 0..n8-1 (n8 a multiple of 8) in the
 // reference's order, product rounded before each add
+template <bool PK = false>
 __device__ __forceinline__ float mid_dot(const float* a, int as, const float* b, int n8) {
     float s = 0.0f;
     MidBlk c, x;
@@ -3387,16 +3399,16 @@ __device__ __forceinline__ float mid_dot(const float* a, int as, const float* b,
     int k = 0;
     for (; k + 16 < n8; k += 16) {
         mid_load(x, a, as, b, k + 8);
-        mid_acc(s, c);
+        mid_acc<PK>(s, c);
         mid_load(c, a, as, b, k + 16);
-        mid_acc(s, x);
+        mid_acc<PK>(s, x);
     }
     if (k + 8 < n8) {
         mid_load(x, a, as, b, k + 8);
-        mid_acc(s, c);
-        mid_acc(s, x);
+        mid_acc<PK>(s, c);
+        mid_acc<PK>(s, x);
     } else {
-        mid_acc(s, c);
+        mid_acc<PK>(s, c);
     }
     return s;
 }
@@ -3411,10 +3423,19 @@ __device__ __forceinline__ void rowdot_load(RowDotBlk& B, const float* a, const 
     B.b0 = *reinterpret_cast<const sf4*>(b + k);
     B.b1 = *reinterpret_cast<const sf4*>(b + k + 4);
 }
+template <bool PK = false>
 __device__ __forceinline__ void rowdot_acc(float& s, const RowDotBlk& B) {
+    if constexpr (PK) {
+        const sf2 p0 = sf2{B.a0.x, B.a0.y} * sf2{B.b0.x, B.b0.y}, p1 = sf2{B.a0.z, B.a0.w} * sf2{B.b0.z, B.b0.w};
+        const sf2 p2 = sf2{B.a1.x, B.a1.y} * sf2{B.b1.x, B.b1.y}, p3 = sf2{B.a1.z, B.a1.w} * sf2{B.b1.z, B.b1.w};
+        s += p0.x; s += p0.y; s += p1.x; s += p1.y;
+        s += p2.x; s += p2.y; s += p3.x; s += p3.y;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += (j < 4 ? B.a0[j] : B.a1[j - 4]) * (j < 4 ? B.b0[j] : B.b1[j - 4]);
+        for (int j = 0; j < 8; ++j) s += (j < 4 ? B.a0[j] : B.a1[j - 4]) * (j < 4 ? B.b0[j] : B.b1[j - 4]);
+    }
 }
+template <bool PK = false>
 __device__ __forceinline__ float mid_dot_row(const float* a, const float* b, int n8) {
     float s = 0.0f;
     RowDotBlk c, x;
@@ -3422,16 +3443,16 @@ __device__ __forceinline__ float mid_dot_row(const float* a, const float* b, int
     int k = 0;
     for (; k + 16 < n8; k += 16) {
         rowdot_load(x, a, b, k + 8);
-        rowdot_acc(s, c);
+        rowdot_acc<PK>(s, c);
         rowdot_load(c, a, b, k + 16);
-        rowdot_acc(s, x);
+        rowdot_acc<PK>(s, x);
     }
     if (k + 8 < n8) {
         rowdot_load(x, a, b, k + 8);
-        rowdot_acc(s, c);
-        rowdot_acc(s, x);
+        rowdot_acc<PK>(s, c);
+        rowdot_acc<PK>(s, x);
     } else {
-        rowdot_acc(s, c);
+        rowdot_acc<PK>(s, c);
     }
     return s;
 }
@@ -4003,6 +4024,21 @@ __device__ __forceinline__ float mid2_row(const float* q, const float* y, int nk
     return num / den * y[i];               // :594
 }
 
+#ifndef PQP_M2_DEC1  // k_solve_mid2, converge mode, lane-side build of up to 16 waves: one wave takes each decision
+#define PQP_M2_DEC1 1
+#endif
+#ifndef PQP_M2PK_T  // k_solve_mid2 (1024 build): packed products in T's dots, checkFeas, the Y'Qd terms, U'Qp
+#define PQP_M2PK_T 1
+#endif
+#ifndef PQP_M2PK_F
+#define PQP_M2PK_F 0  // (packed: the 1024 build spilled)
+#endif
+#ifndef PQP_M2PK_C
+#define PQP_M2PK_C 0  // (packed: the 1024 build spilled)
+#endif
+#ifndef PQP_M2PK_Q
+#define PQP_M2PK_Q 1
+#endif
 template <int MAXT, bool PAIR, int MINW = 1>
 __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -4039,6 +4075,14 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     // wC0 + nCR the costs
     const int crows = (NT / 64 - nUW - 2 >= (N + 31) / 32) ? 32 : 64;
     const int nCR = mid2_cr(N, crows);
+    const int wDec = wC0 + nCR;  // converge mode: the cost wave also takes each decision
+    constexpr bool PK = MINW == 1;  // packed dot products (the 80-VGPR build spilled with them)
+    // one decision per phase (on the cost wave) where the phase is bound by
+    // VALU issue -- the lane-side build, two problems per CU at n_dual 112:
+    // 38.9 -> 37.7 ms; elsewhere the single decider's latency between the
+    // phase's two barriers cost more than the instructions it saved (H = 2 /
+    // 3 / 5: +9 / +3.5 / +2.4 %, profiles/r05/mid2_dec_pk_ab.txt)
+    constexpr bool DEC1 = PQP_M2_DEC1 && PAIR && MINW == 1;
 
     // ---- stage the problem (once per launch; padding zero) ----
     for (int e = tid; e < L.total; e += NT) lds[e] = 0.0f;
@@ -4156,6 +4200,13 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         if (s - h0 >= A.chunk) { status = kStatusContinue; return true; }
         return false;
     };
+    // The phase's end: its barrier, then (converge mode, DEC1) the cost wave alone
+    // takes terminate(s-1)'s decision and posts it in LDS (flag[14] leave,
+    // flag[15] t_out - h0), and a second barrier; every wave reads it (one
+    // decision per phase instead of one per wave: its double-precision gap
+    // tests were ~7 % of the kernel's VALU instructions).  Between the two
+    // barriers every wave also reads Y_{s+1}'s non-finite flag; the next
+    // phase writes the flags only after the second barrier.
     auto phase_end = [&](long long s) -> bool {
         if (tr) busy += __builtin_amdgcn_s_memtime() - t0;
         __syncthreads();
@@ -4163,7 +4214,25 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             t_phase += __builtin_amdgcn_s_memtime() - t0;
             ++n_ph;
         }
-        return decide(s);
+        bool leave;
+        if (conv && DEC1) {
+            if (wave == wDec) {
+                const bool d = decide(s);
+                if (lane == 0) {
+                    flag[14] = d ? 1 : 0;
+                    flag[15] = (int)(t_out - h0);
+                }
+            }
+            y_nonfinite = flag[12 + (int)((s + 1) & 1)] != 0;  // Y_{s+1}, the next phase's Y_s
+            __syncthreads();
+            leave = flag[14] != 0;
+            if (leave) t_out = h0 + flag[15];
+        } else {
+            leave = decide(s);
+            y_nonfinite = flag[12 + (int)((s + 1) & 1)] != 0;
+            __syncthreads();
+        }
+        return leave;
     };
 
     if (wave < nUW) {
@@ -4196,9 +4265,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                     ynext[urow] = yn;
                 }
             }
-            if (phase_end(s)) break;
-            y_nonfinite = flag[12 + (int)((s + 1) & 1)] != 0;  // Y_{s+1}, the next phase's Y_s
-            __syncthreads();  // everyone has read this phase's flags before the next phase writes
+            if (phase_end(s)) break;  // (its second barrier: the flags are read before the next phase writes)
         }
     } else if (conv && wave == wT) {
         // ------------- T: tM = Gp'Y_s + Fp, Fd.Y_s, U_s = -Qp_inv tM -------------
@@ -4209,14 +4276,13 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             const float* ycur = Yr + (int)(s % 3) * nk;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
             if (lane <= M) {
-                const float d = mid_dot_row(grow, ycur, nk);
+                const float d = mid_dot_row<PK && PQP_M2PK_T>(grow, ycur, nk);
                 if (lane < M) tM[lane] = d + 1.0f * fpl;  // :355-356
                 else fdy[s & 1] = d;                      // Fd.Y :656
             }
             __builtin_amdgcn_wave_barrier();
-            if (lane < M) Us[(s & 1) * mk + lane] = -mid_dot_row(qirow, tM, mk);  // :357-358
+            if (lane < M) Us[(s & 1) * mk + lane] = -mid_dot_row<PK && PQP_M2PK_T>(qirow, tM, mk);  // :357-358
             if (phase_end(s)) break;
-            __syncthreads();
         }
     } else if (conv) {
         // ---------------- C: terminate(Y_{s-1}); Y_s'Qd ----------------
@@ -4232,7 +4298,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 int bad = 0;
                 if (pend)
                     for (int i = l; i < lend; i += crows * nCR) {
-                        const float g = mid_dot(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
+                        const float g = mid_dot<PK && PQP_M2PK_F>(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
                         const float kp = Kp[i];
                         if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
                     }
@@ -4242,10 +4308,10 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 if (pend && lane == 0) flag[cw] = any_bad ? 1 : 0;
                 float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
                 for (int j = l; j < lend; j += crows * nCR)  // (Y'Qd)_j Y_j :652-655; column j = row j when Qd is symmetric
-                    tqs[j] = (sym ? mid_dot_row(Qd + j * ldn, ycur, nk) : mid_dot(Qd + j, ldn, ycur, nk)) * ycur[j];
+                    tqs[j] = (sym ? mid_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn, ycur, nk) : mid_dot<PK && PQP_M2PK_C>(Qd + j, ldn, ycur, nk)) * ycur[j];
             } else if (pend && cw == nCR) {
                 if (lane < M) {
-                    tu[lane] = mid_dot(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
+                    tu[lane] = mid_dot<PK && PQP_M2PK_Q>(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
                     fu[lane] = Fp[lane] * Uo[lane];                         // Fp'U :656-657
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -4256,14 +4322,12 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 }
             }
             if (phase_end(s)) break;
-            __syncthreads();
         }
     } else {
         // fixed mode: the waves beside the update keep the barrier count
         for (long long s = h0;; ++s) {
             if (tr) t0 = __builtin_amdgcn_s_memtime();
             if (phase_end(s)) break;
-            __syncthreads();
         }
     }
     // the result: Y and U of iterate t_out (converge) or Y_s (fixed)
@@ -4279,7 +4343,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             T[4] += n_ph;
         }
     }
-    if (tid == 0) {
+    // the state: written by the wave that took the decisions
+    if ((conv && DEC1) ? (wave == wDec && lane == 0) : tid == 0) {
         if (costs) {
             st->Jp = Jp_last;
             st->Jd = Jd_last;

@@ -66,6 +66,8 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
     out["exchange_clocks (last wave done u -> wave 0 staged u+1)"] = float(np.median(ex))
     out["handoff_clocks (wave w done -> wave w+1 turn)"] = float(np.median(
         [t[u, w + 1, 2] - t[u, w, 3] for u in range(lo, hi) for w in range(W - 1)]))
+    out["handoff_clocks_per_pair"] = {f"{w}->{w + 1}": float(np.median([t[u, w + 1, 2] - t[u, w, 3] for u in range(lo, hi)]))
+                                      for w in range(W - 1)}
     out["raw_update_10"] = (t[10] - t[10, 0, 0]).tolist()
     # each later wave's chain in sevenths: clocks per seventh (median over updates)
     out["chain_sevenths_clocks"] = {
