@@ -293,6 +293,29 @@ def test_batch_kernels_vs_oracle_edge_sizes(gpu_lib, orc, N):
         assert_bitwise(up[j], want, f"update N={N} problem {j}")
 
 
+@pytest.mark.parametrize("N,B,ups", [(1024, 5, 23), (2048, 3, 11), (3072, 2, 4)])
+def test_stream_kernel_vs_oracle_and_iterate_v1(gpu_lib, orc, N, B, ups):
+    """k_batch_stream (pqp_batch_iterate where N is a multiple of 1024): ragged
+    batches, 4 to 23 updates in one launch, the first and last problem against
+    the oracle and every problem bit for bit against k_batch_iterate
+    (iterate_v1)."""
+    M = N // 2
+    b = gpu_lib.Batch(B, N).generate(seed=21, inst0=3, M=M)
+    b.iterate(ups)
+    stream = b.result().copy()
+    prev = gpu_lib.tune("iterate_v1", 1)
+    try:
+        b.reset()
+        b.iterate(ups)
+        v1 = b.result().copy()
+    finally:
+        gpu_lib.tune("iterate_v1", prev)
+    assert_bitwise(stream, v1, f"stream vs iterate_v1 N={N}")
+    for j in (0, B - 1):
+        P = orc.synth_problem(21, 3 + j, N, M, with_qp=False)
+        assert_bitwise(stream[j], orc.iterate(P["Qd"], P["Fd"], N, ups), f"N={N} problem {j}")
+
+
 def test_batch_load_bundled_fixed_999(gpu_lib, golden_bundled):
     g = golden_bundled
     N = int(g["N"])
@@ -534,7 +557,7 @@ def _same_bits_or_both_nan(a, b):
     return bool(np.all(nan | (a.view(np.uint32) == b.view(np.uint32))))
 
 
-@pytest.mark.parametrize("N", [7, 300, 1030])
+@pytest.mark.parametrize("N", [7, 300, 1024, 1030, 2048])
 def test_update_special_values_vs_oracle(gpu_lib, orc, N):
     rng = np.random.default_rng(N)
     Qd = rng.standard_normal((N, N)).astype(np.float32)
