@@ -5063,9 +5063,14 @@ __global__ void __launch_bounds__(256) k_gj_blocked3(const float* __restrict__ A
         const int ns = n - p0 < NB ? n - p0 : NB;
         const int rwin = p0 + NB < n ? p0 + NB : n;  // right columns [n, n + rwin) can be nonzero
         if (wv == 0) {  // 1. the pivot rows at their step, every column
+            // (the next pivot row's load in flight while this one takes its steps)
+            float vn[4 * C];
+            gj_load<C>(aug + (size_t)p0 * W, lane, vn);
             for (int s = 0; s < ns; ++s) {
                 float v[4 * C];
-                gj_load<C>(aug + (size_t)(p0 + s) * W, lane, v);
+#pragma unroll
+                for (int e = 0; e < 4 * C; ++e) v[e] = vn[e];
+                if (s + 1 < ns) gj_load<C>(aug + (size_t)(p0 + s + 1) * W, lane, vn);
                 gj_steps_any<C, NB>(v, P, Pd, W, p0, s, -1, lane);
                 gj_store<C>(P + (size_t)s * W, lane, v);
                 const float d = gj_any_col<C>(v, p0 + s);
