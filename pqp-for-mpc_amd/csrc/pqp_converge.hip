@@ -820,10 +820,7 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
                 Jp += s3;
                 Jp += Mp / 2;
                 have = 1;
-                stop = 1;  // the three gap tests :681-685
-                if (Jp > -Jd) stop = 0;
-                if ((double)(Jp + Jd) > kTol) stop = 0;
-                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                stop = gap_stop(Jp, Jd) ? 1 : 0;  // the three gap tests :681-685
             }
             const bool capped = a.cap > 0 && u >= a.cap;
             if (stop || capped || u == a.u_dec_end) {

@@ -19,6 +19,17 @@ __host__ __device__ __forceinline__ float max_ref(float a, float b) { return (a 
 // Tolerances erc = eac = eaj = erj (PQP_CPU.c:19-22).
 constexpr double kTol = 1e-6;
 
+// terminate()'s gap tests (PQP_CPU.c:683-685) in the reference's own order,
+// each returning early: the double division (about ten dependent f64
+// operations) only once the first two tests pass -- Jp > -Jd alone decides
+// almost every iterate short of the stop.  True: terminate() returns 1.
+__host__ __device__ __forceinline__ bool gap_stop(float Jp, float Jd) {
+    if (Jp > -Jd) return false;
+    const double gap = (double)(Jp + Jd);
+    if (gap > kTol) return false;
+    return !(gap / fabs((double)Jd) > kTol);
+}
+
 // ---------------------------------------------------------------------------
 // Relay hand-off wait (k_split_relay, k_lean_relay, k_gemv_relay): spin until
 // every lane's 64-bit LDS word {sequence, bits(running sum)} carries sequence

@@ -2534,10 +2534,7 @@ __global__ void __launch_bounds__(256) k_solve_small(SolveArgs A0, SolveState* _
                     Jd = (float)((double)Jd + 0.5 * (double)sc[0]);
                     Jd += sc[1];
                     Jd += Md / 2;
-                    stop = 1;
-                    if (Jp > -Jd) stop = 0;
-                    if ((double)(Jp + Jd) > kTol) stop = 0;
-                    if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                    stop = gap_stop(Jp, Jd) ? 1 : 0;  // :683-685
                     sc[3] = Jp;
                     sc[4] = Jd;
                     st->Jp = Jp;
@@ -2769,10 +2766,7 @@ __global__ void __launch_bounds__(256) k_solve_tiny(SolveArgs A0, SolveState* __
                     Jd = (float)((double)Jd + 0.5 * (double)sc[par][0]);
                     Jd += sc[par][1];
                     Jd += Md / 2;
-                    stop1 = 1;
-                    if (Jp > -Jd) stop1 = 0;
-                    if ((double)(Jp + Jd) > kTol) stop1 = 0;
-                    if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop1 = 0;
+                    stop1 = gap_stop(Jp, Jd) ? 1 : 0;  // :683-685
                     if (lane == 0) {
                         st->Jp = Jp;
                         st->Jd = Jd;
@@ -3171,9 +3165,7 @@ __global__ void __launch_bounds__(64) k_solve_wave(SolveArgs A0, SolveState* __r
             Jd = (float)((double)Jd + 0.5 * (double)s2);
             Jd += lin_d;
             Jd += Md / 2;
-            // the three tests of :683-685, evaluated lazily (no side effects;
-            // the double division only once the first two pass)
-            stop = !(Jp > -Jd) && !((double)(Jp + Jd) > kTol) && !((double)(Jp + Jd) / fabs((double)Jd) > kTol);
+            stop = gap_stop(Jp, Jd);  // :683-685
             Jp_last = Jp;
             Jd_last = Jd;
             have = true;
@@ -3786,10 +3778,7 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
                     Jp = (float)((double)Jp + 0.5 * (double)quad_p);
                     Jp += lin_p;
                     Jp += Mp / 2;
-                    int sp = 1;
-                    if (Jp > -Jd) sp = 0;
-                    if ((double)(Jp + Jd) > kTol) sp = 0;
-                    if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) sp = 0;
+                    const int sp = gap_stop(Jp, Jd) ? 1 : 0;  // :683-685
                     if (lane == 0) sc[2] = (float)sp;
                     // to SolveState once, at the end: a global store here would
                     // hold the barrier below for its round trip every iterate
@@ -4181,10 +4170,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 Jp = (float)((double)Jp + 0.5 * (double)sums[1]);
                 Jp += sums[2];
                 Jp += Mp / 2;
-                stop = 1;
-                if (Jp > -Jd) stop = 0;
-                if ((double)(Jp + Jd) > kTol) stop = 0;
-                if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+                stop = gap_stop(Jp, Jd) ? 1 : 0;  // :683-685
                 Jp_last = Jp;
                 Jd_last = Jd;
                 costs = true;

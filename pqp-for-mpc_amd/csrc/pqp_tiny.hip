@@ -532,7 +532,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
                 Jd = (float)((double)Jd + 0.5 * (double)s2);
                 Jd += lin_d;
                 Jd += Md / 2;
-                stop = !(Jp > -Jd) && !((double)(Jp + Jd) > kTol) && !((double)(Jp + Jd) / fabs((double)Jd) > kTol);
+                stop = gap_stop(Jp, Jd);  // :683-685
             }
             // decisions in iterate order: r - 1 first
             int d;

@@ -92,10 +92,7 @@ __global__ void __launch_bounds__(256) k_wide_decide(WideArgs a) {
         Jp = (float)((double)Jp + 0.5 * (double)sJ[2]);
         Jp += sJ[3];
         Jp += a.Mp[0] / 2;
-        stop = 1;  // the three gap tests :681-685
-        if (Jp > -Jd) stop = 0;
-        if ((double)(Jp + Jd) > kTol) stop = 0;
-        if ((double)(Jp + Jd) / fabs((double)Jd) > kTol) stop = 0;
+        stop = gap_stop(Jp, Jd) ? 1 : 0;  // the three gap tests :681-685
         if (tid == 0) {
             st->Jp = Jp;
             st->Jd = Jd;
