@@ -11,7 +11,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-for p in (ROOT / "pqp-for-mpc_amd", ROOT / "oracle", ROOT / "tests"):
+for p in (ROOT / "pqp-for-mpc_amd", ROOT / "tests"):
     sys.path.insert(0, str(p))
 
 

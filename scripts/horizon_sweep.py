@@ -1,6 +1,6 @@
 """Batched converge mode across MPC horizon lengths (the reference report's
 stated goal is varying the horizon): the bundled plant as H diagonal blocks
-(oracle.block_diag_problem: n_dual 28H, M 7H; every iterate feasible, and the
+(scripts/problems.py block_diag_problem: n_dual 28H, M 7H; every iterate feasible, and the
 reference stops at h = 313 for every H), B copies solved at once
 (ProblemBatch, one workgroup per problem) and one copy alone (Problem, the
 single-problem path).  Prints one JSON line per H.
@@ -15,7 +15,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "scripts"))
 
 
 def main(Hs):
@@ -23,9 +23,9 @@ def main(Hs):
     import torch
 
     import pqp_amd
-    from oracle import Oracle, block_diag_problem
+    from problems import block_diag_problem, bundled_problem
 
-    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    base = bundled_problem()
     for H in Hs:
         P = block_diag_problem(base, H)
         N, M = P["N"], P["M"]

@@ -15,16 +15,16 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "scripts"))
 
 
 def main(Hs):
     import torch
 
     import pqp_amd
-    from oracle import Oracle, block_diag_problem
+    from problems import block_diag_problem, bundled_problem
 
-    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    base = bundled_problem()
     B = int(os.environ.get("B", "16384"))
     for H in Hs:
         P = block_diag_problem(base, H)

@@ -10,19 +10,19 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "scripts"))
 
 
 def main():
     import torch
 
     import pqp_amd
-    from oracle import Oracle, block_diag_problem
+    from problems import block_diag_problem, bundled_problem
 
     H = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     mode = os.environ.get("MODE", "fixed")
-    P = block_diag_problem(Oracle().bundled_problem(ROOT / "tests" / "golden" / "example"), H)
+    P = block_diag_problem(bundled_problem(), H)
     pb = pqp_amd.ProblemBatch.replicate(P, B)
     if mode == "infeasible":
         pb.Kp.fill_(-1e30)

@@ -14,7 +14,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "scripts"))
 
 
 def timed(pb, torch, **kw):
@@ -31,10 +31,10 @@ def main(Hs):
     import torch
 
     import pqp_amd
-    from oracle import Oracle, block_diag_problem
+    from problems import block_diag_problem, bundled_problem
 
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    base = bundled_problem()
     for H in Hs:
         P = block_diag_problem(base, H)
         N, M = P["N"], P["M"]

@@ -12,7 +12,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "scripts"))
 
 
 def main(Hs):
@@ -22,9 +22,9 @@ def main(Hs):
     import torch
 
     import pqp_amd
-    from oracle import Oracle, block_diag_problem
+    from problems import block_diag_problem, bundled_problem
 
-    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    base = bundled_problem()
     pqp_amd.tune("mid_v1", int(os.environ.get("MID_V1", "0")))
     pqp_amd.tune("mid2_pair", int(os.environ.get("MID2_PAIR", "0")))  # 0 by shape, 1 lane sides, 2 one lane per row
     pqp_amd.tune("mid2_min_n", 0)

@@ -11,16 +11,16 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
-sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "scripts"))
 
 
 def main():
     import torch
 
     import pqp_amd
-    from oracle import Oracle, block_diag_problem
+    from problems import block_diag_problem, bundled_problem
 
-    base = Oracle().bundled_problem(ROOT / "tests" / "golden" / "example")
+    base = bundled_problem()
     cases = []
     import os
     for H in [int(h) for h in os.environ.get("HS", "8,16").split(",")]:
