@@ -139,7 +139,7 @@ def host_cpu() -> dict:
 
 
 def cpu_baseline(n: int, seconds: float, instances: list, tol_cases: dict | None = None,
-                 threads: int = 16) -> dict:
+                 threads: int = 16, horizon: dict | None = None) -> dict:
     """The reference's updateY2 on `instances` (a list of (Qd, Fd) host
     arrays: distinct problems of the bench's own workload, copied from the
     GPU batch), DRAM-resident (8 MiB of split matrices each) and updated
@@ -213,6 +213,22 @@ def cpu_baseline(n: int, seconds: float, instances: list, tol_cases: dict | None
                 h, _, _ = ref.solve(Pc)
                 ref_tol[name] = {"h": h, "ms": (time.perf_counter() - tb) * 1e3}
             bundled["iters_to_tol"] = ref_tol
+        # the horizon leg's problem 0 per H (copied back from its GPU batch):
+        # the reference's solveQuadraticDual, 1 thread, median of 3, and
+        # whether it stops at the GPU's h
+        hz = {}
+        for key, (P0, h_gpu) in (horizon or {}).items():
+            ts = []
+            for _ in range(3):
+                tb = time.perf_counter()
+                hr, _, _ = ref.solve(P0)
+                ts.append(time.perf_counter() - tb)
+            tr = sorted(ts)[1]
+            hz[key] = {"h": hr, "same_h_as_gpu": bool(hr == h_gpu), "ms": tr * 1e3, "qp_solves_per_s": 1.0 / tr,
+                       "what": "PQP_CPU.c solveQuadraticDual (oracle/_ref) on the horizon leg's problem 0, "
+                               "1 thread, median of 3"}
+        if hz:
+            bundled["horizon"] = hz
     else:
         Qd, Fd = instances[0]
         per, _ = orc.time_updates(Qd, Fd, n, 3)
@@ -317,24 +333,20 @@ def mpc_batch_bench(pqp_amd, B: int = 16384) -> dict:
                     "on device, excluded from the timing; each solve bit-exact with PQP_CPU.c (tests)"}
 
 
-def horizon_bench(pqp_amd, Hs=(2, 4, 5), B: int = 16384) -> dict:
+def horizon_bench(pqp_amd, Hs=(2, 4, 5), B: int = 16384, keep: dict | None = None) -> dict:
     """MPC over H horizon stages: B problems of the bundled plant stacked H
     times (pqp_amd.horizon_batch -- block-diagonal primal, each stage at its
     own perturbed state (seed 7), per-stage computeFp / computeMp, Gauss_Jordan
     and convertToDual on the GPU; n_dual 28 H, M 7 H), solved at once in
     converge mode (path 3: k_solve_mid2, one workgroup per problem, every
-    matrix once in LDS, terminate() beside the update).  Beside it the
-    reference's own solveQuadraticDual on problem 0 (copied back from the GPU
-    batch), one host thread (oracle/_ref, median of 3).  Timed: the batched
-    solve only."""
+    matrix once in LDS, terminate() beside the update).  Timed: the batched
+    solve only.  With `keep`, problem 0 of each H (host copy) and its GPU h
+    are left there for the cpu_baseline leg, which runs the reference's own
+    solveQuadraticDual on it (cpu_baseline.horizon)."""
     import torch
-
-    sys.path.insert(0, str(ROOT / "oracle"))
-    from oracle import REF_SO, Reference
 
     ex = ROOT / "tests" / "golden" / "example"
     E = pqp_amd.read_example(ex)
-    ref = Reference() if REF_SO.exists() else None
     out = {}
     for H in Hs:
         xs = pqp_amd.perturbed_states(E["x"], B * H, seed=7).reshape(B, H, -1)
@@ -380,17 +392,8 @@ def horizon_bench(pqp_amd, Hs=(2, 4, 5), B: int = 16384) -> dict:
         row["note"] = ("the H stages are stacked block-diagonally and decoupled (each stage its own copy of "
                        "the bundled plant at its own state): a size class of the MPC horizon (n_dual 28 H), "
                        "not a coupled horizon")
-        if ref is not None:
-            P0 = pb.problem(0)
-            ts = []
-            for _ in range(3):
-                tb = time.perf_counter()
-                hr, _, _ = ref.solve(P0)
-                ts.append(time.perf_counter() - tb)
-            tr = sorted(ts)[1]
-            row["ref_cpu"] = {"h": hr, "same_h_as_gpu": bool(hr == int(h[0])), "ms": tr * 1e3,
-                              "qp_solves_per_s": 1.0 / tr, "cores": 1,
-                              "what": "PQP_CPU.c solveQuadraticDual (oracle/_ref) on problem 0, 1 thread, median of 3"}
+        if keep is not None:
+            keep[f"H{H}"] = (pb.problem(0), int(h[0]))
         out[f"H{H}"] = row
         del pb
         torch.cuda.empty_cache()
@@ -979,6 +982,7 @@ def main():
     # needed: free them before the legs allocate their own
     batch = Yh = None
     torch.cuda.empty_cache()
+    hz_keep = {}  # the horizon leg's problem 0 per H, for the cpu_baseline leg
     if world == 1 and not args.no_bundled:
         # first of the legs: run after the others (their allocations and
         # frees, compute-heavy kernels) the same pass measured 5-9 % slower
@@ -992,7 +996,7 @@ def main():
     if world == 1 and not args.no_bundled:
         em.leg("bundled", lambda: bundled_bench(pqp_amd))
         em.leg("mpc_batch", lambda: mpc_batch_bench(pqp_amd))
-        em.leg("horizon", lambda: horizon_bench(pqp_amd))
+        em.leg("horizon", lambda: horizon_bench(pqp_amd, keep=None if args.no_cpu_baseline else hz_keep))
         em.leg("single_n1024", lambda: single_bench(pqp_amd))
         em.leg("single_converge", lambda: single_converge_bench(pqp_amd))
         em.leg("setup_convert", lambda: setup_bench(pqp_amd))
@@ -1004,7 +1008,7 @@ def main():
             tol_cases = tol_problems(pqp_amd, Path(td))
         em.leg("iters_to_tol", lambda: iters_to_tol_bench(pqp_amd, tol_cases))
     if world == 1 and not args.no_cpu_baseline:
-        cb = em.leg("cpu_baseline", lambda: cpu_baseline(N, args.cpu_seconds, inst, tol_cases))
+        cb = em.leg("cpu_baseline", lambda: cpu_baseline(N, args.cpu_seconds, inst, tol_cases, horizon=hz_keep))
         ref_tol = cb.get("bundled", {}).get("iters_to_tol")
         if ref_tol and "iters_to_tol" in result and "error" not in result["iters_to_tol"]:
             result["iters_to_tol_identical_to_reference"] = all(
