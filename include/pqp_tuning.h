@@ -75,6 +75,9 @@ extern "C" {
  *   mid2_fat [0]           k_solve_mid2 workgroups of <= 6 waves on the
  *                          128-VGPR build (default: the 80-VGPR build, 6 waves
  *                          per SIMD, as many problems per CU as LDS allows)
+ *   mid2_dense [0]         k_solve_mid2 sums every k of each update row and
+ *                          Y'Qd row (default: only the band of k where the
+ *                          wave's rows hold a nonzero, while Y is finite)
  *   batch_chunk [0]        iterates per problem per batched-solve launch
  *                          (0: sized from N and M)
  *   single_scalar [0]      k_solve_single with 4-byte loads only

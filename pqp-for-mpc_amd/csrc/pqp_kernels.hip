@@ -3876,10 +3876,18 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
 // from the saved Y_h.  Every sum keeps the reference's operands and order:
 // the same bits as k_solve_mid.  N <= 160, M < 64 (nUW + 1 + 2 <= 8 waves);
 // other mid sizes, and terminate() alone, stay on k_solve_mid.
+// Band (round 5): the update rows and the Y'Qd rows of a wave sum only the k
+// from the first to the last nonzero entry of the wave's rows and columns
+// (found once, when Qd is staged; the diagonal always inside).  While every
+// y_k is finite, a zero entry's term is +-0, and a sum that starts at +0.0f
+// (and so is never -0) is unchanged by adding +-0: the skipped terms change
+// no bit.  A phase whose Y_s holds a NaN or inf sums every k.  A dense Qd
+// has the whole range as its band; an MPC problem's stage structure (the
+// horizon leg: 28-row blocks) leaves a wave of 32 or 64 rows 28-84 of the k.
 // ---------------------------------------------------------------------------
 struct Mid2Layout {
     int nk, mk, ldn, ldm, ldg, ldi;
-    int y, tq, dP, dN, Fdp, Fdn, Kp, tM, Us, tu, fu, Fp, fdy, flag, sums, Qd, Gp, Qi, Qp, total;
+    int y, tq, dP, dN, Fdp, Fdn, Kp, tM, Us, tu, fu, Fp, fdy, flag, band, sums, Qd, Gp, Qi, Qp, total;
 };
 __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
     Mid2Layout L;
@@ -3897,6 +3905,7 @@ __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
     L.Fdp = o;  o += L.nk;
     L.Fdn = o;  o += L.nk;
     L.flag = o; o += 16;            // [0..11] checkFeas flags per C row wave; [12 + s&1] Y non-finite
+    L.band = o; o += 16;            // nonzero k-bands (mid2_band): 64-row groups [0..2] lo, [3..5] hi; 32-row [6..10], [11..15]
     if (conv) {
         L.Kp = o;   o += L.nk;
         L.tM = o;   o += L.mk;
@@ -3966,16 +3975,16 @@ __device__ __forceinline__ void mid2_block(float& acc, sf4 q0, sf4 q1, sf4 y0, s
     acc += p0.x; acc += p0.y; acc += p1.x; acc += p1.y;
     acc += p2.x; acc += p2.y; acc += p3.x; acc += p3.y;
 }
-// one side of update row i, k = 0..nk-1 in order, the next block's LDS reads
-// in flight while a block is summed
+// one side of update row i, k = klo..khi-1 in order (the row group's band,
+// mid2_band), the next block's LDS reads in flight while a block is summed
 template <bool FAST>
-__device__ __forceinline__ float mid2_side(const float* q, const float* y, int nk, int i, int side, float lim,
-                                           float dv, int w0) {
+__device__ __forceinline__ float mid2_side(const float* q, const float* y, int klo, int khi, int i, int side,
+                                           float lim, float dv, int w0) {
     float acc = 0.0f;
-    sf4 q0 = *reinterpret_cast<const sf4*>(q), q1 = *reinterpret_cast<const sf4*>(q + 4);
-    sf4 y0 = *reinterpret_cast<const sf4*>(y), y1 = *reinterpret_cast<const sf4*>(y + 4);
-    for (int k = 0; k < nk; k += 8) {
-        const int kn = (k + 8 < nk) ? k + 8 : k;  // next block (the last one re-read at the end)
+    sf4 q0 = *reinterpret_cast<const sf4*>(q + klo), q1 = *reinterpret_cast<const sf4*>(q + klo + 4);
+    sf4 y0 = *reinterpret_cast<const sf4*>(y + klo), y1 = *reinterpret_cast<const sf4*>(y + klo + 4);
+    for (int k = klo; k < khi; k += 8) {
+        const int kn = (k + 8 < khi) ? k + 8 : k;  // next block (the last one re-read at the end)
         const sf4 nq0 = *reinterpret_cast<const sf4*>(q + kn), nq1 = *reinterpret_cast<const sf4*>(q + kn + 4);
         const sf4 ny0 = *reinterpret_cast<const sf4*>(y + kn), ny1 = *reinterpret_cast<const sf4*>(y + kn + 4);
         if (k >= w0 && k < w0 + 32) mid2_block<FAST, true>(acc, q0, q1, y0, y1, k, w0, side, lim, dv);
@@ -3988,20 +3997,20 @@ __device__ __forceinline__ float mid2_side(const float* q, const float* y, int n
 // one update row on one lane, both sides packed (k_solve_mid's form,
 // row_step): Y_next[i] = num / den * y_i (PQP_CPU.c:603-618)
 template <bool FAST>
-__device__ __forceinline__ float mid2_row(const float* q, const float* y, int nk, int i, float dp, float dn,
-                                          float fdn, float fdp, int w0) {
+__device__ __forceinline__ float mid2_row(const float* q, const float* y, int klo, int khi, int i, float dp,
+                                          float dn, float fdn, float fdp, int w0) {
     sf2 acc = {0.0f, 0.0f};
     float aq = 0.0f;
     RowBlk c, x;
-    row_load(c, q, y, 0);
-    int k = 0;
-    for (; k + 16 < nk; k += 16) {
+    row_load(c, q, y, klo);
+    int k = klo;
+    for (; k + 16 < khi; k += 16) {
         row_load(x, q, y, k + 8);
         row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
         row_load(c, q, y, k + 16);
         row_step<false, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
     }
-    if (k + 8 < nk) {
+    if (k + 8 < khi) {
         row_load(x, q, y, k + 8);
         row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
         row_step<false, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
@@ -4057,6 +4066,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     float* fdy = lds + L.fdy;
     float* sums = lds + L.sums;
     int* flag = reinterpret_cast<int*>(lds + L.flag);  // [0..11] checkFeas per C row wave, [12 + p] Y non-finite
+    int* band = reinterpret_cast<int*>(lds + L.band);
     const int NT = blockDim.x;  // 64 * mid2_waves(N, conv, PAIR, crows)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nUW = mid2_uw(N, PAIR), wT = nUW, wC0 = nUW + 1;
@@ -4110,15 +4120,34 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     // computeTheta (:503-519), the diagonal literals (:524-537); any NaN in
     // Qd?  Qd bit-symmetric (then Y'Qd's column j is row j's dot, read 16 bytes
     // at a time)?
+    // The band of each row group (mid2_band): the k from the first to the
+    // last nonzero (or NaN) of its rows and columns, the diagonal included,
+    // rounded out to blocks of 8; lo kept as nk - lo so that both ends are
+    // maxima over the zeroed words.
     int nan = 0, asym = 0;
+    const bool dense = (A.tiny_flags & kMid2Dense) != 0;
     for (int i = tid; i < N; i += NT) {
         const float* row = Qd + i * ldn;
         float s = 0.0f;
+        int lo = i, hi = i;
         for (int k = 0; k < N; ++k) {
             s += max_ref(0.0f, -row[k]) * 1.0f;
             if (row[k] != row[k]) nan = 1;
             if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
+            if (row[k] != 0.0f || Qd[k * ldn + i] != 0.0f) {
+                lo = k < lo ? k : lo;
+                hi = k > hi ? k : hi;
+            }
         }
+        if (dense) {
+            lo = 0;
+            hi = nk - 1;
+        }
+        const int lo8 = lo & ~7, hi8 = (hi + 8) & ~7;
+        atomicMax(&band[i >> 6], nk - lo8);
+        atomicMax(&band[3 + (i >> 6)], hi8);
+        atomicMax(&band[6 + (i >> 5)], nk - lo8);
+        atomicMax(&band[11 + (i >> 5)], hi8);
         const float th = max_ref(s, 5.0f), qii = row[i];
         dP[i] = max_ref(0.0f, qii) + 1.0f * th;
         dN[i] = max_ref(0.0f, -qii) + 1.0f * th;
@@ -4224,6 +4253,9 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     if (wave < nUW) {
         // ---------------- UW: Y_{s+1} = updateY2(Y_s) ----------------
         const float* q = Qd + (uw ? urow : 0) * ldn;
+        // the wave's band (its rows' nonzero k), valid while Y_s is finite
+        const int bg = PAIR ? 6 + wave : wave;
+        const int blo = __builtin_amdgcn_readfirstlane(nk - band[bg]), bhi = __builtin_amdgcn_readfirstlane(band[bg + (PAIR ? 5 : 3)]);
         for (long long s = h0;; ++s) {
             const float* ycur = Yr + (int)(s % 3) * nk;
             float* ynext = Yr + (int)((s + 1) % 3) * nk;
@@ -4231,10 +4263,14 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             // read before the previous phase's second barrier
             if (tid == 0) flag[12 + (int)(s & 1)] = 0;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
+            // a zero entry's term is +-0 while y_k is finite, and the sum (from
+            // +0.0f, never -0) is unchanged by it: the terms outside the band
+            // are skipped exactly; a non-finite Y_s (0 * inf = NaN) takes every k
+            const int klo = y_nonfinite ? 0 : blo, khi = y_nonfinite ? nk : bhi;
             if (uw) {
                 if constexpr (PAIR) {
-                    float acc = (fast && !y_nonfinite) ? mid2_side<true>(q, ycur, nk, urow, side, lim, dv, w0)
-                                                       : mid2_side<false>(q, ycur, nk, urow, side, lim, side ? dv : -dv, w0);
+                    float acc = (fast && !y_nonfinite) ? mid2_side<true>(q, ycur, klo, khi, urow, side, lim, dv, w0)
+                                                       : mid2_side<false>(q, ycur, klo, khi, urow, side, lim, side ? dv : -dv, w0);
                     if (fast && !y_nonfinite && !side) acc = 0.0f - acc;  // num's terms were summed negated
                     const float v = acc + 1.0f * fdv;                     // num += Fdn :611; den += Fdp :612
                     const float other = __shfl_xor(v, 1);
@@ -4246,9 +4282,10 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                     }
                 } else {
                     // k_solve_mid's row (max form, or the selects where Qd holds a NaN)
-                    const float yn = fast ? mid2_row<true>(q, ycur, nk, urow, dpr, dnr, fdn, fdp, w0)
-                                          : mid2_row<false>(q, ycur, nk, urow, dpr, dnr, fdn, fdp, w0);
+                    const float yn = fast ? mid2_row<true>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0)
+                                          : mid2_row<false>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
                     ynext[urow] = yn;
+                    if (!(fabsf(yn) <= 3.402823466e38f)) flag[12 + (int)((s + 1) & 1)] = 1;
                 }
             }
             if (phase_end(s)) break;  // (its second barrier: the flags are read before the next phase writes)
@@ -4273,6 +4310,10 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     } else if (conv) {
         // ---------------- C: terminate(Y_{s-1}); Y_s'Qd ----------------
         const int cw = wave - wC0;
+        // the Y'Qd rows' band (the crows-row group of this wave)
+        const int cg = cw < nCR ? (crows == 64 ? cw : 6 + cw) : 0;
+        const int clo = __builtin_amdgcn_readfirstlane(nk - band[cg]);
+        const int chi = __builtin_amdgcn_readfirstlane(band[cg + (crows == 64 ? 3 : 5)]);
         for (long long s = h0;; ++s) {
             const float* ycur = Yr + (int)(s % 3) * nk;
             const bool pend = s > h0;
@@ -4293,8 +4334,12 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 const bool any_bad = __any(bad);
                 if (pend && lane == 0) flag[cw] = any_bad ? 1 : 0;
                 float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
-                for (int j = l; j < lend; j += crows * nCR)  // (Y'Qd)_j Y_j :652-655; column j = row j when Qd is symmetric
-                    tqs[j] = (sym ? mid_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn, ycur, nk) : mid_dot<PK && PQP_M2PK_C>(Qd + j, ldn, ycur, nk)) * ycur[j];
+                // (Y'Qd)_j Y_j :652-655 over the band while Y_s is finite (as
+                // the update's sums); column j = row j when Qd is symmetric
+                const int klo = y_nonfinite ? 0 : clo, kn = (y_nonfinite ? nk : chi) - klo;
+                for (int j = l; j < lend; j += crows * nCR)
+                    tqs[j] = (sym ? mid_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn + klo, ycur + klo, kn)
+                                  : mid_dot<PK && PQP_M2PK_C>(Qd + klo * ldn + j, ldn, ycur + klo, kn)) * ycur[j];
             } else if (pend && cw == nCR) {
                 if (lane < M) {
                     tu[lane] = mid_dot<PK && PQP_M2PK_Q>(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
@@ -4349,7 +4394,9 @@ size_t solve_mid_lds_bytes(int N, int M, bool conv) {
 }
 constexpr size_t kMidLdsBudget = 150 * 1024;
 
-static hipError_t launch_mid_grid(int B, const SolveArgs& a, SolveState* st, hipStream_t s) {
+static hipError_t launch_mid_grid(int B, const SolveArgs& a0, SolveState* st, hipStream_t s) {
+    SolveArgs a = a0;
+    if (g_tune.mid2_dense) a.tiny_flags |= kMid2Dense;
     const bool conv2 = a.mode == kModeConverge;
     // the update rows as lane sides where that measured faster: the horizon
     // sweep (profiles/r04/mid2_arms.jsonl) at n_dual 112 (H = 4) 40.4 vs 43.4

@@ -46,7 +46,8 @@ struct SolveArgs {
 constexpr int kTinyOutUOffset = 32, kTinyOutStateOffset = 64, kTinyOutErrOffset = 72, kTinyOutTagOffset = 73,
               kTinyOutFloats = 80;
 constexpr int kTinyDense = 1;
-constexpr int kTinyStall = 2;  // error-path tests: k_solve_quintet's deciding waves never decide
+constexpr int kTinyStall = 2;
+constexpr int kMid2Dense = 4;  // k_solve_mid2: no band skipping (tune mid2_dense)  // error-path tests: k_solve_quintet's deciding waves never decide
 // one problem with N, M <= 32 (fixed mode; converge mode needs N + M < 64) in one launch
 hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);
 // test hook: 8 * cus workgroups each fill 64 KB of LDS with `bits` (pqp_tune_poison_lds)
@@ -127,6 +128,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int mid_off = 0;  // batched solves of mid-size N through k_solve_small / k_solve_single instead of path 3
     int mid2_pair = 0;  // k_solve_mid2's update rows: 0 by shape, 1 lane sides (v_med3_f32), 2 one lane per row
     int single_occ = 0;  // k_solve_single (wide loads) workgroups per CU by register cap: 0 by shape and batch (3 above n_dual 768), 3 / 4 / 5 forced
+    int mid2_dense = 0;  // k_solve_mid2 sums every k (default: each row group's nonzero band while Y is finite)
     int mid2_fat = 0;  // k_solve_mid2 workgroups of <= 6 waves on the 128-VGPR build (default: 80 VGPRs, 6 waves per SIMD)
     int mid2_min_n = 48;  // smallest N path 3 runs on k_solve_mid2 (below it k_solve_mid)
     int mid_v1 = 0;  // path 3 on k_solve_mid (terminate() after the update) instead of the pipelined k_solve_mid2
