@@ -3994,28 +3994,60 @@ __device__ __forceinline__ float mid2_side(const float* q, const float* y, int k
     return acc;
 }
 
-// one update row on one lane, both sides packed (k_solve_mid's form,
-// row_step): Y_next[i] = num / den * y_i (PQP_CPU.c:603-618)
-template <bool FAST>
+// 8 terms of update row w0 + lane, both sides packed (k_solve_mid's
+// row_block).  DIAG: the block lies in the 64 columns of the wave's diagonal;
+// column k + j is the diagonal of lane k + j - w0 only, which takes the literal
+// by a mask made on the scalar unit (two v_cndmask per k, no compare)
+template <bool DIAG, bool FAST>
+__device__ __forceinline__ void mid2_rblock(const RowBlk& B, int k, int w0, float dp, float dn, sf2& acc) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float q = j < 4 ? B.q0[j] : B.q1[j - 4];
+        const float yk = j < 4 ? B.y0[j] : B.y1[j - 4];
+        float qp, qn;
+        split_q<FAST>(q, qp, qn);
+        if constexpr (DIAG) {
+            const unsigned long long m = 1ull << (k + j - w0);
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(qp) : "v"(qp), "v"(dp), "s"(m));
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(qn) : "v"(qn), "v"(dn), "s"(m));
+        }
+        acc += sf2{qp, qn} * sf2{yk, yk};
+    }
+}
+// SMASK: the scalar-mask diagonal (the 128-VGPR build; the 80-VGPR build
+// keeps k_solve_mid's per-lane compare: the masks' SGPRs made it spill more,
+// H = 2 / 3 +2 / +4 %, profiles/r05/band)
+template <bool FAST, bool SMASK>
+__device__ __forceinline__ void mid2_rstep(const RowBlk& B, int k, int w0, int i, float dp, float dn, sf2& acc) {
+    if constexpr (SMASK) {
+        if (k >= w0 && k < w0 + 64) mid2_rblock<true, FAST>(B, k, w0, dp, dn, acc);
+        else mid2_rblock<false, FAST>(B, k, w0, dp, dn, acc);
+    } else {
+        float aq = 0.0f;
+        row_step<false, FAST>(B, k, w0, i, dp, dn, acc, aq);
+    }
+}
+// one update row on one lane, both sides packed (k_solve_mid's form):
+// Y_next[i] = num / den * y_i (PQP_CPU.c:603-618), k = klo..khi-1
+template <bool FAST, bool SMASK>
 __device__ __forceinline__ float mid2_row(const float* q, const float* y, int klo, int khi, int i, float dp,
                                           float dn, float fdn, float fdp, int w0) {
     sf2 acc = {0.0f, 0.0f};
-    float aq = 0.0f;
     RowBlk c, x;
     row_load(c, q, y, klo);
     int k = klo;
     for (; k + 16 < khi; k += 16) {
         row_load(x, q, y, k + 8);
-        row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
+        mid2_rstep<FAST, SMASK>(c, k, w0, i, dp, dn, acc);
         row_load(c, q, y, k + 16);
-        row_step<false, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
+        mid2_rstep<FAST, SMASK>(x, k + 8, w0, i, dp, dn, acc);
     }
     if (k + 8 < khi) {
         row_load(x, q, y, k + 8);
-        row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
-        row_step<false, FAST>(x, k + 8, w0, i, dp, dn, acc, aq);
+        mid2_rstep<FAST, SMASK>(c, k, w0, i, dp, dn, acc);
+        mid2_rstep<FAST, SMASK>(x, k + 8, w0, i, dp, dn, acc);
     } else {
-        row_step<false, FAST>(c, k, w0, i, dp, dn, acc, aq);
+        mid2_rstep<FAST, SMASK>(c, k, w0, i, dp, dn, acc);
     }
     const float num = acc.y + 1.0f * fdn;  // :611
     const float den = acc.x + 1.0f * fdp;  // :612
@@ -4037,7 +4069,10 @@ __device__ __forceinline__ float mid2_row(const float* q, const float* y, int kl
 #ifndef PQP_M2PK_Q
 #define PQP_M2PK_Q 1
 #endif
-template <int MAXT, bool PAIR, int MINW = 1>
+// BAND: the band sums (the lean one-lane-per-row build also comes without
+// them, for N <= 64: one row group, whose band is all k on any MPC problem,
+// and the band's registers cost that build 7 %, profiles/r05/band)
+template <int MAXT, bool PAIR, int MINW = 1, bool BAND = true>
 __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveState* __restrict__ st0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SolveArgs A = problem_at(A0, blockIdx.x);
@@ -4254,8 +4289,10 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         // ---------------- UW: Y_{s+1} = updateY2(Y_s) ----------------
         const float* q = Qd + (uw ? urow : 0) * ldn;
         // the wave's band (its rows' nonzero k), valid while Y_s is finite
+        // (read from LDS once: per phase it cost 4-8 %, profiles/r05/band)
         const int bg = PAIR ? 6 + wave : wave;
-        const int blo = __builtin_amdgcn_readfirstlane(nk - band[bg]), bhi = __builtin_amdgcn_readfirstlane(band[bg + (PAIR ? 5 : 3)]);
+        const int blo = BAND ? __builtin_amdgcn_readfirstlane(nk - band[bg]) : 0;
+        const int bhi = BAND ? __builtin_amdgcn_readfirstlane(band[bg + (PAIR ? 5 : 3)]) : nk;
         for (long long s = h0;; ++s) {
             const float* ycur = Yr + (int)(s % 3) * nk;
             float* ynext = Yr + (int)((s + 1) % 3) * nk;
@@ -4266,7 +4303,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             // a zero entry's term is +-0 while y_k is finite, and the sum (from
             // +0.0f, never -0) is unchanged by it: the terms outside the band
             // are skipped exactly; a non-finite Y_s (0 * inf = NaN) takes every k
-            const int klo = y_nonfinite ? 0 : blo, khi = y_nonfinite ? nk : bhi;
+            const int klo = (BAND && !y_nonfinite) ? blo : 0, khi = (BAND && !y_nonfinite) ? bhi : nk;
             if (uw) {
                 if constexpr (PAIR) {
                     float acc = (fast && !y_nonfinite) ? mid2_side<true>(q, ycur, klo, khi, urow, side, lim, dv, w0)
@@ -4282,8 +4319,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                     }
                 } else {
                     // k_solve_mid's row (max form, or the selects where Qd holds a NaN)
-                    const float yn = fast ? mid2_row<true>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0)
-                                          : mid2_row<false>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
+                    const float yn = fast ? mid2_row<true, MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0)
+                                          : mid2_row<false, MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
                     ynext[urow] = yn;
                     if (!(fabsf(yn) <= 3.402823466e38f)) flag[12 + (int)((s + 1) & 1)] = 1;
                 }
@@ -4312,8 +4349,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         const int cw = wave - wC0;
         // the Y'Qd rows' band (the crows-row group of this wave)
         const int cg = cw < nCR ? (crows == 64 ? cw : 6 + cw) : 0;
-        const int clo = __builtin_amdgcn_readfirstlane(nk - band[cg]);
-        const int chi = __builtin_amdgcn_readfirstlane(band[cg + (crows == 64 ? 3 : 5)]);
+        const int clo = BAND ? __builtin_amdgcn_readfirstlane(nk - band[cg]) : 0;
+        const int chi = BAND ? __builtin_amdgcn_readfirstlane(band[cg + (crows == 64 ? 3 : 5)]) : nk;
         for (long long s = h0;; ++s) {
             const float* ycur = Yr + (int)(s % 3) * nk;
             const bool pend = s > h0;
@@ -4336,7 +4373,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
                 // (Y'Qd)_j Y_j :652-655 over the band while Y_s is finite (as
                 // the update's sums); column j = row j when Qd is symmetric
-                const int klo = y_nonfinite ? 0 : clo, kn = (y_nonfinite ? nk : chi) - klo;
+                const bool cb = BAND && !y_nonfinite;
+                const int klo = cb ? clo : 0, kn = (cb ? chi : nk) - klo;
                 for (int j = l; j < lend; j += crows * nCR)
                     tqs[j] = (sym ? mid_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn + klo, ycur + klo, kn)
                                   : mid_dot<PK && PQP_M2PK_C>(Qd + klo * ldn + j, ldn, ycur + klo, kn)) * ycur[j];
@@ -4414,7 +4452,8 @@ static hipError_t launch_mid_grid(int B, const SolveArgs& a0, SolveState* st, hi
             // instead of 4, 84: 4 instead of 2)
             const bool lean = nt <= 384 && !g_tune.mid2_fat;
             if (lean && pair) hipLaunchKernelGGL((k_solve_mid2<384, true, 6>), dim3(B), dim3(nt), lds, s, a, st);
-            else if (lean) hipLaunchKernelGGL((k_solve_mid2<384, false, 6>), dim3(B), dim3(nt), lds, s, a, st);
+            else if (lean && a.N > 64) hipLaunchKernelGGL((k_solve_mid2<384, false, 6>), dim3(B), dim3(nt), lds, s, a, st);
+            else if (lean) hipLaunchKernelGGL((k_solve_mid2<384, false, 6, false>), dim3(B), dim3(nt), lds, s, a, st);
             else if (pair) hipLaunchKernelGGL((k_solve_mid2<1024, true>), dim3(B), dim3(nt), lds, s, a, st);
             else hipLaunchKernelGGL((k_solve_mid2<1024, false>), dim3(B), dim3(nt), lds, s, a, st);
             g_last_batch_kernel = 3;
