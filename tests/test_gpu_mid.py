@@ -347,3 +347,70 @@ def test_mid2_y_turning_nonfinite(gpu_lib, orc, knobs, pair):
         assert int(pb.h[b]) == abs(h)
         _same_or_both_nan(pb.Y[b].cpu().numpy(), Y, f"pair={pair} converge problem {b} Y")
         _same_or_both_nan(pb.U[b].cpu().numpy(), U, f"pair={pair} converge problem {b} U")
+
+
+def _growing_banded(N, M, seed, blk=14, negzero=False):
+    """_growing's rows with the three -1 entries inside the row's own block
+    of `blk` rows (an MPC-like block structure: each row group's nonzero band
+    is narrow, so k_solve_mid2 sums bands), Y overflowing to inf and then NaN
+    mid-solve; negzero: every entry outside the blocks is -0.0."""
+    rng = np.random.default_rng(seed)
+    Q = np.full((N, N), -0.0 if negzero else 0.0, np.float32)
+    for i in range(N - 2):
+        b0 = (i // blk) * blk
+        cols = [k for k in range(b0, min(b0 + blk, N)) if k != i]
+        Q[i, i] = 1.0
+        Q[i, rng.choice(cols, 3, replace=False)] = -1.0
+    P = _growing(N, M, seed)
+    P["Qd"] = Q.reshape(-1)
+    return P
+
+
+@pytest.mark.parametrize("N,M,pair", [(56, 14, 2), (84, 21, 2), (112, 28, 1), (112, 28, 2), (140, 35, 2), (140, 35, 1)])
+@pytest.mark.parametrize("negzero", [False, True])
+def test_mid2_band_y_turning_nonfinite(gpu_lib, orc, knobs, N, M, pair, negzero):
+    """Band sums (k_solve_mid2 skips the k outside each row group's nonzero
+    band while Y is finite) on block-structured rows whose Y overflows to inf
+    and then NaN: fixed mode before, across and after, and capped converge
+    solves, against the oracle (NaN positions, every other bit); off-block
+    zeros as +0 and as -0."""
+    knobs("mid2_pair", pair)
+    knobs("mid2_min_n", 0)
+    Ps = [_growing_banded(N, M, s, negzero=negzero) for s in (3, 4)]
+    seen_inf = False
+    for n in (5, 250, 300, 330, 400):
+        pb = _batch(gpu_lib, Ps).solve(gpu_lib.MODE_FIXED, num_iter=n)
+        assert gpu_lib.tune_get("last_batch_kernel") == 3
+        for b, P in enumerate(Ps):
+            _, Y, _ = orc.solve(P, mode=1, num_iter=n)
+            seen_inf |= bool(np.isinf(Y).any() or np.isnan(Y).any())
+            _same_or_both_nan(pb.Y[b].cpu().numpy(), Y, f"N={N} pair={pair} fixed num_iter={n} problem {b}")
+    assert seen_inf
+    for cap in (3, 350):
+        pb = _batch(gpu_lib, Ps).solve(max_updates=cap)
+        for b, P in enumerate(Ps):
+            h, Y, U = orc.solve(P, max_updates=cap)
+            assert int(pb.h[b]) == abs(h)
+            _same_or_both_nan(pb.Y[b].cpu().numpy(), Y, f"N={N} pair={pair} converge cap {cap} problem {b} Y")
+            _same_or_both_nan(pb.U[b].cpu().numpy(), U, f"N={N} pair={pair} converge cap {cap} problem {b} U")
+
+
+@pytest.mark.parametrize("H", [3, 5])
+def test_mid2_band_matches_dense(gpu_lib, golden_bundled, knobs, H):
+    """mid2_dense 1 (every k) and the default band sums give the same bits on
+    the plant over H stages (converge and fixed mode)."""
+    from oracle import block_diag_problem
+
+    knobs("mid2_min_n", 0)
+    Q = block_diag_problem(_bundled(golden_bundled), H)
+    out = {}
+    for dense in (1, 0):
+        knobs("mid2_dense", dense)
+        pb = _batch(gpu_lib, [Q] * 2)
+        c = pb.solve(max_updates=CAP)
+        assert gpu_lib.tune_get("last_batch_kernel") == 3
+        yc, uc, hc = c.Y.cpu().numpy().copy(), c.U.cpu().numpy().copy(), c.h.cpu().numpy().copy()
+        f = _batch(gpu_lib, [Q] * 2).solve(gpu_lib.MODE_FIXED, num_iter=100)
+        out[dense] = (yc, uc, hc, f.Y.cpu().numpy().copy())
+    for a, b in zip(out[1], out[0]):
+        assert_bitwise(b, a, f"H={H} band vs dense")
