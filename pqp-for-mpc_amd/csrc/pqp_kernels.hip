@@ -4103,8 +4103,20 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     int* flag = reinterpret_cast<int*>(lds + L.flag);  // [0..11] checkFeas per C row wave, [12 + p] Y non-finite
     int* band = reinterpret_cast<int*>(lds + L.band);
     const int NT = blockDim.x;  // 64 * mid2_waves(N, conv, PAIR, crows)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int nUW = mid2_uw(N, PAIR), wT = nUW, wC0 = nUW + 1;
+#ifndef PQP_M2_PERM
+#define PQP_M2_PERM 1
+#endif
+    // Roles over the hardware waves: the SIMDs take waves w and w + 4.  With
+    // three update waves, T, three C row waves and the cost wave (the
+    // one-lane-per-row build, 128 < N <= 160: one workgroup per CU), the C row
+    // waves -- whose chains set the phase -- share a SIMD with the short third
+    // update wave and with T, instead of with the first two update waves:
+    // hardware waves 0..7 take roles C0, C1, UW0, UW1, UW2, T, C2, cost.
+    int wave = tid >> 6;
+    if constexpr (PQP_M2_PERM && !PAIR && MINW == 1)
+        if (NT == 512 && nUW == 3) wave = wave < 2 ? wave + 4 : (wave < 6 ? wave - 2 : wave);
     // C waves that take checkFeas rows and the Y'Qd terms (crows each); wave
     // wC0 + nCR the costs
     const int crows = (NT / 64 - nUW - 2 >= (N + 31) / 32) ? 32 : 64;
@@ -4298,7 +4310,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             float* ynext = Yr + (int)((s + 1) % 3) * nk;
             // Y_{s+1}'s non-finite flag goes to slot (s+1)&1; slot s&1 was last
             // read before the previous phase's second barrier
-            if (tid == 0) flag[12 + (int)(s & 1)] = 0;
+            if (wave == 0 && lane == 0) flag[12 + (int)(s & 1)] = 0;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
             // a zero entry's term is +-0 while y_k is finite, and the sum (from
             // +0.0f, never -0) is unchanged by it: the terms outside the band
