@@ -4113,10 +4113,23 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     // one-lane-per-row build, 128 < N <= 160: one workgroup per CU), the C row
     // waves -- whose chains set the phase -- share a SIMD with the short third
     // update wave and with T, instead of with the first two update waves:
-    // hardware waves 0..7 take roles C0, C1, UW0, UW1, UW2, T, C2, cost.
+    // hardware waves 0..7 take roles C0, C1, UW0, UW1, UW2, T, C2, cost
+    // (H = 5: 59.8 -> 57.0 ms).  The lane-side build with four update waves
+    // (96 < N <= 128, two workgroups per CU): C0, C1, cost, T, UW3, UW0, UW1,
+    // UW2 -- the C row waves beside the short fourth update wave and the first
+    // (H = 4: 31.7 -> 28.1 ms).  The lean build with two update waves was
+    // slower so (C0, C1 alone on a SIMD: H = 3 26.3 -> 27.7 ms) and keeps
+    // its order (profiles/r05/band/perm_*.txt).
     int wave = tid >> 6;
     if constexpr (PQP_M2_PERM && !PAIR && MINW == 1)
         if (NT == 512 && nUW == 3) wave = wave < 2 ? wave + 4 : (wave < 6 ? wave - 2 : wave);
+#ifndef PQP_M2_PERM4
+#define PQP_M2_PERM4 1
+#endif
+    if constexpr (PQP_M2_PERM4 && PAIR && MINW == 1)
+        if (NT == 512 && nUW == 4) {
+            wave = wave < 3 ? wave + 5 : (wave == 3 ? 4 : (wave == 4 ? 3 : wave - 5));
+        }
     // C waves that take checkFeas rows and the Y'Qd terms (crows each); wave
     // wC0 + nCR the costs
     const int crows = (NT / 64 - nUW - 2 >= (N + 31) / 32) ? 32 : 64;
