@@ -58,7 +58,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-KERNEL = "k_batch_stream<16,nt>"
+KERNEL = "k_batch_resident<16,2>"
 
 
 def hot_kernel_hash() -> str:
@@ -69,20 +69,29 @@ def hot_kernel_hash() -> str:
     return kernel_src_hash("hot-kernel")
 
 
-def kernel_src_hash(*markers: str) -> str:
+# headers every kernel of pqp_kernels.hip includes (the float rules, gap_stop,
+# SolveArgs / SolveState, the tuning knobs): a change there changes what the
+# measured kernels compute or how they are launched, so it invalidates their
+# PMC / VALU records like a change inside the marked region does
+KERNEL_HEADERS = ("pqp_device.h", "pqp_launch.h")
+
+
+def kernel_src_hash(*markers: str, root: Path | None = None) -> str:
     """SHA-256 (16 hex) of the text between pqp_kernels.hip's <marker> and
-    </marker> comments (each marker's region, in order) plus the library's
-    compile flags."""
+    </marker> comments (each marker's region, in order), the headers the
+    kernels include (KERNEL_HEADERS) and the library's compile flags."""
     import hashlib
     import re
 
-    src = (ROOT / "pqp-for-mpc_amd" / "csrc" / "pqp_kernels.hip").read_text()
+    base = (root or ROOT) / "pqp-for-mpc_amd"
+    src = (base / "csrc" / "pqp_kernels.hip").read_text()
     text = ""
     for marker in markers:
         m = re.search(rf"// <{marker}>.*?// </{marker}>", src, re.S)
         text += m.group(0) if m else src
-    flags = [ln for ln in (ROOT / "pqp-for-mpc_amd" / "Makefile").read_text().splitlines()
-             if ln.startswith("HIPFLAGS")]
+    for h in KERNEL_HEADERS:
+        text += (base / "csrc" / h).read_text()
+    flags = [ln for ln in (base / "Makefile").read_text().splitlines() if ln.startswith("HIPFLAGS")]
     text += "\n".join(flags)
     return hashlib.sha256(text.encode()).hexdigest()[:16]
 
@@ -91,6 +100,51 @@ def alg_bytes(n: int) -> int:
     """Algorithmic HBM bytes per problem-iteration: Qd read once (the split
     matrices and Theta are derived in registers) + theta, Fd, y_in, y_out."""
     return 4 * n * n + 16 * n
+
+
+# VALU issue peak: a SIMD-32 issues one wave64 VALU instruction every 2
+# clocks when it has several waves (MI355X_MICROARCH.md: 4 clocks is what ONE
+# wave alone sustains), 256 CUs x 4 SIMDs x 2.4 GHz / 2
+VALU_PEAK_GWI = 256 * 4 * 2.4e9 / 2 / 1e9  # 1228.8 G wave-instructions/s
+# fp32 VALU lane-op rate, unpacked (no FMA on this path: a multiply and an add
+# are two ops): 256 CUs x 4 SIMDs x 64 lanes / 2 clocks x 2.4 GHz
+VALU_LANE_OPS = 256 * 4 * 64 / 2 * 2.4e9  # 78.6 T op/s
+
+
+def converge_alg_flops(iterates: int, N: int, M: int, feasible: bool = True) -> float:
+    """The reference's arithmetic per converge-mode iterate (terminate() +
+    updateY2, PQP_CPU.c:603-618, :673-687; O(N) terms dropped): the update's
+    two N x N mat-vecs 4N^2; computeUfromY Gp'Y 2NM + Qp_inv tmp 2M^2;
+    checkFeas Gp U 2NM; on a feasible iterate computeCost's Y'Qd 2N^2 and
+    U'Qp 2M^2.  (The last iterate runs no update: counted anyway, < 0.2 %.)"""
+    per = 4.0 * N * N + 4.0 * N * M + 2.0 * M * M + ((2.0 * N * N + 2.0 * M * M) if feasible else 0.0)
+    return iterates * per
+
+
+def valu_roofline(key: str, marker: str, h_sum: int, dt: float, N: int, M: int) -> dict:
+    """VALU roofline of a batched solve whose matrices stay in LDS (bound by
+    instruction issue, not HBM): the wave-level VALU instructions of this exact
+    solve (profiles/pmc_valu.json[key], rocprofv3 SQ_INSTS_VALU, keyed by the
+    kernel source hash and the workload's iteration count) over the timed
+    solve, against VALU_PEAK_GWI; beside it the reference's algorithmic flops
+    (every iterate feasible, as on the bundled plant) against VALU_LANE_OPS."""
+    flops = converge_alg_flops(h_sum, N, M)
+    out = {"bound": "valu", "alg_flops": flops, "alg_TFLOPs": flops / dt / 1e12,
+           "alg_frac": flops / dt / VALU_LANE_OPS,
+           "alg_note": "6N^2 + 4NM + 4M^2 per iterate (PQP_CPU.c:603-618, :673-687), every iterate feasible, over "
+                       "the unpacked fp32 VALU rate 78.6 T op/s"}
+    vf = ROOT / "profiles" / "pmc_valu.json"
+    vrec = json.loads(vf.read_text()).get(key) if vf.exists() else None
+    khash = kernel_src_hash(marker)
+    if vrec and vrec.get("kernel_src_sha256") == khash and vrec.get("h_sum") == h_sum:
+        ach = vrec["sq_insts_valu"] / dt / 1e9
+        out.update({"achieved": ach, "peak": VALU_PEAK_GWI, "unit": "G wave-instr/s", "frac": ach / VALU_PEAK_GWI,
+                    "valu_insts": vrec["sq_insts_valu"], "source": f"profiles/pmc_valu.json {key}"})
+    else:
+        out.update({"achieved": None, "peak": VALU_PEAK_GWI, "unit": "G wave-instr/s", "frac": None,
+                    "source": f"stale or missing VALU record for this kernel source / workload ({khash}); "
+                              "re-run scripts/gpu_r06.sh hpmc + scripts/pmc_valu.py"})
+    return out
 
 
 def parse():
@@ -370,31 +424,63 @@ def horizon_bench(pqp_amd, Hs=(2, 4, 5), B: int = 16384, keep: dict | None = Non
                "h_min": int(h.min()), "h_max": int(h.max()), "h_mean": float(h.mean()), "max_updates": cap,
                "converged_frac": float((pb.status.cpu().numpy() == 1).mean()),
                "capped": int((pb.status.cpu().numpy() == 2).sum())}
-        # VALU-issue roofline (the kernel keeps every matrix in LDS: it is bound
-        # by instruction issue, not HBM): the wave-level VALU instructions of
-        # this exact solve (profiles/pmc_valu.json, rocprofv3 SQ_INSTS_VALU of
-        # scripts/horizon_pmc.py H, keyed by the kernel's source hash and the
-        # workload's iteration count) over this timed solve, against one VALU
-        # instruction per SIMD every 4 clocks (256 CUs x 4 SIMDs x 2.4 GHz / 4)
-        vf = ROOT / "profiles" / "pmc_valu.json"
-        vrec = json.loads(vf.read_text()).get(f"mid2_H{H}") if vf.exists() else None
-        khash = kernel_src_hash("solve-mid2")
-        if vrec and vrec.get("kernel_src_sha256") == khash and vrec.get("h_sum") == int(h.sum()):
-            peak = 256 * 4 * 2.4e9 / 4 / 1e9
-            ach = vrec["sq_insts_valu"] / dt / 1e9
-            row["roofline"] = {"bound": "valu", "achieved": ach, "peak": peak, "unit": "G wave-instr/s",
-                               "frac": ach / peak, "valu_insts": vrec["sq_insts_valu"],
-                               "source": "profiles/pmc_valu.json " + f"mid2_H{H}"}
-        else:
-            row["roofline"] = {"bound": "valu", "achieved": None,
-                               "source": "stale or missing VALU record for this kernel source / workload "
-                                         f"({khash}); re-run scripts/gpu_r05.sh hpmc + scripts/pmc_valu.py"}
+        row["roofline"] = valu_roofline(f"mid2_H{H}", "solve-mid2", int(h.sum()), dt, N, M)
         row["note"] = ("the H stages are stacked block-diagonally and decoupled (each stage its own copy of "
                        "the bundled plant at its own state): a size class of the MPC horizon (n_dual 28 H), "
                        "not a coupled horizon")
         if keep is not None:
             keep[f"H{H}"] = (pb.problem(0), int(h[0]))
         out[f"H{H}"] = row
+        del pb
+        torch.cuda.empty_cache()
+    return out
+
+
+# the dense companion of the horizon leg: n_dual of H = 4 and H = 5, M = N / 4
+# as in the stacked plant, every iterate feasible, h = 313 for every problem
+DENSE_SIZES = ((112, 28), (140, 35))
+DENSE_UPDATES = 312
+
+
+def dense_horizon_batch(pqp_amd, N: int, M: int, B: int = 16384, seed: int = 11):
+    """B synthetic problems of n_dual N, M primal (the generator behind
+    configs[2]-[4]: Gp in {-1, 0, +1}, so Qd = Gp Qp_inv Gp' is dense -- no
+    zero band for k_solve_mid2's band sums to skip), duals built on the GPU;
+    then Kp = 1e30 seen by checkFeas only (Fd keeps the generator's Kp), so
+    every iterate is feasible and runs all of computeCost, as the stacked
+    plant's do.  The generator's problems do not meet the exact gap test, so a
+    solve capped at DENSE_UPDATES updates stops every problem at h = 313, the
+    bundled plant's iteration count."""
+    pb = pqp_amd.ProblemBatch.synthetic(seed, 0, B, N, M)
+    pb.Kp.fill_(1e30)
+    return pb
+
+
+def horizon_dense_bench(pqp_amd, B: int = 16384) -> dict:
+    """The horizon leg's solver on DENSE Qd of the same sizes (VERDICT r5:
+    the stacked plant's Qd is block-diagonal, so its band sums skip zeros a
+    coupled horizon would not have).  Converge mode, DENSE_UPDATES updates per
+    problem, k_solve_mid2 (path 3); timed: the batched solve only."""
+    import torch
+
+    out = {}
+    for N, M in DENSE_SIZES:
+        pb = dense_horizon_batch(pqp_amd, N, M, B)
+        pb.solve(max_updates=DENSE_UPDATES)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pb.solve(max_updates=DENSE_UPDATES)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        h = pb.h.cpu().numpy()
+        row = {"n_dual": N, "m": M, "problems": B, "path": int(pqp_amd.lib().pqp_batch_solve_path(N, M)),
+               "kernel": {3: "k_solve_mid2", 2: "k_solve_mid"}.get(pqp_amd.tune_get("last_batch_kernel"), "other"),
+               "converge_ms": dt * 1e3, "qp_solves_per_s": B / dt, "iterations_per_s": float(h.sum()) / dt,
+               "h_min": int(h.min()), "h_max": int(h.max()), "max_updates": DENSE_UPDATES,
+               "roofline": valu_roofline(f"mid2_dense_N{N}", "solve-mid2", int(h.sum()), dt, N, M),
+               "note": "synthetic dense Qd (seed 11), Kp = 1e30 for checkFeas: every iterate feasible, capped at "
+                       f"{DENSE_UPDATES} updates (h = 313 as on the bundled plant)"}
+        out[f"N{N}"] = row
         del pb
         torch.cuda.empty_cache()
     return out
@@ -752,6 +838,69 @@ def rowshard_bench(pqp_amd, dist, rank: int, world: int, dev, N: int, updates: i
     return out
 
 
+def _dig(d, *path):
+    for k in path:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return d
+
+
+def summary(result: dict) -> dict:
+    """Every leg's headline numbers in one small object, printed as the LAST
+    key of the line (the driver's record keeps only the line's tail, so the
+    legs printed early -- batch_converge first -- would otherwise be cut).
+    A leg that failed or did not run shows as null."""
+    def r(v, nd=4):
+        return round(v, nd) if isinstance(v, float) else v
+
+    S = {"value": r(result.get("value"), 1), "hbm_frac": r(_dig(result, "roofline", "frac")),
+         "avg_launch_ms": r(_dig(result, "roofline", "avg_launch_ms"), 3),
+         "traffic_ratio": (r(_dig(result, "roofline", "traffic") / _dig(result, "roofline", "alg_bytes_per_launch"))
+                           if isinstance(_dig(result, "roofline", "traffic"), (int, float)) else None)}
+    if result.get("n_gpus", 1) > 1:
+        S["per_rank_timed_s"] = _dig(result, "per_rank", "timed_s")
+        S["gather_ms"] = _dig(result, "per_rank", "gather_ms")
+    for case in ("infeasible", "feasible"):
+        S[f"batch_converge_{case}"] = {"ms_per_iter": r(_dig(result, "batch_converge", case, "ms_per_iteration"), 3),
+                                       "hbm_frac": r(_dig(result, "batch_converge", case, "frac_of_hbm_peak"))}
+    for H in ("H2", "H4", "H5"):
+        S[f"horizon_{H}"] = {"ms": r(_dig(result, "horizon", H, "converge_ms"), 2),
+                             "valu_frac": r(_dig(result, "horizon", H, "roofline", "frac")),
+                             "alg_frac": r(_dig(result, "horizon", H, "roofline", "alg_frac"))}
+    for key in ("N112", "N140"):
+        S[f"horizon_dense_{key}"] = {"ms": r(_dig(result, "horizon_dense", key, "converge_ms"), 2),
+                                     "valu_frac": r(_dig(result, "horizon_dense", key, "roofline", "frac")),
+                                     "alg_frac": r(_dig(result, "horizon_dense", key, "roofline", "alg_frac"))}
+    S["bundled_fixed1000_ms"] = r(_dig(result, "bundled", "fixed1000_ms"))
+    S["bundled_converge_ms"] = r(_dig(result, "bundled", "converge_ms"))
+    S["mpc_batch_ms"] = r(_dig(result, "mpc_batch", "converge_ms"), 3)
+    S["single_n1024_ms_per_1000"] = r(_dig(result, "single_n1024", "ms_per_solve"))
+    S["single_converge_us_per_iter"] = r(_dig(result, "single_converge", "us_per_iter"))
+    S["setup_TFLOPs"] = r(_dig(result, "setup_convert", "gemm_TFLOPs"), 2)
+    S["rowshard_us_per_update"] = r(_dig(result, "rowshard", "us_per_update"), 2)
+    S["iters_to_tol_identical"] = result.get("iters_to_tol_identical_to_reference")
+    S["cpu_baseline"] = r(_dig(result, "cpu_baseline", "value"), 1)
+    errors = sorted(k for k, v in result.items() if isinstance(v, dict) and "error" in v)
+    if errors:
+        S["legs_with_errors"] = errors
+    return S
+
+
+def rank_spread(dist, dev, **vals) -> dict:
+    """Min and max over the job's ranks of each named value (two all-reduces;
+    every rank must call it).  At one rank min = max = the value."""
+    import torch
+
+    names = list(vals)
+    lo = torch.tensor([float(vals[k]) for k in names], dtype=torch.float64, device=dev)
+    hi = lo.clone()
+    if dist is not None:
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return {k: {"min": float(lo[i]), "max": float(hi[i])} for i, k in enumerate(names)}
+
+
 class Emitter:
     """Rank 0's one JSON line, printed exactly once.
 
@@ -780,6 +929,8 @@ class Emitter:
     def emit(self):
         with self._lock:
             if self.rank == 0 and not self._printed and self.result is not None:
+                self.result.pop("summary", None)
+                self.result["summary"] = summary(self.result)  # last key: the driver keeps the line's tail
                 print(json.dumps(self.result), flush=True)
             self._printed = True
 
@@ -944,18 +1095,17 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    # the max over ranks is the job's time; the min beside it shows a slow rank
+    spread = rank_spread(dist, dev, timed_s=elapsed, kern_ms=kern_ms)
+    elapsed, kern_ms = spread["timed_s"]["max"], spread["kern_ms"]["max"]
 
     Yh = batch.Y[:, :N]
     finite = bool(torch.isfinite(Yh).all().item()) and bool((Yh >= 0).all().item())
 
     # The headline line is complete here; it is held (rank 0) while the
     # optional legs run, each under the Emitter's guard.
-    result = headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse) \
-        if rank == 0 else None
+    result = headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse,
+                      spread=spread) if rank == 0 else None
     em = Emitter(rank, result, args.leg_timeout, abort_on_failure=world > 1)
 
     if dist is not None:  # gather Y* to rank 0 over RCCL (reported separately, not in `value`)
@@ -965,14 +1115,16 @@ def main():
             g0 = time.perf_counter()
             full = gather_rows(dist, rank, world, y)
             torch.cuda.synchronize(dev)
+            ms = (time.perf_counter() - g0) * 1e3
             ok = None
             if rank == 0:  # rank order = problem order: rank 0's own block leads
                 ok = tuple(full.shape) == (B * world, N) and bool(torch.equal(full[:B], y))
-            return {"ms": (time.perf_counter() - g0) * 1e3, "ok": ok}
+            return {"ms": ms, "ok": ok, "spread": rank_spread(dist, dev, gather_ms=ms)["gather_ms"]}
 
         g = em.leg("gather", gather_leg)
         if result is not None:
             result["gather_ms"], result["gather_ok"] = g.get("ms"), g.get("ok")
+            result.setdefault("per_rank", {})["gather_ms"] = g.get("spread")
     # the CPU baseline's sample: distinct problems of this very workload, from
     # the GPU batch (host copies, 4 MiB of Qd each)
     inst = None
@@ -997,6 +1149,7 @@ def main():
         em.leg("bundled", lambda: bundled_bench(pqp_amd))
         em.leg("mpc_batch", lambda: mpc_batch_bench(pqp_amd))
         em.leg("horizon", lambda: horizon_bench(pqp_amd, keep=None if args.no_cpu_baseline else hz_keep))
+        em.leg("horizon_dense", lambda: horizon_dense_bench(pqp_amd))
         em.leg("single_n1024", lambda: single_bench(pqp_amd))
         em.leg("single_converge", lambda: single_converge_bench(pqp_amd))
         em.leg("setup_convert", lambda: setup_bench(pqp_amd))
@@ -1022,7 +1175,8 @@ def main():
         dist.destroy_process_group()
 
 
-def headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse) -> dict:
+def headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finite, rehearse,
+             spread: dict | None = None) -> dict:
     """The headline JSON object (rank 0): throughput of exactly K steps over
     all ranks, the hot kernel's roofline, the result check."""
     per_launch_ms = kern_ms / launches
@@ -1064,6 +1218,9 @@ def headline(args, rank, world, N, B, K, W, C, elapsed, kern_ms, launches, finit
         "gather_ms": None,
         "gather_ok": None,
     }
+    if world > 1 and spread is not None:
+        # each rank's timed region (s) and HIP-event kernel time (ms): min and max over ranks
+        result["per_rank"] = dict(spread)
     if rehearse:
         result["rehearsal"] = "all ranks on cuda:0 over gloo (PQP_BENCH_REHEARSE=1): control-flow check, not a measurement"
     return result

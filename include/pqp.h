@@ -243,6 +243,13 @@ int pqp_batch_convert_to_dual(int B, int N, int M, const float *d_Qp_inv, const 
                               const float *d_Fp, const float *d_Mp, float *d_Qd, float *d_Fd, float *d_Md,
                               void *stream);
 
+/* pqp_batch_convert_to_dual keeps ONE grow-only device workspace per device
+ * (4*(B*N*M + B*M) bytes at its largest call: 128 MiB at B = 64, N = 1024,
+ * M = 512), shared by every calling thread (calls on one device take turns
+ * while they use it).  This frees every device's workspace; the next call
+ * allocates again; a setup call in progress finishes first. */
+int pqp_release_workspaces(void);
+
 /* computeFp / computeMp (PQP_CPU.c:373-428) for B (D, x) pairs of one plant:
  * m = nInput*pHorizon, nd = nDis*pHorizon, ns = nState.  The plant matrices
  * (Fp1 [m*nd], Fp2 [m*ns], Fp3 [m], Mp1 [ns*ns], Mp2 [nd*ns], Mp3 [nd*nd],

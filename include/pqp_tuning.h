@@ -88,10 +88,18 @@ extern "C" {
  *                          (k_fixed_tiny / k_solve_wave, state copies) instead
  *                          of k_fixed_one / k_solve_quintet (one launch, results
  *                          straight to pinned host memory)
+ *   tiny_chunk [0]         iterates per launch of a one-launch tiny solve (0: about
+ *                          2^26 element updates; a solve that needs more resumes
+ *                          from the device state in further launches)
+ *   tiny_fallback [0]      read a tiny solve's results from its device copies as
+ *                          if the pinned output had missed its tag (tests)
  *   tiny_dense [0]         k_fixed_one / k_solve_quintet without the sparse
  *                          update form (every split entry summed)
- *   iterate_v1 [0]         pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate
- *                          instead of k_batch_stream
+ *   iterate_kind [0]       pqp_batch_iterate's kernel: 0 the default (n_dual 1024:
+ *                          k_batch_resident, Qd's first blocks kept on the CU
+ *                          across a launch's iterations; other multiples of
+ *                          1024: k_batch_stream; else k_batch_iterate),
+ *                          1 k_batch_iterate, 2 k_batch_stream
  *   matvec_lds [0]         convertToDual's mat-vec on the LDS-staged
  *                          k_matvec_rows instead of k_matvec_lane
  *   gj_v1 [0]              batched Gauss_Jordan (n <= 1024): 0 k_gj_blocked3
@@ -137,7 +145,9 @@ int pqp_tune_get(const char *key, long long *value);
  * n problems of a batched k_solve_mid solve -- phase A/B/C/D+E clock totals,
  * iterations, then each wave's phase-A busy clocks, added to what the buffer
  * holds; a k_solve_pipe solve writes phase X / Y / cost clock totals to words
- * 0-2 and iterations to word 4).  n = 0 turns it off.  Timing only. */
+ * 0-2 and iterations to word 4; "tiny": k_solve_quintet's per-wave clocks at
+ * N = 28, M <= 8, which needs n >= 24 words, else PQP_ERR_ARG).  n = 0 turns it
+ * off.  Timing only. */
 int pqp_tune_trace(const char *what, void *d_buf, int n);
 
 /* Test hook: fill the LDS of every CU of the current device with `value`

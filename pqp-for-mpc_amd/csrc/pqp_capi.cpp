@@ -4,6 +4,7 @@
 // host: every drop-in function is computed on the GPU and fails loudly (status
 // code, or exit(EXIT_FAILURE) for the void drop-ins) when no gfx950 device or
 // kernel is available -- there is no CPU fallback.
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
@@ -297,7 +298,7 @@ struct pqp_problem {
     float* hin = nullptr;                            // pinned staging of small problems' inputs
     size_t hin_floats = 0;
     float* hout = nullptr;                           // pinned output of the one-launch tiny solves (kTinyOut* layout)
-    int out_tag = 0;                                 // the last tag a tiny launch was given
+    unsigned out_tag = 0;                            // the last tag a tiny launch was given (1 .. 2^31 - 1)
     void* hout_dev = nullptr;                        // its device address
     ~pqp_problem() {
         if (own_stream && stream) (void)hipStreamDestroy(stream);
@@ -339,7 +340,9 @@ int problem_finish(pqp_problem& P, hipStream_t s) {
     P.small = solve_small_lds_bytes(N, M) <= kLdsBudget;
     PQP_TRY(P.Y.floats(N));
     PQP_TRY(P.U.floats(M));
-    PQP_TRY(P.state.alloc(sizeof(SolveState)));
+    // the state, then the int error word a one-launch tiny solve stores behind it (kTinyDevErr)
+    PQP_TRY(P.state.alloc(sizeof(SolveState) + 16));
+    PQP_HIP(hipMemsetAsync(P.state.p, 0, sizeof(SolveState) + 16, s));
     PQP_HIP(hipMemsetAsync(P.U.p, 0, sizeof(float) * M, s));
     if (!P.hst) PQP_HIP(hipHostMalloc((void**)&P.hst, sizeof(SolveState), hipHostMallocDefault));
     if (P.hio_floats < (size_t)N + M) {
@@ -897,7 +900,7 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
         PQP_HIP(hipHostMalloc((void**)&P.hout, sizeof(float) * kTinyOutFloats,
                               hipHostMallocMapped | hipHostMallocCoherent));
         PQP_HIP(hipHostGetDevicePointer(&P.hout_dev, P.hout, 0));
-        reinterpret_cast<int*>(P.hout)[kTinyOutTagOffset] = 0;
+        std::memset(P.hout, 0, sizeof(float) * kTinyOutFloats);  // tag 0: no launch's
     }
     SolveArgs a{};
     a.Qd = P.Qd.f();
@@ -918,7 +921,13 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
     a.mode = mode;
     a.num_iter = num_iter;
     a.max_updates = max_updates;
-    a.chunk = 1LL << 30;  // one launch: the kernel runs to the stop, the cap or num_iter
+    // iterates per launch: about 2^26 element updates (28.5 k at the bundled
+    // size, so its solves stay one launch), bounded so that a long fixed-mode
+    // solve or an uncapped converge solve is a sequence of launches that
+    // resume from the device state, not one kernel running for minutes
+    // (ADVICE r5); the tiny_chunk knob sets it for the resume tests
+    const double per_update = 3.0 * N * N + 2.0 * N * M + 2.0 * M * M + 1.0;
+    a.chunk = g_tune.tiny_chunk > 0 ? g_tune.tiny_chunk : std::max(1024LL, (long long)((1 << 26) / per_update));
     a.fresh = 1;
     a.hout = P.hout_dev;
     a.tiny_flags = (g_tune.tiny_dense ? kTinyDense : 0) | (g_tune.tiny_stall ? kTinyStall : 0);
@@ -928,22 +937,27 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
     const int* herr = reinterpret_cast<const int*>(P.hout) + kTinyOutErrOffset;
     volatile const int* htag = reinterpret_cast<const int*>(P.hout) + kTinyOutTagOffset;
     for (;;) {
-        a.out_tag = ++P.out_tag;
-        if (a.out_tag == 0) a.out_tag = ++P.out_tag;
+        P.out_tag = (P.out_tag + 1) & 0x7fffffffu;  // positive, never 0 (the zeroed buffer's tag)
+        if (P.out_tag == 0) P.out_tag = 1;
+        a.out_tag = (int)P.out_tag;
         PQP_HIP(launch_one_tiny(a, dst, s));
         PQP_HIP(hipStreamSynchronize(s));
-        if (*htag != a.out_tag) {
-            // not this launch's output (never seen so far): read the device copy instead
+        if (*htag != a.out_tag || g_tune.tiny_fallback) {
+            // not this launch's output (never seen so far; the tiny_fallback
+            // knob forces this path in tests): read the device copies instead --
+            // Y, U, the state and the error word behind it
             ++g_tiny_stale;
             PQP_HIP(hipMemcpyAsync(P.hout, P.Y.p, sizeof(float) * N, hipMemcpyDeviceToHost, s));
             if (mode == kModeConverge)
                 PQP_HIP(hipMemcpyAsync(P.hout + kTinyOutUOffset, P.U.p, sizeof(float) * M, hipMemcpyDeviceToHost, s));
             PQP_HIP(hipMemcpyAsync(P.hout + kTinyOutStateOffset, dst, sizeof(SolveState), hipMemcpyDeviceToHost, s));
+            PQP_HIP(hipMemcpyAsync(P.hout + kTinyOutErrOffset, reinterpret_cast<const char*>(dst) + kTinyDevErr,
+                                   sizeof(int), hipMemcpyDeviceToHost, s));
             PQP_HIP(hipStreamSynchronize(s));
         }
         if (*herr) return set_error(PQP_ERR_HIP, "k_solve_quintet: a wave's hand-off wait expired (N=%d, M=%d)", N, M);
         if (hs->status != kStatusContinue) break;
-        a.fresh = 0;  // (a 2^30-iterate chunk ran out) resume from the device state
+        a.fresh = 0;  // (a chunk ran out) resume from the device state
     }
     std::memcpy(P.hio, P.hout, sizeof(float) * N);
     if (mode == kModeConverge) std::memcpy(P.hio + N, P.hout + kTinyOutUOffset, sizeof(float) * M);
@@ -1058,7 +1072,7 @@ using namespace pqp;
 
 extern "C" {
 
-int pqp_version(void) { return 105; }  // ABI revision: INTEGRATION.md section 6
+int pqp_version(void) { return 106; }  // ABI revision: INTEGRATION.md section 6
 
 // ---------------------------------------------------------------------------
 // 2a. status-returning host API
@@ -1449,30 +1463,69 @@ int pqp_batch_gauss_jordan(int B, int n, const float* d_A, float* d_res, void* s
     return PQP_OK;
 }
 
-// A grow-only device workspace per (thread, device) for the batched setup
-// calls; never freed (a thread's buffer lives until the process ends: freeing
-// it at thread exit could run after the HIP runtime is gone).  Calls on one
-// thread are serialised (each synchronises its stream before returning).
-static int setup_workspace(size_t floats, float** out) {
-    thread_local void* buf[64] = {};
-    thread_local size_t cap[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return set_error(PQP_ERR_NO_DEVICE, "libpqp: cannot query the current device");
-    const size_t bytes = floats * sizeof(float);
-    if (cap[dev] < bytes) {
-        if (buf[dev]) (void)hipFree(buf[dev]);
-        buf[dev] = nullptr;
-        cap[dev] = 0;
-        const hipError_t e = hipMalloc(&buf[dev], bytes);
-        if (e != hipSuccess) {
-            buf[dev] = nullptr;
-            return set_error(PQP_ERR_ALLOC, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
-        }
-        cap[dev] = bytes;
+// One grow-only device workspace per device for the batched setup calls
+// (the round-5 form kept one per (thread, device), so a host that
+// called from many pooled threads kept one buffer per thread it ever used).
+// A call holds its device's lock from the workspace request until its stream
+// has synchronised, so concurrent setup calls on one device take turns (each
+// one fills the device anyway); no hipMalloc / hipFree (which synchronise the
+// device) per call.  pqp_release_workspaces() frees every pool; nothing frees
+// them at exit (a static destructor could run after the HIP runtime is gone).
+namespace {
+struct SetupPool {
+    std::mutex mu;
+    void* buf = nullptr;
+    size_t cap = 0;
+};
+SetupPool g_setup_pool[64];
+
+class SetupWorkspace {
+  public:
+    ~SetupWorkspace() {
+        if (pool_) pool_->mu.unlock();
     }
-    *out = static_cast<float*>(buf[dev]);
-    return PQP_OK;
+    int acquire(size_t floats, float** out) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+            return set_error(PQP_ERR_NO_DEVICE, "libpqp: cannot query the current device");
+        pool_ = &g_setup_pool[dev];
+        pool_->mu.lock();
+        const size_t bytes = floats * sizeof(float);
+        if (pool_->cap < bytes) {
+            if (pool_->buf) (void)hipFree(pool_->buf);
+            pool_->buf = nullptr;
+            pool_->cap = 0;
+            const hipError_t e = hipMalloc(&pool_->buf, bytes);
+            if (e != hipSuccess) {
+                pool_->buf = nullptr;
+                return set_error(PQP_ERR_ALLOC, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+            }
+            pool_->cap = bytes;
+        }
+        *out = static_cast<float*>(pool_->buf);
+        return PQP_OK;
+    }
+
+  private:
+    SetupPool* pool_ = nullptr;
+};
+}  // namespace
+
+int pqp_release_workspaces(void) {
+    int dev0 = 0;
+    const bool restore = hipGetDevice(&dev0) == hipSuccess;
+    int rc = PQP_OK;
+    for (int d = 0; d < 64; ++d) {
+        SetupPool& p = g_setup_pool[d];
+        std::lock_guard<std::mutex> g(p.mu);
+        if (!p.buf) continue;
+        if (hipSetDevice(d) != hipSuccess || hipFree(p.buf) != hipSuccess)
+            rc = set_error(PQP_ERR_HIP, "pqp_release_workspaces: hipFree on device %d failed", d);
+        p.buf = nullptr;
+        p.cap = 0;
+    }
+    if (restore) (void)hipSetDevice(dev0);
+    return rc;
 }
 
 int pqp_batch_convert_to_dual(int B, int N, int M, const float* d_Qp_inv, const float* d_Gp, const float* d_Kp,
@@ -1483,10 +1536,11 @@ int pqp_batch_convert_to_dual(int B, int N, int M, const float* d_Qp_inv, const 
     PQP_TRY(ensure_device());
     hipStream_t s = static_cast<hipStream_t>(stream);
     const long long nm = (long long)N * M, mm = (long long)M * M, nn = (long long)N * N;
-    // Gp Qp_inv (and Fp'Qp_inv) in this thread's grow-only workspace: no
-    // hipMalloc / hipFree (which synchronises the device) per call
+    // Gp Qp_inv (and Fp'Qp_inv) in the device's grow-only workspace, held
+    // until this call's stream has synchronised
+    SetupWorkspace wsp;
     float* ws = nullptr;
-    PQP_TRY(setup_workspace((size_t)B * nm + (size_t)B * M + 64, &ws));
+    PQP_TRY(wsp.acquire((size_t)B * nm + (size_t)B * M + 64, &ws));
     float* GQ = ws;
     float* fq = ws + (((size_t)B * nm + 63) & ~(size_t)63);
     // same sequence as dev_convert_to_dual (PQP_CPU.c:489-498), problem-strided
@@ -2007,7 +2061,9 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_old", &g_tune.tiny_old, nullptr, nullptr},
         {"tiny_dense", &g_tune.tiny_dense, nullptr, nullptr},
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
-        {"iterate_v1", &g_tune.iterate_v1, nullptr, nullptr},
+        {"tiny_fallback", &g_tune.tiny_fallback, nullptr, nullptr},
+        {"tiny_chunk", nullptr, nullptr, &g_tune.tiny_chunk},
+        {"iterate_kind", &g_tune.iterate_kind, nullptr, nullptr},
         {"matvec_lds", &g_tune.matvec_lds, nullptr, nullptr},
         {"gj_v1", &g_tune.gj_v1, nullptr, nullptr},
     };
@@ -2102,6 +2158,9 @@ extern "C" int pqp_tune_trace(const char* what, void* d_buf, int n) {
         pqp::g_tune.mid_trace = buf;
         pqp::g_tune.mid_trace_n = n;
     } else if (std::strcmp(what, "tiny") == 0) {
+        // k_solve_quintet<..., true> writes kTinyTraceWords words unconditionally
+        if (n > 0 && n < pqp::kTinyTraceWords)
+            return pqp::set_error(PQP_ERR_ARG, "pqp_tune_trace: the tiny timeline needs %d words", pqp::kTinyTraceWords);
         pqp::g_tune.tiny_trace = buf;
     } else if (std::strcmp(what, "converge") == 0) {
         pqp::g_tune.converge_trace = buf;

@@ -296,6 +296,94 @@ __global__ void __launch_bounds__(256) k_batch_stream(const float* __restrict__ 
     const float* fin = (updates & 1) ? yb : ya;
     for (int i = tid; i < N; i += 256) Y[(size_t)b * ldv + i] = fin[i];
 }
+
+// ---------------------------------------------------------------------------
+// k_batch_resident (n_dual 1024, the bench shape): k_batch_stream with part of
+// each problem's Qd kept on the CU across the launch's iterations (temporal
+// blocking; one workgroup per CU, so the CU's LDS is this problem's):
+//   blocks 0 .. RL-1 (U k each, 64 KiB per block) are loaded from HBM in the
+//     first iteration, copied into LDS and summed from there afterwards;
+//   block RL -- the first streamed block, loaded at the end of each iteration
+//     for the next one while the LDS blocks are summed -- uses the default
+//     cache policy: 64 KiB per CU = 2 MiB per XCD, which stays in the XCD's
+//     L2 between iterations while the nt stream passes through;
+//   blocks RL+1 .. 63 stream non-temporally as in k_batch_stream.
+// Every row sums the same terms in the same k order as k_batch_stream (only
+// where q comes from differs), so the bits are the same.
+// ---------------------------------------------------------------------------
+template <int U, int RL>
+__global__ void __launch_bounds__(256) k_batch_resident(const float* __restrict__ QdT, long long qstride, int ldq,
+                                                        const float* __restrict__ theta,
+                                                        const float* __restrict__ Fd, int ldv, const float* Y0,
+                                                        float* Y, int updates) {
+    constexpr int N = 1024, nb = N / U;
+    static_assert((nb - RL) % 2 == 0, "the streamed blocks come in pairs");
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* ya = lds;
+    float* yb = lds + ldq;
+    float4* res = reinterpret_cast<float4*>(lds + 2 * ldq);  // [RL][U][256 lanes]
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const float* Q = QdT + (size_t)b * (size_t)qstride;
+    const float* th_g = theta + (size_t)b * ldv;
+    const float* fd_g = Fd + (size_t)b * ldv;
+    for (int i = tid; i < ldq; i += 256) {
+        ya[i] = (i < N) ? (Y0 ? Y0[(size_t)b * ldv + i] : 1000.0f) : 0.0f;  // initMat(Y,1000) :710
+        yb[i] = 0.0f;
+    }
+    const int row = 4 * tid;
+    const int wa = 256 * wave, wbd = wa + 256;  // this wave's diagonal window
+    const float* col = Q + row;
+    float th[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) th[r] = th_g[row + r];
+    float4 qa[U], qb[U];
+    if (updates > 0) stream_load<U, false>(qa, col + (size_t)RL * U * ldq, ldq);
+    __syncthreads();
+    for (int u = 0; u < updates; ++u) {
+        const float* cur = (u & 1) ? yb : ya;
+        float* nxt = (u & 1) ? ya : yb;
+        Acc4 a;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.p[r] = a.n[r] = 0.0f;
+#pragma unroll
+        for (int lb = 0; lb < RL; ++lb) {
+            float4* slot = res + (size_t)lb * U * 256 + tid;  // lane-private: no barrier needed
+            if (u == 0) {
+                stream_load<U, true>(qb, col + (size_t)lb * U * ldq, ldq);
+#pragma unroll
+                for (int j = 0; j < U; ++j) slot[j * 256] = qb[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < U; ++j) qb[j] = slot[j * 256];
+            }
+            const int k0 = lb * U;
+            stream_block<U>(a, qb, k0, k0 >= wa && k0 < wbd, cur, row, th);
+        }
+        for (int kb = RL; kb < nb; kb += 2) {
+            stream_load<U, true>(qb, col + (size_t)(kb + 1) * U * ldq, ldq);
+            int k0 = kb * U;
+            stream_block<U>(a, qa, k0, k0 >= wa && k0 < wbd, cur, row, th);
+            if (kb + 2 < nb)
+                stream_load<U, true>(qa, col + (size_t)(kb + 2) * U * ldq, ldq);
+            else if (u + 1 < updates)  // the next iteration's first streamed block (L2-kept)
+                stream_load<U, false>(qa, col + (size_t)RL * U * ldq, ldq);
+            k0 += U;
+            stream_block<U>(a, qb, k0, k0 >= wa && k0 < wbd, cur, row, th);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = row + r;
+            const float f = fd_g[i];
+            const float num = a.n[r] + 1.0f * max_ref(0.0f, -f);  // matrixAdd(num, Fdn, 1) :611
+            const float den = a.p[r] + 1.0f * max_ref(0.0f, f);   // matrixAdd(den, Fdp, 1) :612
+            nxt[i] = num / den * cur[i];                           // updY :594
+        }
+        __syncthreads();
+    }
+    const float* fin = (updates & 1) ? yb : ya;
+    for (int i = tid; i < N; i += 256) Y[(size_t)b * ldv + i] = fin[i];
+}
 // </hot-kernel>
 
 // ---------------------------------------------------------------------------
@@ -4545,13 +4633,25 @@ static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qs
     // B = 4096, chunk 10.  The other unroll depths (4, 8, 32), default-policy
     // loads and max-based terms were measured and removed (DESIGN.md section 4,
     // profiles/r01/ab_4096*.txt).
-    // n_dual a multiple of 1024 (the bench shape): k_batch_stream, one
-    // workgroup per CU, 16 + 16 float4 loads per lane kept in flight: 7.24-7.26
-    // TB/s against 7.02-7.04 for k_batch_iterate in one process (same bits).
-    // Measured slower and dropped: 8 + 8 (3 workgroups per CU, 7.07-7.09),
-    // 32 + 32 (7.10), 16 + 16 capped to 256 VGPRs (2 per CU, spills: 7.05),
-    // default-policy loads (6.34) -- profiles/r05/iterate_ab_*.json.
-    if (!g_tune.iterate_v1 && N % 1024 == 0) {
+    // n_dual 1024 (the bench shape): k_batch_resident, k_batch_stream with the
+    // first two blocks of each problem's Qd in LDS and the third kept in L2
+    // across the launch's iterations (round 6: 23.9 -> 22.5 ms per launch of
+    // 10 iterations in the probe, scripts/probes/stream_resident.hip,
+    // profiles/r06/stream_resident.jsonl; same bits).
+    const int kind = g_tune.iterate_kind;
+    if (kind == 0 && N == 1024 && ldq == 1024) {
+        const size_t lds = (size_t)2 * ldq * sizeof(float) + (size_t)2 * 16 * 256 * sizeof(float4);
+        hipLaunchKernelGGL((k_batch_resident<16, 2>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, theta, Fd, ldv,
+                           Y0, Y, updates);
+        return hipGetLastError();
+    }
+    // n_dual a multiple of 1024: k_batch_stream, one workgroup per CU, 16 + 16
+    // float4 loads per lane kept in flight: 7.24-7.26 TB/s against 7.02-7.04
+    // for k_batch_iterate in one process (same bits).  Measured slower and
+    // dropped: 8 + 8 (3 workgroups per CU, 7.07-7.09), 32 + 32 (7.10), 16 + 16
+    // capped to 256 VGPRs (2 per CU, spills: 7.05), default-policy loads
+    // (6.34) -- profiles/r05/iterate_ab_*.json.
+    if (kind != 1 && N % 1024 == 0) {
         const size_t lds = (size_t)2 * ldq * sizeof(float);
         hipLaunchKernelGGL((k_batch_stream<16, true>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, N, theta, Fd,
                            ldv, Y0, Y, updates);

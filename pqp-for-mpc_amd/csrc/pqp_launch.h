@@ -45,9 +45,16 @@ struct SolveArgs {
 // SolveState at kTinyOutStateOffset (floats), an int error word at kTinyOutErrOffset
 constexpr int kTinyOutUOffset = 32, kTinyOutStateOffset = 64, kTinyOutErrOffset = 72, kTinyOutTagOffset = 73,
               kTinyOutFloats = 80;
+static_assert(sizeof(SolveState) <= 4 * (kTinyOutErrOffset - kTinyOutStateOffset),
+              "the SolveState must end before the error word of the tiny output");
+static_assert(kTinyOutErrOffset < kTinyOutTagOffset && kTinyOutTagOffset < kTinyOutFloats, "tiny output layout");
+// the device copy of the error word: the int right behind the handle's
+// SolveState (the host reads it when the pinned output lacks the launch's tag)
+constexpr int kTinyDevErr = (int)sizeof(SolveState);
+constexpr int kTinyTraceWords = 24;  // k_solve_quintet's timeline: 4 words per role + 4
 constexpr int kTinyDense = 1;
-constexpr int kTinyStall = 2;
-constexpr int kMid2Dense = 4;  // k_solve_mid2: no band skipping (tune mid2_dense)  // error-path tests: k_solve_quintet's deciding waves never decide
+constexpr int kTinyStall = 2;  // error-path tests: k_solve_quintet's deciding waves never decide
+constexpr int kMid2Dense = 4;  // k_solve_mid2: no band skipping (tune mid2_dense)
 // one problem with N, M <= 32 (fixed mode; converge mode needs N + M < 64) in one launch
 hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s);
 // test hook: 8 * cus workgroups each fill 64 KB of LDS with `bits` (pqp_tune_poison_lds)
@@ -140,10 +147,13 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     long long converge_chunk = 1 << 16;  // iterates decided per persistent converge launch
     int tiny_old = 0;    // one small problem on k_fixed_tiny / k_solve_wave (state copies) instead of k_fixed_one / k_solve_quintet
     int tiny_dense = 0;  // k_fixed_one / k_solve_quintet without the sparse update form
-    int iterate_v1 = 0;  // pqp_batch_iterate of N % 1024 == 0 on k_batch_iterate instead of k_batch_stream
+    int iterate_kind = 0;  // pqp_batch_iterate: 0 default (k_batch_resident at N 1024, k_batch_stream at other
+                           // multiples of 1024, k_batch_iterate otherwise), 1 k_batch_iterate, 2 k_batch_stream
     int matvec_lds = 0;  // setup mat-vecs on the LDS-staged k_matvec_rows instead of k_matvec_lane
     int gj_v1 = 0;  // batched Gauss_Jordan: 1 k_gj_blocked (a division per row and step), 2 k_gj_blocked2 (every column of every row per panel), 0 k_gj_blocked3
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
+    int tiny_fallback = 0;  // the host reads a tiny solve's device copies as if the pinned output were stale (tests)
+    long long tiny_chunk = 0;  // iterates per one-launch tiny solve launch (0: about 2^26 element updates)
     unsigned long long* tiny_trace = nullptr;  // k_solve_quintet per-wave clocks (24 words; N = 28, M <= 8 only)
 };
 extern Tuning g_tune;

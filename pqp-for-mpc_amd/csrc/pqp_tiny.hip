@@ -182,7 +182,10 @@ __device__ __forceinline__ int wave_max(int v) {
 __device__ __forceinline__ void write_out(const SolveArgs& A, SolveState* st, int tid, const float* Y, int N,
                                           const SolveState& s, int err) {
     for (int k = tid; k < N; k += 64) A.Y[k] = Y[k];
-    if (tid == 0) *st = s;
+    if (tid == 0) {
+        *st = s;
+        *reinterpret_cast<int*>(reinterpret_cast<char*>(st) + kTinyDevErr) = err;  // pqp_launch.h
+    }
     if (A.hout) {
         // host memory (fine-grained): system-scope write-through stores of the
         // data, their completion (vmcnt), then the launch's tag -- the host

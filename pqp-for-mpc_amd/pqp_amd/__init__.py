@@ -80,6 +80,7 @@ SIGNATURES = {
                                     C.c_int, _vp]),
     "pqp_batch_gauss_jordan": (C.c_int, [C.c_int, C.c_int, _vp, _vp, _vp]),
     "pqp_batch_convert_to_dual": (C.c_int, [C.c_int] * 3 + [_vp] * 8 + [_vp]),
+    "pqp_release_workspaces": (C.c_int, []),
     "pqp_batch_compute_fp": (C.c_int, [C.c_int] * 4 + [_vp] * 6 + [_vp]),
     "pqp_batch_compute_mp": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [_vp]),
     "pqp_batch_solve": (C.c_int, [C.c_int] * 3 + [_vp] * 9 + [C.c_int, C.c_longlong, C.c_longlong] + [_vp] * 4

@@ -1,4 +1,4 @@
-# Round 5 GPU steps, one script: bash scripts/gpu_r05.sh STEP [TAG]
+# GPU steps, one script: bash scripts/gpu_r06.sh STEP [TAG] (rounds 5-6)
 # Every GPU step runs under its own time limit and the steps are chained
 # with &&, so a fault or a timeout ends the call.
 set -o pipefail
@@ -46,9 +46,11 @@ hpmc)
   # k_solve_mid2's VALU counters on the bench's horizon workload, H = 2, 4, 5:
   # one rocprofv3 pass per H (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_BUSY_CYCLES,
   # GRBM_GUI_ACTIVE) beside a kernel trace of the same command
-  for H in 2 4 5; do
-    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/h$H -o pmc -- python3 scripts/horizon_pmc.py $H > $O/h$H.json 2> $O/h$H.err || { tail -5 $O/h$H.err; exit 1; }
-    cat $O/h$H.json
+  # (and the dense companion d112 / d140 of bench.py's horizon_dense leg)
+  for H in 2 4 5 d112 d140; do
+    D=$O/h$H; case $H in d*) D=$O/$H;; esac
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $D -o pmc -- python3 scripts/horizon_pmc.py $H > $D.json 2> $D.err || { tail -5 $D.err; exit 1; }
+    cat $D.json
   done
   ;;
 hab)

@@ -1,7 +1,8 @@
 """A/B of pqp_batch_iterate's kernels on the headline workload (configs[3]:
 4096 synthetic problems of n_dual 1024, 10 updates per launch), alternating
-in one process: k_batch_stream (the default for n_dual % 1024 == 0) against
-k_batch_iterate (rounds 1-4, pqp_tune iterate_v1).  Reports the
+in one process: k_batch_resident (the default at n_dual 1024, round 6),
+k_batch_stream (round 5, pqp_tune iterate_kind 2) and k_batch_iterate
+(rounds 1-4, iterate_kind 1).  Reports the
 launch time (HIP events) and TB/s of algorithmic bytes; checks that every
 variant gives the same bits."""
 from __future__ import annotations
@@ -24,8 +25,8 @@ def main(B: int = 4096, N: int = 1024, chunk: int = 10, rounds: int = 4, reps: i
     res = {}
     ref = None
     for _ in range(rounds):
-        for v in (0, 1):
-            old = pqp_amd.tune("iterate_v1", v)
+        for v in (0, 2, 1):
+            old = pqp_amd.tune("iterate_kind", v)
             try:
                 b.iterate(chunk)
                 torch.cuda.synchronize()
@@ -40,11 +41,12 @@ def main(B: int = 4096, N: int = 1024, chunk: int = 10, rounds: int = 4, reps: i
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / reps
             finally:
-                pqp_amd.tune("iterate_v1", old)
+                pqp_amd.tune("iterate_kind", old)
             r = res.setdefault(v, {"ms": [], "same_bits": True})
             r["ms"].append(round(ms, 3))
             r["same_bits"] &= same
-    out = {("k_batch_iterate" if v else "k_batch_stream"): {"ms_per_launch": r["ms"], "TBps_best": alg / min(r["ms"]) / 1e9,
+    names = {0: "k_batch_resident", 1: "k_batch_iterate", 2: "k_batch_stream"}
+    out = {names[v]: {"ms_per_launch": r["ms"], "TBps_best": alg / min(r["ms"]) / 1e9,
                                    "frac_of_8TBps_best": alg / min(r["ms"]) / 1e9 / 8.0, "same_bits": r["same_bits"]}
            for v, r in res.items()}
     print(json.dumps(out))

@@ -200,3 +200,108 @@ dist.destroy_process_group()
     assert len(lines) == 1, lines
     rec = json.loads(lines[0])
     assert rec["value"] == 5.0 and "error" in rec["rowshard"] and "rowshard_8" not in rec
+
+
+def _spread_worker(rank, world, port, out_dir):
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    bench = _bench()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=30))
+    dev = torch.device("cpu")
+    spread = bench.rank_spread(dist, dev, timed_s=1.0 + rank, kern_ms=10.0 * (rank + 1))
+    g = bench.rank_spread(dist, dev, gather_ms=3.0 - rank)["gather_ms"]
+    if rank == 0:
+        res = bench.headline(None, rank, world, 1024, 4096, 20, 5, 10, spread["timed_s"]["max"],
+                             spread["kern_ms"]["max"], 2, True, False, spread=spread)
+        res.setdefault("per_rank", {})["gather_ms"] = g
+        with open(os.path.join(out_dir, "r0.json"), "w") as f:
+            json.dump({"result": res, "summary": bench.summary(res)}, f)
+    dist.destroy_process_group()
+
+
+def test_per_rank_spread_at_world_size_2(tmp_path):
+    """at N > 1 the line carries each rank's timed region
+    and gather time as min / max over ranks (a slow or stuck rank is visible
+    in the first 8-GPU record); value uses the max."""
+    mp.spawn(_spread_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    rec = json.loads((tmp_path / "r0.json").read_text())
+    res, S = rec["result"], rec["summary"]
+    assert res["per_rank"]["timed_s"] == {"min": 1.0, "max": 2.0}
+    assert res["per_rank"]["kern_ms"] == {"min": 10.0, "max": 20.0}
+    assert res["per_rank"]["gather_ms"] == {"min": 2.0, "max": 3.0}
+    assert res["value"] == pytest.approx(4096 * 2 * 20 / 2.0)  # whole job over the slowest rank
+    assert S["per_rank_timed_s"] == {"min": 1.0, "max": 2.0} and S["gather_ms"] == {"min": 2.0, "max": 3.0}
+
+
+def test_summary_is_the_last_key(capsys):
+    """every leg's key numbers in a compact object at the
+    END of the line (the driver's record keeps the line's tail)."""
+    bench = _bench()
+    res = {"value": 1.5e6, "n_gpus": 1, "roofline": {"frac": 0.95, "avg_launch_ms": 22.5, "traffic": 1.5e11,
+                                                     "alg_bytes_per_launch": 1.72e11},
+           "batch_converge": {"infeasible": {"ms_per_iteration": 4.4, "frac_of_hbm_peak": 0.85}},
+           "horizon": {"H4": {"converge_ms": 28.0, "roofline": {"frac": 0.32, "alg_frac": 0.21}}},
+           "bundled": {"error": "RuntimeError: x"}}
+    em = bench.Emitter(0, res, leg_timeout_s=30)
+    em.leg("single_n1024", lambda: {"ms_per_solve": 3.6})
+    em.emit()
+    line = [ln for ln in capsys.readouterr().out.splitlines() if ln.strip()][0]
+    rec = json.loads(line)
+    assert list(rec)[-1] == "summary"
+    S = rec["summary"]
+    assert S["hbm_frac"] == 0.95 and S["traffic_ratio"] == pytest.approx(1.5e11 / 1.72e11, abs=1e-4)
+    assert S["batch_converge_infeasible"] == {"ms_per_iter": 4.4, "hbm_frac": 0.85}
+    assert S["batch_converge_feasible"] == {"ms_per_iter": None, "hbm_frac": None}
+    assert S["horizon_H4"] == {"ms": 28.0, "valu_frac": 0.32, "alg_frac": 0.21}
+    assert S["single_n1024_ms_per_1000"] == 3.6 and S["bundled_fixed1000_ms"] is None
+    assert S["legs_with_errors"] == ["bundled"]
+    assert len(line.split('"summary"')[1]) < 2500  # compact
+
+
+def test_kernel_hash_covers_included_headers(tmp_path, monkeypatch):
+    """a change to a header the kernels include (here
+    pqp_device.h, where gap_stop lives) changes the source hash, so the PMC
+    record measured before it is reported as stale, not as `traffic`."""
+    import shutil
+
+    bench = _bench()
+    src = ROOT / "pqp-for-mpc_amd"
+    (tmp_path / "pqp-for-mpc_amd").mkdir()
+    shutil.copytree(src / "csrc", tmp_path / "pqp-for-mpc_amd" / "csrc")
+    shutil.copy(src / "Makefile", tmp_path / "pqp-for-mpc_amd" / "Makefile")
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    h0 = bench.hot_kernel_hash()
+    assert h0 == bench.kernel_src_hash("hot-kernel", root=ROOT)
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(
+        {"n1024_b4096_c10": {"kernel_src_sha256": h0, "hbm_bytes_per_launch": 1.6e11, "source": "test"}}))
+    fresh = bench.headline(None, 0, 1, 1024, 4096, 20, 5, 10, 0.05, 47.0, 2, True, False)
+    assert fresh["roofline"]["traffic"] == 1.6e11
+    for h in bench.KERNEL_HEADERS:
+        f = tmp_path / "pqp-for-mpc_amd" / "csrc" / h
+        f.write_text(f.read_text() + "\n// edited\n")
+        assert bench.hot_kernel_hash() != h0
+        assert bench.kernel_src_hash("solve-mid2") != bench.kernel_src_hash("solve-mid2", root=ROOT)
+        stale = bench.headline(None, 0, 1, 1024, 4096, 20, 5, 10, 0.05, 47.0, 2, True, False)
+        assert stale["roofline"]["traffic"] is None and stale["roofline"]["traffic_source"].startswith("stale")
+        f.write_text(f.read_text().replace("\n// edited\n", ""))
+    assert bench.hot_kernel_hash() == h0
+
+
+def test_horizon_roofline_peak_and_alg_flops():
+    """VALU issue peak = one wave64 instruction per SIMD
+    every 2 clocks (1228.8 G/s), algorithmic flops 6N^2 + 4NM + 4M^2 per
+    feasible iterate against 78.6 T op/s."""
+    bench = _bench()
+    assert bench.VALU_PEAK_GWI == pytest.approx(1228.8)
+    assert bench.VALU_LANE_OPS == pytest.approx(78.6432e12)
+    N, M = 112, 28
+    assert bench.converge_alg_flops(1, N, M) == 6 * N * N + 4 * N * M + 4 * M * M
+    assert bench.converge_alg_flops(1, N, M, feasible=False) == 4 * N * N + 4 * N * M + 2 * M * M
+    r = bench.valu_roofline("no_such_record", "solve-mid2", 5128195, 0.028, N, M)
+    assert r["achieved"] is None and r["peak"] == pytest.approx(1228.8)
+    assert r["alg_TFLOPs"] == pytest.approx(5128195 * 90944 / 0.028 / 1e12)

@@ -293,27 +293,47 @@ def test_batch_kernels_vs_oracle_edge_sizes(gpu_lib, orc, N):
         assert_bitwise(up[j], want, f"update N={N} problem {j}")
 
 
-@pytest.mark.parametrize("N,B,ups", [(1024, 5, 23), (2048, 3, 11), (3072, 2, 4)])
-def test_stream_kernel_vs_oracle_and_iterate_v1(gpu_lib, orc, N, B, ups):
-    """k_batch_stream (pqp_batch_iterate where N is a multiple of 1024): ragged
-    batches, 4 to 23 updates in one launch, the first and last problem against
-    the oracle and every problem bit for bit against k_batch_iterate
-    (iterate_v1)."""
-    M = N // 2
-    b = gpu_lib.Batch(B, N).generate(seed=21, inst0=3, M=M)
-    b.iterate(ups)
-    stream = b.result().copy()
-    prev = gpu_lib.tune("iterate_v1", 1)
+def _iterate_kind(gpu_lib, b, ups, kind):
+    prev = gpu_lib.tune("iterate_kind", kind)
     try:
         b.reset()
         b.iterate(ups)
-        v1 = b.result().copy()
+        return b.result().copy()
     finally:
-        gpu_lib.tune("iterate_v1", prev)
-    assert_bitwise(stream, v1, f"stream vs iterate_v1 N={N}")
+        gpu_lib.tune("iterate_kind", prev)
+
+
+@pytest.mark.parametrize("N,B,ups", [(1024, 5, 23), (1024, 3, 1), (1024, 2, 2), (1024, 3, 3), (2048, 3, 11),
+                                     (3072, 2, 4)])
+def test_stream_kernels_vs_oracle_and_iterate(gpu_lib, orc, N, B, ups):
+    """pqp_batch_iterate where N is a multiple of 1024 -- k_batch_resident
+    (N = 1024: Qd's first blocks in LDS / L2 across the launch's iterations,
+    incl. launches of 1, 2 and 3 updates, where the LDS copy is written and
+    read once or not at all) and k_batch_stream: ragged batches, the first and
+    last problem against the oracle and every problem bit for bit against
+    k_batch_iterate (iterate_kind 1) and k_batch_stream (iterate_kind 2)."""
+    M = N // 2
+    b = gpu_lib.Batch(B, N).generate(seed=21, inst0=3, M=M)
+    b.iterate(ups)
+    first = b.result().copy()
+    assert_bitwise(first, _iterate_kind(gpu_lib, b, ups, 1), f"default vs k_batch_iterate N={N}")
+    assert_bitwise(first, _iterate_kind(gpu_lib, b, ups, 2), f"default vs k_batch_stream N={N}")
     for j in (0, B - 1):
         P = orc.synth_problem(21, 3 + j, N, M, with_qp=False)
-        assert_bitwise(stream[j], orc.iterate(P["Qd"], P["Fd"], N, ups), f"N={N} problem {j}")
+        assert_bitwise(first[j], orc.iterate(P["Qd"], P["Fd"], N, ups), f"N={N} problem {j}")
+
+
+def test_resident_kernel_chained_launches(gpu_lib, orc):
+    """Updates beyond one launch (pqp_batch_iterate splits runs into launches
+    of 256): every launch starts from the previous one's Y and refills its LDS
+    copy of Qd's first blocks."""
+    N, B, ups = 1024, 2, 300
+    b = gpu_lib.Batch(B, N).generate(seed=4, inst0=9, M=N // 2)
+    b.iterate(ups)
+    res = b.result().copy()
+    assert_bitwise(res, _iterate_kind(gpu_lib, b, ups, 1), "resident vs k_batch_iterate, 300 updates")
+    P = orc.synth_problem(4, 9, N, N // 2, with_qp=False)
+    assert_bitwise(res[0], orc.iterate(P["Qd"], P["Fd"], N, ups), "300 updates vs oracle")
 
 
 def test_batch_load_bundled_fixed_999(gpu_lib, golden_bundled):

@@ -172,3 +172,61 @@ def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled):
     # every solve's pinned output carried its own launch's tag (the device-copy
     # fallback never ran)
     assert gpu_lib.tune_get("tiny_stale") == stale0
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 8, 100])
+def test_bundled_resumed_over_launches(gpu_lib, golden_bundled, chunk):
+    """a one-launch tiny solve is bounded to a chunk of iterates per
+    launch and resumes from the device state (fresh = 0) in the next launch.
+    With tiny chunks (the tiny_chunk knob) the bundled solves still stop at h =
+    313 with the reference's Y*, U*, Jp, Jd, and the fixed solves give the
+    reference's Y after 999 and after 99 updates."""
+    g = golden_bundled
+    with tuned(gpu_lib, {"tiny_chunk": chunk}), gpu_lib.Problem(bundled_problem(g)) as prob:
+        r = prob.solve(max_updates=CAP)
+        assert r["converged"] and r["h"] == 313
+        assert_bitwise(r["Y"], g["Ystar"], f"chunk {chunk}: Y*")
+        assert_bitwise(r["U"], g["Ustar"], f"chunk {chunk}: U*")
+        assert np.float32(r["Jp"]) == g["iter_Jp"][-1] and np.float32(r["Jd"]) == g["iter_Jd"][-1]
+        c = prob.solve(max_updates=16)
+        assert not c["converged"] and c["h"] == 17
+        f = prob.solve(gpu_lib.MODE_FIXED, num_iter=1000)
+        assert f["h"] == 1000
+        assert_bitwise(f["Y"], g["Y_fixed999"], f"chunk {chunk}: fixed-999 Y")
+        f = prob.solve(gpu_lib.MODE_FIXED, num_iter=100)
+        assert f["h"] == 100
+        assert_bitwise(f["Y"], g["Y_h100"], f"chunk {chunk}: Y after 99 updates")
+
+
+def test_device_copy_fallback_is_exact_and_reports_errors(gpu_lib, golden_bundled):
+    """the path a solve takes when its pinned output lacks the
+    launch's tag (forced by the tiny_fallback knob) reads Y, U, the state AND
+    the error word from the device: exact results, and an expired wait still
+    raises instead of relaunching forever."""
+    g = golden_bundled
+    stale0 = gpu_lib.tune_get("tiny_stale")
+    with tuned(gpu_lib, {"tiny_fallback": 1}), gpu_lib.Problem(bundled_problem(g)) as prob:
+        r = prob.solve(max_updates=CAP)
+        assert r["h"] == 313
+        assert_bitwise(r["Y"], g["Ystar"], "fallback: Y*")
+        assert_bitwise(r["U"], g["Ustar"], "fallback: U*")
+        f = prob.solve(gpu_lib.MODE_FIXED, num_iter=1000)
+        assert_bitwise(f["Y"], g["Y_fixed999"], "fallback: fixed-999 Y")
+        with tuned(gpu_lib, {"tiny_stall": 1}):
+            with pytest.raises(gpu_lib.PQPError, match="hand-off wait expired"):
+                prob.solve(max_updates=CAP)
+        r = prob.solve(max_updates=CAP)
+        assert r["h"] == 313
+    assert gpu_lib.tune_get("tiny_stale") > stale0
+
+
+def test_tiny_trace_buffer_too_small_is_rejected(gpu_lib):
+    """the quintet's timeline writes 24 words; a shorter buffer is
+    an argument error, not an out-of-bounds device write."""
+    import torch
+
+    buf = torch.zeros(24, dtype=torch.int64, device="cuda")
+    with pytest.raises(gpu_lib.PQPError):
+        gpu_lib._check(gpu_lib.lib().pqp_tune_trace(b"tiny", gpu_lib.C.c_void_p(buf.data_ptr()), 8))
+    gpu_lib._check(gpu_lib.lib().pqp_tune_trace(b"tiny", gpu_lib.C.c_void_p(buf.data_ptr()), 24))
+    gpu_lib._check(gpu_lib.lib().pqp_tune_trace(b"tiny", None, 0))
