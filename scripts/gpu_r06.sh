@@ -66,6 +66,22 @@ gj)
   timeout -k 10 300 python -u scripts/gj_timing.py 512 4096 > $O/gj_timing.json 2>&1 && cat $O/gj_timing.json &&
   timeout -k 10 300 python -u scripts/gj_timing.py 256 4096 > $O/gj_timing_256.json 2>&1 && cat $O/gj_timing_256.json
   ;;
+bcab)
+  # batch_converge (F2) on the round-4, round-5 and current libraries, same box,
+  # alternating (is 0.848 / 0.853 box variance or a
+  # regression?).  ab/r04 and ab/r05 hold each round's bench.py, bc_leg.py and
+  # built pqp_amd (made here from git worktrees of 50a0bfe / a31e5a0)
+  for r in 1 2; do
+    for t in ab/r04 ab/r05 .; do
+      l=$(basename $t); [ "$l" = . ] && l=r06
+      timeout -k 10 240 python -u $t/scripts/bc_leg.py > $O/bc_${l}_$r.json 2> $O/bc_${l}_$r.err || { tail -5 $O/bc_${l}_$r.err; exit 1; }
+      python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], [(c, round(d[c]['ms_per_iteration'],3), round(d[c]['frac_of_hbm_peak'],4)) for c in ('infeasible','feasible')])" $O/bc_${l}_$r.json $l $r
+    done
+  done
+  ;;
+doorbell)
+  timeout -k 10 120 ./scripts/probes/doorbell_probe 2000 > $O/doorbell.json 2>&1; rc=$?; cat $O/doorbell.json; exit $rc
+  ;;
 *)
   echo "unknown step $STEP"; exit 2;;
 esac
