@@ -72,9 +72,6 @@ extern "C" {
  *                          above n_dual 768; below, the fewest rounds of
  *                          resident problems, weighted +10 % per step); 3, 4
  *                          or 5 forces one
- *   mid2_fat [0]           k_solve_mid2 workgroups of <= 6 waves on the
- *                          128-VGPR build (default: the 80-VGPR build, 6 waves
- *                          per SIMD, as many problems per CU as LDS allows)
  *   mid2_dense [0]         k_solve_mid2 sums every k of each update row and
  *                          Y'Qd row (default: only the band of k where the
  *                          wave's rows hold a nonzero, while Y is finite)
@@ -100,11 +97,6 @@ extern "C" {
  *                          across a launch's iterations; other multiples of
  *                          1024: k_batch_stream; else k_batch_iterate),
  *                          1 k_batch_iterate, 2 k_batch_stream
- *   matvec_lds [0]         convertToDual's mat-vec on the LDS-staged
- *                          k_matvec_rows instead of k_matvec_lane
- *   gj_v1 [0]              batched Gauss_Jordan (n <= 1024): 0 k_gj_blocked3
- *                          (only the columns that can still change an output),
- *                          1 k_gj_blocked, 2 k_gj_blocked2 (every column)
  *  Paths and failure tests:
  *   persist_off [0]        fixed mode of n_dual <= 1024 through the graph-replayed
  *                          relay instead of the persistent launch

@@ -2050,7 +2050,6 @@ const KnobRef* find_knob(const char* key) {
         {"mid_v1", &g_tune.mid_v1, nullptr, nullptr},
         {"mid2_pair", &g_tune.mid2_pair, nullptr, nullptr},
         {"mid2_min_n", &g_tune.mid2_min_n, nullptr, nullptr},
-        {"mid2_fat", &g_tune.mid2_fat, nullptr, nullptr},
         {"mid2_dense", &g_tune.mid2_dense, nullptr, nullptr},
         {"single_occ", &g_tune.single_occ, nullptr, nullptr},
         {"matmul_pk_off", &g_tune.matmul_pk_off, nullptr, nullptr},
@@ -2064,8 +2063,6 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_fallback", &g_tune.tiny_fallback, nullptr, nullptr},
         {"tiny_chunk", nullptr, nullptr, &g_tune.tiny_chunk},
         {"iterate_kind", &g_tune.iterate_kind, nullptr, nullptr},
-        {"matvec_lds", &g_tune.matvec_lds, nullptr, nullptr},
-        {"gj_v1", &g_tune.gj_v1, nullptr, nullptr},
     };
     for (const KnobRef& k : knobs)
         if (std::strcmp(k.key, key) == 0) return &k;

@@ -4563,7 +4563,7 @@ static hipError_t launch_mid_grid(int B, const SolveArgs& a0, SolveState* st, hi
             // workgroups of <= 6 waves: the build held to 80 VGPRs (6 waves per
             // SIMD), so as many problems share a CU as LDS allows (n_dual 56: 6
             // instead of 4, 84: 4 instead of 2)
-            const bool lean = nt <= 384 && !g_tune.mid2_fat;
+            const bool lean = nt <= 384;  // (the 128-VGPR build here: H = 2 / 3 13.1 / 37.2 vs 11.2 / 30.2 ms, profiles/r04)
             if (lean && pair) hipLaunchKernelGGL((k_solve_mid2<384, true, 6>), dim3(B), dim3(nt), lds, s, a, st);
             else if (lean && a.N > 64) hipLaunchKernelGGL((k_solve_mid2<384, false, 6>), dim3(B), dim3(nt), lds, s, a, st);
             else if (lean) hipLaunchKernelGGL((k_solve_mid2<384, false, 6, false>), dim3(B), dim3(nt), lds, s, a, st);
@@ -4762,7 +4762,9 @@ hipError_t launch_matmul_seq_b(int B, float* out, const float* A, int tA, const 
             continue;
         }
         if (c == 1 && !tA && a >= 64 && b >= 32 && !g_tune.matmul_tiled_off) {
-            if (b % 4 == 0 && sA % 4 == 0 && aligned16(A) && !g_tune.matvec_lds)
+            // (the LDS-staged k_matvec_rows only where the rows are not 16-byte
+            // aligned: 2.31 vs 2.04-2.12 ms per convertToDual call, profiles/r05)
+            if (b % 4 == 0 && sA % 4 == 0 && aligned16(A))
                 hipLaunchKernelGGL(k_matvec_lane, dim3(cdiv(a, 64), nb), dim3(64), 0, s, out + b0 * sO,
                                    A + b0 * sA, Bm + b0 * sB, a, b, sA, sB, sO);
             else
@@ -4899,215 +4901,10 @@ __device__ __forceinline__ float gj_any_col(const float (&v)[4 * C], int col) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), (col & 255) >> 2));
 }
 
-template <int C, int NB>
-__global__ void __launch_bounds__(256) k_gj_blocked(const float* __restrict__ A, float* __restrict__ aug,
-                                                    float* __restrict__ res, int n) {
-    constexpr int W = 256 * C;  // padded row of the augmented matrix
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* P = lds;             // [NB][W] pivot rows at their step
-    float* Pd = lds + NB * W;   // [NB] their diagonals
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    {
-        const size_t b = blockIdx.x;
-        A += b * n * n;
-        res += b * n * n;
-        aug += b * (size_t)n * W;
-    }
-    // the one bubble pass on column 0 (:280-289) as a row order, then [A | I]
-    // in that order (:262-276), zero-padded to W columns
-    int* perm = reinterpret_cast<int*>(P);
-    float* col0 = P + n;
-    for (int r = tid; r < n; r += 256) col0[r] = A[(size_t)r * n];
-    __syncthreads();
-    if (tid == 0) {
-        for (int r = 0; r < n; ++r) perm[r] = r;
-        for (int r = n - 1; r > 0; --r)
-            if (col0[perm[r - 1]] < col0[perm[r]]) {
-                const int t = perm[r];
-                perm[r] = perm[r - 1];
-                perm[r - 1] = t;
-            }
-    }
-    __syncthreads();
-    for (int r = wv; r < n; r += 4) {
-        const int src = perm[r];
-        float v[4 * C];
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int k = 256 * c + 4 * lane + e;
-                v[4 * c + e] = k < n ? A[(size_t)src * n + k] : (k == n + src ? 1.0f : 0.0f);
-            }
-        gj_store<C>(aug + (size_t)r * W, lane, v);
-    }
-    __syncthreads();
-    for (int p0 = 0; p0 < n; p0 += NB) {
-        const int ns = n - p0 < NB ? n - p0 : NB;
-        if (wv == 0) {  // 1. the pivot rows at their step
-            for (int s = 0; s < ns; ++s) {
-                float v[4 * C];
-                gj_load<C>(aug + (size_t)(p0 + s) * W, lane, v);
-                gj_steps_any<C, NB>(v, P, Pd, W, p0, s, -1, lane);
-                gj_store<C>(P + (size_t)s * W, lane, v);
-                const float d = gj_any_col<C>(v, p0 + s);
-                if (lane == 0) Pd[s] = d;
-            }
-        }
-        __syncthreads();
-        const bool last = p0 + NB >= n;
-        for (int j = wv; j < n; j += 4) {  // 2. every row takes the panel's steps
-            float v[4 * C];
-            gj_load<C>(aug + (size_t)j * W, lane, v);
-            gj_steps_any<C, NB>(v, P, Pd, W, p0, ns, j, lane);
-            if (!last) {
-                gj_store<C>(aug + (size_t)j * W, lane, v);
-            } else {  // temp = m_jj; the row / temp; its right half is res's row j
-                const float d = gj_any_col<C>(v, j);
-#pragma unroll
-                for (int c = 0; c < C; ++c)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int k = 256 * c + 4 * lane + e;
-                        if (k >= n && k < 2 * n) res[(size_t)j * n + (k - n)] = v[4 * c + e] / d;
-                    }
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// k_gj_blocked2: the same panels and the same per-element operations, with
-// each row's multipliers of a panel formed lane-parallel first.  Step p0 + s's
-// multiplier of row j, t = m_j,p0+s / Pd[s], needs only the panel's NB
-// columns of row j as the earlier steps of the panel leave them: lane l of a
-// wave takes row g + l of its group of 64, walks those NB columns through
-// the panel's steps (m -= P[s'][p0+s] * t_s', the reference's own operation
-// on that element, in order) and divides -- one vector division per step for
-// 64 rows instead of one per row (the divisions were ~25 % of the row
-// updates' instructions).  The rows of the group are then updated one at a
-// time as before, each step's t broadcast from its lane by v_readlane.
-template <int C, int NB>
-__global__ void __launch_bounds__(256) k_gj_blocked2(const float* __restrict__ A, float* __restrict__ aug,
-                                                     float* __restrict__ res, int n) {
-    constexpr int W = 256 * C;  // padded row of the augmented matrix
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* P = lds;             // [NB][W] pivot rows at their step
-    float* Pd = lds + NB * W;   // [NB] their diagonals
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    {
-        const size_t b = blockIdx.x;
-        A += b * n * n;
-        res += b * n * n;
-        aug += b * (size_t)n * W;
-    }
-    // the one bubble pass on column 0 (:280-289) as a row order, then [A | I]
-    // in that order (:262-276), zero-padded to W columns
-    int* perm = reinterpret_cast<int*>(P);
-    float* col0 = P + n;
-    for (int r = tid; r < n; r += 256) col0[r] = A[(size_t)r * n];
-    __syncthreads();
-    if (tid == 0) {
-        for (int r = 0; r < n; ++r) perm[r] = r;
-        for (int r = n - 1; r > 0; --r)
-            if (col0[perm[r - 1]] < col0[perm[r]]) {
-                const int t = perm[r];
-                perm[r] = perm[r - 1];
-                perm[r - 1] = t;
-            }
-    }
-    __syncthreads();
-    for (int r = wv; r < n; r += 4) {
-        const int src = perm[r];
-        float v[4 * C];
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int k = 256 * c + 4 * lane + e;
-                v[4 * c + e] = k < n ? A[(size_t)src * n + k] : (k == n + src ? 1.0f : 0.0f);
-            }
-        gj_store<C>(aug + (size_t)r * W, lane, v);
-    }
-    __syncthreads();
-    for (int p0 = 0; p0 < n; p0 += NB) {
-        const int ns = n - p0 < NB ? n - p0 : NB;
-        if (wv == 0) {  // 1. the pivot rows at their step
-            for (int s = 0; s < ns; ++s) {
-                float v[4 * C];
-                gj_load<C>(aug + (size_t)(p0 + s) * W, lane, v);
-                gj_steps_any<C, NB>(v, P, Pd, W, p0, s, -1, lane);
-                gj_store<C>(P + (size_t)s * W, lane, v);
-                const float d = gj_any_col<C>(v, p0 + s);
-                if (lane == 0) Pd[s] = d;
-            }
-        }
-        __syncthreads();
-        const bool last = p0 + NB >= n;
-        for (int g = 64 * wv; g < n; g += 256) {
-            // 2a. row g + lane's multipliers of the panel's steps
-            const int jl = g + lane;
-            float t[NB];
-            {
-                float m[NB];
-#pragma unroll
-                for (int q = 0; q < NB; q += 4) {
-                    // the pivot columns p0 .. p0 + NB - 1 (p0 % NB == 0: 16-byte aligned; past n: zero padding)
-                    const sf4 x = jl < n ? *reinterpret_cast<const sf4*>(aug + (size_t)jl * W + p0 + q) : sf4{0, 0, 0, 0};
-                    m[q] = x.x;
-                    m[q + 1] = x.y;
-                    m[q + 2] = x.z;
-                    m[q + 3] = x.w;
-                }
-#pragma unroll
-                for (int s = 0; s < NB; ++s) {
-                    float x = m[s];
-#pragma unroll
-                    for (int s2 = 0; s2 < s; ++s2)
-                        if (p0 + s2 != jl) x -= P[(size_t)s2 * W + p0 + s] * t[s2];  // (:301) on column p0 + s
-                    t[s] = x / Pd[s];  // temp (:298)
-                }
-            }
-            // 2b. each row of the group takes the panel's steps (its own skipped)
-            const int rend = n - g < 64 ? n - g : 64;
-            for (int r = 0; r < rend; ++r) {
-                const int j = g + r;
-                float v[4 * C];
-                gj_load<C>(aug + (size_t)j * W, lane, v);
-#pragma unroll
-                for (int s = 0; s < NB; ++s) {
-                    if (s < ns && p0 + s != j) {
-                        const float ts = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[s]), r));
-                        const float* prow = P + (size_t)s * W;
-#pragma unroll
-                        for (int c = 0; c < C; ++c) {
-                            const sf4 q = *reinterpret_cast<const sf4*>(prow + 256 * c + 4 * lane);
-                            // (packed multiply / subtract pairs measured the same:
-                            // 0.1136 vs 0.1139 s, profiles/r05/gj_timing_r05v.json --
-                            // the panels are bound by the matrix's HBM traffic, one read
-                            // and write per 16 pivots, ~4.6 TB/s)
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) v[4 * c + e] -= q[e] * ts;  // (:301)
-                        }
-                    }
-                }
-                if (!last) {
-                    gj_store<C>(aug + (size_t)j * W, lane, v);
-                } else {  // temp = m_jj; the row / temp; its right half is res's row j
-                    const float d = gj_any_col<C>(v, j);
-#pragma unroll
-                    for (int c = 0; c < C; ++c)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int k = 256 * c + 4 * lane + e;
-                            if (k >= n && k < 2 * n) res[(size_t)j * n + (k - n)] = v[4 * c + e] / d;
-                        }
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
+// (k_gj_blocked -- one row's multipliers at a time -- and k_gj_blocked2 -- the
+// multipliers lane-parallel, every column -- were the forms before
+// k_gj_blocked3; measured slower and removed in round 6: docs/DESIGN_HISTORY.md
+// section 4b / 4d, profiles/r05/gj_timing_*.json)
 
 // k_gj_blocked3's row update: rows j_i = g + r + i (i < RR) take the panel's
 // steps on their own columns (left [llo, n) and the diagonal, right [n, rhi):
@@ -5346,13 +5143,10 @@ template <int C>
 static void launch_gj_blocked_c(int B, const float* A, float* aug, float* res, int n, hipStream_t s) {
     constexpr int NB = C <= 4 ? 16 : 8;
     const size_t lds = sizeof(float) * ((size_t)NB * 256 * C + NB);
-    // k_gj_blocked2 (multipliers lane-parallel): 4096 n = 512 inverses 0.127-0.130
-    // -> 0.114 s, n = 256 0.018 -> 0.016 s (profiles/r05/gj_timing_*.json)
-    if (g_tune.gj_v1 == 1) hipLaunchKernelGGL((k_gj_blocked<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
-    else if (g_tune.gj_v1 == 2) hipLaunchKernelGGL((k_gj_blocked2<C, NB>), dim3(B), dim3(256), lds, s, A, aug, res, n);
-    else
-        hipLaunchKernelGGL((k_gj_blocked3<C, NB>), dim3(B), dim3(256), lds + sizeof(int) * ((size_t)n + 1), s, A, aug,
-                           res, n);
+    // k_gj_blocked3: 4096 n = 512 inverses in 0.097 s (k_gj_blocked 0.127, its
+    // lane-parallel-multiplier form 0.114: profiles/r05/gj_timing_*.json)
+    hipLaunchKernelGGL((k_gj_blocked3<C, NB>), dim3(B), dim3(256), lds + sizeof(int) * ((size_t)n + 1), s, A, aug,
+                       res, n);
 }
 static hipError_t launch_gj_blocked(int B, const float* A, float* aug, float* res, int n, hipStream_t s) {
     switch (gj_blocked_c(n)) {

@@ -136,7 +136,6 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int mid2_pair = 0;  // k_solve_mid2's update rows: 0 by shape, 1 lane sides (v_med3_f32), 2 one lane per row
     int single_occ = 0;  // k_solve_single (wide loads) workgroups per CU by register cap: 0 by shape and batch (3 above n_dual 768), 3 / 4 / 5 forced
     int mid2_dense = 0;  // k_solve_mid2 sums every k (default: each row group's nonzero band while Y is finite)
-    int mid2_fat = 0;  // k_solve_mid2 workgroups of <= 6 waves on the 128-VGPR build (default: 80 VGPRs, 6 waves per SIMD)
     int mid2_min_n = 48;  // smallest N path 3 runs on k_solve_mid2 (below it k_solve_mid)
     int mid_v1 = 0;  // path 3 on k_solve_mid (terminate() after the update) instead of the pipelined k_solve_mid2
     int pipe_variant = 0;  // k_solve_pipe build: 0 (128 x 96 Gp tiles, 16 update loads per lane in flight, 2 WGs/CU), 3 (two 64 x 64 tiles in flight)
@@ -149,8 +148,6 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int tiny_dense = 0;  // k_fixed_one / k_solve_quintet without the sparse update form
     int iterate_kind = 0;  // pqp_batch_iterate: 0 default (k_batch_resident at N 1024, k_batch_stream at other
                            // multiples of 1024, k_batch_iterate otherwise), 1 k_batch_iterate, 2 k_batch_stream
-    int matvec_lds = 0;  // setup mat-vecs on the LDS-staged k_matvec_rows instead of k_matvec_lane
-    int gj_v1 = 0;  // batched Gauss_Jordan: 1 k_gj_blocked (a division per row and step), 2 k_gj_blocked2 (every column of every row per panel), 0 k_gj_blocked3
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
     int tiny_fallback = 0;  // the host reads a tiny solve's device copies as if the pinned output were stale (tests)
     long long tiny_chunk = 0;  // iterates per one-launch tiny solve launch (0: about 2^26 element updates)

@@ -1,8 +1,8 @@
 """Batched Gauss_Jordan timing (PQP_CPU.c:251-326): B
 matrices of n x n (the synthetic problems' setup: Qp = inverse(Qp_inv)),
-k_gj_blocked3 (default: only the columns that can still change an output),
-k_gj_blocked2 (gj_v1 = 2), k_gj_blocked (gj_v1 = 1) and the one-pivot-per-sweep
-kernel, bit-identical outputs.
+k_gj_blocked3 (default: only the columns that can still change an output) and
+the one-pivot-per-sweep kernel, bit-identical outputs (k_gj_blocked /
+k_gj_blocked2 were removed in round 6; their numbers are in profiles/r05).
 Usage: python scripts/gj_timing.py [n B]"""
 from __future__ import annotations
 
@@ -30,10 +30,8 @@ def main(n=512, B=4096):
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     out = {"n": n, "matrices": B}
     res = {}
-    for name, off, v1 in (("blocked3", 0, 0), ("blocked2", 0, 2), ("blocked_v1", 0, 1), ("per_sweep", 1, 0),
-                          ("blocked3_again", 0, 0)):
+    for name, off in (("blocked3", 0), ("per_sweep", 1), ("blocked3_again", 0)):
         prev = L.pqp_tune_gj_blocked(off)
-        prev_v1 = pqp_amd.tune("gj_v1", v1)
         ts = []
         for _ in range(2 if name == "per_sweep" else 3):
             torch.cuda.synchronize()
@@ -42,7 +40,6 @@ def main(n=512, B=4096):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         L.pqp_tune_gj_blocked(prev)
-        pqp_amd.tune("gj_v1", prev_v1)
         res[name] = R.clone()
         t = min(ts)
         # the reference's operations: n pivots x (n-1) rows x 2n columns of one
@@ -50,8 +47,8 @@ def main(n=512, B=4096):
         ops = 2.0 * n * (n - 1) * 2 * n + 2.0 * n * n
         out[name] = {"s": t, "matrices_per_s": B / t, "Gops": ops * B / t / 1e9}
     out["bit_identical"] = all(torch.equal(res[k].view(torch.int32), res["per_sweep"].view(torch.int32))
-                               for k in ("blocked3", "blocked2", "blocked_v1"))
-    out["speedup_vs_blocked2"] = out["blocked2"]["s"] / out["blocked3"]["s"]
+                               for k in ("blocked3", "blocked3_again"))
+    out["speedup_vs_per_sweep"] = out["per_sweep"]["s"] / out["blocked3"]["s"]
     print(json.dumps(out), flush=True)
 
 

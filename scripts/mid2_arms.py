@@ -17,7 +17,6 @@ sys.path.insert(0, str(ROOT / "scripts"))
 
 ARMS = {
     "def": {},
-    "fat": {"mid2_fat": 1},
     "pair_lean": {"mid2_pair": 1},
     "row_lean": {"mid2_pair": 2},
     "v1": {"mid_v1": 1},

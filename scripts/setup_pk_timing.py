@@ -27,9 +27,9 @@ def main(N=1024, M=512, B=64, reps=3):
     pb.Qp_inv.copy_(torch.from_numpy(dense_qinv(3, M)).cuda().expand(B, -1))
     flops = B * (2.0 * N * M * M + 2.0 * N * N * M)
     out = {"n_dual": N, "m": M, "problems": B}
-    res, times = {}, {"pk": [], "tiled": [], "pk_matvec_lds": []}
+    res, times = {}, {"pk": [], "tiled": []}
     for r in range(reps):
-        for name, knob, off in (("pk", "matmul_pk_off", 0), ("tiled", "matmul_pk_off", 1), ("pk_matvec_lds", "matvec_lds", 1)):
+        for name, knob, off in (("pk", "matmul_pk_off", 0), ("tiled", "matmul_pk_off", 1)):
             prev = pqp_amd.tune(knob, off)
             try:
                 pb.convert_to_dual()  # warm
@@ -44,8 +44,7 @@ def main(N=1024, M=512, B=64, reps=3):
     for name, ts in times.items():
         dt = sorted(ts)[len(ts) // 2]
         out[name] = {"ms": dt * 1e3, "gemm_TFLOPs": flops / dt / 1e12, "all_ms": [t * 1e3 for t in ts]}
-    out["bit_identical"] = bool(torch.equal(res["pk"].view(torch.int32), res["tiled"].view(torch.int32))
-                                and torch.equal(res["pk"].view(torch.int32), res["pk_matvec_lds"].view(torch.int32)))
+    out["bit_identical"] = bool(torch.equal(res["pk"].view(torch.int32), res["tiled"].view(torch.int32)))
     out["speedup"] = out["tiled"]["ms"] / out["pk"]["ms"]
     print(json.dumps(out), flush=True)
 

@@ -222,7 +222,7 @@ def test_tuning_knobs_roundtrip():
 
     L = pqp_amd.lib()
     for key in ("persist_off", "lean_min_n", "batch_opts", "converge_chunk", "wide_min_n", "pipe_off",
-                "pipe_variant", "pipe_force", "mid_v1", "matmul_pk_off"):
+                "pipe_variant", "pipe_force", "mid_v1", "matmul_pk_off", "iterate_kind", "tiny_chunk", "tiny_fallback"):
         old = pqp_amd.tune_get(key)
         assert pqp_amd.tune(key, old + 3) == old
         assert pqp_amd.tune_get(key) == old + 3
@@ -230,8 +230,9 @@ def test_tuning_knobs_roundtrip():
     assert pqp_amd.tune("relay_spin_max", 2**40) == 1 << 20 and pqp_amd.tune_get("relay_spin_max") == 1 << 30
     pqp_amd.tune("relay_spin_max", 0)
     assert pqp_amd.tune_get("relay_spin_max") == 1 << 20
-    for gone in ("no_such_knob", "split_kind", "split_u", "fixed_tiny_old", "single_occ4", "wide_flags", "mid_split"):
-        with pytest.raises(pqp_amd.PQPError):  # round 4 removed the measured-slower arms behind these
+    for gone in ("no_such_knob", "split_kind", "split_u", "fixed_tiny_old", "single_occ4", "wide_flags", "mid_split",
+                 "iterate_v1", "gj_v1", "mid2_fat", "matvec_lds"):
+        with pytest.raises(pqp_amd.PQPError):  # rounds 4 and 6 removed the measured-slower arms behind these
             pqp_amd.tune(gone, 1)
     prev = L.pqp_tune_set_variant((3 << 17) | 0x200)
     assert pqp_amd.tune_get("split_lw") == 32
