@@ -9,6 +9,9 @@
 //                   check the tag -- the per-solve overhead of today's path
 //   launch_spin   : the same launch, the host spinning on the pinned tag
 //                   instead of synchronising the stream
+//   launch_query  : the same launch, the host polling hipStreamQuery until the
+//                   stream is idle (the completion signal: the same ordering
+//                   guarantee as a synchronisation), then reading the tag
 //   doorbell      : ONE kernel launched once; its wave polls a doorbell word
 //                   in pinned host memory (vector system-scope loads), answers
 //                   each ring with a tag store to pinned memory; the host rings
@@ -88,7 +91,7 @@ int main(int argc, char** argv) {
     for (int i = 1; i <= 50; ++i) hipLaunchKernelGGL(k_tag, dim3(1), dim3(64), 0, s, dout, i);
     CK(hipStreamSynchronize(s));
 
-    std::vector<double> t_sync, t_spin, t_bell;
+    std::vector<double> t_sync, t_spin, t_bell, t_query;
     for (int i = 1; i <= R; ++i) {
         const auto a = clk::now();
         hipLaunchKernelGGL(k_tag, dim3(1), dim3(64), 0, s, dout, 100000 + i);
@@ -106,6 +109,16 @@ int main(int argc, char** argv) {
         t_spin.push_back(us(a, b));
     }
     CK(hipStreamSynchronize(s));
+    for (int i = 1; i <= R; ++i) {
+        const auto a = clk::now();
+        hipLaunchKernelGGL(k_tag, dim3(1), dim3(64), 0, s, dout, 300000 + i);
+        hipError_t q;
+        while ((q = hipStreamQuery(s)) == hipErrorNotReady) {}
+        CK(q);
+        const auto b = clk::now();
+        if (*vout != 300000 + i) { fprintf(stderr, "launch_query: tag missing\n"); return 1; }
+        t_query.push_back(us(a, b));
+    }
 
     *vbell = 0;
     *vout = 0;
@@ -124,9 +137,9 @@ int main(int argc, char** argv) {
         t_bell.push_back(us(a, b));
     }
     CK(hipStreamSynchronize(s));
-    printf("{\"requests\": %d, \"launch_sync_us\": %.2f, \"launch_spin_us\": %.2f, \"doorbell_us\": %.2f, "
+    printf("{\"requests\": %d, \"launch_query_us\": %.2f, \"launch_sync_us\": %.2f, \"launch_spin_us\": %.2f, \"doorbell_us\": %.2f, "
            "\"doorbell_ok\": %s, \"launch_sync_p90_us\": %.2f, \"doorbell_p90_us\": %.2f}\n",
-           R, median(t_sync), median(t_spin), t_bell.empty() ? -1.0 : median(t_bell), ok ? "true" : "false",
+           R, median(t_query), median(t_sync), median(t_spin), t_bell.empty() ? -1.0 : median(t_bell), ok ? "true" : "false",
            [&] { auto v = t_sync; std::sort(v.begin(), v.end()); return v[v.size() * 9 / 10]; }(),
            [&] { auto v = t_bell; std::sort(v.begin(), v.end()); return v.empty() ? -1.0 : v[v.size() * 9 / 10]; }());
     return ok ? 0 : 1;
