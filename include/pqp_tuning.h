@@ -98,7 +98,8 @@ extern "C" {
  *                          k_batch_resident, Qd's first blocks kept on the CU
  *                          across a launch's iterations; other multiples of
  *                          1024: k_batch_stream; else k_batch_iterate),
- *                          1 k_batch_iterate, 2 k_batch_stream
+ *                          1 k_batch_iterate, 2 k_batch_stream, 3 k_batch_resident
+ *                          with two more blocks in registers (n_dual 1024)
  *  Paths and failure tests:
  *   persist_off [0]        fixed mode of n_dual <= 1024 through the graph-replayed
  *                          relay instead of the persistent launch

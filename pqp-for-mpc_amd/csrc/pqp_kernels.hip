@@ -300,24 +300,31 @@ __global__ void __launch_bounds__(256) k_batch_stream(const float* __restrict__ 
 // ---------------------------------------------------------------------------
 // k_batch_resident (n_dual 1024, the bench shape): k_batch_stream with part of
 // each problem's Qd kept on the CU across the launch's iterations (temporal
-// blocking; one workgroup per CU, so the CU's LDS is this problem's):
-//   blocks 0 .. RL-1 (U k each, 64 KiB per block) are loaded from HBM in the
-//     first iteration, copied into LDS and summed from there afterwards;
-//   block RL -- the first streamed block, loaded at the end of each iteration
-//     for the next one while the LDS blocks are summed -- uses the default
-//     cache policy: 64 KiB per CU = 2 MiB per XCD, which stays in the XCD's
-//     L2 between iterations while the nt stream passes through;
-//   blocks RL+1 .. 63 stream non-temporally as in k_batch_stream.
-// Every row sums the same terms in the same k order as k_batch_stream (only
-// where q comes from differs), so the bits are the same.
+// blocking; one workgroup per CU, so the CU's LDS and registers are this
+// problem's):
+//   blocks 0 .. RA-1 (U k each, 64 KiB per block over the workgroup) in
+//     registers: loaded from HBM in the first iteration and pinned to AGPRs
+//     (the stream buffers take the arch VGPRs);
+//   blocks RA .. P-1 (P = RA + RL) copied into LDS in the first iteration and
+//     summed from there afterwards;
+//   block P -- the first streamed block, loaded at the end of each iteration
+//     for the next one while the resident blocks are summed -- uses the
+//     default cache policy: 64 KiB per CU = 2 MiB per XCD, which stays in the
+//     XCD's L2 between iterations while the nt stream passes through;
+//   blocks P+1 .. 63 stream non-temporally as in k_batch_stream.
+// RA > 0 reads Qd through a buffer descriptor (one VGPR offset for all U loads
+// of a block, the k offset in SGPRs): the 64-bit per-load addresses of the
+// global form leave no room for the pinned blocks.  Every row sums the same
+// terms in the same k order as k_batch_stream (only where q comes from
+// differs), so the bits are the same.
 // ---------------------------------------------------------------------------
-template <int U, int RL>
+template <int U, int RL, int RA = 0>
 __global__ void __launch_bounds__(256) k_batch_resident(const float* __restrict__ QdT, long long qstride, int ldq,
                                                         const float* __restrict__ theta,
                                                         const float* __restrict__ Fd, int ldv, const float* Y0,
                                                         float* Y, int updates) {
-    constexpr int N = 1024, nb = N / U;
-    static_assert((nb - RL) % 2 == 0, "the streamed blocks come in pairs");
+    constexpr int N = 1024, nb = N / U, P = RA + RL;
+    static_assert((nb - P) % 2 == 0, "the streamed blocks come in pairs");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* ya = lds;
     float* yb = lds + ldq;
@@ -337,37 +344,92 @@ __global__ void __launch_bounds__(256) k_batch_resident(const float* __restrict_
     float th[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) th[r] = th_g[row + r];
+    // block kb's U float4 of this lane (nt: non-temporal)
+    const unsigned long long qaddr = (unsigned long long)Q;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(qaddr >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)qaddr)),
+        (short)0, __builtin_amdgcn_readfirstlane((int)(qstride * 4)), 0x00020000);
+    auto ld = [&](float4(&q)[U], int kb, bool nt) {
+        if constexpr (RA > 0) {
+            const int s0 = kb * U * ldq * 4;
+            if (nt) {
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * tid, s0 + j * ldq * 4, 2);
+                    q[j] = make_float4(v.x, v.y, v.z, v.w);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * tid, s0 + j * ldq * 4, 0);
+                    q[j] = make_float4(v.x, v.y, v.z, v.w);
+                }
+            }
+        } else {
+            if (nt) stream_load<U, true>(q, col + (size_t)kb * U * ldq, ldq);
+            else stream_load<U, false>(q, col + (size_t)kb * U * ldq, ldq);
+        }
+    };
     float4 qa[U], qb[U];
-    if (updates > 0) stream_load<U, false>(qa, col + (size_t)RL * U * ldq, ldq);
+    float4 rr[RA > 0 ? RA * U : 1];
+    if (updates > 0) {
+#pragma unroll
+        for (int rb = 0; rb < RA; ++rb) {
+            float4 t[U];
+            ld(t, rb, true);
+#pragma unroll
+            for (int j = 0; j < U; ++j) rr[rb * U + j] = t[j];
+        }
+        ld(qa, P, false);
+    }
     __syncthreads();
     for (int u = 0; u < updates; ++u) {
         const float* cur = (u & 1) ? yb : ya;
         float* nxt = (u & 1) ? ya : yb;
+        // the register blocks pinned to AGPRs here (an "a" constraint): left to
+        // itself the compiler keeps them in the arch VGPRs the stream needs and
+        // spills to scratch (scripts/probes/stream_resident.hip)
+#pragma unroll
+        for (int j = 0; j < RA * U; ++j) {
+            asm volatile("" : "+a"(rr[j].x));
+            asm volatile("" : "+a"(rr[j].y));
+            asm volatile("" : "+a"(rr[j].z));
+            asm volatile("" : "+a"(rr[j].w));
+        }
         Acc4 a;
 #pragma unroll
         for (int r = 0; r < 4; ++r) a.p[r] = a.n[r] = 0.0f;
 #pragma unroll
+        for (int rb = 0; rb < RA; ++rb) {
+            float4 q[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) q[j] = rr[rb * U + j];
+            const int k0 = rb * U;
+            stream_block<U>(a, q, k0, k0 >= wa && k0 < wbd, cur, row, th);
+        }
+#pragma unroll
         for (int lb = 0; lb < RL; ++lb) {
             float4* slot = res + (size_t)lb * U * 256 + tid;  // lane-private: no barrier needed
             if (u == 0) {
-                stream_load<U, true>(qb, col + (size_t)lb * U * ldq, ldq);
+                ld(qb, RA + lb, true);
 #pragma unroll
                 for (int j = 0; j < U; ++j) slot[j * 256] = qb[j];
             } else {
 #pragma unroll
                 for (int j = 0; j < U; ++j) qb[j] = slot[j * 256];
             }
-            const int k0 = lb * U;
+            const int k0 = (RA + lb) * U;
             stream_block<U>(a, qb, k0, k0 >= wa && k0 < wbd, cur, row, th);
         }
-        for (int kb = RL; kb < nb; kb += 2) {
-            stream_load<U, true>(qb, col + (size_t)(kb + 1) * U * ldq, ldq);
+        for (int kb = P; kb < nb; kb += 2) {
+            ld(qb, kb + 1, true);
             int k0 = kb * U;
             stream_block<U>(a, qa, k0, k0 >= wa && k0 < wbd, cur, row, th);
             if (kb + 2 < nb)
-                stream_load<U, true>(qa, col + (size_t)(kb + 2) * U * ldq, ldq);
+                ld(qa, kb + 2, true);
             else if (u + 1 < updates)  // the next iteration's first streamed block (L2-kept)
-                stream_load<U, false>(qa, col + (size_t)RL * U * ldq, ldq);
+                ld(qa, P, false);
             k0 += U;
             stream_block<U>(a, qb, k0, k0 >= wa && k0 < wbd, cur, row, th);
         }
@@ -4639,10 +4701,15 @@ static hipError_t launch_batch_iterate_one(int B, const float* QdT, long long qs
     // 10 iterations in the probe, scripts/probes/stream_resident.hip,
     // profiles/r06/stream_resident.jsonl; same bits).
     const int kind = g_tune.iterate_kind;
-    if (kind == 0 && N == 1024 && ldq == 1024) {
+    if ((kind == 0 || kind == 3) && N == 1024 && ldq == 1024 && qstride >= (long long)N * ldq &&
+        qstride * 4 <= 0x7fffffffLL) {
         const size_t lds = (size_t)2 * ldq * sizeof(float) + (size_t)2 * 16 * 256 * sizeof(float4);
-        hipLaunchKernelGGL((k_batch_resident<16, 2>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, theta, Fd, ldv,
-                           Y0, Y, updates);
+        if (kind == 3)  // + two register blocks (5/64 of Qd on chip)
+            hipLaunchKernelGGL((k_batch_resident<16, 2, 2>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, theta, Fd,
+                               ldv, Y0, Y, updates);
+        else
+            hipLaunchKernelGGL((k_batch_resident<16, 2>), dim3(B), dim3(256), lds, s, QdT, qstride, ldq, theta, Fd,
+                               ldv, Y0, Y, updates);
         return hipGetLastError();
     }
     // n_dual a multiple of 1024: k_batch_stream, one workgroup per CU, 16 + 16

@@ -147,7 +147,8 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int tiny_old = 0;    // one small problem on k_fixed_tiny / k_solve_wave (state copies) instead of k_fixed_one / k_solve_quintet
     int tiny_dense = 0;  // k_fixed_one / k_solve_quintet without the sparse update form
     int iterate_kind = 0;  // pqp_batch_iterate: 0 default (k_batch_resident at N 1024, k_batch_stream at other
-                           // multiples of 1024, k_batch_iterate otherwise), 1 k_batch_iterate, 2 k_batch_stream
+                           // multiples of 1024, k_batch_iterate otherwise), 1 k_batch_iterate, 2 k_batch_stream,
+                           // 3 k_batch_resident with two register blocks
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
     int tiny_fallback = 0;  // the host reads a tiny solve's device copies as if the pinned output were stale (tests)
     int tiny_sync = 0;  // a one-launch tiny solve ends in hipStreamSynchronize instead of polling hipStreamQuery

@@ -25,7 +25,7 @@ def main(B: int = 4096, N: int = 1024, chunk: int = 10, rounds: int = 4, reps: i
     res = {}
     ref = None
     for _ in range(rounds):
-        for v in (0, 2, 1):
+        for v in (0, 3, 2, 1):
             old = pqp_amd.tune("iterate_kind", v)
             try:
                 b.iterate(chunk)
@@ -45,7 +45,7 @@ def main(B: int = 4096, N: int = 1024, chunk: int = 10, rounds: int = 4, reps: i
             r = res.setdefault(v, {"ms": [], "same_bits": True})
             r["ms"].append(round(ms, 3))
             r["same_bits"] &= same
-    names = {0: "k_batch_resident", 1: "k_batch_iterate", 2: "k_batch_stream"}
+    names = {0: "k_batch_resident", 1: "k_batch_iterate", 2: "k_batch_stream", 3: "k_batch_resident_reg2"}
     out = {names[v]: {"ms_per_launch": r["ms"], "TBps_best": alg / min(r["ms"]) / 1e9,
                                    "frac_of_8TBps_best": alg / min(r["ms"]) / 1e9 / 8.0, "same_bits": r["same_bits"]}
            for v, r in res.items()}
