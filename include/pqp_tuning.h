@@ -90,8 +90,6 @@ extern "C" {
  *                          from the device state in further launches)
  *   tiny_fallback [0]      read a tiny solve's results from its device copies as
  *                          if the pinned output had missed its tag (tests)
- *   tiny_sync [0]          end a one-launch tiny solve with hipStreamSynchronize
- *                          instead of polling the stream (hipStreamQuery)
  *   tiny_dense [0]         k_fixed_one / k_solve_quintet without the sparse
  *                          update form (every split entry summed)
  *   iterate_kind [0]       pqp_batch_iterate's kernel: 0 the default (n_dual 1024:

@@ -887,20 +887,6 @@ int problem_run_wide(pqp_problem& P, long long max_updates, SolveOut& out, hipSt
     return PQP_OK;
 }
 
-// The end of a one-launch tiny solve: poll the stream's completion signal
-// (hipStreamQuery: the same ordering guarantee as a synchronisation -- every
-// store of the kernel, the pinned output included, is visible once the stream
-// is idle) instead of hipStreamSynchronize, whose wake-up costs about 6 us
-// more per solve (scripts/probes/doorbell_probe.hip, profiles/r06/doorbell_*.json).
-// The tiny_sync knob restores the synchronisation (A/B runs).
-static hipError_t tiny_wait(hipStream_t s) {
-    if (g_tune.tiny_sync) return hipStreamSynchronize(s);
-    hipError_t q;
-    while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
-    }
-    return q;
-}
-
 // One small problem (N, M <= 32) from Y = 1000 in ONE launch (pqp_tiny.hip:
 // k_fixed_one / k_solve_quintet): the kernel starts from h = 1 itself (no state
 // upload) and writes Y, U, the state and its error word to pinned host memory,
@@ -955,7 +941,9 @@ int problem_run_tiny(pqp_problem& P, int mode, long long num_iter, long long max
         if (P.out_tag == 0) P.out_tag = 1;
         a.out_tag = (int)P.out_tag;
         PQP_HIP(launch_one_tiny(a, dst, s));
-        PQP_HIP(tiny_wait(s));
+        // (polling hipStreamQuery instead measured 2 us slower per solve, 17.7 vs
+        // 12.2 us for a bare launch: profiles/r06/doorbell_r06e.json)
+        PQP_HIP(hipStreamSynchronize(s));
         if (*htag != a.out_tag || g_tune.tiny_fallback) {
             // not this launch's output (never seen so far; the tiny_fallback
             // knob forces this path in tests): read the device copies instead --
@@ -2075,7 +2063,6 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_dense", &g_tune.tiny_dense, nullptr, nullptr},
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
         {"tiny_fallback", &g_tune.tiny_fallback, nullptr, nullptr},
-        {"tiny_sync", &g_tune.tiny_sync, nullptr, nullptr},
         {"tiny_chunk", nullptr, nullptr, &g_tune.tiny_chunk},
         {"iterate_kind", &g_tune.iterate_kind, nullptr, nullptr},
     };

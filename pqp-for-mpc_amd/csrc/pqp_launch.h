@@ -151,7 +151,6 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
                            // 3 k_batch_resident with two register blocks
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
     int tiny_fallback = 0;  // the host reads a tiny solve's device copies as if the pinned output were stale (tests)
-    int tiny_sync = 0;  // a one-launch tiny solve ends in hipStreamSynchronize instead of polling hipStreamQuery
     long long tiny_chunk = 0;  // iterates per one-launch tiny solve launch (0: about 2^26 element updates)
     unsigned long long* tiny_trace = nullptr;  // k_solve_quintet per-wave clocks (24 words; N = 28, M <= 8 only)
 };

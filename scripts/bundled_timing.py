@@ -2,9 +2,7 @@
 problem is uploaded once; each solve is one pqp_problem_solve call (launch,
 synchronisation, results on the host).  Forms, alternating in one process:
   new    k_fixed_one (sparse form where the split rows allow) / k_solve_quintet,
-         results written by the kernel to pinned host memory, the host polling
-         the stream's completion (round 6)
-  sync   the same, ended by hipStreamSynchronize (round 5, pqp_tune tiny_sync)
+         results written by the kernel to pinned host memory
   dense  k_fixed_one's dense form only (pqp_tune tiny_dense)
   old    the round-4 k_fixed_tiny / k_solve_wave with state copies (tiny_old)
 Each solve's bits are checked against tests/golden/bundled.npz.  Run under
@@ -21,7 +19,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-FORMS = {"new": {}, "sync": {"tiny_sync": 1}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
+FORMS = {"new": {}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
 
 
 def main(reps: int = 200, rounds: int = 3):
