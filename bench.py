@@ -58,7 +58,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-KERNEL = "k_batch_resident<16,2>"
+KERNEL = "k_batch_resident<16,2,2>"
 
 
 def hot_kernel_hash() -> str:

@@ -72,6 +72,9 @@ extern "C" {
  *                          above n_dual 768; below, the fewest rounds of
  *                          resident problems, weighted +10 % per step); 3, 4
  *                          or 5 forces one
+ *   mid2_csplit [0]        k_solve_mid2 (one lane per update row): C waves of 32
+ *                          rows, checkFeas on lanes 0-31 and the Y'Qd terms on
+ *                          lanes 32-63 side by side (1 on)
  *   mid2_dense [0]         k_solve_mid2 sums every k of each update row and
  *                          Y'Qd row (default: only the band of k where the
  *                          wave's rows hold a nonzero, while Y is finite)
@@ -93,11 +96,11 @@ extern "C" {
  *   tiny_dense [0]         k_fixed_one / k_solve_quintet without the sparse
  *                          update form (every split entry summed)
  *   iterate_kind [0]       pqp_batch_iterate's kernel: 0 the default (n_dual 1024:
- *                          k_batch_resident, Qd's first blocks kept on the CU
- *                          across a launch's iterations; other multiples of
- *                          1024: k_batch_stream; else k_batch_iterate),
- *                          1 k_batch_iterate, 2 k_batch_stream, 3 k_batch_resident
- *                          with two more blocks in registers (n_dual 1024)
+ *                          k_batch_resident, Qd's first blocks kept on the CU in
+ *                          registers, LDS and L2 across a launch's iterations;
+ *                          other multiples of 1024: k_batch_stream; else
+ *                          k_batch_iterate), 1 k_batch_iterate, 2 k_batch_stream,
+ *                          3 k_batch_resident without the register blocks
  *  Paths and failure tests:
  *   persist_off [0]        fixed mode of n_dual <= 1024 through the graph-replayed
  *                          relay instead of the persistent launch

@@ -1,6 +1,7 @@
 """A/B of pqp_batch_iterate's kernels on the headline workload (configs[3]:
 4096 synthetic problems of n_dual 1024, 10 updates per launch), alternating
-in one process: k_batch_resident (the default at n_dual 1024, round 6),
+in one process: k_batch_resident (the default at n_dual 1024, round 6; kind 3
+its LDS + L2 form without the register blocks),
 k_batch_stream (round 5, pqp_tune iterate_kind 2) and k_batch_iterate
 (rounds 1-4, iterate_kind 1).  Reports the
 launch time (HIP events) and TB/s of algorithmic bytes; checks that every
@@ -45,7 +46,7 @@ def main(B: int = 4096, N: int = 1024, chunk: int = 10, rounds: int = 4, reps: i
             r = res.setdefault(v, {"ms": [], "same_bits": True})
             r["ms"].append(round(ms, 3))
             r["same_bits"] &= same
-    names = {0: "k_batch_resident", 1: "k_batch_iterate", 2: "k_batch_stream", 3: "k_batch_resident_reg2"}
+    names = {0: "k_batch_resident", 1: "k_batch_iterate", 2: "k_batch_stream", 3: "k_batch_resident_lds_only"}
     out = {names[v]: {"ms_per_launch": r["ms"], "TBps_best": alg / min(r["ms"]) / 1e9,
                                    "frac_of_8TBps_best": alg / min(r["ms"]) / 1e9 / 8.0, "same_bits": r["same_bits"]}
            for v, r in res.items()}

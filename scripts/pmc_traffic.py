@@ -12,7 +12,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNEL = "k_batch_resident<16, 2>"
+KERNEL = "k_batch_resident<16, 2, 2>"
 
 
 def per_launch(path: str, counter: str, skip: int) -> tuple[float, int]:
@@ -36,7 +36,7 @@ def main():
     sys.path.insert(0, str(ROOT))
     from bench import hot_kernel_hash
 
-    rec = {"kernel": "k_batch_resident<16,2>", "kernel_src_sha256": hot_kernel_hash(),
+    rec = {"kernel": "k_batch_resident<16,2,2>", "kernel_src_sha256": hot_kernel_hash(),
            "launches_averaged": min(nf, nw),
            "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write,
            "hbm_bytes_per_launch": (2 * fetch + write) * 1024, "alg_bytes_per_launch": alg,

@@ -318,7 +318,7 @@ def test_stream_kernels_vs_oracle_and_iterate(gpu_lib, orc, N, B, ups):
     first = b.result().copy()
     assert_bitwise(first, _iterate_kind(gpu_lib, b, ups, 1), f"default vs k_batch_iterate N={N}")
     assert_bitwise(first, _iterate_kind(gpu_lib, b, ups, 2), f"default vs k_batch_stream N={N}")
-    assert_bitwise(first, _iterate_kind(gpu_lib, b, ups, 3), f"default vs k_batch_resident + registers N={N}")
+    assert_bitwise(first, _iterate_kind(gpu_lib, b, ups, 3), f"default vs k_batch_resident LDS + L2 N={N}")
     for j in (0, B - 1):
         P = orc.synth_problem(21, 3 + j, N, M, with_qp=False)
         assert_bitwise(first[j], orc.iterate(P["Qd"], P["Fd"], N, ups), f"N={N} problem {j}")
