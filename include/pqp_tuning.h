@@ -72,9 +72,6 @@ extern "C" {
  *                          above n_dual 768; below, the fewest rounds of
  *                          resident problems, weighted +10 % per step); 3, 4
  *                          or 5 forces one
- *   mid2_csplit [0]        k_solve_mid2 (one lane per update row): C waves of 32
- *                          rows, checkFeas on lanes 0-31 and the Y'Qd terms on
- *                          lanes 32-63 side by side (1 on)
  *   mid2_dense [0]         k_solve_mid2 sums every k of each update row and
  *                          Y'Qd row (default: only the band of k where the
  *                          wave's rows hold a nonzero, while Y is finite)

@@ -2053,7 +2053,6 @@ const KnobRef* find_knob(const char* key) {
         {"mid2_pair", &g_tune.mid2_pair, nullptr, nullptr},
         {"mid2_min_n", &g_tune.mid2_min_n, nullptr, nullptr},
         {"mid2_dense", &g_tune.mid2_dense, nullptr, nullptr},
-        {"mid2_csplit", &g_tune.mid2_csplit, nullptr, nullptr},
         {"single_occ", &g_tune.single_occ, nullptr, nullptr},
         {"matmul_pk_off", &g_tune.matmul_pk_off, nullptr, nullptr},
         {"pipe_variant", &g_tune.pipe_variant, nullptr, nullptr},

@@ -3554,32 +3554,6 @@ __device__ __forceinline__ float mid_dot(const float* a, int as, const float* b,
     }
     return s;
 }
-// mid_dot with a per-lane operand stream AND length: lane l sums its own n8
-// terms a[k * as] * b[k], k in order (n8 a multiple of 8, per lane); the wave
-// runs the longest stream (n8max, uniform) and a lane past its own end adds
-// nothing more (its reloads are clamped to its first block).  k_solve_mid2's
-// split C waves: checkFeas rows on half the lanes, Y'Qd terms on the other.
-template <bool PK = false>
-__device__ __forceinline__ float mid_dot_lane(const float* a, int as, const float* b, int n8, int n8max) {
-    float s = 0.0f;
-    MidBlk c, x;
-    mid_load(c, a, as, b, 0);
-    int k = 0;
-    for (; k + 16 < n8max; k += 16) {
-        mid_load(x, a, as, b, k + 8 < n8 ? k + 8 : 0);
-        if (k < n8) mid_acc<PK>(s, c);
-        mid_load(c, a, as, b, k + 16 < n8 ? k + 16 : 0);
-        if (k + 8 < n8) mid_acc<PK>(s, x);
-    }
-    if (k + 8 < n8max) {
-        mid_load(x, a, as, b, k + 8 < n8 ? k + 8 : 0);
-        if (k < n8) mid_acc<PK>(s, c);
-        if (k + 8 < n8) mid_acc<PK>(s, x);
-    } else if (k < n8) {
-        mid_acc<PK>(s, c);
-    }
-    return s;
-}
 // s = sum_k a[k] * b[k] over a 16-byte-aligned LDS row a (per lane, 16-byte
 // loads) and the broadcast b, k = 0..n8-1 in order
 struct RowDotBlk {
@@ -4557,31 +4531,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             const bool pend = s > h0;
             const float* Uo = Us + ((s - 1) & 1) * mk;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
-            if (cw < nCR && crows == 32) {
-                // split C waves (32 rows each): lanes 0..31 run checkFeas row r
-                // (Gp row r . U_{s-1}, :636), lanes 32..63 the Y'Qd term of row
-                // r ((Y_s'Qd)_r Y_s,r, :652-655, the reference's column form
-                // sum_k Y_k Qd[k][r]) -- two chains side by side instead of one
-                // after the other on one lane; each lane's terms in k order
-                const int r = 32 * cw + (lane & 31);
-                const bool fe = lane < 32, live = r < N;
-                const bool cb = BAND && !y_nonfinite;
-                const int klo = cb ? clo : 0, kn = (cb ? chi : nk) - klo;
-                const int n8max = (pend && mk > kn) ? mk : kn;
-                const int n8 = !live ? 0 : (fe ? (pend ? mk : 0) : kn);
-                const int rr = live ? r : 0;
-                const float* pa = fe ? Gp + rr : Qd + klo * ldn + rr;
-                const float* pb = fe ? Uo : ycur + klo;
-                const float d = mid_dot_lane<PK && PQP_M2PK_F>(pa, fe ? ldg : ldn, pb, n8, n8max);
-                int bad = 0;
-                if (fe && live && pend) {
-                    const float kp = Kp[r];
-                    if (d > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
-                }
-                const bool any_bad = __any(bad);
-                if (pend && lane == 0) flag[cw] = any_bad ? 1 : 0;
-                if (!fe && live) tq[(s & 1) * nk + r] = d * ycur[r];
-            } else if (cw < nCR) {
+            if (cw < nCR) {
                 const int l = cw * crows + lane;  // rows [cw * crows, +crows): lanes < crows
                 const int lend = lane < crows ? N : 0;
                 int bad = 0;
@@ -4666,10 +4616,12 @@ static hipError_t launch_mid_grid(int B, const SolveArgs& a0, SolveState* st, hi
     // ms, and slower at 56, 84 and 140 (more waves per workgroup, fewer
     // workgroups per CU); mid2_pair 1 / 2 force either form
     const bool pair = g_tune.mid2_pair == 1 || (g_tune.mid2_pair == 0 && a.N >= 96 && a.N <= 128);
-    // split C waves (32 rows each, checkFeas and Y'Qd on the two halves of the
-    // lanes, round 6) on mid2_csplit 1; 64-row C waves otherwise (32 rows per C
-    // wave WITHOUT the split measured slower at every H: more waves per workgroup)
-    const int crows = (g_tune.mid2_csplit == 1 && !pair) ? 32 : 64;
+    // 32 rows per C wave measured slower at every H (more waves per workgroup);
+    // so did 32-row C waves running checkFeas and the Y'Qd terms side by side on
+    // the two halves of their lanes (round 6: H = 5 58.2 -> 68.0 ms, the dense
+    // n_dual 140 companion 84.9 -> 92.2, H = 2 11.2 -> 19.1;
+    // profiles/r06/mid2_csplit_dropped_r06g.jsonl)
+    const int crows = 64;
     if (a.mode != kModeTerminate && !g_tune.mid_v1 && a.N >= g_tune.mid2_min_n &&
         mid2_fits(a.N, a.M, conv2, pair, crows)) {
         const size_t lds = sizeof(float) * (size_t)mid2_layout(a.N, a.M, conv2).total;

@@ -21,11 +21,9 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 MID = 3
-# form -> (mid_v1, mid2_pair, kernel path 3 launches: pqp_tune_get last_batch_kernel,
-# mid2_csplit); the mid2 forms run on every size here (mid2_min_n 0).  csplit:
-# the one-lane-per-row form with split C waves (round 6: checkFeas and the Y'Qd
-# terms on the two halves of 32-row C waves)
-FORMS = {"mid2": (0, 2, 3, 0), "pair": (0, 1, 3, 0), "v1": (1, 0, 2, 0), "csplit": (0, 2, 3, 1)}
+# form -> (mid_v1, mid2_pair, kernel path 3 launches: pqp_tune_get last_batch_kernel);
+# the mid2 forms run on every size here (mid2_min_n 0)
+FORMS = {"mid2": (0, 2, 3), "pair": (0, 1, 3), "v1": (1, 0, 2)}
 
 
 def _batch(gpu_lib, Ps):
@@ -44,11 +42,10 @@ def _check(pb, b, h, Y, U, what):
 
 
 def _form(knobs, form):
-    v1, pair, _, csplit = FORMS[form]
+    v1, pair, _ = FORMS[form]
     knobs("mid_v1", v1)
     knobs("mid2_pair", pair)
     knobs("mid2_min_n", 0)
-    knobs("mid2_csplit", csplit)
 
 
 @pytest.fixture
@@ -71,7 +68,7 @@ def _bundled(golden_bundled):
 
 
 @pytest.mark.parametrize("H", [2, 3, 4, 5])
-@pytest.mark.parametrize("mid_off,form", [(0, "mid2"), (0, "pair"), (0, "v1"), (1, "mid2"), (0, "csplit")])
+@pytest.mark.parametrize("mid_off,form", [(0, "mid2"), (0, "pair"), (0, "v1"), (1, "mid2")])
 def test_horizon_blocks_stop_like_reference(gpu_lib, golden_bundled, orc, knobs, H, mid_off, form):
     """The bundled plant as H diagonal blocks (n_dual 28 H) stops at h = 313
     (the oracle's, itself pinned to oracle/_ref for 9 and 36 blocks): 8 copies
@@ -190,7 +187,7 @@ def test_nan_in_qd_takes_the_select_form(gpu_lib, orc, knobs, form):
             assert_bitwise(got[ok], Y[ok], f"num_iter={n} problem {b}")
 
 
-@pytest.mark.parametrize("pair", [1, 2, 3])
+@pytest.mark.parametrize("pair", [1, 2])
 @pytest.mark.parametrize("N,M,cap", [(112, 28, 1), (112, 28, 2), (84, 21, 3), (150, 40, 4)])
 def test_mid2_short_caps_and_costs(gpu_lib, orc, knobs, N, M, cap, pair):
     """k_solve_mid2 decides terminate(Y_h) one phase after it was formed:
@@ -200,8 +197,7 @@ def test_mid2_short_caps_and_costs(gpu_lib, orc, knobs, N, M, cap, pair):
     Ps = [orc.synth_problem(35, b, N, M) for b in range(2)]
     for P in Ps:
         P["Kp"] = np.full(N, 1e30, np.float32)
-    knobs("mid2_pair", 2 if pair == 3 else pair)
-    knobs("mid2_csplit", 1 if pair == 3 else 0)  # 3: the split C waves
+    knobs("mid2_pair", pair)
     knobs("mid2_min_n", 0)
     pb = _batch(gpu_lib, Ps).solve(max_updates=cap)
     assert gpu_lib.tune_get("last_batch_kernel") == 3
@@ -264,8 +260,8 @@ def test_horizon_problem_the_reference_never_stops(gpu_lib, orc):
     _check(pb, 0, h, Y, U, "horizon H=2 problem 4160, capped")
 
 
-@pytest.mark.parametrize("H,csplit", [(2, 0), (4, 0), (4, 1)])
-def test_horizon_population_vs_reference(gpu_lib, knobs, H, csplit):
+@pytest.mark.parametrize("H", [2, 4])
+def test_horizon_population_vs_reference(gpu_lib, H):
     """VERDICT r3 (weak 1): the bench's whole horizon leg -- 16384 problems of
     the plant stacked over H stages, each stage at its own perturbed state
     (pqp_amd.perturbed_states(seed 7)), set up on the GPU by the product
@@ -285,9 +281,6 @@ def test_horizon_population_vs_reference(gpu_lib, knobs, H, csplit):
     xs = gpu_lib.perturbed_states(E["x"], B * H, seed=7).reshape(B, H, -1)
     assert hashlib.sha256(xs.tobytes()).digest() == G[f"xs_sha256_{H}"].tobytes(), "the state generator moved"
     pb = gpu_lib.horizon_batch(EXAMPLE_DIR, H, xs)
-    if csplit:  # the split C waves on the one-lane-per-row form
-        knobs("mid2_csplit", 1)
-        knobs("mid2_pair", 2)
     pb.solve(max_updates=int(G["cap"]))
     h, st = pb.h.cpu().numpy(), pb.status.cpu().numpy()
     Y, U = pb.Y.cpu().numpy(), pb.U.cpu().numpy()
@@ -327,7 +320,7 @@ def _same_or_both_nan(got, want, what):
     assert_bitwise(got[ok], want[ok], what)
 
 
-@pytest.mark.parametrize("pair", [1, 2, 3])
+@pytest.mark.parametrize("pair", [1, 2])
 def test_mid2_y_turning_nonfinite(gpu_lib, orc, knobs, pair):
     """ADVICE r4: the lane-pair form sums num's terms negated (v_med3_f32);
     once Y holds an inf or a NaN the phase must take the reference's selects
@@ -335,8 +328,7 @@ def test_mid2_y_turning_nonfinite(gpu_lib, orc, knobs, pair):
     during the solve: fixed mode before, across and after the overflow, and a
     capped converge solve, against the oracle (NaN positions, every other
     bit), on both update forms."""
-    knobs("mid2_pair", 2 if pair == 3 else pair)
-    knobs("mid2_csplit", 1 if pair == 3 else 0)  # 3: the split C waves
+    knobs("mid2_pair", pair)
     knobs("mid2_min_n", 0)
     N, M = 112, 28
     Ps = [_growing(N, M, s) for s in (1, 2)]
@@ -374,8 +366,7 @@ def _growing_banded(N, M, seed, blk=14, negzero=False):
     return P
 
 
-@pytest.mark.parametrize("N,M,pair", [(56, 14, 2), (84, 21, 2), (112, 28, 1), (112, 28, 2), (140, 35, 2), (140, 35, 1),
-                                      (84, 21, 3), (112, 28, 3), (140, 35, 3)])
+@pytest.mark.parametrize("N,M,pair", [(56, 14, 2), (84, 21, 2), (112, 28, 1), (112, 28, 2), (140, 35, 2), (140, 35, 1)])
 @pytest.mark.parametrize("negzero", [False, True])
 def test_mid2_band_y_turning_nonfinite(gpu_lib, orc, knobs, N, M, pair, negzero):
     """Band sums (k_solve_mid2 skips the k outside each row group's nonzero
@@ -383,8 +374,7 @@ def test_mid2_band_y_turning_nonfinite(gpu_lib, orc, knobs, N, M, pair, negzero)
     and then NaN: fixed mode before, across and after, and capped converge
     solves, against the oracle (NaN positions, every other bit); off-block
     zeros as +0 and as -0."""
-    knobs("mid2_pair", 2 if pair == 3 else pair)
-    knobs("mid2_csplit", 1 if pair == 3 else 0)  # 3: the split C waves
+    knobs("mid2_pair", pair)
     knobs("mid2_min_n", 0)
     Ps = [_growing_banded(N, M, s, negzero=negzero) for s in (3, 4)]
     seen_inf = False
