@@ -2063,6 +2063,7 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_dense", &g_tune.tiny_dense, nullptr, nullptr},
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
         {"tiny_fallback", &g_tune.tiny_fallback, nullptr, nullptr},
+        {"tiny_np", &g_tune.tiny_np, nullptr, nullptr},
         {"tiny_chunk", nullptr, nullptr, &g_tune.tiny_chunk},
         {"iterate_kind", &g_tune.iterate_kind, nullptr, nullptr},
     };

@@ -273,41 +273,52 @@ __global__ void __launch_bounds__(64) k_fixed_one(SolveArgs A, SolveState* __res
 // add reading its SGPR ~6.5 here, profiles/r05/trio_trace_*.json).
 // N + M < 64, N, M <= 32.
 // ---------------------------------------------------------------------------
-template <int NMAX, int MMAX>
+template <int NMAX, int MMAX, int NP>
 struct QuintetLds {
     float y[kRing][NMAX];   // Y_h            (A -> B, and the output)
     float t[kRing][MMAX];   // Gp'Y_h + Fp    (B -> C)
     float s2[kRing];        // (Y_h'Qd).Y_h   (B -> C)
     float lind[kRing];      // Fd.Y_h         (B -> C)
-    float q[2][NMAX];       // B_p's (Y'Qd)_j y_j terms, read back as broadcasts
+    float q[NP][NMAX];      // B_p's (Y'Qd)_j y_j terms, read back as broadcasts
     float lsc[12][64];      // A's sparse lists (setup)
     int lsa[12][64];
     SolveState out;         // the final state (by the deciding wave), written out by A after the barrier
     float jp, jd;           // costs of the last decided feasible iterate
     int have;
-    int a_h, b_h[2], decided;  // iterates (relative to the launch's first) published by A, B_p; decided by C0 / C1
+    int a_h, b_h[NP], decided;  // iterates (relative to the launch's first) published by A, B_p; decided by the C_p
     int h_end, err;
 };
 
-template <int NMAX, int MMAX, bool TRACE>
-__global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* __restrict__ st) {
+// NP (round 6): the B and C roles on NP waves each, iterate r on B_{r mod NP}
+// and C_{r mod NP} -- 2 (five waves) or 3 (seven: each B / C wave has three
+// iterates' time for its own)
+template <int NMAX, int MMAX, bool TRACE, int NP = 2>
+__global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A, SolveState* __restrict__ st) {
     static_assert(NMAX % 4 == 0 && MMAX % 4 == 0 && NMAX <= 32 && MMAX <= 32, "one wave per role");
+    static_assert(NP == 2 || NP == 3, "two or three B / C waves");
+    static_assert(!TRACE || NP == 2, "the timeline's layout is the five-wave one");
+    constexpr int NT = 64 * (1 + 2 * NP);
     SolveState s0 = A.fresh ? SolveState{1, kStatusContinue, 0, 0.0f, 0.0f, 0, 0} : *st;
     if (s0.status == kStatusDone || s0.status == kStatusCapped) return;
-    __shared__ __attribute__((aligned(16))) QuintetLds<NMAX, MMAX> S;
+    __shared__ __attribute__((aligned(16))) QuintetLds<NMAX, MMAX, NP> S;
     const int N = A.N, M = A.M;
     const int tid = threadIdx.x, lane = tid & 63;
-    // roles by hardware wave: 0 / 4 (one SIMD) B0 / B1, 1 A, 2 / 3 C0 / C1
+    // roles by hardware wave (waves w and w + 4 share a SIMD): 0 / 4 B0 / B1,
+    // 1 A, 2 / 3 C0 / C1; NP = 3: 5 C2 (beside A), 6 B2 (beside C0).  Role
+    // numbers: 0 A, 1 B0, 4 B1, 6 B2, 2 C0, 3 C1, 5 C2
     const int hw = tid >> 6;
-    const int role = hw == 1 ? 0 : (hw == 0 ? 1 : (hw == 4 ? 4 : hw));  // 0 A, 1 B0, 4 B1, 2 C0, 3 C1
+    const int role = hw == 1 ? 0 : (hw == 0 ? 1 : hw);
+    const bool is_b = role == 1 || role == 4 || role == 6;
+    const int bpar = role == 1 ? 0 : (role == 4 ? 1 : 2);           // B's parity
+    const int cpar = role == 2 ? 0 : (role == 3 ? 1 : 2);           // C's parity
     // padding y_k, t_j = +0: C reads all MMAX entries of t (times qinv's zero
     // padding), and LDS holds whatever the previous kernel left -- a NaN there
     // made 0 * NaN a NaN U (seen after kernels that ran on non-finite data)
-    for (int k = tid; k < kRing * NMAX; k += 320) (&S.y[0][0])[k] = 0.0f;
-    for (int k = tid; k < kRing * MMAX; k += 320) (&S.t[0][0])[k] = 0.0f;
+    for (int k = tid; k < kRing * NMAX; k += NT) (&S.y[0][0])[k] = 0.0f;
+    for (int k = tid; k < kRing * MMAX; k += NT) (&S.t[0][0])[k] = 0.0f;
     if (tid == 0) {
         S.a_h = -1;
-        S.b_h[0] = S.b_h[1] = -1;
+        for (int p = 0; p < NP; ++p) S.b_h[p] = -1;
         S.decided = -1;
         S.h_end = 0;
         S.err = 0;
@@ -368,7 +379,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
             if (own_row) S.y[r & (kRing - 1)][i] = yk;
             lds_publish(&S.a_h, r);
         }
-    } else if (role == 1 || role == 4) {
+    } else if (is_b) {
         // ---------------- waves B0 / B1: the N-long sums of terminate(Y_h) ----------------
         // lane j < N: Qd column j -> (Y'Qd)_j (computeCost :652); lane N + j:
         // Gp column j -> (Gp'Y)_j (computeUfromY :354); lane N + M: Fd -> Fd.Y (:657)
@@ -387,7 +398,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
         const bool is_t = lane >= N && lane < N + M;
         const float fp_own = is_t ? A.Fp[lane - N] : 0.0f;
         const int lown = lane < NMAX ? lane : 0;
-        const int bp = role == 4 ? 1 : 0;  // parity
+        const int bp = bpar;
         int a_seen = -1;
         unsigned long long ph[4] = {0, 0, 0, 0}, tm = 0;  // TRACE: clocks per phase of B's iterate
 #define QT_MARK(k)                                          \
@@ -396,7 +407,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
         ph[k] += t_ - tm;                                   \
         tm = t_;                                            \
     }
-        for (int r = bp;; r += 2) {
+        for (int r = bp;; r += NP) {
             if (TRACE) tm = __builtin_amdgcn_s_memtime();
             if (a_seen < r) {
                 int spin = 0;
@@ -440,7 +451,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
             // back through LDS as broadcasts
             if (lane < NMAX) S.q[bp][lane] = lane < N ? acc * y_own : 0.0f;
             // the next iterate's progress word, read while the terms travel
-            if (a_seen < r + 2) a_seen = lds_ld(&S.a_h);
+            if (a_seen < r + NP) a_seen = lds_ld(&S.a_h);
             f4v q4[NMAX / 4];
 #pragma unroll
             for (int g = 0; g < NMAX / 4; ++g) q4[g] = *reinterpret_cast<const f4v*>(&S.q[bp][4 * g]);
@@ -460,7 +471,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
         // ---------------- waves C0 / C1: the M-side chain and the decision ----------------
         // lane j < M: Qp_inv row j (U = -Qp_inv t); gq[j].x: lane i < N Gp row i
         // (checkFeas), lane N Fp (Fp.U); gq[j].y: lane k < M Qp column k (U'Qp)
-        const int par = role - 2;
+        const int par = cpar;
         const bool stall = (A.tiny_flags & kTinyStall) != 0;  // error-path test: no decision ever comes
         float qinv[MMAX];
         f2v gq[MMAX];
@@ -475,7 +486,7 @@ __global__ void __launch_bounds__(320) k_solve_quintet(SolveArgs A, SolveState* 
         }
         const float kp = lane < N ? A.Kp[lane] : 0.0f;
         const float Md = A.Md[0], Mp = A.Mp[0];
-        for (int r = par; !stall; r += 2) {
+        for (int r = par; !stall; r += NP) {
             int b, spin = 0;
             bool over = false;
             QT_WAIT_BEGIN()
@@ -630,14 +641,21 @@ hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
         return hipGetLastError();
     }
     if (a.mode != kModeConverge || a.N + a.M >= 64) return hipErrorInvalidValue;
-#define PQP_TRIO_M(NN)                                                                                           \
-    do {                                                                                                         \
-        if (a.trace && a.N == 28 && a.M <= 8)                                                                    \
-            hipLaunchKernelGGL((k_solve_quintet<28, 8, true>), dim3(1), dim3(320), 0, s, a, st);                 \
-        else if (a.M <= 8) hipLaunchKernelGGL((k_solve_quintet<NN, 8, false>), dim3(1), dim3(320), 0, s, a, st); \
-        else if (a.M <= 16)                                                                                      \
-            hipLaunchKernelGGL((k_solve_quintet<NN, 16, false>), dim3(1), dim3(320), 0, s, a, st);               \
-        else hipLaunchKernelGGL((k_solve_quintet<NN, 32, false>), dim3(1), dim3(320), 0, s, a, st);              \
+    const int np = g_tune.tiny_np == 3 ? 3 : 2;  // B / C waves per role
+#define PQP_TRIO_NP(NN, MM, NPP) \
+    hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, s, a, st)
+#define PQP_TRIO_MM(NN, MM)                      \
+    do {                                         \
+        if (np == 3) PQP_TRIO_NP(NN, MM, 3);     \
+        else PQP_TRIO_NP(NN, MM, 2);             \
+    } while (0)
+#define PQP_TRIO_M(NN)                                                                                \
+    do {                                                                                              \
+        if (a.trace && a.N == 28 && a.M <= 8)                                                         \
+            hipLaunchKernelGGL((k_solve_quintet<28, 8, true>), dim3(1), dim3(320), 0, s, a, st);      \
+        else if (a.M <= 8) PQP_TRIO_MM(NN, 8);                                                        \
+        else if (a.M <= 16) PQP_TRIO_MM(NN, 16);                                                      \
+        else PQP_TRIO_MM(NN, 32);                                                                     \
     } while (0)
     if (a.N <= 8) PQP_TRIO_M(8);
     else if (a.N <= 16) PQP_TRIO_M(16);
@@ -645,6 +663,8 @@ hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
     else if (a.N <= 28) PQP_TRIO_M(28);
     else PQP_TRIO_M(32);
 #undef PQP_TRIO_M
+#undef PQP_TRIO_MM
+#undef PQP_TRIO_NP
     return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@ problem is uploaded once; each solve is one pqp_problem_solve call (launch,
 synchronisation, results on the host).  Forms, alternating in one process:
   new    k_fixed_one (sparse form where the split rows allow) / k_solve_quintet,
          results written by the kernel to pinned host memory
+  np3    k_solve_quintet with three B and three C waves (pqp_tune tiny_np 3)
   dense  k_fixed_one's dense form only (pqp_tune tiny_dense)
   old    the round-4 k_fixed_tiny / k_solve_wave with state copies (tiny_old)
 Each solve's bits are checked against tests/golden/bundled.npz.  Run under
@@ -19,7 +20,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-FORMS = {"new": {}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
+FORMS = {"new": {}, "np3": {"tiny_np": 3}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
 
 
 def main(reps: int = 200, rounds: int = 3):

@@ -17,7 +17,7 @@ from conftest import CAP, assert_bitwise
 pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
-FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}}
+FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}, "np3": {"tiny_np": 3}}
 
 
 @contextmanager
@@ -62,7 +62,7 @@ def test_bundled_both_modes_every_form(gpu_lib, golden_bundled, form):
             assert_bitwise(f["Y"], g[f"Y_h{k}"], f"{form}: Y after {k - 1} updates")
 
 
-@pytest.mark.parametrize("form", ["sparse", "dense"])
+@pytest.mark.parametrize("form", ["sparse", "dense", "np3"])
 @pytest.mark.parametrize("cap", [1, 2, 3, 7, 8, 9, 16, 311])
 def test_bundled_converge_capped(gpu_lib, golden_bundled, orc, form, cap):
     """A cap inside and at the ring's depth (8 iterates in flight): the solve
@@ -117,14 +117,17 @@ def test_sparse_form_hands_over_at_the_first_nonfinite_y(gpu_lib, orc, N, M):
     assert not np.all(np.isfinite(orc.iterate(P["Qd"], P["Fd"], N, 999)))  # the case is exercised
 
 
+@pytest.mark.parametrize("np_", [2, 3])
 @pytest.mark.parametrize("N,M", [(8, 4), (28, 7), (32, 16)])
-def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M):
+def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M, np_):
     """Converge mode capped past the overflow: k_solve_quintet's update wave
-    (sparse form, then dense) against the oracle's solve, Y and U."""
+    (sparse form, then dense) against the oracle's solve, Y and U; two and
+    three B / C waves per role."""
     P = _growing_problem(N, M, N + 1)
     for cap in (100, 500):
         h, Y, U = orc.solve(P, 0, 1000, cap)
-        r = gpu_lib.solve_dual(P, max_updates=cap)
+        with tuned(gpu_lib, {"tiny_np": np_}):
+            r = gpu_lib.solve_dual(P, max_updates=cap)
         # the oracle returns -h when capped; a NaN cost passes every gap test
         # (NaN comparisons are false), so the reference may also stop there
         assert r["h"] == abs(h) and r["converged"] == (h > 0), (r["h"], h)
@@ -132,12 +135,13 @@ def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M):
         assert _same_bits_or_both_nan(r["U"], U), f"U N={N} cap={cap}"
 
 
-def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled):
+@pytest.mark.parametrize("np_", [2, 3])
+def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled, np_):
     """Every wait of k_solve_quintet is bounded: with its deciding waves
     stalled (test knob), the launch ends and the solve returns PQP_ERR_HIP
     instead of hanging; the next solve on the same handle is exact again."""
     g = golden_bundled
-    with gpu_lib.Problem(bundled_problem(g)) as prob:
+    with tuned(gpu_lib, {"tiny_np": np_}), gpu_lib.Problem(bundled_problem(g)) as prob:
         with tuned(gpu_lib, {"tiny_stall": 1}):
             with pytest.raises(gpu_lib.PQPError, match="hand-off wait expired"):
                 prob.solve(max_updates=CAP)
@@ -146,7 +150,8 @@ def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled):
         assert_bitwise(r["Y"], g["Ystar"], "Y* after the error")
 
 
-def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled):
+@pytest.mark.parametrize("np_", [2, 3])
+def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled, np_):
     """A race between the waves (a ring slot read before it is written) shows
     up as a wrong h or wrong bits in some solves: 400 one-shot solves in a
     row, alternating modes, every one exact (k_solve_quintet's progress words
@@ -155,6 +160,7 @@ def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled):
     P = bundled_problem(g)
     bad = []
     stale0 = gpu_lib.tune_get("tiny_stale")
+    prev_np = gpu_lib.tune("tiny_np", np_)  # round 6: three B / C waves per role
     for n in range(200):
         r = gpu_lib.solve_dual(P, max_updates=CAP)
         if r["h"] != 313 or r["Y"].tobytes() != g["Ystar"].tobytes() or r["U"].tobytes() != g["Ustar"].tobytes():
@@ -168,6 +174,7 @@ def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled):
         f = gpu_lib.solve_dual(P, mode=gpu_lib.MODE_FIXED, num_iter=1000)
         if f["Y"].tobytes() != g["Y_fixed999"].tobytes():
             bad.append(("fixed", 1000, n, f["h"]))
+    gpu_lib.tune("tiny_np", prev_np)
     assert not bad, bad[:10]
     # every solve's pinned output carried its own launch's tag (the device-copy
     # fallback never ran)
