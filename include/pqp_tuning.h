@@ -88,8 +88,8 @@ extern "C" {
  *   tiny_chunk [0]         iterates per launch of a one-launch tiny solve (0: about
  *                          2^26 element updates; a solve that needs more resumes
  *                          from the device state in further launches)
- *   tiny_np [0]            k_solve_quintet's B and C roles on 2 (0: default) or 3
- *                          waves each (iterate r on B / C wave r mod np)
+ *   tiny_np [0]            k_solve_quintet's B and C roles on 2, 3 (0: default)
+ *                          or 4 waves each (iterate r on B / C wave r mod np)
  *   tiny_fallback [0]      read a tiny solve's results from its device copies as
  *                          if the pinned output had missed its tag (tests)
  *   tiny_dense [0]         k_fixed_one / k_solve_quintet without the sparse

@@ -150,7 +150,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
                            // multiples of 1024, k_batch_iterate otherwise), 1 k_batch_iterate, 2 k_batch_stream,
                            // 3 k_batch_resident without its register blocks
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
-    int tiny_np = 0;  // k_solve_quintet's B / C waves per role: 2 (0: default) or 3
+    int tiny_np = 0;  // k_solve_quintet's B / C waves per role: 2, 3 (0: default) or 4
     int tiny_fallback = 0;  // the host reads a tiny solve's device copies as if the pinned output were stale (tests)
     long long tiny_chunk = 0;  // iterates per one-launch tiny solve launch (0: about 2^26 element updates)
     unsigned long long* tiny_trace = nullptr;  // k_solve_quintet per-wave clocks (24 words; N = 28, M <= 8 only)

@@ -290,12 +290,12 @@ struct QuintetLds {
 };
 
 // NP (round 6): the B and C roles on NP waves each, iterate r on B_{r mod NP}
-// and C_{r mod NP} -- 2 (five waves) or 3 (seven: each B / C wave has three
-// iterates' time for its own)
+// and C_{r mod NP} -- 2 (five waves), 3 or 4 (seven / nine: each B / C wave
+// has NP iterates' time for its own)
 template <int NMAX, int MMAX, bool TRACE, int NP = 2>
 __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A, SolveState* __restrict__ st) {
     static_assert(NMAX % 4 == 0 && MMAX % 4 == 0 && NMAX <= 32 && MMAX <= 32, "one wave per role");
-    static_assert(NP == 2 || NP == 3, "two or three B / C waves");
+    static_assert(NP >= 2 && NP <= 4, "two to four B / C waves");
     static_assert(!TRACE || NP == 2, "the timeline's layout is the five-wave one");
     constexpr int NT = 64 * (1 + 2 * NP);
     SolveState s0 = A.fresh ? SolveState{1, kStatusContinue, 0, 0.0f, 0.0f, 0, 0} : *st;
@@ -304,13 +304,14 @@ __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A
     const int N = A.N, M = A.M;
     const int tid = threadIdx.x, lane = tid & 63;
     // roles by hardware wave (waves w and w + 4 share a SIMD): 0 / 4 B0 / B1,
-    // 1 A, 2 / 3 C0 / C1; NP = 3: 5 C2 (beside A), 6 B2 (beside C0).  Role
-    // numbers: 0 A, 1 B0, 4 B1, 6 B2, 2 C0, 3 C1, 5 C2
+    // 1 A, 2 / 3 C0 / C1; beyond, odd waves C_p and even ones B_p (NP = 3: 5 C2
+    // beside A, 6 B2 beside C0; NP = 4: 7 C3 beside C1, 8 B3).  Role numbers
+    // (the five-wave timeline's): 0 A, 1 B0, else the hardware wave
     const int hw = tid >> 6;
     const int role = hw == 1 ? 0 : (hw == 0 ? 1 : hw);
-    const bool is_b = role == 1 || role == 4 || role == 6;
-    const int bpar = role == 1 ? 0 : (role == 4 ? 1 : 2);           // B's parity
-    const int cpar = role == 2 ? 0 : (role == 3 ? 1 : 2);           // C's parity
+    const bool is_b = hw == 0 || (hw >= 4 && !(hw & 1));
+    const int bpar = hw == 0 ? 0 : hw / 2 - 1;                     // B's parity
+    const int cpar = hw == 2 ? 0 : (hw == 3 ? 1 : (hw - 1) / 2);   // C's parity
     // padding y_k, t_j = +0: C reads all MMAX entries of t (times qinv's zero
     // padding), and LDS holds whatever the previous kernel left -- a NaN there
     // made 0 * NaN a NaN U (seen after kernels that ran on non-finite data)
@@ -641,12 +642,13 @@ hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
         return hipGetLastError();
     }
     if (a.mode != kModeConverge || a.N + a.M >= 64) return hipErrorInvalidValue;
-    const int np = g_tune.tiny_np == 3 ? 3 : 2;  // B / C waves per role
+    const int np = (g_tune.tiny_np >= 2 && g_tune.tiny_np <= 4) ? g_tune.tiny_np : 3;  // B / C waves per role
 #define PQP_TRIO_NP(NN, MM, NPP) \
     hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, s, a, st)
 #define PQP_TRIO_MM(NN, MM)                      \
     do {                                         \
         if (np == 3) PQP_TRIO_NP(NN, MM, 3);     \
+        else if (np == 4) PQP_TRIO_NP(NN, MM, 4); \
         else PQP_TRIO_NP(NN, MM, 2);             \
     } while (0)
 #define PQP_TRIO_M(NN)                                                                                \

@@ -3,7 +3,8 @@ problem is uploaded once; each solve is one pqp_problem_solve call (launch,
 synchronisation, results on the host).  Forms, alternating in one process:
   new    k_fixed_one (sparse form where the split rows allow) / k_solve_quintet,
          results written by the kernel to pinned host memory
-  np3    k_solve_quintet with three B and three C waves (pqp_tune tiny_np 3)
+  np2    k_solve_quintet with two B and two C waves (round 5's five waves; the
+         default is three of each since round 6), np4 with four
   dense  k_fixed_one's dense form only (pqp_tune tiny_dense)
   old    the round-4 k_fixed_tiny / k_solve_wave with state copies (tiny_old)
 Each solve's bits are checked against tests/golden/bundled.npz.  Run under
@@ -20,7 +21,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-FORMS = {"new": {}, "np3": {"tiny_np": 3}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
+FORMS = {"new": {}, "np2": {"tiny_np": 2}, "np4": {"tiny_np": 4}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
 
 
 def main(reps: int = 200, rounds: int = 3):

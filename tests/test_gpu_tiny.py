@@ -17,7 +17,8 @@ from conftest import CAP, assert_bitwise
 pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
-FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}, "np3": {"tiny_np": 3}}
+FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}, "np2": {"tiny_np": 2},
+         "np4": {"tiny_np": 4}}
 
 
 @contextmanager
@@ -62,7 +63,7 @@ def test_bundled_both_modes_every_form(gpu_lib, golden_bundled, form):
             assert_bitwise(f["Y"], g[f"Y_h{k}"], f"{form}: Y after {k - 1} updates")
 
 
-@pytest.mark.parametrize("form", ["sparse", "dense", "np3"])
+@pytest.mark.parametrize("form", ["sparse", "dense", "np2", "np4"])
 @pytest.mark.parametrize("cap", [1, 2, 3, 7, 8, 9, 16, 311])
 def test_bundled_converge_capped(gpu_lib, golden_bundled, orc, form, cap):
     """A cap inside and at the ring's depth (8 iterates in flight): the solve
@@ -117,7 +118,7 @@ def test_sparse_form_hands_over_at_the_first_nonfinite_y(gpu_lib, orc, N, M):
     assert not np.all(np.isfinite(orc.iterate(P["Qd"], P["Fd"], N, 999)))  # the case is exercised
 
 
-@pytest.mark.parametrize("np_", [2, 3])
+@pytest.mark.parametrize("np_", [2, 3, 4])
 @pytest.mark.parametrize("N,M", [(8, 4), (28, 7), (32, 16)])
 def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M, np_):
     """Converge mode capped past the overflow: k_solve_quintet's update wave
@@ -135,7 +136,7 @@ def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M, np_):
         assert _same_bits_or_both_nan(r["U"], U), f"U N={N} cap={cap}"
 
 
-@pytest.mark.parametrize("np_", [2, 3])
+@pytest.mark.parametrize("np_", [2, 3, 4])
 def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled, np_):
     """Every wait of k_solve_quintet is bounded: with its deciding waves
     stalled (test knob), the launch ends and the solve returns PQP_ERR_HIP
@@ -150,7 +151,7 @@ def test_stalled_decision_reports_an_error(gpu_lib, golden_bundled, np_):
         assert_bitwise(r["Y"], g["Ystar"], "Y* after the error")
 
 
-@pytest.mark.parametrize("np_", [2, 3])
+@pytest.mark.parametrize("np_", [2, 3, 4])
 def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled, np_):
     """A race between the waves (a ring slot read before it is written) shows
     up as a wrong h or wrong bits in some solves: 400 one-shot solves in a
