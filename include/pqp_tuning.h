@@ -88,6 +88,9 @@ extern "C" {
  *   tiny_chunk [0]         iterates per launch of a one-launch tiny solve (0: about
  *                          2^26 element updates; a solve that needs more resumes
  *                          from the device state in further launches)
+ *   persist_xcds [0]       k_split_persist's workgroups on this many XCDs (the grid
+ *                          padded with workgroups that leave at once; 0: spread
+ *                          over all eight)
  *   tiny_np [0]            k_solve_quintet's B and C roles on 2, 3 (0: default)
  *                          or 4 waves each (iterate r on B / C wave r mod np)
  *   tiny_fallback [0]      read a tiny solve's results from its device copies as

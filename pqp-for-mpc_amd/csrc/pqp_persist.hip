@@ -142,11 +142,20 @@ template <bool TRACE>
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     k_split_persist(const float* __restrict__ SP, const float* __restrict__ fdpn, int N, int updates,
                     const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err, u64* trace,
-                    int trace_n, int stall_wg) {
+                    int trace_n, int stall_wg, int xcds) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    // xcds > 0 (A/B, tune persist_xcds): the grid is 8 / xcds times larger and
+    // only the workgroups with blockIdx % 8 < xcds take part -- under the
+    // round-robin placement of workgroups over the 8 XCDs, the solve's
+    // workgroups sit on xcds XCDs (32 CUs each) instead of all eight
+    int wg = blockIdx.x;
+    if (xcds > 0) {
+        if ((int)(blockIdx.x & 7) >= xcds) return;
+        wg = (int)(blockIdx.x >> 3) * xcds + (int)(blockIdx.x & 7);
+    }
     // tuning (error-path tests): this workgroup never runs, as if it were not
     // resident; every other one's waits expire and report through err
-    if ((int)blockIdx.x == stall_wg) return;
+    if (wg == stall_wg) return;
     gu64* gran = (gu64*)gran_;
     const int KB = split_kblocks(N);
     const int W = persist_waves_of(KB);
@@ -158,13 +167,13 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ll = lane & (kPLanes - 1);  // lanes 32..63 repeat lanes 0..31 (discarded)
-    const int p = blockIdx.x * kPLanes + ll;
+    const int p = wg * kPLanes + ll;
     const bool live = lane < kPLanes && p < 2 * N;
     const int row = p >> 1;
 
     // this workgroup's packets -> LDS (read-only input: plain loads)
     {
-        const f4v* src = reinterpret_cast<const f4v*>(SP) + (size_t)blockIdx.x * KB * kPLanes;
+        const f4v* src = reinterpret_cast<const f4v*>(SP) + (size_t)wg * KB * kPLanes;
         for (int e = tid; e < KP * kPLanes; e += blockDim.x)
             qs[e] = (e < KB * kPLanes) ? src[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
         for (int e = tid; e < 2 * W * 64; e += blockDim.x) slot[e] = 0ull;
@@ -182,7 +191,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     float yrow = 0.0f;  // last wave: y_i of this lane's row (for y_next = num / den * y_i)
     // optional timeline (s_memtime) of workgroup 0: per update and wave,
     // {sweep start, y staged, turn (sums received), chain done}
-    u64* tr = (TRACE && trace && blockIdx.x == 0 && lane == 0) ? trace : nullptr;
+    u64* tr = (TRACE && trace && wg == 0 && lane == 0) ? trace : nullptr;
     auto mark = [&](int u, int e) {
         if constexpr (TRACE)
             if (tr && u < trace_n) tr[((size_t)u * W + w) * 4 + e] = __builtin_amdgcn_s_memtime();
@@ -334,7 +343,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                 acc = __uint_as_float((unsigned)h);
                 mark(u, 2);
                 __builtin_amdgcn_s_setprio(3);
-                if (TRACE && trace && blockIdx.x == 0 && u < trace_n) {
+                if (TRACE && trace && wg == 0 && u < trace_n) {
                     // traced launches only: s_memtime before each seventh of
                     // the chain (stored after it), to see where a slice loses time
                     constexpr int G = 7, PG = (NP + G - 1) / G;
@@ -409,12 +418,18 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
     hipError_t e = hipMemsetAsync(gran, 0, sizeof(u64) * 2 * N, s);
     if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
+    // persist_xcds x: the G workgroups packed onto x XCDs (x * 32 >= G), the
+    // grid padded with workgroups that leave at once
+    const int xcds = (g_tune.persist_xcds > 0 && g_tune.persist_xcds < 8 && g_tune.persist_xcds * 32 >= G)
+                         ? g_tune.persist_xcds : 0;
+    const int grid = xcds ? 8 * ((G + xcds - 1) / xcds) : G;
     if (g_tune.persist_trace)
-        hipLaunchKernelGGL(k_split_persist<true>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
-                           updates, Y0, Yout, gran, err, g_tune.persist_trace, g_tune.persist_trace_n, g_tune.persist_stall_wg);
+        hipLaunchKernelGGL(k_split_persist<true>, dim3(grid), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
+                           updates, Y0, Yout, gran, err, g_tune.persist_trace, g_tune.persist_trace_n,
+                           g_tune.persist_stall_wg, xcds);
     else
-        hipLaunchKernelGGL(k_split_persist<false>, dim3(G), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
-                           updates, Y0, Yout, gran, err, nullptr, 0, g_tune.persist_stall_wg);
+        hipLaunchKernelGGL(k_split_persist<false>, dim3(grid), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,
+                           updates, Y0, Yout, gran, err, nullptr, 0, g_tune.persist_stall_wg, xcds);
     return hipGetLastError();
 }
 

@@ -292,7 +292,7 @@ struct QuintetLds {
 // NP (round 6): the B and C roles on NP waves each, iterate r on B_{r mod NP}
 // and C_{r mod NP} -- 2 (five waves), 3 or 4 (seven / nine: each B / C wave
 // has NP iterates' time for its own)
-template <int NMAX, int MMAX, bool TRACE, int NP = 2>
+template <int NMAX, int MMAX, bool TRACE, int NP = 2, bool A_CACHE = false>
 __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A, SolveState* __restrict__ st) {
     static_assert(NMAX % 4 == 0 && MMAX % 4 == 0 && NMAX <= 32 && MMAX <= 32, "one wave per role");
     static_assert(NP >= 2 && NP <= 4, "two to four B / C waves");
@@ -354,6 +354,7 @@ __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A
         if (own_row) yk = s0.resume ? A.Y[i] : 1000.0f;  // initMat(Y, 1000) :710
         if (own_row) S.y[0][i] = yk;
         lds_publish(&S.a_h, 0);
+        int d_seen = -1;
         for (int r = 1;; ++r) {
             // the sparse form only while every y is finite (the skipped +-0 terms are then exact)
             if (sparse && __any(!__builtin_isfinite(yk))) sparse = false;
@@ -363,19 +364,25 @@ __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A
             } else {
                 yk = update_dense<NMAX>(mat, fd_own, yk, own_row);
             }
-            // room in the ring: iterate r - kRing decided (or the solve over)
-            int d, spin = 0;
-            QT_WAIT_BEGIN()
-            for (;; ++spin) {
-                d = lds_ld(&S.decided);
-                if (d == kStopWord || d >= r - kRing || spin > spin_max) break;
-            }
-            QT_WAIT_END()
-            lds_after_wait();
-            if (d == kStopWord) break;
-            if (spin > spin_max) {
-                S.err = 1;
-                break;
+            // room in the ring: iterate r - kRing decided (or the solve over).
+            // The last decision seen is kept and the word read again only when
+            // it leaves no room (round 6, A_CACHE): no LDS round trip on the
+            // update's path while A runs ahead.  A learns of the stop when the
+            // ring fills (at most kRing discarded updates).
+            if (!A_CACHE || d_seen < r - kRing) {
+                int spin = 0;
+                QT_WAIT_BEGIN()
+                for (;; ++spin) {
+                    d_seen = lds_ld(&S.decided);
+                    if (d_seen == kStopWord || d_seen >= r - kRing || spin > spin_max) break;
+                }
+                QT_WAIT_END()
+                lds_after_wait();
+                if (d_seen == kStopWord) break;
+                if (spin > spin_max) {
+                    S.err = 1;
+                    break;
+                }
             }
             if (own_row) S.y[r & (kRing - 1)][i] = yk;
             lds_publish(&S.a_h, r);
@@ -643,8 +650,15 @@ hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
     }
     if (a.mode != kModeConverge || a.N + a.M >= 64) return hipErrorInvalidValue;
     const int np = (g_tune.tiny_np >= 2 && g_tune.tiny_np <= 4) ? g_tune.tiny_np : 3;  // B / C waves per role
-#define PQP_TRIO_NP(NN, MM, NPP) \
-    hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, s, a, st)
+#define PQP_TRIO_NP(NN, MM, NPP)                                                                                  \
+    do {                                                                                                          \
+        if (g_tune.tiny_acache)                                                                                   \
+            hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP, true>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, \
+                               s, a, st);                                                                         \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, s, a, \
+                               st);                                                                               \
+    } while (0)
 #define PQP_TRIO_MM(NN, MM)                      \
     do {                                         \
         if (np == 3) PQP_TRIO_NP(NN, MM, 3);     \

@@ -21,7 +21,8 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-FORMS = {"new": {}, "np2": {"tiny_np": 2}, "np4": {"tiny_np": 4}, "dense": {"tiny_dense": 1}, "old": {"tiny_old": 1}}
+FORMS = {"new": {}, "acache": {"tiny_acache": 1}, "np4_acache": {"tiny_np": 4, "tiny_acache": 1}, "np2": {"tiny_np": 2},
+         "dense": {"tiny_dense": 1}}
 
 
 def main(reps: int = 200, rounds: int = 3):

@@ -123,3 +123,19 @@ def test_persistent_traced_launch_same_bits(gpu_lib, orc):
     fine = t[n_tr * W * 4:].reshape(n_tr, W, 8)
     assert np.all(coarse[1:] > 0) and np.all(np.diff(coarse[1:], axis=2) >= 0)
     assert np.all(fine[1:, 1:] > 0) and np.all(np.diff(fine[1:, 1:], axis=2) >= 0)
+
+
+@pytest.mark.parametrize("xcds", [2, 4])
+def test_persistent_packed_on_fewer_xcds(gpu_lib, orc, xcds):
+    """persist_xcds (A/B knob): the workgroups of the persistent launch packed
+    onto 2 or 4 XCDs (the rest of a padded grid leaves at once) -- the same
+    bits as the oracle at n_dual 1024 and at a ragged size."""
+    for N in (1024, 437):
+        P = _dual(orc, N)
+        old = gpu_lib.tune("persist_xcds", xcds)
+        try:
+            r = _solve(gpu_lib, P, 257)[0]
+            assert gpu_lib.tune_get("last_path") == 1, "not the persistent launch"
+        finally:
+            gpu_lib.tune("persist_xcds", old)
+        assert_bitwise(r["Y"], orc.iterate(P["Qd"], P["Fd"], N, 256), f"N={N} on {xcds} XCDs")
