@@ -89,8 +89,11 @@ extern "C" {
  *                          2^26 element updates; a solve that needs more resumes
  *                          from the device state in further launches)
  *   persist_xcds [0]       k_split_persist's workgroups on this many XCDs (the grid
- *                          padded with workgroups that leave at once; 0: spread
- *                          over all eight)
+ *                          padded with workgroups that leave at once; 0: 4, 8:
+ *                          spread over all eight)
+ *   converge_xcds [0]      the same for k_converge_persist (0: all eight)
+ *   tiny_apoll [0]         k_solve_quintet's update wave reads the decision word
+ *                          every update (default: only when its ring is full)
  *   tiny_np [0]            k_solve_quintet's B and C roles on 2, 3 (0: default)
  *                          or 4 waves each (iterate r on B / C wave r mod np)
  *   tiny_fallback [0]      read a tiny solve's results from its device copies as

@@ -128,6 +128,7 @@ struct CvArgs {
     u64* trace;           // tuning: [2][iterate][kTraceIds][4] s_memrealtime, then s_memtime marks of workgroup 0 of each role
     int trace_n;
     int stall_wg;  // tuning: this workgroup never runs (error-path tests; -1: none)
+    int xcds;      // > 0: the roles' workgroups on this many XCDs (blockIdx % 8 < xcds take part)
 };
 
 namespace {
@@ -863,7 +864,12 @@ __device__ void decide_role(const CvArgs& a, float* lds) {
 template <bool TRACE>
 __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.x, tid = threadIdx.x;
+    int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (a.xcds > 0) {  // packed onto a.xcds XCDs (round-robin placement): the rest leave at once
+        if ((b & 7) >= a.xcds) return;
+        b = (b >> 3) * a.xcds + (b & 7);
+    }
     if (b == a.stall_wg) return;  // as if not resident: the other roles' waits expire into err
     if (b >= a.g4) {
         decide_role<TRACE>(a, lds);
@@ -1051,16 +1057,20 @@ hipError_t launch_converge_persist(const ConvergeLaunch& L, hipStream_t s) {
     a.trace = g_tune.converge_trace;
     a.trace_n = g_tune.converge_trace_n;
     a.stall_wg = g_tune.persist_stall_wg;
+    // converge_xcds x (A/B): the G workgroups packed onto x XCDs (x * 32 >= G)
+    a.xcds = (g_tune.converge_xcds > 0 && g_tune.converge_xcds < 8 && g_tune.converge_xcds * 32 >= G)
+                 ? g_tune.converge_xcds : 0;
+    const int grid = a.xcds ? 8 * ((G + a.xcds - 1) / a.xcds) : G;
     hipError_t e = hipMemsetAsync(ring, 0, sizeof(u64) * converge_ring_words(L.N, L.M), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_converge_init, dim3(4), dim3(256), 0, s, L.Y, L.N, L.u0, a.ry, L.ctl, L.decided, L.err);
     const int W = waves_of(split_kblocks(L.N > L.M ? L.N : L.M));
     const int threads = 64 * (W > kDecW ? W : kDecW);
     if (a.trace)
-        hipLaunchKernelGGL(k_converge_persist<true>, dim3(G), dim3(threads), converge_persist_lds_bytes(L.N, L.M), s,
-                           a);
+        hipLaunchKernelGGL(k_converge_persist<true>, dim3(grid), dim3(threads), converge_persist_lds_bytes(L.N, L.M),
+                           s, a);
     else
-        hipLaunchKernelGGL(k_converge_persist<false>, dim3(G), dim3(threads), converge_persist_lds_bytes(L.N, L.M),
+        hipLaunchKernelGGL(k_converge_persist<false>, dim3(grid), dim3(threads), converge_persist_lds_bytes(L.N, L.M),
                            s, a);
     return hipGetLastError();
 }

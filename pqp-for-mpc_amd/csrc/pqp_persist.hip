@@ -418,10 +418,12 @@ hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int u
     hipError_t e = hipMemsetAsync(gran, 0, sizeof(u64) * 2 * N, s);
     if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    // persist_xcds x: the G workgroups packed onto x XCDs (x * 32 >= G), the
-    // grid padded with workgroups that leave at once
-    const int xcds = (g_tune.persist_xcds > 0 && g_tune.persist_xcds < 8 && g_tune.persist_xcds * 32 >= G)
-                         ? g_tune.persist_xcds : 0;
+    // the G workgroups packed onto x XCDs (x * 32 >= G), the grid padded with
+    // workgroups that leave at once: 4 by default (n_dual 1024, 64 workgroups:
+    // 3.58 -> 3.49 ms per 1000 updates against all eight XCDs, 3.71 on two;
+    // profiles/r06/persist_xcd_ab_r06l.json); persist_xcds 8 spreads them
+    const int want = g_tune.persist_xcds > 0 ? g_tune.persist_xcds : 4;
+    const int xcds = (want < 8 && want * 32 >= G) ? want : 0;
     const int grid = xcds ? 8 * ((G + xcds - 1) / xcds) : G;
     if (g_tune.persist_trace)
         hipLaunchKernelGGL(k_split_persist<true>, dim3(grid), dim3(64 * W), persist_lds_bytes(N), s, SP, fdpn, N,

@@ -3,8 +3,10 @@ problem is uploaded once; each solve is one pqp_problem_solve call (launch,
 synchronisation, results on the host).  Forms, alternating in one process:
   new    k_fixed_one (sparse form where the split rows allow) / k_solve_quintet,
          results written by the kernel to pinned host memory
-  np2    k_solve_quintet with two B and two C waves (round 5's five waves; the
-         default is three of each since round 6), np4 with four
+  np4    k_solve_quintet with four B and four C waves (the default: three of
+         each since round 6)
+  apoll  the update wave reads the decision word every update (default: only
+         when its ring is full); np2_apoll is round 5's kernel
   dense  k_fixed_one's dense form only (pqp_tune tiny_dense)
   old    the round-4 k_fixed_tiny / k_solve_wave with state copies (tiny_old)
 Each solve's bits are checked against tests/golden/bundled.npz.  Run under
@@ -21,7 +23,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-FORMS = {"new": {}, "acache": {"tiny_acache": 1}, "np4_acache": {"tiny_np": 4, "tiny_acache": 1}, "np2": {"tiny_np": 2},
+FORMS = {"new": {}, "apoll": {"tiny_apoll": 1}, "np4": {"tiny_np": 4}, "np2_apoll": {"tiny_np": 2, "tiny_apoll": 1},
          "dense": {"tiny_dense": 1}}
 
 

@@ -189,3 +189,33 @@ def test_persistent_feasible_chunked(gpu_lib, orc, persistent, chunk):
     _same(r, h, Y, U, f"feasible chunk={chunk}")
     _, Jp, Jd = _terminate_costs(orc, P, Y)
     assert np.float32(r["Jp"]) == np.float32(Jp) and np.float32(r["Jd"]) == np.float32(Jd)
+
+
+@pytest.mark.parametrize("xcds", [6, 7])
+def test_persistent_converge_packed_on_fewer_xcds(gpu_lib, golden_converge, orc, persistent, xcds):
+    """converge_xcds (A/B knob): the roles' workgroups packed onto 6 or 7 XCDs
+    (the rest of a padded grid leaves at once) -- the reference's h, Y*, U*
+    on the converging fixtures, and a capped n_dual 1024 solve equal to the
+    spread launch's."""
+    old = gpu_lib.tune("converge_xcds", xcds)
+    try:
+        cases, Ys, Us = golden_converge["cases"], golden_converge["Y"], golden_converge["U"]
+        yo = uo = 0
+        for (N, M, seed, h_ref) in cases:
+            N, M = int(N), int(M)
+            P = orc.synth_problem(int(seed), 0, N, M)
+            r = gpu_lib.solve_dual(P, max_updates=CAP)
+            assert r["converged"] and r["h"] == int(h_ref), (N, M, seed, r["h"])
+            assert_bitwise(r["Y"], Ys[yo:yo + N], f"Y {N}/{M}/{seed} on {xcds} XCDs")
+            assert_bitwise(r["U"], Us[uo:uo + M], f"U {N}/{M}/{seed} on {xcds} XCDs")
+            yo += N
+            uo += M
+        P = orc.synth_problem(3, 0, 1024, 512)
+        packed = gpu_lib.solve_dual(P, max_updates=40)
+        assert gpu_lib.tune_get("last_path") == 3
+    finally:
+        gpu_lib.tune("converge_xcds", old)
+    spread = gpu_lib.solve_dual(P, max_updates=40)
+    assert packed["h"] == spread["h"] == 41
+    assert_bitwise(packed["Y"], spread["Y"], "n_dual 1024 Y, packed vs spread")
+    assert_bitwise(packed["U"], spread["U"], "n_dual 1024 U, packed vs spread")

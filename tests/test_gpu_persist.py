@@ -125,10 +125,11 @@ def test_persistent_traced_launch_same_bits(gpu_lib, orc):
     assert np.all(fine[1:, 1:] > 0) and np.all(np.diff(fine[1:, 1:], axis=2) >= 0)
 
 
-@pytest.mark.parametrize("xcds", [2, 4])
+@pytest.mark.parametrize("xcds", [2, 3, 8])
 def test_persistent_packed_on_fewer_xcds(gpu_lib, orc, xcds):
-    """persist_xcds (A/B knob): the workgroups of the persistent launch packed
-    onto 2 or 4 XCDs (the rest of a padded grid leaves at once) -- the same
+    """persist_xcds: the workgroups of the persistent launch packed onto 2 or 3
+    XCDs, or spread over all 8 (the default packs them onto 4, which every
+    other test takes; the rest of a padded grid leaves at once) -- the same
     bits as the oracle at n_dual 1024 and at a ragged size."""
     for N in (1024, 437):
         P = _dual(orc, N)

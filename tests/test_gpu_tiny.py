@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}, "np2": {"tiny_np": 2},
-         "np4": {"tiny_np": 4}, "acache": {"tiny_acache": 1}}
+         "np4": {"tiny_np": 4}, "apoll": {"tiny_apoll": 1}}
 
 
 @contextmanager
@@ -63,7 +63,7 @@ def test_bundled_both_modes_every_form(gpu_lib, golden_bundled, form):
             assert_bitwise(f["Y"], g[f"Y_h{k}"], f"{form}: Y after {k - 1} updates")
 
 
-@pytest.mark.parametrize("form", ["sparse", "dense", "np2", "np4", "acache"])
+@pytest.mark.parametrize("form", ["sparse", "dense", "np2", "np4", "apoll"])
 @pytest.mark.parametrize("cap", [1, 2, 3, 7, 8, 9, 16, 311])
 def test_bundled_converge_capped(gpu_lib, golden_bundled, orc, form, cap):
     """A cap inside and at the ring's depth (8 iterates in flight): the solve
@@ -162,7 +162,7 @@ def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled, np_):
     bad = []
     stale0 = gpu_lib.tune_get("tiny_stale")
     prev_np = gpu_lib.tune("tiny_np", np_)  # round 6: three B / C waves per role
-    prev_ac = gpu_lib.tune("tiny_acache", 1 if np_ == 3 else 0)
+    prev_ac = gpu_lib.tune("tiny_apoll", 1 if np_ == 2 else 0)  # np 2 with polling: round 5's kernel
     for n in range(200):
         r = gpu_lib.solve_dual(P, max_updates=CAP)
         if r["h"] != 313 or r["Y"].tobytes() != g["Ystar"].tobytes() or r["U"].tobytes() != g["Ustar"].tobytes():
@@ -177,7 +177,7 @@ def test_repeated_one_shot_solves_stay_exact(gpu_lib, golden_bundled, np_):
         if f["Y"].tobytes() != g["Y_fixed999"].tobytes():
             bad.append(("fixed", 1000, n, f["h"]))
     gpu_lib.tune("tiny_np", prev_np)
-    gpu_lib.tune("tiny_acache", prev_ac)
+    gpu_lib.tune("tiny_apoll", prev_ac)
     assert not bad, bad[:10]
     # every solve's pinned output carried its own launch's tag (the device-copy
     # fallback never ran)
