@@ -869,6 +869,7 @@ __global__ void __launch_bounds__(64 * kMaxW, 1) k_converge_persist(CvArgs a) {
     if (a.xcds > 0) {  // packed onto a.xcds XCDs (round-robin placement): the rest leave at once
         if ((b & 7) >= a.xcds) return;
         b = (b >> 3) * a.xcds + (b & 7);
+        if (b > a.g4) return;  // past the G = g4 + 1 workgroups (G not a multiple of xcds)
     }
     if (b == a.stall_wg) return;  // as if not resident: the other roles' waits expire into err
     if (b >= a.g4) {

@@ -152,6 +152,9 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     if (xcds > 0) {
         if ((int)(blockIdx.x & 7) >= xcds) return;
         wg = (int)(blockIdx.x >> 3) * xcds + (int)(blockIdx.x & 7);
+        // the padded grid's last row of participants can run past the G
+        // workgroups the problem has (G not a multiple of xcds)
+        if (wg >= (2 * N + kPLanes - 1) / kPLanes) return;
     }
     // tuning (error-path tests): this workgroup never runs, as if it were not
     // resident; every other one's waits expire and report through err
