@@ -91,7 +91,8 @@ extern "C" {
  *   persist_xcds [0]       k_split_persist's workgroups on this many XCDs (the grid
  *                          padded with workgroups that leave at once; 0: 4, 8:
  *                          spread over all eight)
- *   converge_xcds [0]      the same for k_converge_persist (0: all eight)
+ *   converge_xcds [0]      the same for k_converge_persist (0: 6 where the grid
+ *                          fits, 8: all eight)
  *   tiny_apoll [0]         k_solve_quintet's update wave reads the decision word
  *                          every update (default: only when its ring is full)
  *   tiny_np [0]            k_solve_quintet's B and C roles on 2, 3 (0: default)
