@@ -335,6 +335,8 @@ class Problem:
     KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 
     def __init__(self, P: dict, device: int | None = None, stream=None):
+        import threading
+
         self.N, self.M = int(P["N"]), int(P["M"])
         a = [_f32(P[k]) for k in self.KEYS]
         h = C.c_void_p()
@@ -343,20 +345,28 @@ class Problem:
         _check(lib().pqp_problem_create_on(-1 if device is None else int(device), stream, *[_buf(x) for x in a],
                                            self.N, self.M, C.byref(h)))
         self._h = h
+        # the outputs and their ctypes pointers are made once (building a
+        # pointer per call cost ~4 us each -- a fifth of a bundled solve); a
+        # lock keeps two threads solving this handle from sharing them (the
+        # library serializes the solves of one handle anyway)
+        self._Y, self._U = np.zeros(self.N, np.float32), np.zeros(self.M, np.float32)
+        self._jp, self._jd = np.zeros(1, np.float32), np.zeros(1, np.float32)
+        self._hv = C.c_longlong(0)
+        self._args = (_buf(self._Y), _buf(self._U), C.byref(self._hv), _buf(self._jp), _buf(self._jd))
+        self._solve = lib().pqp_problem_solve
+        self._lock = threading.Lock()
 
     @property
     def device(self) -> int:
         return int(lib().pqp_problem_device(self._h))
 
     def solve(self, mode: int = MODE_CONVERGE, num_iter: int = 1000, max_updates: int = 0) -> dict:
-        Y, U = np.zeros(self.N, np.float32), np.zeros(self.M, np.float32)
-        h = C.c_longlong(0)
-        jp, jd = np.zeros(1, np.float32), np.zeros(1, np.float32)
-        rc = lib().pqp_problem_solve(self._h, mode, num_iter, max_updates, _buf(Y), _buf(U), C.byref(h), _buf(jp),
-                                     _buf(jd))
-        if rc not in (PQP_OK, PQP_ERR_NOT_CONVERGED):
-            _check(rc)
-        return dict(h=int(h.value), Y=Y, U=U, Jp=float(jp[0]), Jd=float(jd[0]), converged=(rc == PQP_OK))
+        with self._lock:
+            rc = self._solve(self._h, mode, num_iter, max_updates, *self._args)
+            if rc not in (PQP_OK, PQP_ERR_NOT_CONVERGED):
+                _check(rc)
+            return dict(h=int(self._hv.value), Y=self._Y.copy(), U=self._U.copy(), Jp=float(self._jp[0]),
+                        Jd=float(self._jd[0]), converged=(rc == PQP_OK))
 
     def close(self):
         if self._h:
