@@ -232,12 +232,30 @@ __global__ void __launch_bounds__(64) k_fixed_one(SolveArgs A, SolveState* __res
     int n = todo > 0 ? (int)todo : 0;
     int dense_from = 0;  // updates done in the sparse form
     if (!(A.tiny_flags & kTinyDense) && pmax <= 12) {
-        // the sparse form while every y is finite
+        // the sparse form while every y is finite.  Blocks of 8 updates test
+        // the finiteness of each update's input once per block (a per-lane
+        // flag beside the chain, not a branch on it; round 6); a block that met
+        // a non-finite y is done again from its start in the dense form.  The
+        // last < 8 updates test before each update.
 #define PQP_SPARSE_LOOP(PP)                                                   \
-    for (; dense_from < n; ++dense_from) {                                    \
-        if (__any(!__builtin_isfinite(yk))) break;                            \
-        yk = update_sparse<PP>(sc, sa, fd_own, yk, own_row);                  \
-    }
+    while (dense_from + 8 <= n) {                                             \
+        const float y_blk = yk;                                               \
+        bool nf = false;                                                      \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                       \
+            nf |= !__builtin_isfinite(yk);                                    \
+            yk = update_sparse<PP>(sc, sa, fd_own, yk, own_row);              \
+        }                                                                     \
+        if (__any(nf)) {                                                      \
+            yk = y_blk;                                                       \
+            break;                                                            \
+        }                                                                     \
+        dense_from += 8;                                                      \
+    }                                                                         \
+    if (dense_from + 8 > n)                                                   \
+        for (; dense_from < n; ++dense_from) {                                \
+            if (__any(!__builtin_isfinite(yk))) break;                        \
+            yk = update_sparse<PP>(sc, sa, fd_own, yk, own_row);              \
+        }
         if (pmax <= 2) {
             PQP_SPARSE_LOOP(2)
         } else if (pmax <= 4) {
