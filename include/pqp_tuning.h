@@ -95,6 +95,8 @@ extern "C" {
  *                          fits, 8: all eight)
  *   tiny_apoll [0]         k_solve_quintet's update wave reads the decision word
  *                          every update (default: only when its ring is full)
+ *   tiny_ablk [0]          k_solve_quintet's update wave publishes every update
+ *                          (1) instead of every second one (0: two per pass)
  *   tiny_np [0]            k_solve_quintet's B and C roles on 2, 3 (0: default)
  *                          or 4 waves each (iterate r on B / C wave r mod np)
  *   tiny_fallback [0]      read a tiny solve's results from its device copies as

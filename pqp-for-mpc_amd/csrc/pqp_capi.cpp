@@ -2064,6 +2064,7 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_stall", &g_tune.tiny_stall, nullptr, nullptr},
         {"tiny_fallback", &g_tune.tiny_fallback, nullptr, nullptr},
         {"tiny_np", &g_tune.tiny_np, nullptr, nullptr},
+        {"tiny_ablk", &g_tune.tiny_ablk, nullptr, nullptr},
         {"tiny_apoll", &g_tune.tiny_apoll, nullptr, nullptr},
         {"persist_xcds", &g_tune.persist_xcds, nullptr, nullptr},
         {"converge_xcds", &g_tune.converge_xcds, nullptr, nullptr},

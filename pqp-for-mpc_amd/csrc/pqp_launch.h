@@ -153,6 +153,7 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
     int persist_xcds = 0;  // k_split_persist's workgroups packed onto this many XCDs (0: 4, 8: spread over all)
     int converge_xcds = 0;  // k_converge_persist's workgroups packed onto this many XCDs (0: 6, 8: spread over all)
     int tiny_apoll = 0;  // k_solve_quintet's update wave polls the decision word every update (default: only when the ring is full)
+    int tiny_ablk = 0;  // k_solve_quintet's update wave: 1 = publish every update (round 6 before r06q); default 2 per pass
     int tiny_np = 0;  // k_solve_quintet's B / C waves per role: 2, 3 (0: default) or 4
     int tiny_fallback = 0;  // the host reads a tiny solve's device copies as if the pinned output were stale (tests)
     long long tiny_chunk = 0;  // iterates per one-launch tiny solve launch (0: about 2^26 element updates)

@@ -310,7 +310,7 @@ struct QuintetLds {
 // NP (round 6): the B and C roles on NP waves each, iterate r on B_{r mod NP}
 // and C_{r mod NP} -- 2 (five waves), 3 or 4 (seven / nine: each B / C wave
 // has NP iterates' time for its own)
-template <int NMAX, int MMAX, bool TRACE, int NP = 2, bool A_CACHE = false>
+template <int NMAX, int MMAX, bool TRACE, int NP = 2, bool A_CACHE = false, int ABLK = 1>
 __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A, SolveState* __restrict__ st) {
     static_assert(NMAX % 4 == 0 && MMAX % 4 == 0 && NMAX <= 32 && MMAX <= 32, "one wave per role");
     static_assert(NP >= 2 && NP <= 4, "two to four B / C waves");
@@ -373,14 +373,31 @@ __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A
         if (own_row) S.y[0][i] = yk;
         lds_publish(&S.a_h, 0);
         int d_seen = -1;
-        for (int r = 1;; ++r) {
-            // the sparse form only while every y is finite (the skipped +-0 terms are then exact)
-            if (sparse && __any(!__builtin_isfinite(yk))) sparse = false;
+        for (int r = 1;; r += ABLK) {
+            // ABLK updates per pass.  The sparse form only while every input y
+            // is finite (the skipped +-0 terms are then exact): one test per
+            // pass, a per-lane flag beside the chain (round 6); a pass that met
+            // a non-finite y is done again densely from its start
+            float yb[ABLK];
             if (sparse) {
-                if (pmax <= 2) yk = update_sparse<2>(sc, sa, fd_own, yk, own_row);
-                else yk = update_sparse<4>(sc, sa, fd_own, yk, own_row);
+                const float y_blk = yk;
+                bool nf = false;
+#pragma unroll
+                for (int j = 0; j < ABLK; ++j) {
+                    nf |= !__builtin_isfinite(yk);
+                    if (pmax <= 2) yk = update_sparse<2>(sc, sa, fd_own, yk, own_row);
+                    else yk = update_sparse<4>(sc, sa, fd_own, yk, own_row);
+                    yb[j] = yk;
+                }
+                if (__any(nf)) {
+                    sparse = false;
+                    yk = y_blk;
+#pragma unroll
+                    for (int j = 0; j < ABLK; ++j) yb[j] = yk = update_dense<NMAX>(mat, fd_own, yk, own_row);
+                }
             } else {
-                yk = update_dense<NMAX>(mat, fd_own, yk, own_row);
+#pragma unroll
+                for (int j = 0; j < ABLK; ++j) yb[j] = yk = update_dense<NMAX>(mat, fd_own, yk, own_row);
             }
             // room in the ring: iterate r - kRing decided (or the solve over).
             // The last decision seen is kept and the word read again only when
@@ -388,12 +405,13 @@ __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A
             // 0.1144 -> 0.1045 ms per solve): no LDS round trip on the update's
             // path while A runs ahead.  A learns of the stop when the ring
             // fills (at most kRing discarded updates).
-            if (!A_CACHE || d_seen < r - kRing) {
+            // (a pass of ABLK updates needs its last slot free: iterate r + ABLK - 1 - kRing decided)
+            if (!A_CACHE || d_seen < r + ABLK - 1 - kRing) {
                 int spin = 0;
                 QT_WAIT_BEGIN()
                 for (;; ++spin) {
                     d_seen = lds_ld(&S.decided);
-                    if (d_seen == kStopWord || d_seen >= r - kRing || spin > spin_max) break;
+                    if (d_seen == kStopWord || d_seen >= r + ABLK - 1 - kRing || spin > spin_max) break;
                 }
                 QT_WAIT_END()
                 lds_after_wait();
@@ -403,8 +421,10 @@ __global__ void __launch_bounds__(64 * (1 + 2 * NP)) k_solve_quintet(SolveArgs A
                     break;
                 }
             }
-            if (own_row) S.y[r & (kRing - 1)][i] = yk;
-            lds_publish(&S.a_h, r);
+#pragma unroll
+            for (int j = 0; j < ABLK; ++j)
+                if (own_row) S.y[(r + j) & (kRing - 1)][i] = yb[j];
+            lds_publish(&S.a_h, r + ABLK - 1);
         }
     } else if (is_b) {
         // ---------------- waves B0 / B1: the N-long sums of terminate(Y_h) ----------------
@@ -671,12 +691,15 @@ hipError_t launch_one_tiny(const SolveArgs& a, SolveState* st, hipStream_t s) {
     const int np = (g_tune.tiny_np >= 2 && g_tune.tiny_np <= 4) ? g_tune.tiny_np : 3;  // B / C waves per role
 #define PQP_TRIO_NP(NN, MM, NPP)                                                                                  \
     do {                                                                                                          \
-        if (!g_tune.tiny_apoll)                                                                                   \
+        if (g_tune.tiny_apoll)                                                                                    \
+            hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, s, a, \
+                               st);                                                                               \
+        else if (g_tune.tiny_ablk == 1)                                                                           \
             hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP, true>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, \
                                s, a, st);                                                                         \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP>), dim3(1), dim3(64 * (1 + 2 * NPP)), 0, s, a, \
-                               st);                                                                               \
+            hipLaunchKernelGGL((k_solve_quintet<NN, MM, false, NPP, true, 2>), dim3(1), dim3(64 * (1 + 2 * NPP)), \
+                               0, s, a, st);                                                                      \
     } while (0)
 #define PQP_TRIO_MM(NN, MM)                      \
     do {                                         \

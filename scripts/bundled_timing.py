@@ -23,8 +23,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "pqp-for-mpc_amd"))
 
-FORMS = {"new": {}, "apoll": {"tiny_apoll": 1}, "np4": {"tiny_np": 4}, "np2_apoll": {"tiny_np": 2, "tiny_apoll": 1},
-         "dense": {"tiny_dense": 1}}
+FORMS = {"new": {}, "ablk1": {"tiny_ablk": 1}, "apoll": {"tiny_apoll": 1}, "np4": {"tiny_np": 4}}
 
 
 def main(reps: int = 200, rounds: int = 3):

@@ -3,6 +3,7 @@ its host-only pieces (file reader, argument validation) behave like the
 reference.  No GPU compute is issued here."""
 from __future__ import annotations
 
+import functools
 import re
 import subprocess
 from pathlib import Path
@@ -71,7 +72,9 @@ def test_python_mirror_arity_matches_header():
     assert not bad, bad
 
 
+@functools.lru_cache(maxsize=None)
 def _gfx950_asm(name: str) -> str:
+    """The gfx950 assembly of one kernel TU, compiled once per session."""
     import tempfile
 
     hipcc = Path("/opt/rocm/bin/hipcc")
@@ -115,7 +118,10 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
 
 
 @pytest.mark.parametrize("src,name", [
-    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_ii"),
+    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_iii"),
+    # the headline kernel: its register blocks pinned in AGPRs across the
+    # launch (pqp_kernels.hip k_batch_resident) must stay there
+    ("pqp_kernels.hip", "_ZN3pqp16k_batch_residentILi16ELi2ELi2EEEvPKfxiS2_S2_iS2_Pfi"),
     ("pqp_converge.hip", "_ZN3pqp12_GLOBAL__N_118k_converge_persistILb0EEEvNS_6CvArgsE"),
     ("pqp_kernels.hip", "_ZN3pqp12k_solve_pipeILi256ELi2ELi16ELi2ELb1EEEvNS_9SolveArgsEPNS_10SolveStateE"),
     ("pqp_kernels.hip", "_ZN3pqp12k_solve_pipeILi256ELi2ELi16ELi2ELb0EEEvNS_9SolveArgsEPNS_10SolveStateE"),
@@ -126,7 +132,8 @@ def test_persistent_kernels_do_not_spill(src, name):
     spill to scratch costs 0.3 us per update (measured on k_converge_persist),
     so the default instantiations must have no scratch.  k_solve_pipe's
     builds at two workgroups per CU (up to 256 VGPRs: a 128 x 96 Gp tile, or two
-    64 x 64 ones, and 16 update loads per lane in flight) must not spill either."""
+    64 x 64 ones, and 16 update loads per lane in flight) must not spill either,
+    nor may k_batch_resident's AGPR-held Qd blocks."""
     asm = _gfx950_asm(src)
     i = asm.index("\n" + name + ":")
     m = re.search(r"; ScratchSize: (\d+)", asm[i:])
@@ -222,7 +229,8 @@ def test_tuning_knobs_roundtrip():
 
     L = pqp_amd.lib()
     for key in ("persist_off", "lean_min_n", "batch_opts", "converge_chunk", "wide_min_n", "pipe_off",
-                "pipe_variant", "pipe_force", "mid_v1", "matmul_pk_off", "iterate_kind", "tiny_chunk", "tiny_fallback"):
+                "pipe_variant", "pipe_force", "mid_v1", "matmul_pk_off", "iterate_kind", "tiny_chunk", "tiny_fallback",
+                "tiny_np", "tiny_apoll", "tiny_ablk", "persist_xcds", "converge_xcds"):
         old = pqp_amd.tune_get(key)
         assert pqp_amd.tune(key, old + 3) == old
         assert pqp_amd.tune_get(key) == old + 3

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 KEYS = ("Qd", "Fd", "Md", "Qp", "Qp_inv", "Fp", "Mp", "Gp", "Kp")
 FORMS = {"sparse": {}, "dense": {"tiny_dense": 1}, "round4": {"tiny_old": 1}, "np2": {"tiny_np": 2},
-         "np4": {"tiny_np": 4}, "apoll": {"tiny_apoll": 1}}
+         "np4": {"tiny_np": 4}, "apoll": {"tiny_apoll": 1}, "ablk1": {"tiny_ablk": 1}, "ablk1_np4": {"tiny_ablk": 1, "tiny_np": 4}}
 
 
 @contextmanager
@@ -63,7 +63,7 @@ def test_bundled_both_modes_every_form(gpu_lib, golden_bundled, form):
             assert_bitwise(f["Y"], g[f"Y_h{k}"], f"{form}: Y after {k - 1} updates")
 
 
-@pytest.mark.parametrize("form", ["sparse", "dense", "np2", "np4", "apoll"])
+@pytest.mark.parametrize("form", ["sparse", "dense", "np2", "np4", "apoll", "ablk1", "ablk1_np4"])
 @pytest.mark.parametrize("cap", [1, 2, 3, 7, 8, 9, 16, 311])
 def test_bundled_converge_capped(gpu_lib, golden_bundled, orc, form, cap):
     """A cap inside and at the ring's depth (8 iterates in flight): the solve
@@ -127,7 +127,7 @@ def test_converge_sparse_update_past_overflow(gpu_lib, orc, N, M, np_):
     P = _growing_problem(N, M, N + 1)
     for cap in (100, 500):
         h, Y, U = orc.solve(P, 0, 1000, cap)
-        with tuned(gpu_lib, {"tiny_np": np_}):
+        with tuned(gpu_lib, {"tiny_np": np_, "tiny_ablk": {2: 1, 3: 2, 4: 1}[np_]}):
             r = gpu_lib.solve_dual(P, max_updates=cap)
         # the oracle returns -h when capped; a NaN cost passes every gap test
         # (NaN comparisons are false), so the reference may also stop there
