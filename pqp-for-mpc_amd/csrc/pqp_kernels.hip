@@ -3627,6 +3627,63 @@ __device__ __forceinline__ float mid_sum(const float* v, int n8) {
     return s;
 }
 
+// A walk over nb blocks with the loads of D - 1 blocks in flight ahead of the
+// block being summed (round 6, k_solve_mid2): at 8 waves per CU an LDS read
+// returns later than one block's few instructions take, which left every
+// block of the one-block-ahead forms above waiting.  buf[u] holds block
+// jb + u; a load past the end re-reads the last block (harmless, no branch).
+// Blocks are summed in order, so every sum keeps its k order.
+template <int D, class Blk, class Load, class Acc>
+__device__ __forceinline__ void ring_walk(int nb, Load load, Acc acc) {
+    Blk buf[D];
+#pragma unroll
+    for (int u = 0; u < D - 1; ++u) load(buf[u], u < nb ? u : nb - 1);
+    int jb = 0;
+    for (; jb + D <= nb; jb += D) {
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+            const int nxt = jb + u + D - 1;
+            load(buf[(u + D - 1) % D], nxt < nb ? nxt : nb - 1);
+            acc(buf[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < D - 1; ++u)
+        if (jb + u < nb) acc(buf[u]);
+}
+// mid_dot_row / mid_sum / mid_dot through ring_walk (n8 a multiple of 8, >= 8)
+template <int D, bool PK = false>
+__device__ __forceinline__ float mid_dot_row_ring(const float* a, const float* b, int n8) {
+    float s = 0.0f;
+    ring_walk<D, RowDotBlk>(
+        n8 >> 3, [&](RowDotBlk& B, int j) { rowdot_load(B, a, b, 8 * j); },
+        [&](const RowDotBlk& B) { rowdot_acc<PK>(s, B); });
+    return s;
+}
+struct SumBlk {
+    sf4 c0, c1;
+};
+template <int D>
+__device__ __forceinline__ float mid_sum_ring(const float* v, int n8) {
+    float s = 0.0f;
+    ring_walk<D, SumBlk>(
+        n8 >> 3,
+        [&](SumBlk& B, int j) {
+            B.c0 = *reinterpret_cast<const sf4*>(v + 8 * j);
+            B.c1 = *reinterpret_cast<const sf4*>(v + 8 * j + 4);
+        },
+        [&](const SumBlk& B) { mid_add8(s, B.c0, B.c1); });
+    return s;
+}
+template <int D, bool PK = false>
+__device__ __forceinline__ float mid_dot_ring(const float* a, int as, const float* b, int n8) {
+    float s = 0.0f;
+    ring_walk<D, MidBlk>(
+        n8 >> 3, [&](MidBlk& B, int j) { mid_load(B, a, as, b, 8 * j); },
+        [&](const MidBlk& B) { mid_acc<PK>(s, B); });
+    return s;
+}
+
 // The split entries of one off-diagonal Qd value q in max form, qp =
 // (q<0?0:q) and qn = (q>0?0:-q) (bit-identical to the reference's
 // max(0,+-q)+0.0f products).  FAST (the problem's Qd holds no NaN,
@@ -4035,6 +4092,34 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
 // has the whole range as its band; an MPC problem's stage structure (the
 // horizon leg: 28-row blocks) leaves a wave of 32 or 64 rows 28-84 of the k.
 // ---------------------------------------------------------------------------
+// Round 6 (profiles/r06/mid2_ring_qpt_r06t.txt, bits identical): the T, C and
+// cost waves' row dots and sums keep their loads three blocks deep and the
+// strided checkFeas dots two (ring_walk), and Qp is staged transposed so the
+// cost wave's U'Qp terms read 16-byte rows instead of strided words: H = 4 /
+// 5 28.2 / 57.4 -> 25.2 / 51.2 ms, the dense n_dual 140 companion 84.7 -> 77.7
+#ifndef PQP_M2_QPT  // k_solve_mid2: Qp kept transposed (the cost wave's U'Qp terms read rows)
+#define PQP_M2_QPT 1
+#endif
+#ifndef PQP_M2_RING  // k_solve_mid2's row dots and sums: loads this many blocks deep (0: one ahead)
+#define PQP_M2_RING 3
+#endif
+#ifndef PQP_M2_RINGD  // ... and the strided dots (checkFeas rows)
+#define PQP_M2_RINGD 2
+#endif
+template <bool PK>
+__device__ __forceinline__ float m2_dot_row(const float* a, const float* b, int n8) {
+    if constexpr (PQP_M2_RING >= 2) return mid_dot_row_ring<PQP_M2_RING, PK>(a, b, n8);
+    else return mid_dot_row<PK>(a, b, n8);
+}
+template <bool PK>
+__device__ __forceinline__ float m2_dot(const float* a, int as, const float* b, int n8) {
+    if constexpr (PQP_M2_RINGD >= 2) return mid_dot_ring<PQP_M2_RINGD, PK>(a, as, b, n8);
+    else return mid_dot<PK>(a, as, b, n8);
+}
+__device__ __forceinline__ float m2_sum(const float* v, int n8) {
+    if constexpr (PQP_M2_RING >= 2) return mid_sum_ring<PQP_M2_RING + 1>(v, n8);
+    else return mid_sum(v, n8);
+}
 struct Mid2Layout {
     int nk, mk, ldn, ldm, ldg, ldi;
     int y, tq, dP, dN, Fdp, Fdn, Kp, tM, Us, tu, fu, Fp, fdy, flag, band, sums, Qd, Gp, Qi, Qp, total;
@@ -4044,7 +4129,7 @@ __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
     L.nk = round8(N);
     L.mk = round8(M);
     L.ldn = L.nk + 4;
-    L.ldm = L.mk + 1;
+    L.ldm = PQP_M2_QPT ? L.mk + 4 : L.mk + 1;  // QPT: Qp' rows, 16-byte aligned
     L.ldg = L.nk + 4;
     L.ldi = L.mk + 4;
     int o = 0;
@@ -4314,7 +4399,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         for (int e = tid; e < M * M; e += NT) {
             const int i = e / M, j = e - i * M;
             Qi[i * ldi + j] = A.Qinv[e];
-            Qp[i * ldm + j] = A.Qp[e];
+            if (PQP_M2_QPT) Qp[j * ldm + i] = A.Qp[e];
+            else Qp[i * ldm + j] = A.Qp[e];
         }
         for (int i = tid; i < N; i += NT) Kp[i] = A.Kp[i];
         for (int j = tid; j < M; j += NT) Fp[j] = A.Fp[j];
@@ -4511,12 +4597,12 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             const float* ycur = Yr + (int)(s % 3) * nk;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
             if (lane <= M) {
-                const float d = mid_dot_row<PK && PQP_M2PK_T>(grow, ycur, nk);
+                const float d = m2_dot_row<PK && PQP_M2PK_T>(grow, ycur, nk);
                 if (lane < M) tM[lane] = d + 1.0f * fpl;  // :355-356
                 else fdy[s & 1] = d;                      // Fd.Y :656
             }
             __builtin_amdgcn_wave_barrier();
-            if (lane < M) Us[(s & 1) * mk + lane] = -mid_dot_row<PK && PQP_M2PK_T>(qirow, tM, mk);  // :357-358
+            if (lane < M) Us[(s & 1) * mk + lane] = -m2_dot_row<PK && PQP_M2PK_T>(qirow, tM, mk);  // :357-358
             if (phase_end(s)) break;
         }
     } else if (conv) {
@@ -4537,7 +4623,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 int bad = 0;
                 if (pend)
                     for (int i = l; i < lend; i += crows * nCR) {
-                        const float g = mid_dot<PK && PQP_M2PK_F>(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
+                        const float g = m2_dot<PK && PQP_M2PK_F>(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
                         const float kp = Kp[i];
                         if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
                     }
@@ -4551,17 +4637,19 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 const bool cb = BAND && !y_nonfinite;
                 const int klo = cb ? clo : 0, kn = (cb ? chi : nk) - klo;
                 for (int j = l; j < lend; j += crows * nCR)
-                    tqs[j] = (sym ? mid_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn + klo, ycur + klo, kn)
-                                  : mid_dot<PK && PQP_M2PK_C>(Qd + klo * ldn + j, ldn, ycur + klo, kn)) * ycur[j];
+                    tqs[j] = (sym ? m2_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn + klo, ycur + klo, kn)
+                                  : m2_dot<PK && PQP_M2PK_C>(Qd + klo * ldn + j, ldn, ycur + klo, kn)) * ycur[j];
             } else if (pend && cw == nCR) {
                 if (lane < M) {
-                    tu[lane] = mid_dot<PK && PQP_M2PK_Q>(Qp + lane, ldm, Uo, mk) * Uo[lane];  // (U'Qp).U terms :652-655
+                    tu[lane] = (PQP_M2_QPT ? m2_dot_row<PK && PQP_M2PK_Q>(Qp + lane * ldm, Uo, mk)
+                                           : m2_dot<PK && PQP_M2PK_Q>(Qp + lane, ldm, Uo, mk)) *
+                               Uo[lane];  // (U'Qp).U terms :652-655 (column lane of Qp)
                     fu[lane] = Fp[lane] * Uo[lane];                         // Fp'U :656-657
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (lane < 3) {
                     const float* v = lane == 0 ? tq + ((s - 1) & 1) * nk : (lane == 1 ? tu : fu);
-                    const float r = mid_sum(v, lane == 0 ? nk : mk);
+                    const float r = m2_sum(v, lane == 0 ? nk : mk);
                     sums[lane] = r;
                 }
             }

@@ -53,6 +53,15 @@ hpmc)
     cat $D.json
   done
   ;;
+hlds)
+  # k_solve_mid2's wave-state and LDS counters (where the phase's cycles go):
+  # one pass per workload, SQ only (8 counters)
+  for H in ${HLDS_SET:-4 5 d140}; do
+    D=$O/l$H
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS --kernel-trace --output-format csv -d $D -o pmc -- python3 scripts/horizon_pmc.py $H > $D.json 2> $D.err || { tail -5 $D.err; exit 1; }
+    cat $D.json
+  done
+  ;;
 hab)
   # horizon A/B: bash scripts/gpu_r05.sh hab TAG "H knob=v ..." "H knob=v ..." ...
   shift 2
