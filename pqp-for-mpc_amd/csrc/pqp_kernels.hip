@@ -4106,18 +4106,25 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
 #ifndef PQP_M2_RINGD  // ... and the strided dots (checkFeas rows)
 #define PQP_M2_RINGD 2
 #endif
-template <bool PK>
+#ifndef PQP_M2_RING_LEAN  // the same in the 80-VGPR builds (H = 2 / 3: 11.0 / 25.8 -> 10.0 / 23.8 ms at 2)
+#define PQP_M2_RING_LEAN 2
+#endif
+#ifndef PQP_M2_RINGD_LEAN
+#define PQP_M2_RINGD_LEAN 2
+#endif
+template <bool PK, int D>
 __device__ __forceinline__ float m2_dot_row(const float* a, const float* b, int n8) {
-    if constexpr (PQP_M2_RING >= 2) return mid_dot_row_ring<PQP_M2_RING, PK>(a, b, n8);
+    if constexpr (D >= 2) return mid_dot_row_ring<D, PK>(a, b, n8);
     else return mid_dot_row<PK>(a, b, n8);
 }
-template <bool PK>
+template <bool PK, int D>
 __device__ __forceinline__ float m2_dot(const float* a, int as, const float* b, int n8) {
-    if constexpr (PQP_M2_RINGD >= 2) return mid_dot_ring<PQP_M2_RINGD, PK>(a, as, b, n8);
+    if constexpr (D >= 2) return mid_dot_ring<D, PK>(a, as, b, n8);
     else return mid_dot<PK>(a, as, b, n8);
 }
+template <int D>
 __device__ __forceinline__ float m2_sum(const float* v, int n8) {
-    if constexpr (PQP_M2_RING >= 2) return mid_sum_ring<PQP_M2_RING + 1>(v, n8);
+    if constexpr (D >= 2) return mid_sum_ring<D + 1>(v, n8);
     else return mid_sum(v, n8);
 }
 struct Mid2Layout {
@@ -4233,8 +4240,44 @@ __device__ __forceinline__ float mid2_side(const float* q, const float* y, int k
 // row_block).  DIAG: the block lies in the 64 columns of the wave's diagonal;
 // column k + j is the diagonal of lane k + j - w0 only, which takes the literal
 // by a mask made on the scalar unit (two v_cndmask per k, no compare)
-template <bool DIAG, bool FAST>
+// product first in the one-lane-per-row update (round 6, H = 5 51.5 -> 49.9 ms,
+// dense n_dual 140 78.1 -> 73.8, profiles/r06/mid2_pf_r06v.txt); FAST then also
+// needs Qd finite and Y finite and >= 0 (the staged and per-phase flags)
+#ifndef PQP_M2_PF
+#define PQP_M2_PF 1
+#endif
+// (the one-lane-per-row build's last, 12-row update wave at n_dual 140 as lane
+// sides: slower, H = 5 50.3 -> 50.9 ms, dense 73.8 -> 79.9; profiles/r06/
+// mid2_tail_lean_r06w.txt)
+template <bool DIAG, bool FAST, bool PF = false>
 __device__ __forceinline__ void mid2_rblock(const RowBlk& B, int k, int w0, float dp, float dn, sf2& acc) {
+    if constexpr (PF) {
+        // product first (round 6): p = q y_k, then max(0, p) and max(0, -p) --
+        // the same values as max(0, +-q) y_k while Qd is finite and every y_k
+        // finite and >= 0 (PF: the staged Qd flag and the phase's Y flag; a
+        // zero's sign never matters in these sums): one multiply per k instead
+        // of two.  The diagonal's literal products (dp, dn = dP_i y_i, dN_i y_i,
+        // formed by the caller) replace the split terms by the scalar mask.
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            const sf2 q2 = j < 4 ? sf2{B.q0[j], B.q0[j + 1]} : sf2{B.q1[j - 4], B.q1[j - 3]};
+            const sf2 y2 = j < 4 ? sf2{B.y0[j], B.y0[j + 1]} : sf2{B.y1[j - 4], B.y1[j - 3]};
+            const sf2 p = q2 * y2;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float tp, tn;
+                asm("v_max_f32 %0, %1, 0" : "=v"(tp) : "v"(p[h]));
+                asm("v_max_f32_e64 %0, -%1, 0" : "=v"(tn) : "v"(p[h]));
+                if constexpr (DIAG) {
+                    const unsigned long long m = 1ull << (k + j + h - w0);
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(tp) : "v"(tp), "v"(dp), "s"(m));
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(tn) : "v"(tn), "v"(dn), "s"(m));
+                }
+                acc += sf2{tp, tn};
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const float q = j < 4 ? B.q0[j] : B.q1[j - 4];
@@ -4252,11 +4295,11 @@ __device__ __forceinline__ void mid2_rblock(const RowBlk& B, int k, int w0, floa
 // SMASK: the scalar-mask diagonal (the 128-VGPR build; the 80-VGPR build
 // keeps k_solve_mid's per-lane compare: the masks' SGPRs made it spill more,
 // H = 2 / 3 +2 / +4 %, profiles/r05/band)
-template <bool FAST, bool SMASK>
+template <bool FAST, bool SMASK, bool PF = false>
 __device__ __forceinline__ void mid2_rstep(const RowBlk& B, int k, int w0, int i, float dp, float dn, sf2& acc) {
     if constexpr (SMASK) {
-        if (k >= w0 && k < w0 + 64) mid2_rblock<true, FAST>(B, k, w0, dp, dn, acc);
-        else mid2_rblock<false, FAST>(B, k, w0, dp, dn, acc);
+        if (k >= w0 && k < w0 + 64) mid2_rblock<true, FAST, PF>(B, k, w0, dp, dn, acc);
+        else mid2_rblock<false, FAST, PF>(B, k, w0, dp, dn, acc);
     } else {
         float aq = 0.0f;
         row_step<false, FAST>(B, k, w0, i, dp, dn, acc, aq);
@@ -4264,25 +4307,31 @@ __device__ __forceinline__ void mid2_rstep(const RowBlk& B, int k, int w0, int i
 }
 // one update row on one lane, both sides packed (k_solve_mid's form):
 // Y_next[i] = num / den * y_i (PQP_CPU.c:603-618), k = klo..khi-1
-template <bool FAST, bool SMASK>
+template <bool FAST, bool SMASK, bool PF = false>
 __device__ __forceinline__ float mid2_row(const float* q, const float* y, int klo, int khi, int i, float dp,
                                           float dn, float fdn, float fdp, int w0) {
+    static_assert(!PF || (FAST && SMASK), "the product-first form is a form of the scalar-mask max form");
+    if constexpr (PF) {  // mid2_rblock's product-first form takes the diagonal's products
+        const float yi = y[i];
+        dp = dp * yi;
+        dn = dn * yi;
+    }
     sf2 acc = {0.0f, 0.0f};
     RowBlk c, x;
     row_load(c, q, y, klo);
     int k = klo;
     for (; k + 16 < khi; k += 16) {
         row_load(x, q, y, k + 8);
-        mid2_rstep<FAST, SMASK>(c, k, w0, i, dp, dn, acc);
+        mid2_rstep<FAST, SMASK, PF>(c, k, w0, i, dp, dn, acc);
         row_load(c, q, y, k + 16);
-        mid2_rstep<FAST, SMASK>(x, k + 8, w0, i, dp, dn, acc);
+        mid2_rstep<FAST, SMASK, PF>(x, k + 8, w0, i, dp, dn, acc);
     }
     if (k + 8 < khi) {
         row_load(x, q, y, k + 8);
-        mid2_rstep<FAST, SMASK>(c, k, w0, i, dp, dn, acc);
-        mid2_rstep<FAST, SMASK>(x, k + 8, w0, i, dp, dn, acc);
+        mid2_rstep<FAST, SMASK, PF>(c, k, w0, i, dp, dn, acc);
+        mid2_rstep<FAST, SMASK, PF>(x, k + 8, w0, i, dp, dn, acc);
     } else {
-        mid2_rstep<FAST, SMASK>(c, k, w0, i, dp, dn, acc);
+        mid2_rstep<FAST, SMASK, PF>(c, k, w0, i, dp, dn, acc);
     }
     const float num = acc.y + 1.0f * fdn;  // :611
     const float den = acc.x + 1.0f * fdp;  // :612
@@ -4371,6 +4420,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     const int nCR = mid2_cr(N, crows);
     const int wDec = wC0 + nCR;  // converge mode: the cost wave also takes each decision
     constexpr bool PK = MINW == 1;  // packed dot products (the 80-VGPR build spilled with them)
+    constexpr int RD = MINW == 1 ? PQP_M2_RING : PQP_M2_RING_LEAN;     // load depth of the row dots / sums
+    constexpr int RDD = MINW == 1 ? PQP_M2_RINGD : PQP_M2_RINGD_LEAN;  // ... of the strided dots
     // one decision per phase (on the cost wave) where the phase is bound by
     // VALU issue -- the lane-side build, two problems per CU at n_dual 112:
     // 38.9 -> 37.7 ms; elsewhere the single decider's latency between the
@@ -4410,7 +4461,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     for (int i = tid; i < N; i += NT) {
         const float y = st->resume ? A.Y[i] : 1000.0f;  // initMat(Y,1000) :710
         Yr[(int)(h0 % 3) * nk + i] = y;
-        if (!(fabsf(y) <= 3.402823466e38f)) ynf = 1;
+        if (!(PQP_M2_PF ? (y >= 0.0f && y <= 3.402823466e38f) : fabsf(y) <= 3.402823466e38f)) ynf = 1;
     }
     __syncthreads();
     // computeTheta (:503-519), the diagonal literals (:524-537); any NaN in
@@ -4420,7 +4471,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     // last nonzero (or NaN) of its rows and columns, the diagonal included,
     // rounded out to blocks of 8; lo kept as nk - lo so that both ends are
     // maxima over the zeroed words.
-    int nan = 0, asym = 0;
+    int nan = 0, asym = 0, qinf = 0;
     const bool dense = (A.tiny_flags & kMid2Dense) != 0;
     for (int i = tid; i < N; i += NT) {
         const float* row = Qd + i * ldn;
@@ -4429,6 +4480,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         for (int k = 0; k < N; ++k) {
             s += max_ref(0.0f, -row[k]) * 1.0f;
             if (row[k] != row[k]) nan = 1;
+            if (fabsf(row[k]) == __builtin_inff()) qinf = 1;
             if (k > i && __float_as_uint(row[k]) != __float_as_uint(Qd[k * ldn + i])) asym = 1;
             if (row[k] != 0.0f || Qd[k * ldn + i] != 0.0f) {
                 lo = k < lo ? k : lo;
@@ -4450,6 +4502,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     }
     const bool sym = !__syncthreads_or(asym);
     const bool fast = !__syncthreads_or(nan);
+    const bool qfinite = fast && !__syncthreads_or(qinf);  // the product-first update form's Qd condition
     bool y_nonfinite = __syncthreads_or(ynf);
     const float Md = conv ? A.Md[0] : 0.0f, Mp = conv ? A.Mp[0] : 0.0f;
 
@@ -4469,6 +4522,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     __syncthreads();  // dP / dN read: the tq ring may be written from here on
     const bool tr = A0.trace && (int)blockIdx.x < A0.trace_n;
     unsigned long long busy = 0, t_phase = 0, n_ph = 0, t0 = 0;
+    unsigned long long seg_a = 0;  // trace: the first part of the T / C / cost roles
 
     float Jp_last = 0.0f, Jd_last = 0.0f;
     bool costs = false;
@@ -4576,14 +4630,21 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                         const float y = ycur[urow];
                         const float yn = other / v * y;  // updY :594
                         ynext[urow] = yn;
-                        if (!(fabsf(yn) <= 3.402823466e38f)) flag[12 + (int)((s + 1) & 1)] = 1;
+                        if (!(PQP_M2_PF ? (yn >= 0.0f && yn <= 3.402823466e38f) : fabsf(yn) <= 3.402823466e38f))
+                            flag[12 + (int)((s + 1) & 1)] = 1;
                     }
                 } else {
                     // k_solve_mid's row (max form, or the selects where Qd holds a NaN)
-                    const float yn = fast ? mid2_row<true, MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0)
-                                          : mid2_row<false, MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
+                    float yn;
+                    if (PQP_M2_PF && MINW == 1 && qfinite && !y_nonfinite)
+                        yn = mid2_row<true, MINW == 1, PQP_M2_PF && MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
+                    else if (fast)
+                        yn = mid2_row<true, MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
+                    else
+                        yn = mid2_row<false, MINW == 1>(q, ycur, klo, khi, urow, dpr, dnr, fdn, fdp, w0);
                     ynext[urow] = yn;
-                    if (!(fabsf(yn) <= 3.402823466e38f)) flag[12 + (int)((s + 1) & 1)] = 1;
+                    if (!(PQP_M2_PF ? (yn >= 0.0f && yn <= 3.402823466e38f) : fabsf(yn) <= 3.402823466e38f))
+                            flag[12 + (int)((s + 1) & 1)] = 1;
                 }
             }
             if (phase_end(s)) break;  // (its second barrier: the flags are read before the next phase writes)
@@ -4597,12 +4658,13 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             const float* ycur = Yr + (int)(s % 3) * nk;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
             if (lane <= M) {
-                const float d = m2_dot_row<PK && PQP_M2PK_T>(grow, ycur, nk);
+                const float d = m2_dot_row<PK && PQP_M2PK_T, RD>(grow, ycur, nk);
                 if (lane < M) tM[lane] = d + 1.0f * fpl;  // :355-356
                 else fdy[s & 1] = d;                      // Fd.Y :656
             }
             __builtin_amdgcn_wave_barrier();
-            if (lane < M) Us[(s & 1) * mk + lane] = -m2_dot_row<PK && PQP_M2PK_T>(qirow, tM, mk);  // :357-358
+            if (tr) seg_a += __builtin_amdgcn_s_memtime() - t0;
+            if (lane < M) Us[(s & 1) * mk + lane] = -m2_dot_row<PK && PQP_M2PK_T, RD>(qirow, tM, mk);  // :357-358
             if (phase_end(s)) break;
         }
     } else if (conv) {
@@ -4623,7 +4685,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 int bad = 0;
                 if (pend)
                     for (int i = l; i < lend; i += crows * nCR) {
-                        const float g = m2_dot<PK && PQP_M2PK_F>(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
+                        const float g = m2_dot<PK && PQP_M2PK_F, RDD>(Gp + i, ldg, Uo, mk);  // row i of Gp . U  :636
                         const float kp = Kp[i];
                         if (g > kp + max_ref((float)(kTol * kp), (float)kTol)) bad = 1;  // compare :338
                     }
@@ -4631,25 +4693,27 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 // active (inside `lane == 0` it would see lane 0's rows only)
                 const bool any_bad = __any(bad);
                 if (pend && lane == 0) flag[cw] = any_bad ? 1 : 0;
+                if (tr) seg_a += __builtin_amdgcn_s_memtime() - t0;
                 float* tqs = tq + (s & 1) * nk;  // for terminate(s), next phase
                 // (Y'Qd)_j Y_j :652-655 over the band while Y_s is finite (as
                 // the update's sums); column j = row j when Qd is symmetric
                 const bool cb = BAND && !y_nonfinite;
                 const int klo = cb ? clo : 0, kn = (cb ? chi : nk) - klo;
                 for (int j = l; j < lend; j += crows * nCR)
-                    tqs[j] = (sym ? m2_dot_row<PK && PQP_M2PK_C>(Qd + j * ldn + klo, ycur + klo, kn)
-                                  : m2_dot<PK && PQP_M2PK_C>(Qd + klo * ldn + j, ldn, ycur + klo, kn)) * ycur[j];
+                    tqs[j] = (sym ? m2_dot_row<PK && PQP_M2PK_C, RD>(Qd + j * ldn + klo, ycur + klo, kn)
+                                  : m2_dot<PK && PQP_M2PK_C, RDD>(Qd + klo * ldn + j, ldn, ycur + klo, kn)) * ycur[j];
             } else if (pend && cw == nCR) {
                 if (lane < M) {
-                    tu[lane] = (PQP_M2_QPT ? m2_dot_row<PK && PQP_M2PK_Q>(Qp + lane * ldm, Uo, mk)
-                                           : m2_dot<PK && PQP_M2PK_Q>(Qp + lane, ldm, Uo, mk)) *
+                    tu[lane] = (PQP_M2_QPT ? m2_dot_row<PK && PQP_M2PK_Q, RD>(Qp + lane * ldm, Uo, mk)
+                                           : m2_dot<PK && PQP_M2PK_Q, RDD>(Qp + lane, ldm, Uo, mk)) *
                                Uo[lane];  // (U'Qp).U terms :652-655 (column lane of Qp)
                     fu[lane] = Fp[lane] * Uo[lane];                         // Fp'U :656-657
                 }
                 __builtin_amdgcn_wave_barrier();
+                if (tr) seg_a += __builtin_amdgcn_s_memtime() - t0;
                 if (lane < 3) {
                     const float* v = lane == 0 ? tq + ((s - 1) & 1) * nk : (lane == 1 ? tu : fu);
-                    const float r = m2_sum(v, lane == 0 ? nk : mk);
+                    const float r = m2_sum<RD>(v, lane == 0 ? nk : mk);
                     sums[lane] = r;
                 }
             }
@@ -4674,6 +4738,11 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
             T[0] += t_phase;
             T[4] += n_ph;
         }
+        // the first part of T (Gp'Y), of the first C wave (checkFeas) and of
+        // the cost wave (the U'Qp terms); each role's rest is its busy - this
+        if (conv && wave == wT) T[1] += seg_a;
+        if (conv && wave == wC0) T[2] += seg_a;
+        if (conv && wave == wC0 + nCR) T[3] += seg_a;
     }
     // the state: written by the wave that took the decisions
     if ((conv && DEC1) ? (wave == wDec && lane == 0) : tid == 0) {

@@ -32,10 +32,18 @@ def main(Hs):
     ntr = 256
     buf = torch.zeros(ntr * 16, dtype=torch.int64, device="cuda")
     for H in Hs:
-        P = block_diag_problem(base, H)
-        pb = pqp_amd.ProblemBatch.replicate(P, B)
+        if isinstance(H, str):  # dN: bench.py's dense companion at n_dual N (feasible mode only)
+            sys.path.insert(0, str(ROOT))
+            from bench import DENSE_SIZES, dense_horizon_batch
+
+            pb = dense_horizon_batch(pqp_amd, int(H[1:]), dict(DENSE_SIZES)[int(H[1:])], B)
+            P = {"N": int(H[1:])}
+        else:
+            P = block_diag_problem(base, H)
+            pb = pqp_amd.ProblemBatch.replicate(P, B)
         for mode in os.environ.get("MODES", "fixed,infeasible,feasible").split(","):
-            pb.Kp.copy_(torch.as_tensor(np.tile(P["Kp"], (B, 1)), device=pb.device))
+            if not isinstance(H, str):
+                pb.Kp.copy_(torch.as_tensor(np.tile(P["Kp"], (B, 1)), device=pb.device))
             if mode == "infeasible":
                 pb.Kp.fill_(-1e30)
             buf.zero_()
@@ -44,7 +52,7 @@ def main(Hs):
                 if mode == "fixed":
                     pb.solve(pqp_amd.MODE_FIXED, num_iter=314)
                 else:
-                    pb.solve(max_updates=312 if mode == "infeasible" else 200000)
+                    pb.solve(max_updates=312 if (mode == "infeasible" or isinstance(H, str)) else 200000)
                 torch.cuda.synchronize()
             finally:
                 pqp_amd.lib().pqp_tune_trace(b"mid", None, 0)
@@ -54,10 +62,12 @@ def main(Hs):
             per = lambda c: float(np.median(T[ok, c] / it[ok]))  # noqa: E731
             print(json.dumps({"H": H, "n_dual": P["N"], "mode": mode, "iters": float(np.median(it[ok])),
                               "cyc_A": per(0), "cyc_B": per(1), "cyc_C": per(2), "cyc_DE": per(3),
+                              # k_solve_mid2: T's Gp'Y part, C0's checkFeas part, the cost wave's U'Qp part
+                              "m2_seg": {"T_gpy": per(1), "C0_checkfeas": per(2), "cost_uqp": per(3)},
                               "busyA_wave": [per(8 + w) for w in range(8)]}), flush=True)
         del pb
         torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
-    main([int(a) for a in sys.argv[1:]] or [2, 4, 5])
+    main([a if a.startswith("d") else int(a) for a in sys.argv[1:]] or [2, 4, 5])

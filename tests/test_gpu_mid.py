@@ -349,6 +349,24 @@ def test_mid2_y_turning_nonfinite(gpu_lib, orc, knobs, pair):
         _same_or_both_nan(pb.U[b].cpu().numpy(), U, f"pair={pair} converge problem {b} U")
 
 
+def _first_nonfinite(orc, P, hi):
+    """The least fixed-mode iterate count whose oracle Y holds an inf or a NaN
+    (bisection; hi must have one)."""
+    def bad(n):
+        _, Y, _ = orc.solve(P, mode=1, num_iter=n)
+        return bool(np.isinf(Y).any() or np.isnan(Y).any())
+
+    assert bad(hi)
+    lo = 0
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if bad(mid):
+            hi = mid
+        else:
+            lo = mid
+    return hi
+
+
 def _growing_banded(N, M, seed, blk=14, negzero=False):
     """_growing's rows with the three -1 entries inside the row's own block
     of `blk` rows (an MPC-like block structure: each row group's nonzero band
@@ -378,7 +396,13 @@ def test_mid2_band_y_turning_nonfinite(gpu_lib, orc, knobs, N, M, pair, negzero)
     knobs("mid2_min_n", 0)
     Ps = [_growing_banded(N, M, s, negzero=negzero) for s in (3, 4)]
     seen_inf = False
-    for n in (5, 250, 300, 330, 400):
+    # every iterate count just before, at and after each problem's first
+    # non-finite Y (the update forms switch there), besides the coarse grid
+    near = set()
+    for P in Ps:
+        n0 = _first_nonfinite(orc, P, 400)
+        near |= set(range(max(1, n0 - 2), n0 + 7))
+    for n in sorted({5, 250, 300, 330, 400} | near):
         pb = _batch(gpu_lib, Ps).solve(gpu_lib.MODE_FIXED, num_iter=n)
         assert gpu_lib.tune_get("last_batch_kernel") == 3
         for b, P in enumerate(Ps):
