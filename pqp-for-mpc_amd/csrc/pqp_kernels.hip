@@ -4097,6 +4097,9 @@ __global__ void __launch_bounds__(NT) k_solve_mid(SolveArgs A0, SolveState* __re
 // strided checkFeas dots two (ring_walk), and Qp is staged transposed so the
 // cost wave's U'Qp terms read 16-byte rows instead of strided words: H = 4 /
 // 5 28.2 / 57.4 -> 25.2 / 51.2 ms, the dense n_dual 140 companion 84.7 -> 77.7
+#ifndef PQP_M2_TSUM  // k_solve_mid2: the T wave's spare lane 63 takes the cost wave's longest sum
+#define PQP_M2_TSUM 1
+#endif
 #ifndef PQP_M2_QPT  // k_solve_mid2: Qp kept transposed (the cost wave's U'Qp terms read rows)
 #define PQP_M2_QPT 1
 #endif
@@ -4129,7 +4132,7 @@ __device__ __forceinline__ float m2_sum(const float* v, int n8) {
 }
 struct Mid2Layout {
     int nk, mk, ldn, ldm, ldg, ldi;
-    int y, tq, dP, dN, Fdp, Fdn, Kp, tM, Us, tu, fu, Fp, fdy, flag, band, sums, Qd, Gp, Qi, Qp, total;
+    int y, tq, dP, dN, Fdp, Fdn, Kp, tM, Us, tu, fu, Fp, fdy, flag, band, sums, ones, Qd, Gp, Qi, Qp, total;
 };
 __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
     Mid2Layout L;
@@ -4157,8 +4160,9 @@ __host__ __device__ inline Mid2Layout mid2_layout(int N, int M, bool conv) {
         L.Fp = o;   o += L.mk;
         L.fdy = o;  o += 4;         // Fd.Y_s: ring by s & 1
         L.sums = o; o += 4;         // (Y'Qd).Y, (U'Qp).U, Fp.U of iterate s-1
+        L.ones = o; o += PQP_M2_TSUM ? L.nk : 0;  // 1.0f: T's lane 63 sums (Y'Qd)_j Y_j as a dot
     } else {
-        L.Kp = L.tM = L.Us = L.tu = L.fu = L.Fp = L.fdy = L.sums = 0;
+        L.Kp = L.tM = L.Us = L.tu = L.fu = L.Fp = L.fdy = L.sums = L.ones = 0;
     }
     L.Qd = o;  o += L.nk * L.ldn;
     if (conv) {
@@ -4419,6 +4423,10 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
     const int crows = (NT / 64 - nUW - 2 >= (N + 31) / 32) ? 32 : 64;
     const int nCR = mid2_cr(N, crows);
     const int wDec = wC0 + nCR;  // converge mode: the cost wave also takes each decision
+    // T's lane 63 sums (Y'Qd).Y (below): H = 5 51.9 -> 50.3 ms, dense n_dual 140
+    // 75.4 -> 74.1; the lane-side build (two problems per CU) measured 25.75 ->
+    // 25.93 at H = 4 and keeps the cost wave's sum (profiles/r06/mid2_tsum_r06x.txt)
+    const bool tsum = PQP_M2_TSUM && !PAIR && M < 63;
     constexpr bool PK = MINW == 1;  // packed dot products (the 80-VGPR build spilled with them)
     constexpr int RD = MINW == 1 ? PQP_M2_RING : PQP_M2_RING_LEAN;     // load depth of the row dots / sums
     constexpr int RDD = MINW == 1 ? PQP_M2_RINGD : PQP_M2_RINGD_LEAN;  // ... of the strided dots
@@ -4455,6 +4463,8 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         }
         for (int i = tid; i < N; i += NT) Kp[i] = A.Kp[i];
         for (int j = tid; j < M; j += NT) Fp[j] = A.Fp[j];
+        if (PQP_M2_TSUM)
+            for (int k = tid; k < nk; k += NT) lds[L.ones + k] = 1.0f;
     }
     long long h0 = st->h;
     int ynf = 0;
@@ -4654,13 +4664,20 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
         const float* grow = Gp + (lane < M ? lane : mk) * ldg;
         const float* qirow = Qi + (lane < M ? lane : 0) * ldi;
         const float fpl = lane < M ? Fp[lane] : 0.0f;
+        // lane 63, spare when M < 63, sums the previous iterate's (Y'Qd)_j Y_j
+        // (:652-655) as the dot with a vector of ones, in j order (x * 1.0f is
+        // x): the cost wave's 1 + n_dual-long single-lane chain rides in T's
+        // own instructions (round 6)
+        const bool l63 = tsum && lane == 63;
         for (long long s = h0;; ++s) {
             const float* ycur = Yr + (int)(s % 3) * nk;
             if (tr) t0 = __builtin_amdgcn_s_memtime();
-            if (lane <= M) {
-                const float d = m2_dot_row<PK && PQP_M2PK_T, RD>(grow, ycur, nk);
+            if (lane <= M || l63) {
+                const float d = m2_dot_row<PK && PQP_M2PK_T, RD>(l63 ? tq + ((s - 1) & 1) * nk : grow,
+                                                                 l63 ? lds + L.ones : ycur, nk);
                 if (lane < M) tM[lane] = d + 1.0f * fpl;  // :355-356
-                else fdy[s & 1] = d;                      // Fd.Y :656
+                else if (lane == M) fdy[s & 1] = d;       // Fd.Y :656
+                else sums[0] = d;                         // (Y'Qd).Y of iterate s-1
             }
             __builtin_amdgcn_wave_barrier();
             if (tr) seg_a += __builtin_amdgcn_s_memtime() - t0;
@@ -4711,7 +4728,7 @@ __global__ void __launch_bounds__(MAXT, MINW) k_solve_mid2(SolveArgs A0, SolveSt
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (tr) seg_a += __builtin_amdgcn_s_memtime() - t0;
-                if (lane < 3) {
+                if (lane < 3 && !(tsum && lane == 0)) {
                     const float* v = lane == 0 ? tq + ((s - 1) & 1) * nk : (lane == 1 ? tu : fu);
                     const float r = m2_sum<RD>(v, lane == 0 ? nk : mk);
                     sums[lane] = r;
