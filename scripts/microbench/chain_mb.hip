@@ -10,7 +10,7 @@ typedef float sf4 __attribute__((ext_vector_type(4)));
 //    v_med3_f32 against +-inf gives max(q,0) / min(q,0), odd lanes multiply by -y): plain,
 //    with the fused Y'Qd term, two rows per lane, with the diagonal select
 template <int V>
-__global__ void __launch_bounds__(256) mb(const float* g, float* out, unsigned long long* cyc, int n, int reps) {
+__global__ void __launch_bounds__(1024) mb(const float* g, float* out, unsigned long long* cyc, int n, int reps) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
     const int ld = n + 4;
@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(256) mb(const float* g, float* out, unsigned l
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * blockDim.x + tid] = s + s2 + acc.x + acc.y + acc2.x + acc2.y;
-    if ((tid & 63) == 0) cyc[blockIdx.x * 4 + (tid >> 6)] = t1 - t0;
+    if ((tid & 63) == 0) cyc[blockIdx.x * 16 + (tid >> 6)] = t1 - t0;
 }
 
 template <int V>
@@ -114,9 +114,13 @@ void run(const float* g, float* out, unsigned long long* cyc, int n, int threads
     hipLaunchKernelGGL(mb<V>, dim3(1), dim3(threads), lds, 0, g, out, cyc, n, reps);
     hipLaunchKernelGGL(mb<V>, dim3(1), dim3(threads), lds, 0, g, out, cyc, n, reps);
     hipDeviceSynchronize();
-    unsigned long long h[4];
+    unsigned long long h[16];
     hipMemcpy(h, cyc, sizeof h, hipMemcpyDeviceToHost);
-    printf("%-28s threads %3d: %.1f cycles per k (wave0)\n", name, threads, (double)h[0] / (reps * (double)n));
+    const int w = threads / 64;
+    double mx = 0, mn = 1e30;
+    for (int i = 0; i < w; ++i) { mx = h[i] > mx ? h[i] : mx; mn = h[i] < mn ? h[i] : mn; }
+    printf("%-28s threads %4d: %.1f cycles per k (slowest wave), %.1f (fastest)\n", name, threads,
+           mx / (reps * (double)n), mn / (reps * (double)n));
 }
 
 int main() {
@@ -129,7 +133,7 @@ int main() {
     for (int i = 0; i < 4000; ++i) hg[i] = (float)((i * 7919) % 1000) - 500.0f;
     hipMemcpy(g, hg.data(), 16000, hipMemcpyHostToDevice);
     const int n = 144;
-    for (int t : {64, 256}) {
+    for (int t : {64, 256, 512, 1024}) {
         run<5>(g, out, cyc, n, t, "reg add chain (y bcast)");
         run<0>(g, out, cyc, n, t, "add chain (row ld)");
         run<1>(g, out, cyc, n, t, "mul+add chain");
