@@ -619,7 +619,7 @@ int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, 
     PQP_TRY(ensure_persist_split(P, s));
     // the one-XCD lean form only when asked for (persist_lean: it measured
     // 5.1 against 3.5 us per update, profiles/r06/persist_lean_ab_r06c.json)
-    bool lean = g_tune.persist_lean && !g_tune.persist_trace && lean_persist_fits(N);
+    bool lean = g_tune.persist_lean && lean_persist_fits(N);
     if (lean) {
         PQP_TRY(ensure_persist_lean(P, s));
         lean = P.lean_ok == 1;

@@ -133,7 +133,13 @@ __device__ __forceinline__ bool lds_wait_sums(u64* word, unsigned want, u64& h) 
 // the 0.36 us the probe predicts, but forming the terms on the fly (two packed
 // multiplies and four v_med3_f32 per packet instead of two multiplies, the
 // diagonal test per packet) costs ~1.6 us more per update, so it is NOT the
-// default: pqp_tune persist_lean 1 selects it (A/B, tests).
+// default: pqp_tune persist_lean 1 selects it (A/B, tests).  Timelines of
+// workgroup 0 (scripts/persist_trace.py, profiles/r06/persist_trace_*_r06{e,g}
+// .json): the exchange drops from 1954-2151 to 1307-1319 clocks, but wave 0's
+// in-chain lean terms took 2652 clocks against 936 (now stored split entries:
+// 888), and wave 1's 40 packets of lean terms are not formed when wave 0
+// hands over (0 -> 1 hand-off 3279 clocks against 308): 5.27 us per update,
+// 4.28 without the diagonal fix.
 //
 // Placement: the grid is 8 G workgroups and only every eighth takes part
 // (blockIdx % 8 == 0: one XCD under the observed round-robin placement).  A
@@ -155,7 +161,11 @@ __device__ __forceinline__ bool lds_wait_sums(u64* word, unsigned want, u64& h) 
 // diagonal term (k == i) is the literal split entry times y_i, dg * y_i, with
 // dg = max_ref(0, q_ii) + Theta_i (den) or its num twin negated, put in place
 // in the eight packets that hold the workgroup's diagonal (one uniform test
-// per packet, then a per-lane select on the component).
+// per packet, then a per-lane select on the component; marking the test
+// unlikely moved the fix out of line and cost 0.16 us per update more).  Wave 0 -- whose products are formed
+// inside its chain, where three more instructions per packet lengthen the
+// critical path -- keeps its kLW0 packets as stored split entries per lane
+// (num's negated) instead: 24 KiB of LDS, and exactly the split form's chain.
 // Preconditions checked: every Qd entry and Theta finite (the build's flag;
 // else the host uses k_split_persist), and every y a workgroup stages finite
 // and >= 0 and every published y_next finite (else the launch reports code 4
@@ -196,35 +206,6 @@ __device__ __forceinline__ void lean_products_inplace(f4v (&prod)[NP], const f4v
     }
 }
 
-// Wave 0's slice, lean: as chain_qreg, each packet's terms formed in the chain.
-template <int NP>
-__device__ __forceinline__ float lean_chain_qreg(float acc, const f4v (&q)[NP], const f4v* yw, float b, int pd,
-                                                 int rr, float dg) {
-    constexpr int D = NP < 8 ? NP : 8;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) yr[j] = yw[j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
-        const f4v y = yr[j % (D + 1)];
-        const f2v lo = f2v{q[j].x, q[j].y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q[j].z, q[j].w} * f2v{y.z, y.w};
-        f4v t = f4v{__builtin_amdgcn_fmed3f(0.0f, lo.x, b), __builtin_amdgcn_fmed3f(0.0f, lo.y, b),
-                    __builtin_amdgcn_fmed3f(0.0f, hi.x, b), __builtin_amdgcn_fmed3f(0.0f, hi.y, b)};
-        if ((unsigned)(pd + j) < 8u) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) t[c] = (rr == 4 * j + c) ? dg * y[c] : t[c];
-        }
-        acc += t.x;  // :608-609, k in order
-        acc += t.y;
-        acc += t.z;
-        acc += t.w;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return acc;
-}
 }  // namespace
 
 int lean_persist_groups(int N) { return (N + kLRows - 1) / kLRows; }
@@ -262,25 +243,26 @@ size_t persist_lds_bytes(int N) {
     return sizeof(float) * ((size_t)KP * kPLanes * 4 + (size_t)2 * KP * 4) + sizeof(u64) * 2 * W * 64;
 }
 
-// the split form's LDS with the lean slices, + 16 B for the census word
+// the split form's LDS with the lean slices, wave 0's packets per lane (32 x
+// 16 B more per packet), + 16 B for the census word
 size_t lean_persist_lds_bytes(int N) {
     const int W = persist_waves(N, true), KP = persist_packets(W, true);
-    return sizeof(float) * ((size_t)KP * kPLanes * 4 + (size_t)2 * KP * 4) + sizeof(u64) * 2 * W * 64 + 16;
+    return sizeof(float) * ((size_t)(KP + kLW0) * kPLanes * 4 + (size_t)2 * KP * 4) + sizeof(u64) * 2 * W * 64 + 16;
 }
 
 // SP: the k_build_split layout with lw = 32 (workgroup-major packets).
 // gran: 2 * N granules, zeroed before the launch.  err: zeroed before the launch.
 // TRACE: the timeline instantiation (pqp_tune_trace("persist", ...)); the default one
 // carries no trace branches on its critical path.  LEAN: the one-XCD form over
-// Qd itself (above): SP = the k_build_lean_persist packets, trace = the census
-// words, xcds = 1, theta / Qd for the diagonal entries; err = 2 ints.
+// Qd itself (above): SP = the k_build_lean_persist packets, census_ = the census
+// words, xcds = 1, theta / Qd for the diagonal entries; err = 2 ints (the
+// traced lean build takes its A/B flags from the traced launch's defaults).
 template <bool TRACE, bool LEAN = false>
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     k_split_persist(const float* __restrict__ SP, const float* __restrict__ fdpn, int N, int updates,
                     const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err, u64* trace,
                     int trace_n, int stall_wg, int xcds, const float* __restrict__ theta = nullptr,
-                    const float* __restrict__ Qd = nullptr) {
-    static_assert(!(TRACE && LEAN), "the timeline is the split form's");
+                    const float* __restrict__ Qd = nullptr, u64* census_ = nullptr) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // xcds > 0 (A/B, tune persist_xcds): the grid is 8 / xcds times larger and
     // only the workgroups with blockIdx % 8 < xcds take part -- under the
@@ -301,8 +283,13 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     const int KB = split_kblocks(N);
     const int W = persist_waves_of(KB, LEAN);
     const int KP = persist_packets(W, LEAN);      // packets incl. the zero padding
-    f4v* qs = reinterpret_cast<f4v*>(lds);        // [KP][32] packets of this workgroup
-    float* ysb = lds + (size_t)KP * kPLanes * 4;  // [2][4 KP] y by update parity
+    // split: [KP][32] packets of this workgroup.  lean: wave 0's kLW0 packets as
+    // split entries per lane ([kLW0][64], num negated), then the later packets
+    // as Qd packets [KP - kLW0][32]; qs is biased so that qs + pk * 32 + row
+    // addresses lean packet pk >= kLW0
+    f4v* q0s = reinterpret_cast<f4v*>(lds);
+    f4v* qs = q0s + (LEAN ? kLW0 * kPLanes : 0);
+    float* ysb = lds + (size_t)(KP + (LEAN ? kLW0 : 0)) * kPLanes * 4;  // [2][4 KP] y by update parity
     u64* slot = reinterpret_cast<u64*>(ysb + 2 * KP * 4);  // [2][W][64] hand-off words
     const int ny = KP * 4;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -322,7 +309,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             unsigned xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
             xcc &= 0xfu;
-            gu64* census = (gu64*)trace;
+            gu64* census = (gu64*)census_;
             __hip_atomic_store(census + wg, (1ull << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int G = (N + kLRows - 1) / kLRows;
             int res = 1;
@@ -348,8 +335,24 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     // this workgroup's packets -> LDS (read-only input: plain loads)
     {
         const f4v* src = reinterpret_cast<const f4v*>(SP) + (size_t)wg * KB * kPLanes;
-        for (int e = tid; e < KP * kPLanes; e += blockDim.x)
+        for (int e = (LEAN ? kLW0 * kPLanes : 0) + tid; e < KP * kPLanes; e += blockDim.x)
             qs[e] = (e < KB * kPLanes) ? src[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (LEAN) {
+            // wave 0's packets as the split entries of each lane's side (computeQdp /
+            // Qdn_theta :524-537: max_ref(0, +-q) + 1 * [k == i] Theta_i; num negated)
+            for (int e = tid; e < kLW0 * 64; e += blockDim.x) {
+                const int pk = e >> 6, l = e & 63, r = wg * kLRows + (l >> 1);
+                const f4v q = (pk < KB) ? src[pk * kPLanes + (l >> 1)] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+                const float t = r < N ? theta[r] : 0.0f;
+                f4v v;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float tc = (4 * pk + c == r) ? t : 0.0f;
+                    v[c] = (l & 1) ? max_ref(0.0f, q[c]) + 1.0f * tc : -(max_ref(0.0f, -q[c]) + 1.0f * tc);
+                }
+                q0s[e] = v;
+            }
+        }
         for (int e = tid; e < 2 * W * 64; e += blockDim.x) slot[e] = 0ull;
         // y past N (read by the last packet's products) stays +0 for the whole
         // solve: zeroed once in both parity buffers
@@ -370,7 +373,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     int local = 0;  // lean: every workgroup on one XCD (plain granule stores)
     if constexpr (LEAN) {
         local = __builtin_amdgcn_readfirstlane(s_local);
-        if (trace_n & 1) local = local < 0 ? local : 0;  // A/B (persist_lean_flags bit 0): sc1 stores
+        if (!TRACE && (trace_n & 1)) local = local < 0 ? local : 0;  // A/B (persist_lean_flags bit 0): sc1 stores
         if (local < 0) {
             if (tid == 0) fail(err, 1);
             return;
@@ -466,7 +469,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         // update (left loop-invariant, every packet's tests were hoisted and spilled)
         int pdl = 0, rrl = 0;
         if constexpr (LEAN) {
-            pdl = (trace_n & 4) ? 1 << 20 : pk0 - 8 * wg;  // A/B bit 2: no diagonal fix (timing only, wrong bits)
+            pdl = (!TRACE && (trace_n & 4)) ? 1 << 20 : pk0 - 8 * wg;  // A/B bit 2: no diagonal fix (timing only, wrong bits)
             rrl = row - 4 * pk0;
             asm volatile("" : "+s"(pdl), "+v"(rrl));
         }
@@ -531,7 +534,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             constexpr int NP0 = LEAN ? kLW0 : kPW0;
             f4v q0[NP0];
 #pragma unroll
-            for (int j = 0; j < NP0; ++j) q0[j] = qs[(size_t)j * kPLanes + ll];
+            for (int j = 0; j < NP0; ++j) q0[j] = LEAN ? q0s[(size_t)j * 64 + lane] : qs[(size_t)j * kPLanes + ll];
             if (!stage_y()) {
                 fail(err, 1);
                 return;
@@ -539,11 +542,8 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             // ---- 2/3 (wave 0). the chain starts here, right after its products ----
             mark(u, 2);
             __builtin_amdgcn_s_setprio(3);
-            if constexpr (LEAN) {
-                if (!finish(lean_chain_qreg(acc, q0, yw, bnd, pdl, rrl, dg))) return;
-            } else {
-                if (!finish(chain_qreg(acc, q0, yw))) return;
-            }
+            // (lean: the stored split entries, num's negated: (-S) * y = -(S * y))
+            if (!finish(chain_qreg(acc, q0, yw))) return;
         } else {
             // products ahead of the turn, the running sums of the previous
             // slice, then this slice's adds; NP = the slice's packets
@@ -698,9 +698,14 @@ hipError_t launch_lean_persist(const float* LP, const float* fdpn, const float* 
     // persist_lean_flags (A/B): bit 0 sc1 stores, bit 1 grid G (spread over the
     // XCDs: the census then picks sc1), bit 2 no diagonal fix (timing only)
     const int fl = g_tune.persist_lean_flags;
-    hipLaunchKernelGGL((k_split_persist<false, true>), dim3((fl & 2) ? G : 8 * G), dim3(64 * W),
-                       lean_persist_lds_bytes(N), s, LP, fdpn, N, updates, Y0, Yout, gran, err, census, fl & 5,
-                       g_tune.persist_stall_wg, (fl & 2) ? 0 : 1, theta, Qd);
+    if (g_tune.persist_trace)  // the timeline (scripts/persist_trace.py LEAN=1)
+        hipLaunchKernelGGL((k_split_persist<true, true>), dim3(8 * G), dim3(64 * W), lean_persist_lds_bytes(N), s, LP,
+                           fdpn, N, updates, Y0, Yout, gran, err, g_tune.persist_trace, g_tune.persist_trace_n,
+                           g_tune.persist_stall_wg, 1, theta, Qd, census);
+    else
+        hipLaunchKernelGGL((k_split_persist<false, true>), dim3((fl & 2) ? G : 8 * G), dim3(64 * W),
+                           lean_persist_lds_bytes(N), s, LP, fdpn, N, updates, Y0, Yout, gran, err, nullptr, fl & 5,
+                           g_tune.persist_stall_wg, (fl & 2) ? 0 : 1, theta, Qd, census);
     return hipGetLastError();
 }
 

@@ -118,7 +118,7 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
 
 
 @pytest.mark.parametrize("src,name", [
-    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0ELb0EEEvPKfS2_iiS2_PfPyPiS4_iiiS2_S2_"),
+    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0ELb0EEEvPKfS2_iiS2_PfPyPiS4_iiiS2_S2_S4_"),
     # the headline kernel: its register blocks pinned in AGPRs across the
     # launch (pqp_kernels.hip k_batch_resident) must stay there
     ("pqp_kernels.hip", "_ZN3pqp16k_batch_residentILi16ELi2ELi2EEEvPKfxiS2_S2_iS2_Pfi"),
