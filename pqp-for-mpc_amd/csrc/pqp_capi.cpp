@@ -276,8 +276,6 @@ struct pqp_problem {
     pqp::DevBuf SP, fdpn, Yb;                        // large path, fixed mode (built on first use)
     pqp::DevBuf rerr;                                // sticky relay hand-off error word (relay / graph paths)
     pqp::DevBuf SPp, fdpnp, gran, perr;              // persistent fixed mode: split matrices (lw = 32), y granules, error word
-    pqp::DevBuf LPp, lcensus, lflag;                 // its one-XCD form: Qd packets, the XCC census, the finiteness flag
-    int lean_ok = -1;                                // LPp usable (every Qd / Theta entry finite); -1: not built
     int split_lw = 0;                                // lanes per workgroup SP was built with
     bool split_lean = false;                         // SP holds Qd packets (k_lean_relay), not the split matrices
     hipGraphExec_t graph = nullptr;                  // captured fixed-mode updates (the remainder)
@@ -378,7 +376,7 @@ int ensure_single(pqp_problem& P, hipStream_t s) {
 // Drop everything derived from a problem's data (built on first use by the
 // solve paths): called before new data goes into an existing handle.
 void problem_reset_derived(pqp_problem& P) {
-    for (DevBuf* b : {&P.QdT, &P.theta, &P.SP, &P.fdpn, &P.Yb, &P.rerr, &P.SPp, &P.fdpnp, &P.gran, &P.perr, &P.LPp, &P.lcensus, &P.lflag, &P.QinvT, &P.GpT,
+    for (DevBuf* b : {&P.QdT, &P.theta, &P.SP, &P.fdpn, &P.Yb, &P.rerr, &P.SPp, &P.fdpnp, &P.gran, &P.perr, &P.QinvT, &P.GpT,
                       &P.tM, &P.tq, &P.tu, &P.gu, &P.wflag, &P.wcap, &P.CA1, &P.CA2, &P.CA3, &P.crings, &P.cwords})
         b->reset();
     for (hipGraphExec_t* g : {&P.graph, &P.chunk_graph, &P.wgraph, &P.wgraph_first, &P.wgraph4, &P.wgraph8})
@@ -566,37 +564,17 @@ int ensure_persist_split(pqp_problem& P, hipStream_t s) {
     PQP_HIP(hipMemsetAsync(P.SPp.p, 0, sizeof(float) * split_floats(N, N, 32), s));
     PQP_HIP(launch_build_split(P.Qd.f(), N, P.theta.f(), P.Fd.f(), N, N, 0, 32, P.SPp.f(), P.fdpnp.f(), s));
     PQP_TRY(P.gran.alloc(sizeof(unsigned long long) * 2 * N));
-    PQP_TRY(P.perr.alloc(2 * sizeof(int)));
-    return PQP_OK;
-}
-
-// The one-XCD form's Qd packets, built once per problem (and only where the
-// split form's preconditions hold: N small enough for one XCD).  lean_ok = 0
-// when an entry of Qd or Theta is not finite (the lean terms assume finite q).
-int ensure_persist_lean(pqp_problem& P, hipStream_t s) {
-    if (P.lean_ok >= 0) return PQP_OK;
-    const int N = P.N;
-    PQP_TRY(P.LPp.floats(lean_persist_floats(N)));
-    PQP_TRY(P.lcensus.alloc(sizeof(unsigned long long) * lean_persist_groups(N)));
-    PQP_TRY(P.lflag.alloc(sizeof(int)));
-    PQP_HIP(launch_build_lean_persist(P.Qd.f(), N, P.theta.f(), P.LPp.f(), static_cast<int*>(P.lflag.p), s));
-    int flag = 1;
-    PQP_HIP(hipMemcpyAsync(&flag, P.lflag.p, sizeof flag, hipMemcpyDeviceToHost, s));
-    PQP_HIP(hipStreamSynchronize(s));
-    P.lean_ok = flag == 0 ? 1 : 0;
+    PQP_TRY(P.perr.alloc(sizeof(int)));
     return PQP_OK;
 }
 
 // Which solver the last single-problem solve ran (pqp_tune_get("last_path")), and
 // how many persistent launches fell back to the relay / graph path.
 enum SolvePath : int {
-    kPathFixedPersist = 1, kPathFixedRelay = 2, kPathConvergePersist = 3, kPathConvergeWide = 4, kPathOneWorkgroup = 5,
-    kPathFixedPersistLean = 6,  // the one-XCD lean form (persist_lean 1) for every chunk
-    kPathFixedPersistLeanRerun = 7  // the lean form, a chunk re-run on the split form (a y precondition failed)
+    kPathFixedPersist = 1, kPathFixedRelay = 2, kPathConvergePersist = 3, kPathConvergeWide = 4, kPathOneWorkgroup = 5
 };
 thread_local int g_last_path = 0;               // of the calling thread's last solve
 std::atomic<long long> g_persist_fallbacks{0};
-std::atomic<long long> g_lean_reruns{0};  // lean persistent chunks re-run on the split form
 std::atomic<long long> g_tiny_stale{0};  // tiny solves whose pinned output did not carry their tag
 // problem_run_*_persist: a wait of the persistent launch expired (its
 // workgroups were not all resident); the caller falls back
@@ -617,44 +595,21 @@ std::mutex& persist_lock() {
 int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, hipStream_t s) {
     const int N = P.N;
     PQP_TRY(ensure_persist_split(P, s));
-    // the one-XCD lean form only when asked for (persist_lean: it measured
-    // 5.1 against 3.5 us per update, profiles/r06/persist_lean_ab_r06c.json)
-    bool lean = g_tune.persist_lean && lean_persist_fits(N);
-    if (lean) {
-        PQP_TRY(ensure_persist_lean(P, s));
-        lean = P.lean_ok == 1;
-    }
     auto* gran = static_cast<unsigned long long*>(P.gran.p);
     int* err = static_cast<int*>(P.perr.p);
     PQP_HIP(launch_fill(P.Y.f(), 1000.0f, N, s));  // initMat(Y, 1000) :710
     std::lock_guard<std::mutex> one_at_a_time(persist_lock());
-    bool rerun = false;
     for (long long done = 0; done < updates;) {
         const long long n = std::min(kPersistChunk, updates - done);
         // the launch reads its initial iterate from Yb while it writes P.Y
         PQP_HIP(hipMemcpyAsync(P.Yb.p, P.Y.p, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
-        int herr[2] = {0, 0};
-        if (lean) {
-            PQP_HIP(launch_lean_persist(P.LPp.f(), P.fdpnp.f(), P.theta.f(), P.Qd.f(), N, (int)n, P.Yb.f(), P.Y.f(), gran,
-                                        static_cast<unsigned long long*>(P.lcensus.p), err, s));
-            PQP_HIP(hipMemcpyAsync(herr, err, sizeof herr, hipMemcpyDeviceToHost, s));
-            PQP_HIP(hipStreamSynchronize(s));
-        }
-        if (!lean || (!herr[0] && herr[1])) {
-            // the split form: by choice, or again from the chunk's initial
-            // iterate because a y of the lean launch was negative or not finite
-            if (lean) {
-                rerun = true;
-                ++g_lean_reruns;
-            }
-            PQP_HIP(launch_split_persist(P.SPp.f(), P.fdpnp.f(), N, (int)n, P.Yb.f(), P.Y.f(), gran, err, s));
-            PQP_HIP(hipMemcpyAsync(herr, err, sizeof(int), hipMemcpyDeviceToHost, s));
-            PQP_HIP(hipStreamSynchronize(s));
-        }
-        if (herr[0]) {  // not all workgroups resident (other work on the device): fall back
+        PQP_HIP(launch_split_persist(P.SPp.f(), P.fdpnp.f(), N, (int)n, P.Yb.f(), P.Y.f(), gran, err, s));
+        int herr = 0;
+        PQP_HIP(hipMemcpyAsync(&herr, err, sizeof herr, hipMemcpyDeviceToHost, s));
+        PQP_HIP(hipStreamSynchronize(s));
+        if (herr) {  // not all workgroups resident (other work on the device): fall back
             set_error(PQP_ERR_HIP, "persistent fixed-mode update: workgroup hand-off timed out (code %d); "
-                      "its %d workgroups must be resident at once", herr[0],
-                      lean ? lean_persist_groups(N) : (2 * N + 31) / 32);
+                      "its %d workgroups must be resident at once", herr, (2 * N + 31) / 32);
             return kPersistStalled;
         }
         done += n;
@@ -662,7 +617,7 @@ int problem_run_fixed_persist(pqp_problem& P, long long updates, SolveOut& out, 
     PQP_HIP(hipStreamSynchronize(s));
     out.h = updates + 1;
     out.status = kStatusDone;
-    g_last_path = !lean ? kPathFixedPersist : (rerun ? kPathFixedPersistLeanRerun : kPathFixedPersistLean);
+    g_last_path = kPathFixedPersist;
     return PQP_OK;
 }
 
@@ -2111,8 +2066,6 @@ const KnobRef* find_knob(const char* key) {
         {"tiny_np", &g_tune.tiny_np, nullptr, nullptr},
         {"tiny_ablk", &g_tune.tiny_ablk, nullptr, nullptr},
         {"tiny_apoll", &g_tune.tiny_apoll, nullptr, nullptr},
-        {"persist_lean", &g_tune.persist_lean, nullptr, nullptr},
-        {"persist_lean_flags", &g_tune.persist_lean_flags, nullptr, nullptr},
         {"persist_xcds", &g_tune.persist_xcds, nullptr, nullptr},
         {"converge_xcds", &g_tune.converge_xcds, nullptr, nullptr},
         {"tiny_chunk", nullptr, nullptr, &g_tune.tiny_chunk},
@@ -2180,10 +2133,6 @@ extern "C" int pqp_tune_get(const char* key, long long* value) {
     }
     if (std::strcmp(key, "persist_fallbacks") == 0) {
         *value = pqp::g_persist_fallbacks;
-        return PQP_OK;
-    }
-    if (std::strcmp(key, "lean_reruns") == 0) {  // lean persistent chunks re-run on the split form
-        *value = pqp::g_lean_reruns;
         return PQP_OK;
     }
     if (std::strcmp(key, "batch_chunk_for") == 0) {  // in: N << 32 | M; out: iterates per batched launch

@@ -150,8 +150,6 @@ struct Tuning {  // every tuning knob of the library (pqp_tune, include/pqp_tuni
                            // multiples of 1024, k_batch_iterate otherwise), 1 k_batch_iterate, 2 k_batch_stream,
                            // 3 k_batch_resident without its register blocks
     int tiny_stall = 0;  // k_solve_quintet's deciding waves return at once: every wait expires (error path)
-    int persist_lean = 0;  // fixed mode of n_dual <= 1024 on the one-XCD lean form (k_split_persist<false, true>; measured slower, A/B)
-    int persist_lean_flags = 0;  // k_split_persist<false, true> A/B: bit 0 sc1 stores, bit 1 spread, bit 2 no diagonal fix
     int persist_xcds = 0;  // k_split_persist's workgroups packed onto this many XCDs (0: 4, 8: spread over all)
     int converge_xcds = 0;  // k_converge_persist's workgroups packed onto this many XCDs (0: 6, 8: spread over all)
     int tiny_apoll = 0;  // k_solve_quintet's update wave polls the decision word every update (default: only when the ring is full)
@@ -173,17 +171,6 @@ size_t persist_lds_bytes(int N);
 hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,
                                 unsigned long long* gran, int* err, hipStream_t s);
 bool split_persist_fits(int N);  // all of k_split_persist's workgroups co-resident on this device
-// the same on one XCD over Qd itself (k_split_persist<false, true>, pqp_persist.hip): LP from
-// launch_build_lean_persist (flag = 1: a non-finite Qd / Theta entry, not usable);
-// err = 2 ints (err[1] = 4: a y precondition failed, re-run on k_split_persist);
-// census = lean_persist_groups(N) words
-int lean_persist_groups(int N);
-size_t lean_persist_floats(int N);
-bool lean_persist_fits(int N);
-hipError_t launch_build_lean_persist(const float* Qd, int N, const float* theta, float* LP, int* flag, hipStream_t s);
-hipError_t launch_lean_persist(const float* LP, const float* fdpn, const float* theta, const float* Qd, int N,
-                               int updates, const float* Y0, float* Yout, unsigned long long* gran,
-                               unsigned long long* census, int* err, hipStream_t s);
 size_t split_floats(int N, int rows, int lw);  // size of a row block's packed split matrices
 // lean relay (k_lean_relay): Qd packets (4 B per entry, lw / 2 rows per
 // workgroup) and aux[row] = {Fdn, Fdp, Theta, 0} + NaN flags; used for blocks

@@ -113,124 +113,15 @@ __device__ __forceinline__ bool lds_wait_sums(u64* word, unsigned want, u64& h) 
 }  // namespace
 
 
-// ---------------------------------------------------------------------------
-// k_split_persist<false, true> ("lean"): the same kernel on ONE XCD.  The split kernel's 64
-// workgroups (32 live row sides each) need 64 CUs, so its y granules cross
-// XCDs, and an sc1 granule store drops the line from the writer's L2: every
-// reader goes to the fabric (≈0.53 µs one way even between two CUs of one
-// XCD, ≈0.60 across).  A plain store keeps the line in the XCD's L2, where a
-// same-XCD sc1 load (L1 bypassed) finds it in ≈0.24 µs -- but a reader on
-// another XCD never sees it (scripts/probes/xcd_handoff_probe.hip,
-// profiles/r06/xcd_handoff_r06.json).  So: 32 rows = 64 row sides per
-// workgroup (every lane live), n_dual 1024 in 32 workgroups = one XCD's 32
-// CUs; Qd itself in LDS (4 B per entry: 32 rows x 1024 k = 128 KiB) instead of
-// the two split matrices (8 B), the split entries formed on the fly.
-//
-// Measured (profiles/r06/persist_lean_ab_r06{b,c}.json, n_dual 1024, 1000
-// updates, same bits): split form 3.50 us per update, this form 5.07-5.12 with
-// plain stores on one XCD, 5.43-5.46 with sc1 stores (one XCD or spread), 4.79
-// without the diagonal fix (wrong bits, timing only).  The plain store saves
-// the 0.36 us the probe predicts, but forming the terms on the fly (two packed
-// multiplies and four v_med3_f32 per packet instead of two multiplies, the
-// diagonal test per packet) costs ~1.6 us more per update, so it is NOT the
-// default: pqp_tune persist_lean 1 selects it (A/B, tests).  Timelines of
-// workgroup 0 (scripts/persist_trace.py, profiles/r06/persist_trace_*_r06{e,g}
-// .json): the exchange drops from 1954-2151 to 1307-1319 clocks, but wave 0's
-// in-chain lean terms took 2652 clocks against 936 (now stored split entries:
-// 888), and wave 1's 40 packets of lean terms are not formed when wave 0
-// hands over (0 -> 1 hand-off 3279 clocks against 308): 5.27 us per update,
-// 4.28 without the diagonal fix.
-//
-// Placement: the grid is 8 G workgroups and only every eighth takes part
-// (blockIdx % 8 == 0: one XCD under the observed round-robin placement).  A
-// census at the start (each workgroup's HW_REG_XCC_ID, exchanged as agent-
-// coherent granules) decides the store flavour for the whole launch: plain
-// when every workgroup reads the same XCC id, sc1 otherwise -- placement
-// changes the speed, never the result.
-//
-// Terms (each lane one side of row i; even lane: num, odd lane: den):
-//   reference  t = (max(0, +-q) + [k == i] Theta_i) * y   (:524-537, :608-609)
-//   den lane   t = med3(0, q * y, +inf)            = max(0, q * y)
-//   num lane   t'= med3(0, q * y, -inf)            = min(0, q * y) = -t
-// i.e. the num lane sums the NEGATED terms (RNE is symmetric: the running sum
-// is the exact negation of the reference's whenever that is non-zero, and a
-// zero of either sign when it is zero -- the reference's sum starts at +0 and
-// is never -0), and recovers num's sum as 0 - s' (+0 for either zero).  The
-// product-first form max(0, q) * y = max(0, q * y) holds for finite q and
-// finite y >= 0, up to the sign of a zero term, which adds nothing.  The
-// diagonal term (k == i) is the literal split entry times y_i, dg * y_i, with
-// dg = max_ref(0, q_ii) + Theta_i (den) or its num twin negated, put in place
-// in the eight packets that hold the workgroup's diagonal (one uniform test
-// per packet, then a per-lane select on the component; marking the test
-// unlikely moved the fix out of line and cost 0.16 us per update more).  Wave 0 -- whose products are formed
-// inside its chain, where three more instructions per packet lengthen the
-// critical path -- keeps its kLW0 packets as stored split entries per lane
-// (num's negated) instead: 24 KiB of LDS, and exactly the split form's chain.
-// Preconditions checked: every Qd entry and Theta finite (the build's flag;
-// else the host uses k_split_persist), and every y a workgroup stages finite
-// and >= 0 and every published y_next finite (else the launch reports code 4
-// in err[1] and the host re-runs that chunk on k_split_persist).
-// ---------------------------------------------------------------------------
-// The lean form is an instantiation of k_split_persist (below): the same
-// waves, slices, hand-offs and sweep, so the same register allocation
-// (written as a separate kernel, the compiler spilled its slices).
-// ---------------------------------------------------------------------------
-namespace {
-constexpr int kLRows = 32;  // rows per workgroup (64 row sides, every lane live)
-
-// Lean products of one slice in place: prod[j] = term(q_j, y_j), see above.
-// pd = the slice's first packet minus the workgroup's first diagonal packet,
-// rr = this lane's row minus the slice's first k (both laundered per update by
-// the caller), dg = this lane's diagonal entry.
-template <int NP>
-__device__ __forceinline__ void lean_products_inplace(f4v (&prod)[NP], const f4v* yw, float b, int pd, int rr,
-                                                      float dg) {
-    constexpr int D = NP < 4 ? NP : 4;
-    f4v yr[D + 1];
-#pragma unroll
-    for (int j = 0; j < D; ++j) yr[j] = yw[j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        if (j + D < NP) yr[(j + D) % (D + 1)] = yw[j + D];
-        const f4v q = prod[j], y = yr[j % (D + 1)];
-        const f2v lo = f2v{q.x, q.y} * f2v{y.x, y.y};
-        const f2v hi = f2v{q.z, q.w} * f2v{y.z, y.w};
-        f4v t = f4v{__builtin_amdgcn_fmed3f(0.0f, lo.x, b), __builtin_amdgcn_fmed3f(0.0f, lo.y, b),
-                    __builtin_amdgcn_fmed3f(0.0f, hi.x, b), __builtin_amdgcn_fmed3f(0.0f, hi.y, b)};
-        if ((unsigned)(pd + j) < 8u) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) t[c] = (rr == 4 * j + c) ? dg * y[c] : t[c];
-        }
-        prod[j] = t;
-    }
-}
-
-}  // namespace
-
-int lean_persist_groups(int N) { return (N + kLRows - 1) / kLRows; }
-size_t lean_persist_floats(int N) { return (size_t)lean_persist_groups(N) * split_kblocks(N) * kLRows * 4; }
-
-// waves: slices of kPW0, kPW1, then kPW packets (lean: kLW0, kLW1, kLW -- the
-// later slices one packet shorter, for the registers the lean terms take)
-#ifndef PQP_LEAN_SLICES  // A/B builds: -DPQP_LEAN_SLICES=P0,P1,PW
-#define PQP_LEAN_SLICES 24, 40, 48
-#endif
-constexpr int kLSlices[3] = {PQP_LEAN_SLICES};
-constexpr int kLW0 = kLSlices[0], kLW1 = kLSlices[1], kLW = kLSlices[2];
-static_assert(kLW0 + kLW1 + 4 * kLW >= 256, "six waves must cover n_dual 1024");
-static_assert(kLW0 <= 64 && kLW1 <= 64 && kLW <= 64, "a slice is at most 4 granules per lane (one sweep)");
-__host__ __device__ inline int persist_slice0(int w, bool lean = false) {
-    const int a = lean ? kLW0 : kPW0, b = lean ? kLW1 : kPW1, c = lean ? kLW : kPW;
-    return w == 0 ? 0 : (w == 1 ? a : a + b + (w - 2) * c);
-}
-__host__ __device__ inline int persist_packets(int W, bool lean = false) { return persist_slice0(W, lean); }
-__host__ __device__ inline int persist_waves_of(int KB, bool lean = false) {
+// waves: slices of kPW0, kPW1, then kPW packets
+__host__ __device__ inline int persist_slice0(int w) { return w == 0 ? 0 : (w == 1 ? kPW0 : kPW0 + kPW1 + (w - 2) * kPW); }
+__host__ __device__ inline int persist_packets(int W) { return persist_slice0(W); }
+__host__ __device__ inline int persist_waves_of(int KB) {
     int W = 1;
-    while (persist_packets(W, lean) < KB) ++W;
+    while (persist_packets(W) < KB) ++W;
     return W;
 }
-int persist_waves(int N, bool lean = false) { return persist_waves_of(split_kblocks(N), lean); }
+int persist_waves(int N) { return persist_waves_of(split_kblocks(N)); }
 int persist_max_n() {
     const int n = 4 * persist_packets(kPMaxWaves);
     return n > 1024 ? 1024 : n;
@@ -243,26 +134,15 @@ size_t persist_lds_bytes(int N) {
     return sizeof(float) * ((size_t)KP * kPLanes * 4 + (size_t)2 * KP * 4) + sizeof(u64) * 2 * W * 64;
 }
 
-// the split form's LDS with the lean slices, wave 0's packets per lane (32 x
-// 16 B more per packet), + 16 B for the census word
-size_t lean_persist_lds_bytes(int N) {
-    const int W = persist_waves(N, true), KP = persist_packets(W, true);
-    return sizeof(float) * ((size_t)(KP + kLW0) * kPLanes * 4 + (size_t)2 * KP * 4) + sizeof(u64) * 2 * W * 64 + 16;
-}
-
 // SP: the k_build_split layout with lw = 32 (workgroup-major packets).
 // gran: 2 * N granules, zeroed before the launch.  err: zeroed before the launch.
 // TRACE: the timeline instantiation (pqp_tune_trace("persist", ...)); the default one
-// carries no trace branches on its critical path.  LEAN: the one-XCD form over
-// Qd itself (above): SP = the k_build_lean_persist packets, census_ = the census
-// words, xcds = 1, theta / Qd for the diagonal entries; err = 2 ints (the
-// traced lean build takes its A/B flags from the traced launch's defaults).
-template <bool TRACE, bool LEAN = false>
+// carries no trace branches on its critical path.
+template <bool TRACE>
 __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
     k_split_persist(const float* __restrict__ SP, const float* __restrict__ fdpn, int N, int updates,
                     const float* __restrict__ Y0, float* __restrict__ Yout, u64* gran_, int* err, u64* trace,
-                    int trace_n, int stall_wg, int xcds, const float* __restrict__ theta = nullptr,
-                    const float* __restrict__ Qd = nullptr, u64* census_ = nullptr) {
+                    int trace_n, int stall_wg, int xcds) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // xcds > 0 (A/B, tune persist_xcds): the grid is 8 / xcds times larger and
     // only the workgroups with blockIdx % 8 < xcds take part -- under the
@@ -274,115 +154,41 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         wg = (int)(blockIdx.x >> 3) * xcds + (int)(blockIdx.x & 7);
         // the padded grid's last row of participants can run past the G
         // workgroups the problem has (G not a multiple of xcds)
-        if (wg >= (LEAN ? (N + kLRows - 1) / kLRows : (2 * N + kPLanes - 1) / kPLanes)) return;
+        if (wg >= (2 * N + kPLanes - 1) / kPLanes) return;
     }
     // tuning (error-path tests): this workgroup never runs, as if it were not
     // resident; every other one's waits expire and report through err
     if (wg == stall_wg) return;
     gu64* gran = (gu64*)gran_;
     const int KB = split_kblocks(N);
-    const int W = persist_waves_of(KB, LEAN);
-    const int KP = persist_packets(W, LEAN);      // packets incl. the zero padding
-    // split: [KP][32] packets of this workgroup.  lean: wave 0's kLW0 packets as
-    // split entries per lane ([kLW0][64], num negated), then the later packets
-    // as Qd packets [KP - kLW0][32]; qs is biased so that qs + pk * 32 + row
-    // addresses lean packet pk >= kLW0
-    f4v* q0s = reinterpret_cast<f4v*>(lds);
-    f4v* qs = q0s + (LEAN ? kLW0 * kPLanes : 0);
-    float* ysb = lds + (size_t)(KP + (LEAN ? kLW0 : 0)) * kPLanes * 4;  // [2][4 KP] y by update parity
+    const int W = persist_waves_of(KB);
+    const int KP = persist_packets(W);            // packets incl. the zero padding
+    f4v* qs = reinterpret_cast<f4v*>(lds);        // [KP][32] packets of this workgroup
+    float* ysb = lds + (size_t)KP * kPLanes * 4;  // [2][4 KP] y by update parity
     u64* slot = reinterpret_cast<u64*>(ysb + 2 * KP * 4);  // [2][W][64] hand-off words
     const int ny = KP * 4;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // split: lane ll = row side (lanes 32..63 repeat lanes 0..31, discarded);
-    // lean: lane = 2 (row in the workgroup) + side, every lane live, ll = the
-    // row's packet slot
-    const int ll = LEAN ? lane >> 1 : lane & (kPLanes - 1);
-    const int p = LEAN ? 2 * (wg * kLRows + ll) + (lane & 1) : wg * kPLanes + ll;
-    const bool live = LEAN ? (p >> 1) < N : lane < kPLanes && p < 2 * N;
+    const int ll = lane & (kPLanes - 1);  // lanes 32..63 repeat lanes 0..31 (discarded)
+    const int p = wg * kPLanes + ll;
+    const bool live = lane < kPLanes && p < 2 * N;
     const int row = p >> 1;
-    int& s_local = *reinterpret_cast<int*>(slot + 2 * W * 64);  // lean: the census result (16 B past the slots)
-    if constexpr (LEAN) {
-        if (tid == 0) {
-            // census by one lane (a wave-wide form made the compiler spill the
-            // slices): every workgroup's XCC id, all equal to this one's?
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            xcc &= 0xfu;
-            gu64* census = (gu64*)census_;
-            __hip_atomic_store(census + wg, (1ull << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int G = (N + kLRows - 1) / kLRows;
-            int res = 1;
-            Deadline dl;
-            for (int c = 0; c < G && res >= 0; ++c) {
-                for (unsigned spins = 0;; ++spins) {
-                    const u64 h = __hip_atomic_load(census + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((unsigned)(h >> 32) == 1u) {
-                        if ((unsigned)h != xcc) res = 0;
-                        break;
-                    }
-                    if ((spins & 63) == 63 && dl.expired()) {
-                        res = -1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            s_local = res;
-        }
-    }
 
     // this workgroup's packets -> LDS (read-only input: plain loads)
     {
         const f4v* src = reinterpret_cast<const f4v*>(SP) + (size_t)wg * KB * kPLanes;
-        for (int e = (LEAN ? kLW0 * kPLanes : 0) + tid; e < KP * kPLanes; e += blockDim.x)
+        for (int e = tid; e < KP * kPLanes; e += blockDim.x)
             qs[e] = (e < KB * kPLanes) ? src[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (LEAN) {
-            // wave 0's packets as the split entries of each lane's side (computeQdp /
-            // Qdn_theta :524-537: max_ref(0, +-q) + 1 * [k == i] Theta_i; num negated)
-            for (int e = tid; e < kLW0 * 64; e += blockDim.x) {
-                const int pk = e >> 6, l = e & 63, r = wg * kLRows + (l >> 1);
-                const f4v q = (pk < KB) ? src[pk * kPLanes + (l >> 1)] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-                const float t = r < N ? theta[r] : 0.0f;
-                f4v v;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float tc = (4 * pk + c == r) ? t : 0.0f;
-                    v[c] = (l & 1) ? max_ref(0.0f, q[c]) + 1.0f * tc : -(max_ref(0.0f, -q[c]) + 1.0f * tc);
-                }
-                q0s[e] = v;
-            }
-        }
         for (int e = tid; e < 2 * W * 64; e += blockDim.x) slot[e] = 0ull;
         // y past N (read by the last packet's products) stays +0 for the whole
         // solve: zeroed once in both parity buffers
         for (int e = tid; e < 2 * (KP * 4 - N); e += blockDim.x) ysb[(e & 1) * KP * 4 + N + (e >> 1)] = 0.0f;
     }
     const float fd = live ? fdpn[p] : 0.0f;
-    // lean: med3 bound (den +inf: max(0, .); num -inf: min(0, .)) and this lane's
-    // diagonal split entry (computeQdp / Qdn_theta :524-537 at k = i), negated for num
-    float bnd = 0.0f, dg = 0.0f;
-    if constexpr (LEAN) {
-        bnd = (lane & 1) ? __builtin_inff() : -__builtin_inff();
-        if (live) {
-            const float qd = Qd[(size_t)row * N + row], th = theta[row];
-            dg = (lane & 1) ? max_ref(0.0f, qd) + 1.0f * th : -(max_ref(0.0f, -qd) + 1.0f * th);
-        }
-    }
     __syncthreads();
-    int local = 0;  // lean: every workgroup on one XCD (plain granule stores)
-    if constexpr (LEAN) {
-        local = __builtin_amdgcn_readfirstlane(s_local);
-        if (!TRACE && (trace_n & 1)) local = local < 0 ? local : 0;  // A/B (persist_lean_flags bit 0): sc1 stores
-        if (local < 0) {
-            if (tid == 0) fail(err, 1);
-            return;
-        }
-    }
-    bool bad_y = false;  // lean: a y below zero or not finite (err[1] = 4: the host re-runs on the split form)
 
-    const int pk0 = persist_slice0(w, LEAN);                     // first packet of this wave's slice
-    const int pk1 = persist_slice0(w + 1, LEAN);                 // one past its last
+    const int pk0 = persist_slice0(w);                           // first packet of this wave's slice
+    const int pk1 = persist_slice0(w + 1);                       // one past its last
     const int k0 = 4 * pk0, k1 = 4 * pk1 < N ? 4 * pk1 : N;      // y[k0, k1) of the slice
     const bool last = (w == W - 1);
     float yrow = 0.0f;  // last wave: y_i of this lane's row (for y_next = num / den * y_i)
@@ -402,11 +208,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         // ---- 1. y of this slice (k in [k0, k1)), staged in LDS ----
         auto stage_y = [&]() -> bool {
         if (u == 0) {
-            for (int k = k0 + lane; k < k1; k += 64) {
-                const float v0 = Y0 ? Y0[k] : 1000.0f;  // initMat(Y, 1000) :710
-                if constexpr (LEAN) bad_y |= !(__builtin_isfinite(v0) && !(v0 < 0.0f));
-                ys[k] = v0;
-            }
+            for (int k = k0 + lane; k < k1; k += 64) ys[k] = Y0 ? Y0[k] : 1000.0f;  // initMat(Y, 1000) :710
             if (last) yrow = (Y0 && row < N) ? Y0[row] : 1000.0f;
         } else {
             // the sweep: the slice's granules (4 per lane, indices clamped into
@@ -464,15 +266,6 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         mark(u, 1);
         return true;
         };
-        // lean: the slice's first packet relative to the workgroup's diagonal
-        // packets and this lane's row relative to the slice, laundered per
-        // update (left loop-invariant, every packet's tests were hoisted and spilled)
-        int pdl = 0, rrl = 0;
-        if constexpr (LEAN) {
-            pdl = (!TRACE && (trace_n & 4)) ? 1 << 20 : pk0 - 8 * wg;  // A/B bit 2: no diagonal fix (timing only, wrong bits)
-            rrl = row - 4 * pk0;
-            asm volatile("" : "+s"(pdl), "+v"(rrl));
-        }
         // one base address per operand, the packet index as an immediate offset
         const f4v* qw = qs + (size_t)pk0 * kPLanes + ll;
         const f4v* yw = reinterpret_cast<const f4v*>(ys) + pk0;
@@ -497,31 +290,14 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             }
             __builtin_amdgcn_s_setprio(0);
             // ---- 4. the last slice's wave finishes the rows ----
-            // lean: num's sum from its negated terms, 0 - s' (+0 for a zero of either sign)
-            const float sacc = (LEAN && !(lane & 1)) ? 0.0f - acc : acc;
-            const float v = sacc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
+            const float v = acc + 1.0f * fd;  // even lane: num (:611), odd lane: den (:612)
             // the partner lane's sum by a DPP swap of lane pairs (quad_perm 1,0,3,2),
             // not an LDS permute; every lane divides (odd lanes' quotients unused)
             const float den = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
             yn = v / den * yrow;  // :594
-            if constexpr (LEAN) {
-                if (!(p & 1) && live) {
-                    // the row laundered: a loop-invariant 64-bit address was spilled
-                    int rl = row;
-                    asm volatile("" : "+v"(rl));
-                    const u64 gv = ((u64)want << 32) | __float_as_uint(yn);
-                    gu64* dst = gran + (size_t)(par ^ 1) * N + rl;
-                    if (local)  // plain: the line stays in this XCD's L2, where every reader is
-                        asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(gv) : "memory");
-                    else
-                        __hip_atomic_store(dst, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // every y a wave stages was published by some workgroup's last wave
-                    bad_y |= !(__builtin_isfinite(yn) && !(yn < 0.0f));
-                }
-            } else if (!(p & 1) && live) {
+            if (!(p & 1) && live)
                 __hip_atomic_store(gran + (size_t)(par ^ 1) * N + row, ((u64)want << 32) | __float_as_uint(yn),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
             if (bad) {
                 fail(err, bad);
                 return false;
@@ -531,10 +307,9 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         if (w == 0) {
             // wave 0 reads its slice's split entries while it waits for y:
             // its products start the chain, and then need only the y reads
-            constexpr int NP0 = LEAN ? kLW0 : kPW0;
-            f4v q0[NP0];
+            f4v q0[kPW0];
 #pragma unroll
-            for (int j = 0; j < NP0; ++j) q0[j] = LEAN ? q0s[(size_t)j * 64 + lane] : qs[(size_t)j * kPLanes + ll];
+            for (int j = 0; j < kPW0; ++j) q0[j] = qs[(size_t)j * kPLanes + ll];
             if (!stage_y()) {
                 fail(err, 1);
                 return;
@@ -542,7 +317,6 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
             // ---- 2/3 (wave 0). the chain starts here, right after its products ----
             mark(u, 2);
             __builtin_amdgcn_s_setprio(3);
-            // (lean: the stored split entries, num's negated: (-S) * y = -(S * y))
             if (!finish(chain_qreg(acc, q0, yw))) return;
         } else {
             // products ahead of the turn, the running sums of the previous
@@ -561,10 +335,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                     // the first waves' products and chains run alone
                     if (!lds_wait(sl + kLateGate * 64 + lane, want, true)) bad = 2;
                 }
-                if constexpr (LEAN)
-                    lean_products_inplace(prod, yw, bnd, pdl, rrl, dg);
-                else
-                    slice_products_inplace(prod, yw);
+                slice_products_inplace(prod, yw);
                 // pinned here: otherwise the compiler sinks the multiplies into the chain
 #pragma unroll
                 for (int j = 0; j < NP; ++j) asm volatile("" : "+v"(prod[j]));
@@ -613,8 +384,7 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
                 }
                 return finish(acc) ? 0 : 3;
             };
-            constexpr int NP1 = LEAN ? kLW1 : kPW1, NPW = LEAN ? kLW : kPW;
-            const int rc = (w == 1) ? turn(std::integral_constant<int, NP1>{}) : turn(std::integral_constant<int, NPW>{});
+            const int rc = (w == 1) ? turn(std::integral_constant<int, kPW1>{}) : turn(std::integral_constant<int, kPW>{});
             if (rc) {
                 if (rc == 1) fail(err, rc);  // 3: reported by finish
                 return;
@@ -622,8 +392,6 @@ __global__ void __launch_bounds__(64 * kPMaxWaves, 1)
         }
     }
     if (last && updates > 0 && !(p & 1) && live) Yout[row] = yn;
-    if constexpr (LEAN)
-        if (__any(bad_y) && lane == 0) __hip_atomic_store(err + 1, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
@@ -643,70 +411,6 @@ bool split_persist_fits(int N) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, persist_lds_bytes(N)) != hipSuccess)
         return false;
     return (long long)per * cus >= G;
-}
-
-// LP[g][kb][i] = Qd[32 g + i][4 kb .. 4 kb + 3] (zero past N); flag = 1 if any
-// entry of Qd or Theta is not finite (then the lean launch is not used)
-__global__ void __launch_bounds__(256) k_build_lean_persist(const float* __restrict__ Qd, int N,
-                                                            const float* __restrict__ theta, float* __restrict__ LP,
-                                                            int* __restrict__ flag) {
-    const int KB = split_kblocks(N), G = (N + kLRows - 1) / kLRows;
-    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (row, k), k fastest
-    if (e < (long long)G * kLRows * 4 * KB) {
-        const int r = (int)(e / (4 * KB)), k = (int)(e % (4 * KB));
-        const float q = (r < N && k < N) ? Qd[(size_t)r * N + k] : 0.0f;
-        LP[(((size_t)(r / kLRows) * KB + (k >> 2)) * kLRows + (r % kLRows)) * 4 + (k & 3)] = q;
-        bool bad = !__builtin_isfinite(q);
-        if (k == 0 && r < N) bad |= !__builtin_isfinite(theta[r]);
-        if (bad) atomicOr(flag, 1);
-    }
-}
-
-bool lean_persist_fits(int N) {
-    if (N < 1 || N > persist_max_n() || lean_persist_groups(N) > 32) return false;
-    const int threads = 64 * persist_waves(N, true);
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    if (g_tune.persist_fit_cus > 0) cus = g_tune.persist_fit_cus;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_split_persist<false, true>),
-                                                     threads, lean_persist_lds_bytes(N)) != hipSuccess)
-        return false;
-    return (long long)per * cus >= 8LL * lean_persist_groups(N);  // the whole padded grid resident
-}
-
-hipError_t launch_build_lean_persist(const float* Qd, int N, const float* theta, float* LP, int* flag, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(flag, 0, sizeof(int), s);
-    if (e != hipSuccess) return e;
-    const long long n = (long long)lean_persist_groups(N) * kLRows * 4 * split_kblocks(N);
-    hipLaunchKernelGGL(k_build_lean_persist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Qd, N, theta, LP, flag);
-    return hipGetLastError();
-}
-
-// err: 2 ints (err[0]: an expired wait, err[1]: 4 = a precondition on y failed);
-// census: lean_persist_groups(N) words
-hipError_t launch_lean_persist(const float* LP, const float* fdpn, const float* theta, const float* Qd, int N,
-                               int updates, const float* Y0, float* Yout, unsigned long long* gran,
-                               unsigned long long* census, int* err, hipStream_t s) {
-    if (updates <= 0) return hipSuccess;
-    const int G = lean_persist_groups(N), W = persist_waves(N, true);
-    hipError_t e = hipMemsetAsync(gran, 0, sizeof(u64) * 2 * N, s);
-    if (e == hipSuccess) e = hipMemsetAsync(census, 0, sizeof(u64) * G, s);
-    if (e == hipSuccess) e = hipMemsetAsync(err, 0, 2 * sizeof(int), s);
-    if (e != hipSuccess) return e;
-    // grid 8 G, every eighth workgroup takes part (xcds = 1); LDS + the census word.
-    // persist_lean_flags (A/B): bit 0 sc1 stores, bit 1 grid G (spread over the
-    // XCDs: the census then picks sc1), bit 2 no diagonal fix (timing only)
-    const int fl = g_tune.persist_lean_flags;
-    if (g_tune.persist_trace)  // the timeline (scripts/persist_trace.py LEAN=1)
-        hipLaunchKernelGGL((k_split_persist<true, true>), dim3(8 * G), dim3(64 * W), lean_persist_lds_bytes(N), s, LP,
-                           fdpn, N, updates, Y0, Yout, gran, err, g_tune.persist_trace, g_tune.persist_trace_n,
-                           g_tune.persist_stall_wg, 1, theta, Qd, census);
-    else
-        hipLaunchKernelGGL((k_split_persist<false, true>), dim3((fl & 2) ? G : 8 * G), dim3(64 * W),
-                           lean_persist_lds_bytes(N), s, LP, fdpn, N, updates, Y0, Yout, gran, err, nullptr, fl & 5,
-                           g_tune.persist_stall_wg, (fl & 2) ? 0 : 1, theta, Qd, census);
-    return hipGetLastError();
 }
 
 hipError_t launch_split_persist(const float* SP, const float* fdpn, int N, int updates, const float* Y0, float* Yout,

@@ -26,15 +26,10 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
     P = dict(Qd=b.qd_rowmajor(0), Fd=b.Fd[0, :N].cpu().numpy(), Md=b.Md[:1].cpu().numpy(),
              Qp=np.zeros(M * M, np.float32), Qp_inv=np.zeros(M * M, np.float32), Fp=np.zeros(M, np.float32),
              Mp=np.zeros(1, np.float32), Gp=np.zeros(N * M, np.float32), Kp=np.zeros(N, np.float32), N=N, M=M)
-    import os
-
     L = pqp_amd.lib()
     KB = (N + 3) // 4
-    lean = os.environ.get("LEAN", "0") == "1"  # the one-XCD form (persist_lean 1)
-    pqp_amd.tune("persist_lean", 1 if lean else 0)
-    # pqp_persist.hip: slices of 24, 36, then 49 packets (persist_slice0); lean 24, 40, 48
-    a, b_, c = (24, 40, 48) if lean else (24, 36, 49)
-    first = lambda w: 0 if w == 0 else (a if w == 1 else a + b_ + (w - 2) * c)  # noqa: E731
+    # pqp_persist.hip: slices of 24, 36, then 49 packets (persist_slice0)
+    first = lambda w: 0 if w == 0 else (24 if w == 1 else 60 + (w - 2) * 49)  # noqa: E731
     W = 1
     while first(W) < KB:
         W += 1
@@ -55,7 +50,7 @@ def main(N: int = 1024, iters: int = 1000, n_trace: int = 40):
     lo, hi = 10, 30
     period = float(np.median(np.diff(t[lo:hi, 0, 2])))  # wave 0's turn, update to update
     us_per_update = untraced / (iters - 1) * 1e6
-    out = {"form": "lean" if lean else "split", "n_dual": N, "waves": W, "us_per_update_untraced": us_per_update,
+    out = {"n_dual": N, "waves": W, "us_per_update_untraced": us_per_update,
            "us_per_update_traced": traced / (iters - 1) * 1e6, "clocks_per_update": period,
            "clock_GHz_implied": period / us_per_update / 1e3, "per_wave_median_clocks": {}}
     for w in range(W):

@@ -118,7 +118,7 @@ def test_hot_kernels_compile_for_gfx950_without_fma(src, pattern, min_kernels):
 
 
 @pytest.mark.parametrize("src,name", [
-    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0ELb0EEEvPKfS2_iiS2_PfPyPiS4_iiiS2_S2_S4_"),
+    ("pqp_persist.hip", "_ZN3pqp15k_split_persistILb0EEEvPKfS2_iiS2_PfPyPiS4_iii"),
     # the headline kernel: its register blocks pinned in AGPRs across the
     # launch (pqp_kernels.hip k_batch_resident) must stay there
     ("pqp_kernels.hip", "_ZN3pqp16k_batch_residentILi16ELi2ELi2EEEvPKfxiS2_S2_iS2_Pfi"),
@@ -230,7 +230,7 @@ def test_tuning_knobs_roundtrip():
     L = pqp_amd.lib()
     for key in ("persist_off", "lean_min_n", "batch_opts", "converge_chunk", "wide_min_n", "pipe_off",
                 "pipe_variant", "pipe_force", "mid_v1", "matmul_pk_off", "iterate_kind", "tiny_chunk", "tiny_fallback",
-                "tiny_np", "tiny_apoll", "tiny_ablk", "persist_xcds", "converge_xcds", "persist_lean", "persist_lean_flags"):
+                "tiny_np", "tiny_apoll", "tiny_ablk", "persist_xcds", "converge_xcds"):
         old = pqp_amd.tune_get(key)
         assert pqp_amd.tune(key, old + 3) == old
         assert pqp_amd.tune_get(key) == old + 3

@@ -14,7 +14,6 @@ from conftest import assert_bitwise
 pytestmark = pytest.mark.gpu
 
 FIXED_PERSIST, FIXED_RELAY, CONV_PERSIST, CONV_WIDE = 1, 2, 3, 4
-FIXED_LEAN = 6  # the fixed-mode persistent launch's one-XCD lean form (persist_lean 1)
 
 
 def _path(L):
@@ -92,33 +91,6 @@ def test_fixed_persist_stall_restarts_on_relay(gpu_lib, orc, stall, wg):
         r = prob.solve(gpu_lib.MODE_FIXED, num_iter=30)
         assert _path(L) == (FIXED_PERSIST, fb1)
         assert_bitwise(r["Y"], want, "persistent again")
-
-
-@pytest.mark.parametrize("wg", [0, 5])
-def test_fixed_lean_persist_stall_restarts_on_relay(gpu_lib, orc, stall, wg):
-    """The same with the one-XCD lean form asked for (persist_lean): a
-    workgroup that never runs leaves the census (or a hand-off) waiting, the
-    launch reports it, and the solve restarts on the relay with the oracle's
-    bits."""
-    L = stall
-    N, M = 1024, 512
-    P = orc.synth_problem(2, 4, N, M)
-    want = orc.iterate(P["Qd"], P["Fd"], N, 29)
-    old = gpu_lib.tune("persist_lean", 1)
-    try:
-        with gpu_lib.Problem(P) as prob:
-            _, fb0 = _path(L)
-            L.pqp_tune_persist_stall(wg)
-            r = prob.solve(gpu_lib.MODE_FIXED, num_iter=30)
-            path, fb1 = _path(L)
-            assert path == FIXED_RELAY and fb1 == fb0 + 1
-            assert_bitwise(r["Y"], want, "after the stalled lean launch")
-            L.pqp_tune_persist_stall(-1)
-            r = prob.solve(gpu_lib.MODE_FIXED, num_iter=30)
-            assert _path(L) == (FIXED_LEAN, fb1)
-            assert_bitwise(r["Y"], want, "lean persistent again")
-    finally:
-        gpu_lib.tune("persist_lean", old)
 
 
 @pytest.mark.parametrize("wg", [0, -2])
