@@ -1195,15 +1195,6 @@ hipError_t launch_synth_primal(uint32_t seed, long long inst0, int B, int N, int
     return hipGetLastError();
 }
 
-// Zero the padding rows [N, ldq) of every column k < N (used when the
-// generator's tiles do not cover them).
-__global__ void k_zero_pad(float* __restrict__ QdT, int N, int ldq, long long qstride) {
-    const int b = blockIdx.y;
-    const int k = blockIdx.x;
-    float* col = QdT + (size_t)b * qstride + (size_t)k * ldq;
-    for (int i = N + threadIdx.x; i < ldq; i += blockDim.x) col[i] = 0.0f;
-}
-
 // ---------------------------------------------------------------------------
 typedef float sf4 __attribute__((ext_vector_type(4)));  // (repeated, same type, in the solve-single region)
 
